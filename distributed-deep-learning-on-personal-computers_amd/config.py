@@ -1,0 +1,188 @@
+"""Typed training configuration.
+
+The reference keeps every knob as a module global or a literal:
+``frequency_sending_gradients``/``batch_size``/``NN_in_model`` (ref.py:685-687),
+``compress_model``/``model_bytes`` (ref.py:24-25), ``N_conn`` (ref.py:223), the
+hard-coded server IP/port (ref.py:176-178), ``out_classes=6`` (ref.py:702), the
+up-sample mode default (ref.py:621), 100 epochs (ref.py:720), 127 samples of 512²
+(ref.py:737) and the last-30 test split (ref.py:672-673).
+
+Here they are one dataclass, settable from a YAML/JSON file and from CLI flags.
+Rendezvous is NOT part of the config: it comes from the torchrun environment
+(RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT).
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import json
+import os
+from dataclasses import dataclass, field, fields
+from typing import Any, Dict, Optional
+
+GRAD_CODECS = ("none", "fp16_absmax", "int8_absmax")
+CODEC_SCALES = ("global", "bucket", "tensor")
+REDUCE_OPS = ("mean", "sum", "reference")
+UP_MODES = ("conv_transpose", "bilinear")
+DATA_KINDS = ("synthetic", "vaihingen_dir")
+
+
+@dataclass
+class ModelConfig:
+    """U-Net architecture knobs (ref.py:620-641)."""
+
+    in_channels: int = 3
+    out_classes: int = 6                 # ref.py:702
+    width_divisor: int = 2               # NN_in_model, ref.py:687
+    depth: int = 5                       # 5 levels in the reference; 4 for config #1
+    up_sample_mode: str = "conv_transpose"  # ref.py:621
+    dims: int = 2                        # 2 = images; 3 = volumes (BASELINE config #5)
+    base_widths: tuple = (64, 128, 256, 512, 512)
+
+    def widths(self):
+        return [w // self.width_divisor for w in self.base_widths[: self.depth]]
+
+    def validate(self):
+        if self.up_sample_mode not in UP_MODES:
+            raise ValueError(
+                "Unsupported `up_sample_mode` (can take one of `conv_transpose` or `bilinear`)")
+        if self.dims not in (2, 3):
+            raise ValueError("dims must be 2 or 3")
+        if not 1 <= self.depth <= len(self.base_widths):
+            raise ValueError(f"depth must be in [1, {len(self.base_widths)}]")
+
+
+@dataclass
+class TrainConfig:
+    model: ModelConfig = field(default_factory=ModelConfig)
+    # ---- data ----------------------------------------------------------------
+    data: str = "synthetic"              # synthetic | vaihingen_dir
+    data_dir: Optional[str] = None       # directory of image + .npy label pairs (ref.py:660-674)
+    tile: int = 256                      # H = W (D too for dims=3); reference: 512 (ref.py:737)
+    num_samples: int = 127               # synthetic dataset length (ref.py:750: 127 tiles/epoch)
+    test_holdout: int = 30               # last N pairs are the test split (ref.py:672-673)
+    shard_data: bool = True              # False = reference "replicated data" mode (§2.2)
+    shuffle: bool = True
+    # ---- optimisation ----------------------------------------------------------
+    batch_per_gpu: int = 1               # batch_size, ref.py:686
+    accum_steps: int = 1                 # frequency_sending_gradients, ref.py:685
+    epochs: int = 1                      # reference: 100 (ref.py:720)
+    max_steps: Optional[int] = None      # optimizer steps cap (benchmarks / smoke)
+    lr: float = 1e-3                     # torch.optim.Adam defaults (ref.py:704)
+    betas: tuple = (0.9, 0.999)
+    eps: float = 1e-8
+    weight_decay: float = 0.0
+    dtype: str = "bf16"                  # compute dtype on GPU (fp32 master weights)
+    seed: int = 0
+    # ---- data parallel -----------------------------------------------------------
+    backend: Optional[str] = None        # None = nccl(RCCL) on GPU, gloo on CPU
+    bucket_mb: float = 8.0
+    reduce: str = "mean"                 # mean | sum | reference (the W=2 "sum" parity mode)
+    grad_codec: str = "none"             # none | fp16_absmax | int8_absmax (ref.py:25)
+    codec_scale: str = "bucket"          # global (reference parity) | bucket | tensor
+    overlap_comm: bool = True
+    broadcast_buffers: bool = False      # BN running stats from rank 0 (reference: off)
+    check_consistency_every: int = 0     # debug: all-reduce a param checksum every K steps
+    timeout_s: int = 1800
+    # ---- io ----------------------------------------------------------------------
+    ckpt_dir: Optional[str] = None
+    ckpt_every: int = 0                  # optimizer steps; 0 = only at end of train()
+    resume: Optional[str] = None
+    log_dir: Optional[str] = None        # JSONL metrics + otus_<codec>.txt
+    png_dir: Optional[str] = None        # prediction/label/image dumps (ref.py:785-790)
+    png_count: int = 5
+    log_every: int = 10
+    # ---- execution -----------------------------------------------------------------
+    impl: str = "auto"                   # auto | hip | torch   (hip = hand-written kernels)
+    hip_graph: bool = False              # capture the train step in a hipGraph
+
+    def validate(self):
+        self.model.validate()
+        for name, val, allowed in (("grad_codec", self.grad_codec, GRAD_CODECS),
+                                   ("codec_scale", self.codec_scale, CODEC_SCALES),
+                                   ("reduce", self.reduce, REDUCE_OPS),
+                                   ("data", self.data, DATA_KINDS),
+                                   ("impl", self.impl, ("auto", "hip", "torch")),
+                                   ("dtype", self.dtype, ("bf16", "fp32"))):
+            if val not in allowed:
+                raise ValueError(f"{name}={val!r} not in {allowed}")
+        if self.accum_steps < 1 or self.batch_per_gpu < 1:
+            raise ValueError("accum_steps and batch_per_gpu must be >= 1")
+        return self
+
+    # ---- (de)serialisation ---------------------------------------------------------
+    def to_dict(self) -> Dict[str, Any]:
+        d = dataclasses.asdict(self)
+        d["model"]["base_widths"] = list(self.model.base_widths)
+        d["betas"] = list(self.betas)
+        return d
+
+    @classmethod
+    def from_dict(cls, d: Dict[str, Any]) -> "TrainConfig":
+        d = dict(d)
+        m = dict(d.pop("model", {}) or {})
+        if "base_widths" in m:
+            m["base_widths"] = tuple(m["base_widths"])
+        known = {f.name for f in fields(cls)}
+        unknown = set(d) - known
+        if unknown:
+            raise ValueError(f"unknown config keys: {sorted(unknown)}")
+        if "betas" in d:
+            d["betas"] = tuple(d["betas"])
+        return cls(model=ModelConfig(**m), **d).validate()
+
+    @classmethod
+    def load(cls, path: str) -> "TrainConfig":
+        with open(path) as f:
+            if path.endswith((".yaml", ".yml")):
+                import yaml
+                d = yaml.safe_load(f)
+            else:
+                d = json.load(f)
+        return cls.from_dict(d or {})
+
+    def save(self, path: str):
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(self.to_dict(), f, indent=2)
+
+
+def _flag_type(tp, default):
+    if tp in ("bool", bool) or isinstance(default, bool):
+        return lambda s: str(s).lower() in ("1", "true", "yes", "on")
+    if isinstance(default, float):
+        return float
+    if isinstance(default, int):
+        return int
+    if isinstance(default, tuple):
+        return lambda s: tuple(float(x) for x in s.split(","))
+    return lambda s: None if s in ("", "none", "None") else s
+
+
+def add_config_args(p: argparse.ArgumentParser):
+    """Expose every TrainConfig/ModelConfig field as ``--name`` (model fields too)."""
+    p.add_argument("--config", default=None, help="YAML/JSON config file")
+    base = TrainConfig()
+    for f in fields(TrainConfig):
+        if f.name == "model":
+            continue
+        p.add_argument("--" + f.name.replace("_", "-"), dest=f.name, default=None,
+                       type=_flag_type(f.type, getattr(base, f.name)))
+    for f in fields(ModelConfig):
+        if f.name == "base_widths":
+            continue
+        p.add_argument("--" + f.name.replace("_", "-"), dest="model__" + f.name, default=None,
+                       type=_flag_type(f.type, getattr(base.model, f.name)))
+    return p
+
+
+def config_from_args(args: argparse.Namespace) -> TrainConfig:
+    cfg = TrainConfig.load(args.config) if getattr(args, "config", None) else TrainConfig()
+    for k, v in vars(args).items():
+        if v is None or k == "config":
+            continue
+        if k.startswith("model__"):
+            setattr(cfg.model, k[len("model__"):], v)
+        elif hasattr(cfg, k):
+            setattr(cfg, k, v)
+    return cfg.validate()

@@ -1,0 +1,53 @@
+"""Loader for the in-tree HIP kernel library (``csrc/`` -> ``_lib/libddlpc_hip.so``).
+
+The library is built by ``__graft_entry__.build()`` / ``python scripts/build_ext.py`` with
+``hipcc --offload-arch=gfx950`` and registers its operators with ``TORCH_LIBRARY(ddlpc)``
+so they appear as ``torch.ops.ddlpc.*`` (and by kernel name in rocprof).  Nothing here
+falls back silently: requesting the ops on a machine with a GPU but without the built
+library raises.
+"""
+from __future__ import annotations
+
+import os
+import threading
+
+import torch
+
+_LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib")
+LIB_PATH = os.path.join(_LIB_DIR, "libddlpc_hip.so")
+_lock = threading.Lock()
+_loaded = False
+_error = None
+
+
+def load(strict: bool = True) -> bool:
+    global _loaded, _error
+    with _lock:
+        if _loaded:
+            return True
+        if not os.path.exists(LIB_PATH):
+            _error = f"HIP kernel library not built: {LIB_PATH} (run scripts/build_ext.py)"
+        else:
+            try:
+                torch.ops.load_library(LIB_PATH)
+                _loaded = True
+                return True
+            except Exception as e:       # pragma: no cover - depends on the box
+                _error = f"failed to load {LIB_PATH}: {e}"
+        if strict:
+            raise RuntimeError(_error)
+        return False
+
+
+def available() -> bool:
+    return load(strict=False)
+
+
+def ops():
+    """``torch.ops.ddlpc`` — raises if the library is missing (no silent fallback)."""
+    load(strict=True)
+    return torch.ops.ddlpc
+
+
+def last_error():
+    return _error

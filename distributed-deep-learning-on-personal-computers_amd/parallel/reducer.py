@@ -1,0 +1,216 @@
+"""Bucketed data-parallel gradient reducer, overlapped with backward.
+
+Replaces the reference's star exchange: workers encode
+their accumulated gradients, send them to rank 0 over TCP, rank 0 merges, re-encodes and
+sends back, everyone steps Adam (ref.py:255-556).  That serialises a 2*M*msg transfer
+through one link and round-trips every tensor through the host.
+
+MI355X design:
+
+* gradients are views into ONE flat fp32 buffer (``FlatParams``); buckets are contiguous
+  slices of it in backward order, sized by ``bucket_mb`` (few, large: on 7 point-to-point
+  xGMI links per GPU a ring all-reduce is per-link bound, and per-collective latency is
+  tens of µs, so 3-5 buckets of ~8 MB beat many small ones);
+* ``register_post_accumulate_grad_hook`` marks parameters ready; when the LAST
+  micro-batch's backward completes a bucket, its collective is launched immediately
+  (async) so it runs on RCCL's own stream while backward continues on the compute
+  stream: the deep decoder/bottleneck gradients (most of the bytes) reduce while the
+  high-resolution encoder layers are still in backward;
+* accumulation micro-batches (``frequency_sending_gradients``, ref.py:685/759) launch
+  nothing (no_sync semantics);
+* ``finish()`` makes the compute stream wait for every bucket (no host sync) before the
+  optimizer step;
+* reduction: correct mean (sum * 1/W, or RCCL ``AVG``), ``sum``, or ``reference`` (the
+  reference's skewed weights; for W=2 that is a plain sum);
+* optional lossy codec (fp16/int8 absmax, ref.py:25) as an all-gather of packed payloads
+  + scales, decoded and summed in rank order (``parallel.codec``; fused HIP kernels on GPU).
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from . import codec as C
+from .flat import FlatParams
+
+
+class _Bucket:
+    __slots__ = ("idx", "start", "end", "params", "pending", "work", "payload", "scales",
+                 "gathered", "launched")
+
+    def __init__(self, idx, start, end, params):
+        self.idx, self.start, self.end, self.params = idx, start, end, params
+        self.pending = len(params)
+        self.work = None
+        self.payload = self.scales = self.gathered = None
+        self.launched = False
+
+
+class GradBucketReducer:
+    def __init__(self, flat: FlatParams, group=None, bucket_mb: float = 8.0,
+                 reduce: str = "mean", grad_codec: str = "none", codec_scale: str = "bucket",
+                 overlap: bool = True):
+        self.flat = flat
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.backend = dist.get_backend(group) if dist.is_initialized() else None
+        self.reduce, self.codec, self.codec_scale = reduce, grad_codec, codec_scale
+        self.overlap = overlap and not (grad_codec != "none" and codec_scale == "global")
+        if reduce == "mean":
+            self.weight = 1.0 / self.world
+        elif reduce == "sum":
+            self.weight = 1.0
+        elif reduce == "reference":
+            self.weight = C.reference_weights(self.world)[self.rank]
+        else:
+            raise ValueError(reduce)
+        self.buckets = self._make_buckets(bucket_mb)
+        self._bucket_of: Dict[int, _Bucket] = {}
+        for b in self.buckets:
+            for p in b.params:
+                self._bucket_of[id(p)] = b
+        self._sync = True
+        self._hooks = []
+        if self.world > 1:
+            for p in flat.order:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
+        self.stats = {"buckets": len(self.buckets), "launched_in_backward": 0}
+
+    # ------------------------------------------------------------------ setup
+    def _make_buckets(self, bucket_mb: float) -> List[_Bucket]:
+        cap = max(1, int(bucket_mb * (1 << 20) // 4))
+        buckets, cur, start = [], [], None
+        end = 0
+        for p in self.flat.order:
+            a, b = self.flat.span(p)
+            if start is None:
+                start = a
+            if cur and (b - start) > cap:
+                buckets.append(_Bucket(len(buckets), start, end, cur))
+                cur, start = [], a
+            cur.append(p)
+            end = b
+        if cur:
+            buckets.append(_Bucket(len(buckets), start, end, cur))
+        # last bucket extends over trailing alignment padding (harmless zeros)
+        return buckets
+
+    def bucket_ranges(self) -> List[Tuple[int, int]]:
+        return [(b.start, b.end) for b in self.buckets]
+
+    # ------------------------------------------------------------------ per step
+    @contextlib.contextmanager
+    def no_sync(self):
+        prev, self._sync = self._sync, False
+        try:
+            yield
+        finally:
+            self._sync = prev
+
+    def prepare(self, sync: bool = True):
+        """Call before each micro-batch backward: ``sync`` only on the last one."""
+        self._sync = sync
+        if sync:
+            for b in self.buckets:
+                b.pending = len(b.params)
+                b.work = None
+                b.launched = False
+                b.payload = b.scales = b.gathered = None
+
+    def _on_grad_ready(self, p):
+        if not self._sync or not self.overlap:
+            return
+        b = self._bucket_of.get(id(p))
+        if b is None:
+            return
+        b.pending -= 1
+        if b.pending == 0 and not b.launched:
+            self._launch(b)
+            self.stats["launched_in_backward"] += 1
+
+    def _seg(self, b: _Bucket) -> torch.Tensor:
+        return self.flat.grad_buf[b.start:b.end]
+
+    def _launch(self, b: _Bucket):
+        b.launched = True
+        g = self._seg(b)
+        if self.codec == "none":
+            if self.reduce == "mean" and self.backend == "nccl":
+                b.work = dist.all_reduce(g, op=dist.ReduceOp.AVG, group=self.group,
+                                         async_op=True)
+            else:
+                if self.weight != 1.0:
+                    g.mul_(self.weight)
+                b.work = dist.all_reduce(g, group=self.group, async_op=True)
+            return
+        # lossy codec: encode -> all_gather(payload, scales) -> decode+sum at finish()
+        segs = self._codec_segments(b)
+        from ..ops import codec_ops
+        b.payload, b.scales = codec_ops.encode_segments(g, segs, self.codec)
+        b.gathered = ([torch.empty_like(b.payload) for _ in range(self.world)],
+                      [torch.empty_like(b.scales) for _ in range(self.world)])
+        w1 = dist.all_gather(b.gathered[0], b.payload, group=self.group, async_op=True)
+        w2 = dist.all_gather(b.gathered[1], b.scales, group=self.group, async_op=True)
+        b.work = (w1, w2)
+
+    def _codec_segments(self, b: _Bucket) -> List[Tuple[int, int]]:
+        if self.codec_scale == "tensor":
+            return [(s - b.start, e - b.start) for s, e in (self.flat.span(p) for p in b.params)]
+        return [(0, b.end - b.start)]
+
+    def finish(self):
+        """Complete all reductions (launch stragglers); compute stream waits, host does not."""
+        if self.world == 1:
+            if self.reduce == "sum" or self.weight == 1.0:
+                return
+            return
+        if self.codec != "none" and self.codec_scale == "global":
+            self._finish_global_codec()
+            return
+        for b in self.buckets:
+            if not b.launched:
+                self._launch(b)
+        for b in self.buckets:
+            if b.work is None:
+                continue
+            if isinstance(b.work, tuple):
+                for w in b.work:
+                    w.wait()
+                self._decode_bucket(b)
+            else:
+                b.work.wait()
+            b.work = None
+        self._sync = True
+
+    def _decode_bucket(self, b: _Bucket):
+        from ..ops import codec_ops
+        g = self._seg(b)
+        segs = self._codec_segments(b)
+        weights = (C.reference_weights(self.world) if self.reduce == "reference"
+                   else [self.weight] * self.world)
+        codec_ops.decode_sum_segments(g, b.gathered[0], b.gathered[1], segs, self.codec,
+                                      weights)
+        b.gathered = b.payload = b.scales = None
+
+    def _finish_global_codec(self):
+        """Reference-parity mode: one absmax over the WHOLE gradient (ref.py:328-340)."""
+        from ..ops import codec_ops
+        g = self.flat.grad_buf
+        segs = [(0, g.numel())]
+        payload, scales = codec_ops.encode_segments(g, segs, self.codec)
+        qs = [torch.empty_like(payload) for _ in range(self.world)]
+        ss = [torch.empty_like(scales) for _ in range(self.world)]
+        dist.all_gather(qs, payload, group=self.group)
+        dist.all_gather(ss, scales, group=self.group)
+        weights = (C.reference_weights(self.world) if self.reduce == "reference"
+                   else [self.weight] * self.world)
+        codec_ops.decode_sum_segments(g, qs, ss, segs, self.codec, weights)
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

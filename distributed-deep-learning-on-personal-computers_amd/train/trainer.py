@@ -1,0 +1,295 @@
+"""``train()`` / ``validate()`` entrypoints and the data-parallel training step.
+
+Reference training drivers: rank 0 ("server", ref.py:690-790)
+and rank>0 ("worker", ref.py:792-895) run the same loop — forward, ``CrossEntropyLoss``,
+``backward()`` accumulating into ``.grad`` WITHOUT zero_grad, and every
+``frequency_sending_gradients``-th micro-batch a gradient exchange + ``optimizer.step()``
++ ``zero_grad()`` (ref.py:750-766, 864-879).
+
+This trainer keeps those semantics — ``accum_steps`` micro-batches of ``batch_per_gpu``
+per optimizer step, gradients accumulated in place, one synchronous exchange per step so
+every rank applies identical gradients — with the MI355X machinery underneath:
+
+* one process per GPU, ``torch.distributed`` over RCCL (gloo on CPU);
+* the U-Net hot path in hand-written HIP kernels (``impl="hip"``: NHWC bf16 MFMA
+  convolutions with fused BN/ReLU/pool/concat, fused head+CE) or stock PyTorch
+  (``impl="torch"``: the CPU path and the MIOpen in-house baseline);
+* flat fp32 parameters/gradients, a bucketed all-reduce launched from backward hooks on
+  the last micro-batch only, one fused Adam launch;
+* metrics accumulate on the device and are reduced across ranks only at log points.
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+import os
+import time
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..config import TrainConfig
+from ..data import ShardedSampler, SyntheticTiles, TileDataset
+from ..models.unet import UNet
+from ..ops import _ext
+from ..ops.adam import FlatAdam
+from ..parallel import (GradBucketReducer, assert_replicas_identical, broadcast_buffers,
+                        broadcast_module, flatten_module, init_distributed)
+from ..utils.metrics import DeviceMeter, RunLogger, StepTimer, dump_pngs, iou_per_class
+from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
+
+
+def resolve_impl(impl: str, device: torch.device) -> str:
+    if device.type != "cuda":
+        if impl == "hip":
+            raise RuntimeError("impl='hip' needs a GPU")
+        return "torch"
+    if impl == "auto":
+        return "hip"
+    return impl
+
+
+class Trainer:
+    def __init__(self, cfg: TrainConfig, device: Optional[str] = None):
+        cfg.validate()
+        self.cfg = cfg
+        self.info = init_distributed(cfg.backend, cfg.timeout_s, device)
+        self.device = self.info.device
+        self.rank, self.world = self.info.rank, self.info.world_size
+        torch.manual_seed(cfg.seed)                  # identical init on every rank ...
+        model = UNet.from_config(cfg.model).to(self.device)
+        self.impl = resolve_impl(cfg.impl, self.device)
+        self.model = model
+        self.flat = flatten_module(model)
+        broadcast_module(model, src=0)               # ... and rank 0 is authoritative
+        if self.impl == "hip":
+            _ext.ops()                               # fail loudly if kernels are missing
+            model.to_hip()
+        self.optimizer = FlatAdam(self.flat, lr=cfg.lr, betas=cfg.betas, eps=cfg.eps,
+                                  weight_decay=cfg.weight_decay)
+        if self.impl == "hip":
+            self.optimizer.weight_pack = model._engine.pack_weights
+        self.reducer = None
+        if self.world > 1:
+            self.reducer = GradBucketReducer(self.flat, bucket_mb=cfg.bucket_mb,
+                                             reduce=cfg.reduce, grad_codec=cfg.grad_codec,
+                                             codec_scale=cfg.codec_scale,
+                                             overlap=cfg.overlap_comm)
+        self.autocast = (self.device.type == "cuda" and self.impl == "torch"
+                         and cfg.dtype == "bf16")
+        if self.device.type == "cuda" and self.impl == "torch":
+            model.to(memory_format=torch.channels_last)
+            self.flat.rebind_grads()
+        self.meter = DeviceMeter(self.device)
+        self.logger = RunLogger(cfg.log_dir, self.rank, cfg.grad_codec)
+        self.step_count = 0
+        self.micro_count = 0
+        self.epoch = 0
+        self.train_set, self.test_set = self._build_data()
+        self.sampler = ShardedSampler(len(self.train_set), self.rank, self.world,
+                                      shard=cfg.shard_data, shuffle=cfg.shuffle, seed=cfg.seed)
+        if cfg.resume:
+            path = latest_checkpoint(cfg.ckpt_dir) if cfg.resume == "auto" else cfg.resume
+            if path:
+                self.load(path)
+
+    # ------------------------------------------------------------------ data
+    def _build_data(self):
+        c = self.cfg
+        if c.data == "vaihingen_dir":
+            if not c.data_dir:
+                raise ValueError("data=vaihingen_dir needs data_dir")
+            return TileDataset.from_dir(c.data_dir, c.test_holdout)
+        n_total = c.num_samples + c.test_holdout
+        full = SyntheticTiles(n_total, c.tile, c.model.out_classes, c.model.in_channels,
+                              seed=c.seed, dims=c.model.dims)
+        return _Subset(full, 0, c.num_samples), _Subset(full, c.num_samples, n_total)
+
+    def _to_device(self, x, y):
+        x = x.to(self.device, non_blocking=True)
+        y = y.to(self.device, non_blocking=True)
+        if self.device.type == "cuda" and self.cfg.model.dims == 2:
+            x = x.to(memory_format=torch.channels_last)
+            if self.impl == "hip":
+                x = x.to(torch.bfloat16)
+        return x, y
+
+    # ------------------------------------------------------------------ step
+    def _micro(self, x, y, sync: bool):
+        if self.reducer is not None:
+            self.reducer.prepare(sync=sync)
+        ctx = (torch.autocast("cuda", dtype=torch.bfloat16) if self.autocast
+               else contextlib.nullcontext())
+        with ctx:
+            loss, correct = self.model.loss_and_correct(x, y)
+        loss.backward()
+        self.meter.add(loss, correct, y.numel())
+        self.micro_count += 1
+        return loss
+
+    def train_step(self, micro_batches: List[Tuple[torch.Tensor, torch.Tensor]]):
+        """One optimizer step over ``len(micro_batches)`` accumulated micro-batches."""
+        self.model.train()
+        n = len(micro_batches)
+        for i, (x, y) in enumerate(micro_batches):
+            self._micro(x, y, sync=(i == n - 1))
+        if self.reducer is not None:
+            self.reducer.finish()
+        self.optimizer.step()
+        self.optimizer.zero_grad()
+        if self.cfg.broadcast_buffers:
+            broadcast_buffers(self.model)
+        self.step_count += 1
+        k = self.cfg.check_consistency_every
+        if k and self.step_count % k == 0:
+            assert_replicas_identical(self.model)
+
+    def fit(self) -> Dict[str, float]:
+        c = self.cfg
+        self.logger.header(c.batch_per_gpu, self.world, c.accum_steps, c.model.width_divisor)
+        last = {}
+        t_start = time.perf_counter()
+        while self.epoch < c.epochs:
+            self.sampler.set_epoch(self.epoch)
+            self.meter.reset()
+            t_ep = time.perf_counter()
+            pending: List[Tuple[torch.Tensor, torch.Tensor]] = []
+            steps_this_epoch = 0
+            for idx in self.sampler.batches(c.batch_per_gpu):
+                pending.append(self._to_device(*self.train_set.get(idx)))
+                if len(pending) < c.accum_steps:
+                    continue
+                self.train_step(pending)
+                pending = []
+                steps_this_epoch += 1
+                if c.log_every and self.step_count % c.log_every == 0:
+                    m = self.meter.reduce()
+                    rec = {"epoch": self.epoch, "step": self.step_count, **m,
+                           "elapsed_s": time.perf_counter() - t_start}
+                    self.logger.log(rec)
+                if c.ckpt_dir and c.ckpt_every and self.step_count % c.ckpt_every == 0:
+                    self.save()
+                if c.max_steps and self.step_count >= c.max_steps:
+                    break
+            # leftover micro-batches: gradients stay accumulated into the next epoch's first
+            # step, as in the reference (ref.py:748: 127 % 50 = 27 carry over).
+            for x, y in pending:
+                self._micro(x, y, sync=False)
+            ep_s = time.perf_counter() - t_ep
+            last = self.meter.reduce()
+            last.update(epoch=self.epoch, epoch_s=ep_s, steps=self.step_count)
+            self.logger.epoch_line(self.epoch, last["loss"], last["pixel_acc"], ep_s,
+                                   ep_s / max(steps_this_epoch, 1))
+            self.logger.log({"epoch_end": self.epoch, **last})
+            if c.png_dir and self.rank == 0:
+                x, y = self.train_set.get(list(range(min(c.png_count, len(self.train_set)))))
+                dump_pngs(self.model, *self._to_device(x, y), c.png_dir, c.png_count)
+            self.epoch += 1
+            if c.max_steps and self.step_count >= c.max_steps:
+                break
+        if c.ckpt_dir:
+            self.save()
+        return last
+
+    # ------------------------------------------------------------------ eval
+    @torch.no_grad()
+    def validate(self, dataset=None, batch: Optional[int] = None) -> Dict[str, float]:
+        """Held-out loss, pixel accuracy and per-class IoU (the reference never evaluates its
+        30-tile test split, ref.py:672-673), sharded over ranks and all-reduced."""
+        ds = dataset if dataset is not None else self.test_set
+        if ds is None or len(ds) == 0:
+            return {}
+        self.model.eval()
+        k = self.cfg.model.out_classes
+        bs = batch or self.cfg.batch_per_gpu
+        acc = torch.zeros(3, dtype=torch.float64, device=self.device)
+        cm = torch.zeros(k * k, dtype=torch.float64, device=self.device)
+        idx_all = list(range(len(ds)))[self.rank::self.world]
+        for i in range(0, len(idx_all), bs):
+            x, y = self._to_device(*ds.get(idx_all[i:i + bs]))
+            ctx = (torch.autocast("cuda", dtype=torch.bfloat16) if self.autocast
+                   else contextlib.nullcontext())
+            with ctx:
+                logits = self.model(x)
+            logits = logits.float()
+            loss = torch.nn.functional.cross_entropy(logits, y, reduction="sum")
+            pred = logits.argmax(1)
+            acc += torch.stack([loss.double(), (pred == y).sum().double(),
+                                torch.tensor(float(y.numel()), device=self.device,
+                                             dtype=torch.float64)])
+            cm += torch.bincount((y * k + pred).reshape(-1), minlength=k * k).double()
+        if dist.is_available() and dist.is_initialized():
+            dist.all_reduce(acc)
+            dist.all_reduce(cm)
+        self.model.train()
+        cmm = cm.reshape(k, k)
+        inter = cmm.diag()
+        union = cmm.sum(0) + cmm.sum(1) - inter
+        iou = (inter / union.clamp_min(1)).tolist()
+        valid = (union > 0).tolist()
+        miou = [v for v, ok in zip(iou, valid) if ok]
+        a = acc.tolist()
+        return {"val_loss": a[0] / max(a[2], 1), "val_pixel_acc": a[1] / max(a[2], 1),
+                "val_iou": iou, "val_miou": sum(miou) / max(len(miou), 1)}
+
+    # ------------------------------------------------------------------ checkpoint
+    def save(self, path: Optional[str] = None) -> Optional[str]:
+        path = path or os.path.join(self.cfg.ckpt_dir, f"ckpt_{self.step_count}.pt")
+        if self.rank == 0:
+            save_checkpoint(path, self.model, self.optimizer, epoch=self.epoch,
+                            step=self.step_count, micro_step=self.micro_count,
+                            config=self.cfg.to_dict())
+        if dist.is_available() and dist.is_initialized():
+            dist.barrier()
+        return path
+
+    def load(self, path: str):
+        blob = load_checkpoint(path, self.model, self.optimizer)
+        self.epoch = int(blob.get("epoch", 0))
+        self.step_count = int(blob.get("step", 0))
+        self.micro_count = int(blob.get("micro_step", 0))
+        if self.model._engine is not None:
+            self.model._engine.pack_weights()
+        return blob
+
+    def close(self):
+        self.logger.close()
+        if self.reducer is not None:
+            self.reducer.remove_hooks()
+
+
+class _Subset:
+    def __init__(self, base, start, end):
+        self.base, self.start, self.end = base, start, end
+
+    def __len__(self):
+        return self.end - self.start
+
+    def get(self, idx):
+        idx = [self.start + int(i) for i in torch.as_tensor(idx).reshape(-1).tolist()]
+        return self.base.get(idx)
+
+
+def train(cfg: TrainConfig, device: Optional[str] = None, return_trainer: bool = False):
+    """Train per ``cfg``; returns the last epoch's reduced metrics (and the trainer)."""
+    tr = Trainer(cfg, device)
+    try:
+        m = tr.fit()
+    finally:
+        tr.close()
+    return (m, tr) if return_trainer else m
+
+
+def validate(cfg_or_trainer, checkpoint: Optional[str] = None,
+             device: Optional[str] = None) -> Dict[str, float]:
+    """Evaluate a trainer, or build one from ``cfg`` (+ optional checkpoint) and evaluate."""
+    if isinstance(cfg_or_trainer, Trainer):
+        return cfg_or_trainer.validate()
+    tr = Trainer(cfg_or_trainer, device)
+    if checkpoint:
+        tr.load(checkpoint)
+    try:
+        return tr.validate()
+    finally:
+        tr.close()
