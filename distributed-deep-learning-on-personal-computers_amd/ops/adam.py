@@ -28,7 +28,7 @@ from . import _ext
 
 class FlatAdam(torch.optim.Optimizer):
     def __init__(self, flat, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0):
+                 weight_decay: float = 0.0, use_hip: Optional[bool] = None):
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
                         amsgrad=False, maximize=False, foreach=None, capturable=False,
                         differentiable=False, fused=None)
@@ -40,7 +40,7 @@ class FlatAdam(torch.optim.Optimizer):
         self.step_count = 0
         self._bind_state()
         self.weight_pack = None          # set by ops.fused_unet (bf16 conv-weight copies)
-        self._use_hip = dev.type == "cuda"
+        self._use_hip = (dev.type == "cuda") if use_hip is None else use_hip
         if self._use_hip:
             _ext.ops()                   # fail loudly if the kernel library is missing
 
@@ -49,8 +49,8 @@ class FlatAdam(torch.optim.Optimizer):
             a, b = self.flat.span(p)
             st = self.state[p]
             st["step"] = torch.tensor(float(self.step_count))
-            st["exp_avg"] = self.exp_avg[a:b].view_as(p)
-            st["exp_avg_sq"] = self.exp_avg_sq[a:b].view_as(p)
+            st["exp_avg"] = self.flat._view(self.exp_avg, a, p)
+            st["exp_avg_sq"] = self.flat._view(self.exp_avg_sq, a, p)
 
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero_grad()
@@ -90,8 +90,8 @@ class FlatAdam(torch.optim.Optimizer):
                 st = self.state.get(p, {})
                 a, b = self.flat.span(p)
                 if "exp_avg" in st:
-                    self.exp_avg[a:b].copy_(st["exp_avg"].reshape(-1))
-                    self.exp_avg_sq[a:b].copy_(st["exp_avg_sq"].reshape(-1))
+                    self.flat._view(self.exp_avg, a, p).copy_(st["exp_avg"])
+                    self.flat._view(self.exp_avg_sq, a, p).copy_(st["exp_avg_sq"])
                 if "step" in st:
                     steps.append(int(float(st["step"])))
         self.step_count = max(steps) if steps else 0

@@ -39,10 +39,17 @@ class FlatParams:
         with torch.no_grad():
             for p in order:
                 o = offs[id(p)]
-                view = self.param_buf[o:o + p.numel()].view_as(p)
+                view = self._view(self.param_buf, o, p)
                 view.copy_(p.data.float())
                 p.data = view
-                p.grad = self.grad_buf[o:o + p.numel()].view_as(p)
+                p.grad = self._view(self.grad_buf, o, p)
+
+    @staticmethod
+    def _view(buf, o, p):
+        # keep the parameter's strides (e.g. channels_last conv weights) on the flat buffer
+        if p.is_contiguous():
+            return buf[o:o + p.numel()].view_as(p)
+        return buf.as_strided(p.shape, p.stride(), o)
 
     def span(self, p) -> Tuple[int, int]:
         o = self.offsets[id(p)]
@@ -56,7 +63,7 @@ class FlatParams:
         for p in self.order:
             o = self.offsets[id(p)]
             if p.grad is None or p.grad.data_ptr() != self.grad_buf[o:].data_ptr():
-                p.grad = self.grad_buf[o:o + p.numel()].view_as(p)
+                p.grad = self._view(self.grad_buf, o, p)
 
     def check_bound(self) -> bool:
         for p in self.order:

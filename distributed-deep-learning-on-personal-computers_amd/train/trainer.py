@@ -61,13 +61,16 @@ class Trainer:
         model = UNet.from_config(cfg.model).to(self.device)
         self.impl = resolve_impl(cfg.impl, self.device)
         self.model = model
+        if self.device.type == "cuda" and self.impl == "torch":
+            model.to(memory_format=torch.channels_last)    # MIOpen NHWC path (baseline)
         self.flat = flatten_module(model)
         broadcast_module(model, src=0)               # ... and rank 0 is authoritative
         if self.impl == "hip":
             _ext.ops()                               # fail loudly if kernels are missing
             model.to_hip()
         self.optimizer = FlatAdam(self.flat, lr=cfg.lr, betas=cfg.betas, eps=cfg.eps,
-                                  weight_decay=cfg.weight_decay)
+                                  weight_decay=cfg.weight_decay,
+                                  use_hip=(self.impl == "hip"))
         if self.impl == "hip":
             self.optimizer.weight_pack = model._engine.pack_weights
         self.reducer = None
@@ -78,9 +81,6 @@ class Trainer:
                                              overlap=cfg.overlap_comm)
         self.autocast = (self.device.type == "cuda" and self.impl == "torch"
                          and cfg.dtype == "bf16")
-        if self.device.type == "cuda" and self.impl == "torch":
-            model.to(memory_format=torch.channels_last)
-            self.flat.rebind_grads()
         self.meter = DeviceMeter(self.device)
         self.logger = RunLogger(cfg.log_dir, self.rank, cfg.grad_codec)
         self.step_count = 0
