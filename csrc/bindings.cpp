@@ -1,0 +1,570 @@
+// PyTorch operator registration for the gfx950 kernel library: TORCH_LIBRARY(ddlpc, ...)
+// exposes every kernel as torch.ops.ddlpc.<name> (CUDA/HIP dispatch key only: no CPU
+// fallback is registered, so a CPU tensor reaching these ops fails loudly).
+//
+// Tensor conventions: activations are channel-last tensors whose SHAPE is [N, (D,) H, W, C]
+// (contiguous), bf16.  Parameters are fp32 in standard PyTorch layouts; packed bf16 weight
+// copies are produced by weight_pack.
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <vector>
+
+#include "ops.h"
+
+namespace ddlpc {
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bf16")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be fp32")
+
+const bf16_t* bptr(const at::Tensor& t) { return reinterpret_cast<const bf16_t*>(t.data_ptr()); }
+bf16_t* bptr_mut(at::Tensor& t) { return reinterpret_cast<bf16_t*>(t.data_ptr()); }
+const float* fptr_opt(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
+}
+
+struct Geo {
+  int dims, N, D, H, W, C;
+};
+Geo geo_of(const at::Tensor& x) {
+  TORCH_CHECK(x.dim() == 4 || x.dim() == 5, "expected [N,(D,)H,W,C] channel-last tensor");
+  Geo g;
+  g.dims = (int)x.dim() - 2;
+  g.N = (int)x.size(0);
+  g.D = g.dims == 3 ? (int)x.size(1) : 1;
+  g.H = (int)x.size(g.dims == 3 ? 2 : 1);
+  g.W = (int)x.size(g.dims == 3 ? 3 : 2);
+  g.C = (int)x.size(-1);
+  return g;
+}
+std::vector<int64_t> shape_with_c(const Geo& g, int C, int scale = 1) {
+  if (g.dims == 2) return {g.N, (int64_t)g.H * scale, (int64_t)g.W * scale, C};
+  return {g.N, (int64_t)g.D * scale, (int64_t)g.H * scale, (int64_t)g.W * scale, C};
+}
+
+int pow2ceil(int v) { int p = 1; while (p < v) p <<= 1; return p; }
+
+// pixel tile for the 3x3 conv kernels: BM pixels as TD x TH x TW
+void conv_tile(int dims, int BM, int D, int H, int W, int& TD, int& TH, int& TW) {
+  if (dims == 2) {
+    TD = 1;
+    TW = std::max(8, std::min(16, pow2ceil(W)));
+    if (BM == 256 && W >= 32 && H < 16) TW = 32;
+    TH = BM / TW;
+  } else {
+    TW = W <= 8 ? 8 : 16;
+    TH = 4;
+    TD = BM / (TW * TH);
+  }
+  (void)D; (void)H;
+}
+
+int pick_bn(int Cout) {
+  if (Cout <= 32) return 32;
+  if (Cout <= 64) return 64;
+  // minimise padding waste, prefer larger tiles
+  const int w128 = ((Cout + 127) / 128) * 128 - Cout;
+  const int w64 = ((Cout + 63) / 64) * 64 - Cout;
+  return w128 <= w64 ? 128 : 64;
+}
+
+int num_cus() {
+  static int n = -1;
+  if (n < 0) {
+    hipDeviceProp_t prop;
+    int dev = 0;
+    hipGetDevice(&dev);
+    n = (hipGetDeviceProperties(&prop, dev) == hipSuccess) ? prop.multiProcessorCount : 256;
+  }
+  return n;
+}
+
+// ------------------------------------------------------------------------ conv3 forward
+std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::Tensor>& x2,
+                                  const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                                  const c10::optional<at::Tensor>& pscale,
+                                  const c10::optional<at::Tensor>& pshift, int64_t cout,
+                                  int64_t co1, bool want_stats) {
+  CHECK_DEV(x1); CHECK_CONTIG(x1); CHECK_BF16(x1); CHECK_BF16(w); CHECK_CONTIG(w);
+  c10::DeviceGuard guard(x1.device());
+  const Geo g = geo_of(x1);
+  ConvFwdArgs a{};
+  a.dims = g.dims; a.N = g.N; a.D = g.D; a.H = g.H; a.W = g.W;
+  a.C1 = g.C;
+  a.C2 = 0;
+  const bool dual = x2.has_value() && x2->defined();
+  if (dual) {
+    CHECK_CONTIG(*x2); CHECK_BF16(*x2);
+    const Geo g2 = geo_of(*x2);
+    TORCH_CHECK(g2.N == g.N && g2.H == g.H && g2.W == g.W && g2.D == g.D, "concat shape mismatch");
+    TORCH_CHECK(g.C % 8 == 0 && g2.C % 8 == 0, "concat inputs need C % 8 == 0");
+    a.C2 = g2.C;
+  }
+  a.Cin = a.C1 + a.C2;
+  a.taps = g.dims == 2 ? 9 : 27;
+  TORCH_CHECK(w.dim() == 3 && w.size(0) == cout && w.size(1) == a.taps && w.size(2) >= a.Cin,
+              "packed weight must be [Cout][taps][CinW>=Cin]");
+  a.CinW = (int)w.size(2);
+  TORCH_CHECK(a.CinW % 8 == 0, "packed weight ci stride must be a multiple of 8");
+  a.Cout = (int)cout;
+  a.Co1 = co1 > 0 ? (int)co1 : (int)cout;
+  TORCH_CHECK(a.Cout % 8 == 0 && a.Co1 % 8 == 0, "Cout and Co1 must be multiples of 8");
+  if (pscale.has_value() && pscale->defined()) TORCH_CHECK(a.C1 <= 512, "prologue supports C1 <= 512");
+  a.X1 = bptr(x1);
+  a.X2 = dual ? bptr(*x2) : nullptr;
+  a.pscale = fptr_opt(pscale);
+  a.pshift = fptr_opt(pshift);
+  a.Wt = bptr(w);
+  a.bias = fptr_opt(bias);
+  const int bn = pick_bn(a.Cout);
+  const int BM = conv3_fwd_bm(bn);
+  conv_tile(g.dims, BM, g.D, g.H, g.W, a.TD, a.TH, a.TW);
+  TORCH_CHECK(a.TD * a.TH * a.TW == BM, "internal tile error");
+  TORCH_CHECK((a.TD + (g.dims == 3 ? 2 : 0)) * (a.TH + 2) * (a.TW + 2) <= conv3_halo_cap(g.dims),
+              "halo exceeds LDS capacity");
+  a.tilesD = (g.D + a.TD - 1) / a.TD;
+  a.tilesH = (g.H + a.TH - 1) / a.TH;
+  a.tilesW = (g.W + a.TW - 1) / a.TW;
+  a.nTilesM = g.N * a.tilesD * a.tilesH * a.tilesW;
+  a.nTilesN = (a.Cout + bn - 1) / bn;
+  auto opts = x1.options();
+  at::Tensor y1 = at::empty(shape_with_c(g, a.Co1), opts);
+  at::Tensor y2;
+  if (a.Co1 < a.Cout) y2 = at::empty(shape_with_c(g, a.Cout - a.Co1), opts);
+  at::Tensor stats;
+  if (want_stats) stats = at::empty({a.nTilesM, 2, a.Cout}, opts.dtype(at::kFloat));
+  a.Y1 = bptr_mut(y1);
+  a.Y2 = y2.defined() ? bptr_mut(y2) : nullptr;
+  a.stats = want_stats ? stats.data_ptr<float>() : nullptr;
+  conv3_fwd_launch(a, bn, cur_stream());
+  at::Tensor none = at::empty({0}, opts);
+  return {y1, y2.defined() ? y2 : none, stats.defined() ? stats : none};
+}
+
+// ------------------------------------------------------------------------ conv3 wgrad
+at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
+                       const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& pscale,
+                       const c10::optional<at::Tensor>& pshift) {
+  CHECK_DEV(dy); CHECK_CONTIG(dy); CHECK_BF16(dy); CHECK_CONTIG(x1); CHECK_BF16(x1);
+  c10::DeviceGuard guard(dy.device());
+  const Geo g = geo_of(x1);
+  const Geo gy = geo_of(dy);
+  TORCH_CHECK(gy.N == g.N && gy.H == g.H && gy.W == g.W && gy.D == g.D, "dy/x shape mismatch");
+  ConvWgradArgs a{};
+  a.dims = g.dims; a.N = g.N; a.D = g.D; a.H = g.H; a.W = g.W;
+  a.C1 = g.C; a.C2 = 0;
+  const bool dual = x2.has_value() && x2->defined();
+  if (dual) { CHECK_CONTIG(*x2); a.C2 = (int)x2->size(-1); }
+  a.Cin = a.C1 + a.C2;
+  a.Cout = gy.C;
+  TORCH_CHECK(a.Cout % 8 == 0, "Cout must be a multiple of 8");
+  a.taps = g.dims == 2 ? 9 : 27;
+  a.dY = bptr(dy);
+  a.X1 = bptr(x1);
+  a.X2 = dual ? bptr(*x2) : nullptr;
+  a.pscale = fptr_opt(pscale);
+  a.pshift = fptr_opt(pshift);
+  if (a.pscale) TORCH_CHECK(a.C1 <= 512, "prologue supports C1 <= 512");
+  const int bco = a.Cout <= 32 ? 32 : 64;
+  // 128-pixel tiles
+  if (g.dims == 2) { a.TD = 1; a.TW = g.W >= 16 ? 16 : 8; a.TH = 128 / a.TW; }
+  else { a.TW = g.W >= 16 ? 16 : 8; a.TH = 4; a.TD = 128 / (a.TW * a.TH); }
+  TORCH_CHECK((a.TD + (g.dims == 3 ? 2 : 0)) * (a.TH + 2) * (a.TW + 2) <= conv3_wgrad_halo_cap(g.dims),
+              "wgrad halo exceeds LDS capacity");
+  a.tilesD = (g.D + a.TD - 1) / a.TD;
+  a.tilesH = (g.H + a.TH - 1) / a.TH;
+  a.tilesW = (g.W + a.TW - 1) / a.TW;
+  a.nTiles = g.N * a.tilesD * a.tilesH * a.tilesW;
+  a.coTiles = (a.Cout + bco - 1) / bco;
+  a.ciChunks = (a.Cin + 31) / 32;
+  a.planes = g.dims == 2 ? 1 : 3;
+  const int base = a.coTiles * a.ciChunks * a.planes;
+  const int target = 4 * num_cus();
+  int splits = std::max(1, (target + base - 1) / base);
+  splits = std::min(splits, std::max(1, a.nTiles / 2));
+  a.splits = splits;
+  auto part = at::empty({(int64_t)splits * a.Cout * a.taps * a.Cin}, dy.options().dtype(at::kFloat));
+  a.partial = part.data_ptr<float>();
+  conv3_wgrad_launch(a, bco, cur_stream());
+  std::vector<int64_t> wshape = {a.Cout, a.Cin, 3, 3};
+  if (g.dims == 3) wshape.push_back(3);
+  at::Tensor dW = at::empty(wshape, dy.options().dtype(at::kFloat));
+  conv3_wgrad_reduce_launch(a.partial, dW.data_ptr<float>(), a.Cout, a.taps, a.Cin, splits, false,
+                            cur_stream());
+  return dW;
+}
+
+// ------------------------------------------------------------------------ BatchNorm
+// returns stats4 [4][C] = (mean, invstd, scale, shift)
+at::Tensor bn_finalize(const at::Tensor& partial, double count, const at::Tensor& gamma,
+                       const at::Tensor& beta, at::Tensor running_mean, at::Tensor running_var,
+                       double momentum, double eps, bool update_running,
+                       const c10::optional<at::Tensor>& nbt) {
+  CHECK_F32(partial); CHECK_F32(gamma); CHECK_F32(beta);
+  c10::DeviceGuard guard(partial.device());
+  const int C = (int)gamma.numel();
+  const int P = (int)(partial.numel() / (2 * C));
+  at::Tensor st = at::empty({4, C}, partial.options());
+  float* s = st.data_ptr<float>();
+  bn_finalize_launch(partial.data_ptr<float>(), P, C, count, gamma.data_ptr<float>(),
+                     beta.data_ptr<float>(), running_mean.data_ptr<float>(),
+                     running_var.data_ptr<float>(), (float)momentum, (float)eps, s, s + C,
+                     s + 2 * C, s + 3 * C, update_running,
+                     (nbt.has_value() && nbt->defined()) ? nbt->data_ptr<int64_t>() : nullptr,
+                     cur_stream());
+  return st;
+}
+
+std::vector<at::Tensor> bn_relu_apply(const at::Tensor& y, const at::Tensor& stats4, bool pool) {
+  CHECK_DEV(y); CHECK_CONTIG(y); CHECK_BF16(y);
+  c10::DeviceGuard guard(y.device());
+  const Geo g = geo_of(y);
+  TORCH_CHECK(g.C % 8 == 0, "C must be a multiple of 8");
+  const float* s = stats4.data_ptr<float>();
+  at::Tensor a = at::empty_like(y);
+  at::Tensor p;
+  if (pool) {
+    TORCH_CHECK(g.H % 2 == 0 && g.W % 2 == 0 && (g.dims == 2 || g.D % 2 == 0), "pool needs even dims");
+    std::vector<int64_t> ps = g.dims == 2 ? std::vector<int64_t>{g.N, g.H / 2, g.W / 2, g.C}
+                                          : std::vector<int64_t>{g.N, g.D / 2, g.H / 2, g.W / 2, g.C};
+    p = at::empty(ps, y.options());
+  }
+  bn_relu_apply_launch(bptr(y), s + 2 * g.C, s + 3 * g.C, bptr_mut(a),
+                       pool ? bptr_mut(p) : nullptr, g.dims, g.N, g.D, g.H, g.W, g.C, cur_stream());
+  return {a, p.defined() ? p : at::empty({0}, y.options())};
+}
+
+// dY, dgamma, dbeta from dA (+ unpool(dP)) through ReLU and BN
+std::vector<at::Tensor> bn_backward(const c10::optional<at::Tensor>& dA,
+                                    const c10::optional<at::Tensor>& dP, const at::Tensor& y,
+                                    const at::Tensor& stats4, const at::Tensor& gamma,
+                                    const c10::optional<at::Tensor>& gscale) {
+  CHECK_DEV(y); CHECK_CONTIG(y); CHECK_BF16(y);
+  c10::DeviceGuard guard(y.device());
+  const Geo g = geo_of(y);
+  const int C = g.C;
+  TORCH_CHECK(C % 8 == 0, "C must be a multiple of 8");
+  const bool hasA = dA.has_value() && dA->defined();
+  const bool hasP = dP.has_value() && dP->defined();
+  TORCH_CHECK(hasA || hasP, "bn_backward needs dA or dP");
+  if (hasA) { CHECK_CONTIG(*dA); CHECK_BF16(*dA); }
+  if (hasP) { CHECK_CONTIG(*dP); CHECK_BF16(*dP); }
+  if (!hasP) TORCH_CHECK(hasA, "dA required without pool");
+  const float* s = stats4.data_ptr<float>();
+  const float* gs = fptr_opt(gscale);
+  const long long items = (long long)g.N * (hasP ? (g.dims == 3 ? g.D / 2 : 1) * (g.H / 2) * (g.W / 2)
+                                                 : (long long)g.D * g.H * g.W);
+  const int nb = bn_bwd_reduce_blocks(items);
+  auto fopts = y.options().dtype(at::kFloat);
+  at::Tensor partial = at::empty({nb, 2, C}, fopts);
+  const bf16_t* pA = hasA ? bptr(*dA) : nullptr;
+  const bf16_t* pP = hasP ? bptr(*dP) : nullptr;
+  bn_bwd_reduce_launch(pA, pP, bptr(y), s + 2 * C, s + 3 * C, s, s + C, gs,
+                       partial.data_ptr<float>(), nb, g.dims, g.N, g.D, g.H, g.W, C, cur_stream());
+  at::Tensor dgamma = at::empty({C}, fopts), dbeta = at::empty({C}, fopts);
+  at::Tensor coefs = at::empty({3, C}, fopts);
+  const double count = (double)g.N * g.D * g.H * g.W;
+  bn_bwd_finalize_launch(partial.data_ptr<float>(), nb, C, count, gamma.data_ptr<float>(), s + C,
+                         dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), coefs.data_ptr<float>(),
+                         cur_stream());
+  at::Tensor dY = at::empty_like(y);
+  bn_bwd_apply_launch(pA, pP, bptr(y), s + 2 * C, s + 3 * C, s, s + C, coefs.data_ptr<float>(), gs,
+                      bptr_mut(dY), g.dims, g.N, g.D, g.H, g.W, C, cur_stream());
+  return {dY, dgamma, dbeta};
+}
+
+// ------------------------------------------------------------------------ transposed conv
+at::Tensor convt_fwd(const at::Tensor& x, const at::Tensor& wt, const c10::optional<at::Tensor>& bias,
+                     int64_t cout) {
+  CHECK_DEV(x); CHECK_CONTIG(x); CHECK_BF16(x); CHECK_BF16(wt);
+  c10::DeviceGuard guard(x.device());
+  const Geo g = geo_of(x);
+  const int S = g.dims == 2 ? 4 : 8;
+  TORCH_CHECK(g.C % 8 == 0 && cout % 8 == 0, "channels must be multiples of 8");
+  TORCH_CHECK(wt.numel() == (int64_t)S * cout * g.C, "packed convT weight size mismatch");
+  GemmArgs a{};
+  a.mode = GEMM_CONVT_FWD;
+  a.M = g.N * g.D * g.H * g.W;
+  a.N = S * (int)cout;
+  a.K = g.C;
+  a.A = bptr(x);
+  a.B = bptr(wt);
+  a.bias = fptr_opt(bias);
+  a.dims = g.dims; a.Nimg = g.N; a.D = g.D; a.H = g.H; a.W = g.W;
+  a.Cin = g.C; a.Cout = (int)cout;
+  at::Tensor out = at::empty(shape_with_c(g, (int)cout, 2), x.options());
+  a.C = out.data_ptr();
+  gemm_launch(a, cur_stream());
+  return out;
+}
+
+at::Tensor convt_dgrad(const at::Tensor& dout, const at::Tensor& wd, int64_t cin) {
+  CHECK_DEV(dout); CHECK_CONTIG(dout); CHECK_BF16(dout); CHECK_BF16(wd);
+  c10::DeviceGuard guard(dout.device());
+  const Geo go = geo_of(dout);
+  Geo g = go;
+  g.H /= 2; g.W /= 2; if (g.dims == 3) g.D /= 2;
+  const int S = g.dims == 2 ? 4 : 8;
+  GemmArgs a{};
+  a.mode = GEMM_CONVT_DGRAD;
+  a.M = g.N * g.D * g.H * g.W;
+  a.N = (int)cin;
+  a.K = S * go.C;
+  a.A = bptr(dout);
+  a.B = bptr(wd);
+  a.dims = g.dims; a.Nimg = g.N; a.D = g.D; a.H = g.H; a.W = g.W;
+  a.Cin = (int)cin; a.Cout = go.C;
+  TORCH_CHECK(go.C % 32 == 0, "convT dgrad needs Cout % 32 == 0");
+  at::Tensor dx = at::empty(shape_with_c(g, (int)cin), dout.options());
+  a.C = dx.data_ptr();
+  gemm_launch(a, cur_stream());
+  return dx;
+}
+
+std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout) {
+  CHECK_DEV(x); CHECK_CONTIG(x); CHECK_CONTIG(dout);
+  c10::DeviceGuard guard(x.device());
+  const Geo g = geo_of(x);
+  const Geo go = geo_of(dout);
+  const int S = g.dims == 2 ? 4 : 8;
+  GemmArgs a{};
+  a.mode = GEMM_CONVT_WGRAD;
+  a.M = g.C;
+  a.N = S * go.C;
+  a.K = g.N * g.D * g.H * g.W;
+  a.A = bptr(x);
+  a.B = bptr(dout);
+  a.dims = g.dims; a.Nimg = g.N; a.D = g.D; a.H = g.H; a.W = g.W;
+  a.Cin = g.C; a.Cout = go.C;
+  const int base = ((a.M + 63) / 64) * ((a.N + 63) / 64);
+  int splits = std::max(1, (4 * num_cus() + base - 1) / base);
+  splits = std::min(splits, std::max(1, a.K / 256));
+  a.splits = splits;
+  auto fopts = x.options().dtype(at::kFloat);
+  at::Tensor part = at::empty({(int64_t)splits * a.M * a.N}, fopts);
+  a.partial = part.data_ptr<float>();
+  gemm_launch(a, cur_stream());
+  std::vector<int64_t> ws = {g.C, go.C, 2, 2};
+  if (g.dims == 3) ws.push_back(2);
+  at::Tensor dW = at::empty(ws, fopts);
+  gemm_wgrad_reduce_launch(a.partial, dW.data_ptr<float>(), nullptr, g.C, go.C, S, splits,
+                           cur_stream());
+  // bias gradient: per-channel sum of dOut
+  const long long P = (long long)go.N * go.D * go.H * go.W;
+  const int nb = (int)std::max<long long>(1, std::min<long long>((P + 1023) / 1024, 1024));
+  at::Tensor cpart = at::empty({nb, go.C}, fopts);
+  channel_sum_launch(bptr(dout), P, go.C, cpart.data_ptr<float>(), nb, cur_stream());
+  at::Tensor db = at::empty({go.C}, fopts);
+  partial_sum_launch(cpart.data_ptr<float>(), nb, go.C, db.data_ptr<float>(), 1.f, false, cur_stream());
+  return {dW, db};
+}
+
+// ------------------------------------------------------------------------ head + CE
+at::Tensor head_ce_fwd(const at::Tensor& a, const at::Tensor& Wh, const at::Tensor& bh,
+                       const at::Tensor& labels, int64_t ignore_index) {
+  CHECK_DEV(a); CHECK_CONTIG(a); CHECK_BF16(a); CHECK_F32(Wh); CHECK_CONTIG(Wh);
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous(), "labels must be int64");
+  c10::DeviceGuard guard(a.device());
+  const int C = (int)a.size(-1), K = (int)Wh.size(0);
+  TORCH_CHECK(head_supported(C, K), "head kernel: unsupported (C, K)");
+  const long long P = a.numel() / C;
+  TORCH_CHECK(labels.numel() == P, "labels size mismatch");
+  const int nb = (int)std::max<long long>(1, std::min<long long>((P + 255) / 256, 2048));
+  auto fopts = a.options().dtype(at::kFloat);
+  at::Tensor partial = at::empty({nb, 3}, fopts);
+  at::Tensor out3 = at::empty({3}, fopts);
+  head_ce_fwd_launch(bptr(a), Wh.data_ptr<float>(), bh.data_ptr<float>(), labels.data_ptr<int64_t>(),
+                     partial.data_ptr<float>(), out3.data_ptr<float>(), nullptr, nb, P, C, K,
+                     (int)ignore_index, cur_stream());
+  return out3;
+}
+
+std::vector<at::Tensor> head_ce_bwd(const at::Tensor& a, const at::Tensor& Wh, const at::Tensor& bh,
+                                    const at::Tensor& labels, const at::Tensor& out3,
+                                    const c10::optional<at::Tensor>& gscale, int64_t ignore_index) {
+  CHECK_DEV(a); CHECK_CONTIG(a);
+  c10::DeviceGuard guard(a.device());
+  const int C = (int)a.size(-1), K = (int)Wh.size(0);
+  const long long P = a.numel() / C;
+  const int nb = (int)std::max<long long>(1, std::min<long long>((P + 255) / 256, 1024));
+  auto fopts = a.options().dtype(at::kFloat);
+  at::Tensor dA = at::empty_like(a);
+  at::Tensor part = at::empty({nb, K * C + K}, fopts);
+  head_ce_bwd_launch(bptr(a), Wh.data_ptr<float>(), bh.data_ptr<float>(), labels.data_ptr<int64_t>(),
+                     fptr_opt(gscale), out3.data_ptr<float>(), 0, bptr_mut(dA),
+                     part.data_ptr<float>(), nb, P, C, K, (int)ignore_index, cur_stream());
+  at::Tensor red = at::empty({K * C + K}, fopts);
+  partial_sum_launch(part.data_ptr<float>(), nb, K * C + K, red.data_ptr<float>(), 1.f, false,
+                     cur_stream());
+  at::Tensor dW = red.narrow(0, 0, K * C).view({K, C});
+  at::Tensor db = red.narrow(0, K * C, K);
+  return {dA, dW, db};
+}
+
+at::Tensor head_logits(const at::Tensor& a, const at::Tensor& Wh, const at::Tensor& bh) {
+  CHECK_DEV(a); CHECK_CONTIG(a);
+  c10::DeviceGuard guard(a.device());
+  const Geo g = geo_of(a);
+  const int C = g.C, K = (int)Wh.size(0);
+  TORCH_CHECK(head_supported(C, K), "head kernel: unsupported (C, K)");
+  const long long HW = (long long)g.D * g.H * g.W;
+  std::vector<int64_t> os = g.dims == 2 ? std::vector<int64_t>{g.N, K, g.H, g.W}
+                                        : std::vector<int64_t>{g.N, K, g.D, g.H, g.W};
+  at::Tensor out = at::empty(os, a.options().dtype(at::kFloat));
+  head_logits_launch(bptr(a), Wh.data_ptr<float>(), bh.data_ptr<float>(), out.data_ptr<float>(),
+                     (long long)g.N * HW, HW, C, K, cur_stream());
+  return out;
+}
+
+// ------------------------------------------------------------------------ optimizer / pack
+void adam_step(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, double b1, double b2,
+               double eps, double wd, double step_size, double inv_sqrt_bc2) {
+  CHECK_DEV(p); CHECK_F32(p); CHECK_F32(g); CHECK_F32(m); CHECK_F32(v);
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "size");
+  c10::DeviceGuard guard(p.device());
+  adam_launch(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+              p.numel(), (float)b1, (float)b2, (float)eps, (float)wd, (float)step_size,
+              (float)inv_sqrt_bc2, cur_stream());
+}
+
+void weight_pack(const at::Tensor& entries, int64_t n, int64_t max_elems) {
+  CHECK_DEV(entries);
+  TORCH_CHECK(entries.scalar_type() == at::kLong && entries.numel() == n * 6,
+              "entries must be int64 [n, 6] (48-byte PackEntry records)");
+  static_assert(sizeof(PackEntry) == 48, "PackEntry layout");
+  c10::DeviceGuard guard(entries.device());
+  weight_pack_launch(reinterpret_cast<const PackEntry*>(entries.data_ptr()), (int)n, max_elems,
+                     cur_stream());
+}
+
+// ------------------------------------------------------------------------ codec
+at::Tensor codec_absmax(const at::Tensor& x, const at::Tensor& seg) {
+  CHECK_DEV(x); CHECK_F32(x);
+  c10::DeviceGuard guard(x.device());
+  const int nseg = (int)(seg.numel() / 2);
+  at::Tensor s = at::empty({nseg}, x.options());
+  codec_absmax_launch(x.data_ptr<float>(), seg.data_ptr<int64_t>(), nseg, s.data_ptr<float>(),
+                      cur_stream());
+  return s;
+}
+
+at::Tensor codec_encode(const at::Tensor& x, const at::Tensor& seg, const at::Tensor& scales,
+                        int64_t codec) {
+  CHECK_DEV(x); CHECK_F32(x);
+  c10::DeviceGuard guard(x.device());
+  const int nseg = (int)(seg.numel() / 2);
+  at::Tensor out = at::zeros({x.numel()}, x.options().dtype(codec == 0 ? at::kHalf : at::kChar));
+  codec_encode_launch(x.data_ptr<float>(), seg.data_ptr<int64_t>(), nseg, scales.data_ptr<float>(),
+                      out.data_ptr(), (int)codec, x.numel(), cur_stream());
+  return out;
+}
+
+void codec_decode_sum(at::Tensor out, const at::Tensor& q, const at::Tensor& scales,
+                      const at::Tensor& w, const at::Tensor& seg, int64_t codec) {
+  CHECK_DEV(out); CHECK_F32(out); CHECK_CONTIG(q);
+  c10::DeviceGuard guard(out.device());
+  const int nseg = (int)(seg.numel() / 2);
+  const int world = (int)q.size(0);
+  codec_decode_sum_launch(out.data_ptr<float>(), q.data_ptr(), scales.data_ptr<float>(),
+                          w.data_ptr<float>(), seg.data_ptr<int64_t>(), nseg, world, (int)codec,
+                          out.numel(), cur_stream());
+}
+
+// ------------------------------------------------------------------------ misc
+at::Tensor bilinear_up2(const at::Tensor& x) {
+  CHECK_DEV(x); CHECK_CONTIG(x); CHECK_BF16(x);
+  c10::DeviceGuard guard(x.device());
+  const Geo g = geo_of(x);
+  at::Tensor y = at::empty(shape_with_c(g, g.C, 2), x.options());
+  bilinear_up2_launch(bptr(x), bptr_mut(y), g.dims, g.N, g.D, g.H, g.W, g.C, false, cur_stream());
+  return y;
+}
+
+at::Tensor bilinear_up2_bwd(const at::Tensor& dy) {
+  CHECK_DEV(dy); CHECK_CONTIG(dy); CHECK_BF16(dy);
+  c10::DeviceGuard guard(dy.device());
+  Geo g = geo_of(dy);
+  g.H /= 2; g.W /= 2; if (g.dims == 3) g.D /= 2;
+  at::Tensor dx = at::empty(shape_with_c(g, g.C), dy.options());
+  at::Tensor tmp = at::empty({dx.numel()}, dy.options().dtype(at::kFloat));
+  bilinear_up2_bwd_launch(bptr(dy), tmp.data_ptr<float>(), bptr_mut(dx), g.dims, g.N, g.D, g.H,
+                          g.W, g.C, cur_stream());
+  return dx;
+}
+
+// NCHW / NCDHW (fp32 or bf16) -> channel-last bf16 [N, (D,) H, W, C]
+at::Tensor to_nhwc_bf16(const at::Tensor& x) {
+  CHECK_DEV(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "fp32/bf16 input");
+  c10::DeviceGuard guard(x.device());
+  const int N = (int)x.size(0), C = (int)x.size(1);
+  const long long S = x.numel() / ((long long)N * C);
+  std::vector<int64_t> shape = {N};
+  for (int i = 2; i < x.dim(); ++i) shape.push_back(x.size(i));
+  shape.push_back(C);
+  at::Tensor y = at::empty(shape, x.options().dtype(at::kBFloat16));
+  nchw_to_nhwc_bf16_launch(x.data_ptr(), x.scalar_type() == at::kFloat ? 0 : 1, bptr_mut(y), N, C,
+                           S, cur_stream());
+  return y;
+}
+
+}  // namespace
+
+}  // namespace ddlpc
+
+TORCH_LIBRARY(ddlpc, m) {
+  m.def("conv3_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, Tensor? pscale, Tensor? pshift, "
+        "int cout, int co1, bool stats) -> Tensor[]");
+  m.def("conv3_wgrad(Tensor dy, Tensor x1, Tensor? x2, Tensor? pscale, Tensor? pshift) -> Tensor");
+  m.def("bn_finalize(Tensor partial, float count, Tensor gamma, Tensor beta, Tensor(a!) running_mean, "
+        "Tensor(b!) running_var, float momentum, float eps, bool update_running, Tensor(c!)? nbt) -> Tensor");
+  m.def("bn_relu_apply(Tensor y, Tensor stats4, bool pool) -> Tensor[]");
+  m.def("bn_backward(Tensor? dA, Tensor? dP, Tensor y, Tensor stats4, Tensor gamma, Tensor? gscale) "
+        "-> Tensor[]");
+  m.def("convt_fwd(Tensor x, Tensor wt, Tensor? bias, int cout) -> Tensor");
+  m.def("convt_dgrad(Tensor dout, Tensor wd, int cin) -> Tensor");
+  m.def("convt_wgrad(Tensor x, Tensor dout) -> Tensor[]");
+  m.def("head_ce_fwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, int ignore_index) -> Tensor");
+  m.def("head_ce_bwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, Tensor out3, Tensor? gscale, "
+        "int ignore_index) -> Tensor[]");
+  m.def("head_logits(Tensor a, Tensor Wh, Tensor bh) -> Tensor");
+  m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float eps, "
+        "float wd, float step_size, float inv_sqrt_bc2) -> ()");
+  m.def("weight_pack(Tensor entries, int n, int max_elems) -> ()");
+  m.def("codec_absmax(Tensor x, Tensor seg) -> Tensor");
+  m.def("codec_encode(Tensor x, Tensor seg, Tensor scales, int codec) -> Tensor");
+  m.def("codec_decode_sum(Tensor(a!) out, Tensor q, Tensor scales, Tensor w, Tensor seg, int codec) -> ()");
+  m.def("bilinear_up2(Tensor x) -> Tensor");
+  m.def("bilinear_up2_bwd(Tensor dy) -> Tensor");
+  m.def("to_nhwc_bf16(Tensor x) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
+  m.impl("conv3_fwd", &ddlpc::conv3_fwd);
+  m.impl("conv3_wgrad", &ddlpc::conv3_wgrad);
+  m.impl("bn_finalize", &ddlpc::bn_finalize);
+  m.impl("bn_relu_apply", &ddlpc::bn_relu_apply);
+  m.impl("bn_backward", &ddlpc::bn_backward);
+  m.impl("convt_fwd", &ddlpc::convt_fwd);
+  m.impl("convt_dgrad", &ddlpc::convt_dgrad);
+  m.impl("convt_wgrad", &ddlpc::convt_wgrad);
+  m.impl("head_ce_fwd", &ddlpc::head_ce_fwd);
+  m.impl("head_ce_bwd", &ddlpc::head_ce_bwd);
+  m.impl("head_logits", &ddlpc::head_logits);
+  m.impl("adam_step", &ddlpc::adam_step);
+  m.impl("weight_pack", &ddlpc::weight_pack);
+  m.impl("codec_absmax", &ddlpc::codec_absmax);
+  m.impl("codec_encode", &ddlpc::codec_encode);
+  m.impl("codec_decode_sum", &ddlpc::codec_decode_sum);
+  m.impl("bilinear_up2", &ddlpc::bilinear_up2);
+  m.impl("bilinear_up2_bwd", &ddlpc::bilinear_up2_bwd);
+  m.impl("to_nhwc_bf16", &ddlpc::to_nhwc_bf16);
+}

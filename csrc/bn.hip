@@ -1,0 +1,363 @@
+// Training-mode BatchNorm + ReLU (+ 2x max-pool) — K4-K7 of SURVEY.md §2.5.
+// Reference: nn.BatchNorm2d -> nn.ReLU(inplace=True) inside DoubleConv (ref.py:580-584) and
+// nn.MaxPool2d(2) in DownBlock (ref.py:595,599).
+//
+// Forward data flow (per conv):  conv epilogue writes y (bf16, pre-BN) + per-tile channel
+// (sum, sum^2)  ->  bn_finalize (fp64 reduction: mean, invstd, scale = gamma*invstd,
+// shift = beta - mean*scale, running stats with momentum 0.1 and the unbiased variance)
+// ->  consumers apply relu(y*scale + shift) on the fly (next conv prologue) or
+// bn_relu_apply materialises it once, writing the 2x2(x2) max-pooled tensor in the same
+// pass for encoder blocks.
+//
+// Backward:  bn_bwd_reduce recomputes a = relu(y*scale+shift) and the pool arg-max from y,
+// forms dyhat = (dA + unpool(dP)) * [a > 0] (times the loss-gradient scale), and reduces
+// per-channel sum(dyhat), sum(dyhat*xhat); bn_bwd_finalize turns them into dgamma, dbeta
+// and the three coefficients of dY = gamma*invstd*(dyhat - mean(dyhat) - xhat*mean(dyhat*xhat));
+// bn_bwd_apply writes dY (bf16) for the conv's data/weight gradients.  The pool backward
+// and the skip-gradient sum are folded into both passes (no unpooled tensor is stored).
+#include "common.h"
+#include "ops.h"
+
+namespace ddlpc {
+
+namespace {
+
+// --------------------------------------------------------------------- finalize
+__global__ void bn_finalize_kernel(const float* __restrict__ partial, int P, int C, double count,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* running_mean, float* running_var, float momentum,
+                                   float eps, float* mean_o, float* invstd_o, float* scale_o,
+                                   float* shift_o, int update_running, int64_t* nbt) {
+  const int c = blockIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    s1 += partial[(long long)p * 2 * C + c];
+    s2 += partial[(long long)p * 2 * C + C + c];
+  }
+  __shared__ double r1[4], r2[4];
+  s1 = wave_sum_d(s1);
+  s2 = wave_sum_d(s2);
+  if ((threadIdx.x & 63) == 0) { r1[threadIdx.x >> 6] = s1; r2[threadIdx.x >> 6] = s2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t1 = 0, t2 = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { t1 += r1[w]; t2 += r2[w]; }
+    const double mean = t1 / count;
+    double var = t2 / count - mean * mean;
+    if (var < 0) var = 0;
+    const float inv = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = gamma[c] * inv;
+    mean_o[c] = (float)mean;
+    invstd_o[c] = inv;
+    scale_o[c] = sc;
+    shift_o[c] = beta[c] - (float)mean * sc;
+    if (update_running && c == 0 && nbt != nullptr) nbt[0] += 1;
+    if (update_running) {
+      const double unb = count > 1 ? var * count / (count - 1) : var;
+      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+    }
+  }
+}
+
+// --------------------------------------------------------------------- apply (+ pool)
+template <int DIMS, bool POOL>
+__global__ void bn_relu_apply_kernel(const bf16_t* __restrict__ y, const float* __restrict__ scale,
+                                     const float* __restrict__ shift, bf16_t* __restrict__ out,
+                                     bf16_t* __restrict__ pooled, int N, int D, int H, int W,
+                                     int C) {
+  const int G = C / 8;
+  if (!POOL) {
+    const long long total = (long long)N * D * H * W * G;
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+         e += (long long)gridDim.x * blockDim.x) {
+      const int c8 = (int)(e % G) * 8;
+      float f[8];
+      unpack8(reinterpret_cast<const uint4*>(y)[e], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], scale[c8 + j], shift[c8 + j]), 0.f);
+      reinterpret_cast<uint4*>(out)[e] = pack8(f);
+    }
+    return;
+  }
+  const int Do = DIMS == 3 ? D / 2 : 1, Ho = H / 2, Wo = W / 2;
+  const long long total = (long long)N * Do * Ho * Wo * G;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(e % G);
+    long long q = e / G;
+    const int wo = (int)(q % Wo); q /= Wo;
+    const int ho = (int)(q % Ho); q /= Ho;
+    const int dd = DIMS == 3 ? (int)(q % Do) : 0;
+    const int n = (int)(DIMS == 3 ? q / Do : q);
+    const int c8 = cg * 8;
+    float sc[8], sh[8], mx[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sc[j] = scale[c8 + j]; sh[j] = shift[c8 + j]; mx[j] = -INFINITY; }
+#pragma unroll
+    for (int kd = 0; kd < (DIMS == 3 ? 2 : 1); ++kd)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 2; ++kw) {
+          const int d = DIMS == 3 ? 2 * dd + kd : 0;
+          const long long pix = ((long long)(n * D + d) * H + 2 * ho + kh) * W + 2 * wo + kw;
+          float f[8];
+          unpack8(*reinterpret_cast<const uint4*>(y + pix * C + c8), f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
+          }
+          const uint4 v = pack8(f);
+          *reinterpret_cast<uint4*>(out + pix * C + c8) = v;
+          float r[8];
+          unpack8(v, r);                       // pool the bf16-rounded activations
+#pragma unroll
+          for (int j = 0; j < 8; ++j) mx[j] = fmaxf(mx[j], r[j]);
+        }
+    const long long opix = ((long long)(n * Do + dd) * Ho + ho) * Wo + wo;
+    *reinterpret_cast<uint4*>(pooled + opix * C + c8) = pack8(mx);
+  }
+}
+
+// --------------------------------------------------------------------- backward passes
+// Per work item: 8 channels of one pixel (no pool) or of one pooling window (pool).
+// MODE 0: reduce (write per-block partial sums), MODE 1: apply (write dY).
+template <int DIMS, bool POOL, int MODE>
+__global__ void bn_bwd_kernel(const bf16_t* __restrict__ dA, const bf16_t* __restrict__ dP,
+                              const bf16_t* __restrict__ y, const float* __restrict__ scale,
+                              const float* __restrict__ shift, const float* __restrict__ mean,
+                              const float* __restrict__ invstd, const float* __restrict__ coefs,
+                              const float* __restrict__ gscale, float* __restrict__ partial,
+                              bf16_t* __restrict__ dY, int N, int D, int H, int W, int C) {
+  const int G = C / 8;
+  const int per_block = (blockDim.x / G) * G;           // threads with a fixed channel group
+  const int tid = threadIdx.x;
+  const bool active = tid < per_block;
+  const int cg = tid % G;
+  const int c8 = cg * 8;
+  const float gs = gscale != nullptr ? gscale[0] : 1.0f;
+  float sc[8], sh[8], mu[8], is[8], k1[8], m1[8], m2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = scale[c8 + j]; sh[j] = shift[c8 + j]; mu[j] = mean[c8 + j]; is[j] = invstd[c8 + j];
+    if (MODE == 1) { k1[j] = coefs[c8 + j]; m1[j] = coefs[C + c8 + j]; m2[j] = coefs[2 * C + c8 + j]; }
+  }
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+
+  const int Do = POOL ? (DIMS == 3 ? D / 2 : 1) : D;
+  const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
+  const long long items = (long long)N * Do * Ho * Wo;
+  const long long stride = (long long)gridDim.x * (per_block / G);
+  if (active) {
+    for (long long it = blockIdx.x * (long long)(per_block / G) + tid / G; it < items; it += stride) {
+      if (!POOL) {
+        const long long off = it * C + c8;
+        float fy[8], fd[8];
+        unpack8(*reinterpret_cast<const uint4*>(y + off), fy);
+        unpack8(*reinterpret_cast<const uint4*>(dA + off), fd);
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float a = fmaf(fy[j], sc[j], sh[j]);
+          const float dyh = a > 0.f ? fd[j] * gs : 0.f;
+          const float xh = (fy[j] - mu[j]) * is[j];
+          if (MODE == 0) { s1[j] += dyh; s2[j] += dyh * xh; }
+          else o[j] = k1[j] * (dyh - m1[j] - xh * m2[j]);
+        }
+        if (MODE == 1) *reinterpret_cast<uint4*>(dY + off) = pack8(o);
+      } else {
+        long long q = it;
+        const int wo = (int)(q % Wo); q /= Wo;
+        const int ho = (int)(q % Ho); q /= Ho;
+        const int dd = DIMS == 3 ? (int)(q % Do) : 0;
+        const int n = (int)(DIMS == 3 ? q / Do : q);
+        constexpr int NW = DIMS == 3 ? 8 : 4;
+        float fy[NW][8];
+        long long offs[NW];
+        int best[8];
+        float bv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { best[j] = 0; bv[j] = -INFINITY; }
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          const int kd = DIMS == 3 ? (w >> 2) : 0, kh = (w >> 1) & 1, kw = w & 1;
+          const int d = DIMS == 3 ? 2 * dd + kd : 0;
+          offs[w] = (((long long)(n * D + d) * H + 2 * ho + kh) * W + 2 * wo + kw) * C + c8;
+          unpack8(*reinterpret_cast<const uint4*>(y + offs[w]), fy[w]);
+          // arg-max over the bf16-rounded activations, first maximum wins (PyTorch order)
+          float a[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) a[j] = fmaxf(fmaf(fy[w][j], sc[j], sh[j]), 0.f);
+          const uint4 av = pack8(a);
+          float ar[8];
+          unpack8(av, ar);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (ar[j] > bv[j]) { bv[j] = ar[j]; best[j] = w; }
+        }
+        const long long popix = ((long long)(n * Do + dd) * Ho + ho) * Wo + wo;
+        float fp[8];
+        unpack8(*reinterpret_cast<const uint4*>(dP + popix * C + c8), fp);
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          float fd[8], o[8];
+          if (dA != nullptr) unpack8(*reinterpret_cast<const uint4*>(dA + offs[w]), fd);
+          else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) fd[j] = 0.f;
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float a = fmaf(fy[w][j], sc[j], sh[j]);
+            const float dt = fd[j] + (best[j] == w ? fp[j] : 0.f);
+            const float dyh = a > 0.f ? dt * gs : 0.f;
+            const float xh = (fy[w][j] - mu[j]) * is[j];
+            if (MODE == 0) { s1[j] += dyh; s2[j] += dyh * xh; }
+            else o[j] = k1[j] * (dyh - m1[j] - xh * m2[j]);
+          }
+          if (MODE == 1) *reinterpret_cast<uint4*>(dY + offs[w]) = pack8(o);
+        }
+      }
+    }
+  }
+  if (MODE == 0) {
+    // block reduction: threads with equal cg hold the same channels
+    __shared__ float red[256 * 8];
+    for (int half = 0; half < 2; ++half) {
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[j * 256 + tid] = active ? (half ? s2[j] : s1[j]) : 0.f;
+      __syncthreads();
+      for (int c = tid; c < C; c += blockDim.x) {
+        const int g2 = c / 8, j = c % 8;
+        float t = 0.f;
+        for (int k = g2; k < per_block; k += G) t += red[j * 256 + k];
+        partial[(long long)blockIdx.x * 2 * C + half * C + c] = t;
+      }
+    }
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int P, int C,
+                                       double count, const float* __restrict__ gamma,
+                                       const float* __restrict__ invstd, float* dgamma,
+                                       float* dbeta, float* coefs) {
+  const int c = blockIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    s1 += partial[(long long)p * 2 * C + c];
+    s2 += partial[(long long)p * 2 * C + C + c];
+  }
+  __shared__ double r1[4], r2[4];
+  s1 = wave_sum_d(s1);
+  s2 = wave_sum_d(s2);
+  if ((threadIdx.x & 63) == 0) { r1[threadIdx.x >> 6] = s1; r2[threadIdx.x >> 6] = s2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t1 = 0, t2 = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { t1 += r1[w]; t2 += r2[w]; }
+    dbeta[c] = (float)t1;
+    dgamma[c] = (float)t2;
+    coefs[c] = gamma[c] * invstd[c];
+    coefs[C + c] = (float)(t1 / count);
+    coefs[2 * C + c] = (float)(t2 / count);
+  }
+}
+
+int grid_for(long long items, int per_block) {
+  long long g = (items + per_block - 1) / per_block;
+  return (int)std::max<long long>(1, std::min<long long>(g, 2048));
+}
+
+}  // namespace
+
+int bn_bwd_reduce_blocks(long long items) { return grid_for(items, 64); }
+
+void bn_finalize_launch(const float* partial, int P, int C, double count, const float* gamma,
+                        const float* beta, float* running_mean, float* running_var,
+                        float momentum, float eps, float* mean, float* invstd, float* scale,
+                        float* shift, bool update_running, int64_t* nbt, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, partial, P, C, count, gamma,
+                     beta, running_mean, running_var, momentum, eps, mean, invstd, scale, shift,
+                     update_running ? 1 : 0, nbt);
+}
+
+void bn_relu_apply_launch(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
+                          bf16_t* pooled, int dims, int N, int D, int H, int W, int C,
+                          hipStream_t st) {
+  const long long G = C / 8;
+  if (pooled == nullptr) {
+    const long long items = (long long)N * D * H * W * G;
+    const int grid = grid_for(items, 256) * 1;
+    if (dims == 2)
+      hipLaunchKernelGGL((bn_relu_apply_kernel<2, false>), dim3(std::min(grid, 8192)), dim3(256), 0,
+                         st, y, scale, shift, out, pooled, N, D, H, W, C);
+    else
+      hipLaunchKernelGGL((bn_relu_apply_kernel<3, false>), dim3(std::min(grid, 8192)), dim3(256), 0,
+                         st, y, scale, shift, out, pooled, N, D, H, W, C);
+    return;
+  }
+  const long long items = (long long)N * (dims == 3 ? D / 2 : 1) * (H / 2) * (W / 2) * G;
+  const int grid = std::min(grid_for(items, 256), 8192);
+  if (dims == 2)
+    hipLaunchKernelGGL((bn_relu_apply_kernel<2, true>), dim3(grid), dim3(256), 0, st, y, scale,
+                       shift, out, pooled, N, D, H, W, C);
+  else
+    hipLaunchKernelGGL((bn_relu_apply_kernel<3, true>), dim3(grid), dim3(256), 0, st, y, scale,
+                       shift, out, pooled, N, D, H, W, C);
+}
+
+#define BN_BWD_DISPATCH(MODE, grid)                                                         \
+  do {                                                                                      \
+    if (dims == 2) {                                                                        \
+      if (pool) hipLaunchKernelGGL((bn_bwd_kernel<2, true, MODE>), dim3(grid), dim3(256), 0, \
+                                   st, dA, dP, y, scale, shift, mean, invstd, coefs, gscale,  \
+                                   partial, dY, N, D, H, W, C);                              \
+      else hipLaunchKernelGGL((bn_bwd_kernel<2, false, MODE>), dim3(grid), dim3(256), 0, st,  \
+                              dA, dP, y, scale, shift, mean, invstd, coefs, gscale, partial,  \
+                              dY, N, D, H, W, C);                                           \
+    } else {                                                                                \
+      if (pool) hipLaunchKernelGGL((bn_bwd_kernel<3, true, MODE>), dim3(grid), dim3(256), 0, \
+                                   st, dA, dP, y, scale, shift, mean, invstd, coefs, gscale,  \
+                                   partial, dY, N, D, H, W, C);                              \
+      else hipLaunchKernelGGL((bn_bwd_kernel<3, false, MODE>), dim3(grid), dim3(256), 0, st,  \
+                              dA, dP, y, scale, shift, mean, invstd, coefs, gscale, partial,  \
+                              dY, N, D, H, W, C);                                           \
+    }                                                                                       \
+  } while (0)
+
+void bn_bwd_reduce_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y,
+                          const float* scale, const float* shift, const float* mean,
+                          const float* invstd, const float* gscale, float* partial, int nblocks,
+                          int dims, int N, int D, int H, int W, int C, hipStream_t st) {
+  const bool pool = dP != nullptr;
+  const float* coefs = nullptr;
+  bf16_t* dY = nullptr;
+  BN_BWD_DISPATCH(0, nblocks);
+}
+
+void bn_bwd_finalize_launch(const float* partial, int P, int C, double count,
+                            const float* gamma, const float* invstd, float* dgamma,
+                            float* dbeta, float* coefs, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partial, P, C, count,
+                     gamma, invstd, dgamma, dbeta, coefs);
+}
+
+void bn_bwd_apply_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y, const float* scale,
+                         const float* shift, const float* mean, const float* invstd,
+                         const float* coefs, const float* gscale, bf16_t* dY, int dims, int N,
+                         int D, int H, int W, int C, hipStream_t st) {
+  const bool pool = dP != nullptr;
+  float* partial = nullptr;
+  const int G = C / 8;
+  const long long items = (long long)N * (pool ? (dims == 3 ? D / 2 : 1) * (H / 2) * (W / 2)
+                                                : (long long)D * H * W);
+  const int per = std::max(1, 256 / G);
+  const int grid = std::min(grid_for(items, per), 16384);
+  BN_BWD_DISPATCH(1, grid);
+}
+
+}  // namespace ddlpc

@@ -1,0 +1,101 @@
+// Shared helpers for the gfx950 (CDNA4, MI355X) kernel library.
+//
+// Conventions used by every kernel in csrc/:
+//   * activations are NHWC / NDHWC bf16 (channel fastest), stored as uint16_t;
+//   * accumulation, BatchNorm statistics and optimizer state are fp32 (fp64 for the final
+//     BN reductions);
+//   * wave = 64 lanes; MFMA tiles are v_mfma_f32_16x16x32_bf16 (A/B: 8 bf16 per lane,
+//     C/D: 4 fp32 per lane, col = lane&15, row = 4*(lane>>4) + i).
+#pragma once
+
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#define DDLPC_HOST_DEVICE __host__ __device__ __forceinline__
+#define DDLPC_DEVICE __device__ __forceinline__
+
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short i16x8_t __attribute__((ext_vector_type(8)));
+typedef short i16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+DDLPC_HOST_DEVICE float bf2f(bf16_t h) {
+  union { uint32_t u; float f; } v;
+  v.u = static_cast<uint32_t>(h) << 16;
+  return v.f;
+}
+
+// round-to-nearest-even (NaN kept quiet)
+DDLPC_HOST_DEVICE bf16_t f2bf(float f) {
+  union { uint32_t u; float f; } v;
+  v.f = f;
+  uint32_t u = v.u;
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return static_cast<bf16_t>((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<bf16_t>(u >> 16);
+}
+
+DDLPC_DEVICE uint32_t pack2(float a, float b) {
+  return static_cast<uint32_t>(f2bf(a)) | (static_cast<uint32_t>(f2bf(b)) << 16);
+}
+
+DDLPC_DEVICE float lo_bf(uint32_t w) { return bf2f(static_cast<bf16_t>(w & 0xffffu)); }
+DDLPC_DEVICE float hi_bf(uint32_t w) { return bf2f(static_cast<bf16_t>(w >> 16)); }
+
+// 16-byte (8 x bf16) vector <-> 8 floats
+DDLPC_DEVICE void unpack8(const uint4& v, float (&f)[8]) {
+  f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
+  f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
+}
+DDLPC_DEVICE uint4 pack8(const float (&f)[8]) {
+  return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+}
+
+DDLPC_DEVICE f32x4_t mfma16x16x32(const uint4& a, const uint4& b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                 __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+
+DDLPC_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+DDLPC_DEVICE double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+DDLPC_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies &M[row q][cols 4p..4p+3];
+// lane i receives column i of the 4 rows (row q in element q).  EXEC must be all ones.
+DDLPC_DEVICE uint2 lds_read_tr16(const void* lds_ptr) {
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  v4s r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4s*)(
+          (__attribute__((address_space(3))) char*)((size_t)lds_ptr)));
+  return __builtin_bit_cast(uint2, r);
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md §5, T1): blocks that share
+// an XCD (hardware round-robin: id % 8) receive a contiguous range of logical ids.
+DDLPC_DEVICE int xcd_remap(int bid, int nblocks) {
+  constexpr int kX = 8;
+  if (nblocks < kX) return bid;
+  const int q = nblocks / kX, r = nblocks % kX, x = bid % kX;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / kX;
+}
+
+inline int ceil_div(long a, long b) { return static_cast<int>((a + b - 1) / b); }

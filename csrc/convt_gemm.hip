@@ -1,0 +1,300 @@
+// ConvTranspose 2x2 stride 2 (and 2x2x2 for 3-D) as MFMA GEMMs — K8 of SURVEY.md §2.5.
+// Reference: UpBlock.up_sample = nn.ConvTranspose2d(in-out, in-out, kernel_size=2, stride=2)
+// (ref.py:606-607,615).  The kernel windows do not overlap, so
+//
+//   forward  out[2h+i, 2w+j, co] = b[co] + sum_ci x[h,w,ci] W[ci][co][i][j]
+//            = GEMM  M = input pixels, N = S*Cout (S = 4 or 8 sub-positions), K = Cin,
+//              with a pixel-shuffle scatter epilogue (+ bias);
+//   dgrad    dx[h,w,ci] = sum_{sub,co} dOut[up(h,w,sub), co] W[ci][co][sub]
+//            = GEMM  M = input pixels, N = Cin, K = S*Cout with a gathering A loader;
+//   wgrad    dW[ci][(sub,co)] = sum_px x[px][ci] dOut[up(px,sub)][co]
+//            = "TN" GEMM (both operands pixel-major), split-K over pixels, operands read
+//              through ds_read_b64_tr_b16, fp32 partial slabs reduced in fixed order.
+//
+// NT tile: 128 x 64 per 256-thread workgroup, 4 waves of 64 x 32 (4 x 2 v_mfma 16x16x32),
+// 32-deep K chunks staged through swizzled LDS with register prefetch (same scheme as the
+// 3x3 conv).  TN tile: 64 x 64, 4 waves of 32 x 32, 64-pixel K chunks.
+#include "common.h"
+#include "ops.h"
+
+namespace ddlpc {
+
+namespace {
+
+constexpr int BK = 32;
+DDLPC_DEVICE int swz(int row, int chunk) { return chunk ^ (((row >> 2) & 1) << 1); }
+DDLPC_DEVICE int lds_off(int row, int chunk) { return row * 64 + (swz(row, chunk) << 4); }
+
+// output (high-res) pixel of input pixel m and sub-position sub
+DDLPC_DEVICE long long up_pixel(long long m, int sub, int dims, int D, int H, int W) {
+  const int w = (int)(m % W);
+  long long q = m / W;
+  const int h = (int)(q % H);
+  q /= H;
+  if (dims == 2) {
+    const long long n = q;
+    const int i = sub >> 1, j = sub & 1;
+    return (n * (2 * H) + 2 * h + i) * (2 * W) + 2 * w + j;
+  }
+  const int d = (int)(q % D);
+  const long long n = q / D;
+  const int kd = sub >> 2, i = (sub >> 1) & 1, j = sub & 1;
+  return ((n * (2 * D) + 2 * d + kd) * (2 * H) + 2 * h + i) * (2 * W) + 2 * w + j;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs p) {
+  constexpr int BM = 128, BN = 64;
+  __shared__ __attribute__((aligned(16))) char smem[(BM + BN) * 64 > BM * BN * 2 ? (BM + BN) * 64 : BM * BN * 2];
+  char* sA = smem;
+  char* sB = smem + BM * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nTilesN = (p.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = bid % nTilesN, mtile = bid / nTilesN;
+  const long long m0 = (long long)mtile * BM;
+  const int n0 = ntile * BN;
+  const int S = p.dims == 2 ? 4 : 8;
+  const int g = lane >> 4;
+
+  uint4 ra[2], rb[1];
+  auto load = [&](int kc) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 256 * i;
+      const int row = e >> 2, cq = e & 3;
+      const long long m = m0 + row;
+      const int k8 = kc * BK + cq * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (m < p.M && k8 < p.K) {
+        if (MODE == GEMM_CONVT_FWD) {
+          v = *reinterpret_cast<const uint4*>(p.A + m * p.K + k8);
+        } else {   // DGRAD: k = sub*Cout + co gathered from the high-res gradient
+          const int sub = k8 / p.Cout, co = k8 % p.Cout;
+          const long long up = up_pixel(m, sub, p.dims, p.D, p.H, p.W);
+          v = *reinterpret_cast<const uint4*>(p.A + up * p.Cout + co);
+        }
+      }
+      ra[i] = v;
+    }
+    {
+      const int e = tid;
+      const int row = e >> 2, cq = e & 3;
+      const int n = n0 + row;
+      const int k8 = kc * BK + cq * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (n < p.N && k8 < p.K) v = *reinterpret_cast<const uint4*>(p.B + (long long)n * p.K + k8);
+      rb[0] = v;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 256 * i;
+      *reinterpret_cast<uint4*>(sA + lds_off(e >> 2, e & 3)) = ra[i];
+    }
+    *reinterpret_cast<uint4*>(sB + lds_off(tid >> 2, tid & 3)) = rb[0];
+  };
+
+  f32x4_t acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + BK - 1) / BK;
+  load(0);
+  for (int kc = 0; kc < nk; ++kc) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (kc + 1 < nk) load(kc + 1);
+    uint4 af[4], bfr[2];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+      af[mt] = *reinterpret_cast<const uint4*>(sA + lds_off(wm * 64 + mt * 16 + (lane & 15), g));
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      bfr[nt] = *reinterpret_cast<const uint4*>(sB + lds_off(wn * 32 + nt * 16 + (lane & 15), g));
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma16x16x32(af[mt], bfr[nt], acc[mt][nt]);
+  }
+
+  __syncthreads();
+  bf16_t* sO = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int col = wn * 32 + nt * 16 + (lane & 15);
+    float b = 0.f;
+    if (MODE == GEMM_CONVT_FWD && p.bias != nullptr && n0 + col < p.N) b = p.bias[(n0 + col) % p.Cout];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        sO[(wm * 64 + mt * 16 + 4 * (lane >> 4) + i) * BN + col] = f2bf(acc[mt][nt][i] + b);
+  }
+  __syncthreads();
+  bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+  for (int e = tid; e < BM * (BN / 8); e += 256) {
+    const int row = e / (BN / 8), cg = e % (BN / 8);
+    const long long m = m0 + row;
+    const int n = n0 + cg * 8;
+    if (m >= p.M || n >= p.N) continue;
+    const uint4 v = *reinterpret_cast<const uint4*>(sO + row * BN + cg * 8);
+    if (MODE == GEMM_CONVT_FWD) {
+      const int sub = n / p.Cout, co = n % p.Cout;
+      const long long up = up_pixel(m, sub, p.dims, p.D, p.H, p.W);
+      *reinterpret_cast<uint4*>(C + up * p.Cout + co) = v;
+    } else {
+      *reinterpret_cast<uint4*>(C + m * p.N + n) = v;
+    }
+  }
+  (void)S;
+}
+
+// ---------------------------------------------------------------- TN (weight gradient)
+// C[m = ci][n = (sub, co)] = sum_px x[px][ci] * dOut[up(px, sub)][co]
+__global__ __launch_bounds__(256, 2) void gemm_tn_wgrad_kernel(GemmArgs p) {
+  constexpr int BM = 64, BN = 64, KT = 64;
+  __shared__ __attribute__((aligned(16))) char smem[2 * KT * 128];
+  char* sA = smem;               // [KT px][BM ci]   128-B rows
+  char* sB = smem + KT * 128;    // [KT px][BN n]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nTilesN = (p.N + BN - 1) / BN, nTilesM = (p.M + BM - 1) / BM;
+  int b = blockIdx.x;
+  const int split = b % p.splits; b /= p.splits;
+  const int ntile = b % nTilesN; b /= nTilesN;
+  const int mtile = b;
+  const int m0 = mtile * BM, n0 = ntile * BN;
+  const long long npx = (long long)p.K;
+  const long long per = (npx + p.splits - 1) / p.splits;
+  const long long k_begin = per * split;
+  const long long k_end = k_begin + per < npx ? k_begin + per : npx;
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  (void)nTilesM;
+
+  f32x4_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[2], rb[2];
+  auto load = [&](long long k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 256 * i;               // 512 elements: 64 rows x 8 chunks
+      const int row = e >> 3, cg = e & 7;
+      const long long px = k0 + row;
+      uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
+      if (px < k_end) {
+        const int ci = m0 + cg * 8;
+        if (ci < p.M) va = *reinterpret_cast<const uint4*>(p.A + px * p.Cin + ci);
+        const int n = n0 + cg * 8;
+        if (n < p.N) {
+          const int sub = n / p.Cout, co = n % p.Cout;
+          const long long up = up_pixel(px, sub, p.dims, p.D, p.H, p.W);
+          vb = *reinterpret_cast<const uint4*>(p.B + up * p.Cout + co);
+        }
+      }
+      ra[i] = va;
+      rb[i] = vb;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 256 * i;
+      const int row = e >> 3, cg = e & 7;
+      *reinterpret_cast<uint4*>(sA + row * 128 + cg * 16) = ra[i];
+      *reinterpret_cast<uint4*>(sB + row * 128 + cg * 16) = rb[i];
+    }
+  };
+
+  if (k_begin < k_end) load(k_begin);
+  for (long long k0 = k_begin; k0 < k_end; k0 += KT) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (k0 + KT < k_end) load(k0 + KT);
+#pragma unroll
+    for (int ks = 0; ks < KT / 32; ++ks) {
+      uint4 af[2], bfr[2];
+      const int r0 = ks * 32 + 8 * g + q;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int c = wm * 32 + mt * 16 + 4 * pp;
+        const uint2 lo = lds_read_tr16(sA + r0 * 128 + c * 2);
+        const uint2 hi = lds_read_tr16(sA + (r0 + 4) * 128 + c * 2);
+        af[mt] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int c = wn * 32 + nt * 16 + 4 * pp;
+        const uint2 lo = lds_read_tr16(sB + r0 * 128 + c * 2);
+        const uint2 hi = lds_read_tr16(sB + (r0 + 4) * 128 + c * 2);
+        bfr[nt] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma16x16x32(af[mt], bfr[nt], acc[mt][nt]);
+    }
+  }
+  float* out = p.partial + (long long)split * p.M * p.N;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int n = n0 + wn * 32 + nt * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * 32 + mt * 16 + 4 * (lane >> 4) + i;
+        if (m < p.M && n < p.N) out[(long long)m * p.N + n] = acc[mt][nt][i];
+      }
+    }
+}
+
+// sum splits; slab [ci][(sub, co)] -> IOHW dW[ci][co][sub] (fp32)
+__global__ void convt_wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dW,
+                                          int Cin, int Cout, int S, int splits) {
+  const long long total = (long long)Cin * S * Cout;
+  for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < total;
+       o += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(o % Cout);
+    const int sub = (int)((o / Cout) % S);
+    const int ci = (int)(o / ((long long)Cout * S));
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += part[k * total + o];
+    dW[((long long)ci * Cout + co) * S + sub] = s;
+  }
+}
+
+}  // namespace
+
+void gemm_launch(GemmArgs& a, hipStream_t st) {
+  if (a.mode == GEMM_CONVT_WGRAD) {
+    const int grid = ((a.M + 63) / 64) * ((a.N + 63) / 64) * a.splits;
+    hipLaunchKernelGGL(gemm_tn_wgrad_kernel, dim3(grid), dim3(256), 0, st, a);
+    return;
+  }
+  const long long grid = ((a.M + 127) / 128) * (long long)((a.N + 63) / 64);
+  if (a.mode == GEMM_CONVT_FWD)
+    hipLaunchKernelGGL((gemm_nt_kernel<GEMM_CONVT_FWD>), dim3((unsigned)grid), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<GEMM_CONVT_DGRAD>), dim3((unsigned)grid), dim3(256), 0, st, a);
+}
+
+void gemm_wgrad_reduce_launch(const float* part, float* dW, float* /*db*/, int Cin, int Cout,
+                              int subs, int splits, hipStream_t st) {
+  const long long total = (long long)Cin * subs * Cout;
+  const int grid = (int)std::min<long long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(convt_wgrad_reduce_kernel, dim3(grid), dim3(256), 0, st, part, dW, Cin, Cout,
+                     subs, splits);
+}
+
+}  // namespace ddlpc

@@ -1,0 +1,260 @@
+// Fused 1x1 head + softmax cross-entropy + pixel accuracy — K11-K13 of SURVEY.md §2.5.
+// Reference: conv_last = nn.Conv2d(64//N, out_classes, 1) (ref.py:641,655),
+// nn.CrossEntropyLoss() with mean reduction / ignore_index=-100 (ref.py:703,755) and the
+// per-iteration pixel accuracy argmax(outputs,1)==y (ref.py:775).
+//
+// The logits never touch HBM during training: the forward kernel computes per-pixel logits
+// from the bf16 activation (C <= 64 channels, K <= 16 classes, fp32 math), the
+// log-sum-exp loss, the arg-max hit and the valid-pixel count, reduced per block.  The
+// backward kernel recomputes the logits (192 MACs/pixel: far cheaper than storing them),
+// forms dlogits = (softmax - onehot) * dL / count, writes dA = dlogits . Wh (bf16) and
+// reduces dWh = sum a (x) dlogits, dbh = sum dlogits through an LDS tile per 256 pixels.
+#include "common.h"
+#include "ops.h"
+
+namespace ddlpc {
+
+namespace {
+
+constexpr int MAXC = 64, MAXK = 16;
+
+template <int C, int K>
+DDLPC_DEVICE void logits_of(const bf16_t* ap, const float* sW, const float* sb, float (&z)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) z[k] = sb[k];
+#pragma unroll
+  for (int c8 = 0; c8 < C; c8 += 8) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(ap + c8), f);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[k] = fmaf(f[j], sW[k * C + c8 + j], z[k]);
+  }
+}
+
+template <int C, int K>
+__global__ __launch_bounds__(256) void head_ce_fwd_kernel(
+    const bf16_t* __restrict__ a, const float* __restrict__ Wh, const float* __restrict__ bh,
+    const int64_t* __restrict__ labels, float* __restrict__ partial, long long P,
+    int ignore_index) {
+  __shared__ float sW[K * C], sb[K];
+  for (int i = threadIdx.x; i < K * C; i += blockDim.x) sW[i] = Wh[i];
+  if (threadIdx.x < K) sb[threadIdx.x] = bh[threadIdx.x];
+  __syncthreads();
+  float loss = 0.f, correct = 0.f, count = 0.f;
+  for (long long px = blockIdx.x * (long long)blockDim.x + threadIdx.x; px < P;
+       px += (long long)gridDim.x * blockDim.x) {
+    float z[K];
+    logits_of<C, K>(a + px * C, sW, sb, z);
+    const int64_t y = labels[px];
+    float m = z[0];
+    int am = 0;
+#pragma unroll
+    for (int k = 1; k < K; ++k)
+      if (z[k] > m) { m = z[k]; am = k; }
+    float se = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) se += __expf(z[k] - m);
+    const float lse = m + __logf(se);
+    float zy = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) zy = (k == y) ? z[k] : zy;
+    if (y != ignore_index) {
+      loss += lse - zy;
+      count += 1.f;
+    }
+    correct += (am == y) ? 1.f : 0.f;
+  }
+  __shared__ float red[3][4];
+  loss = wave_sum(loss);
+  correct = wave_sum(correct);
+  count = wave_sum(count);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][w] = loss; red[1][w] = correct; red[2][w] = count; }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    float t = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[threadIdx.x][i];
+    partial[blockIdx.x * 3 + threadIdx.x] = t;
+  }
+}
+
+// out[0] = sum loss / count, out[1] = correct, out[2] = count
+__global__ void ce_finalize_kernel(const float* __restrict__ partial, int nb, float* out) {
+  double s[3] = {0, 0, 0};
+  for (int i = threadIdx.x; i < nb; i += blockDim.x)
+    for (int j = 0; j < 3; ++j) s[j] += partial[i * 3 + j];
+  __shared__ double red[3][4];
+  for (int j = 0; j < 3; ++j) {
+    s[j] = wave_sum_d(s[j]);
+    if ((threadIdx.x & 63) == 0) red[j][threadIdx.x >> 6] = s[j];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t[3] = {0, 0, 0};
+    for (int j = 0; j < 3; ++j)
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t[j] += red[j][w];
+    out[0] = (float)(t[0] / (t[2] > 0 ? t[2] : 1.0));
+    out[1] = (float)t[1];
+    out[2] = (float)t[2];
+  }
+}
+
+template <int C, int K>
+__global__ __launch_bounds__(256) void head_ce_bwd_kernel(
+    const bf16_t* __restrict__ a, const float* __restrict__ Wh, const float* __restrict__ bh,
+    const int64_t* __restrict__ labels, const float* __restrict__ gscale,
+    const float* __restrict__ stats3, bf16_t* __restrict__ dA, float* __restrict__ dWp,
+    long long P, int ignore_index) {
+  __shared__ float sW[K * C], sb[K];
+  __shared__ __attribute__((aligned(16))) bf16_t sA[256 * C];
+  __shared__ float sD[256 * K];
+  for (int i = threadIdx.x; i < K * C; i += blockDim.x) sW[i] = Wh[i];
+  if (threadIdx.x < K) sb[threadIdx.x] = bh[threadIdx.x];
+  __syncthreads();
+  const float cnt = stats3[2];
+  const float gs = (gscale != nullptr ? gscale[0] : 1.0f) / (cnt > 0.f ? cnt : 1.f);
+  const int t = threadIdx.x;
+  float accw = 0.f;                                  // thread t < K*C: dW[k][c]; < K*C+K: db
+  const long long nper = (long long)gridDim.x * blockDim.x;
+  for (long long base = blockIdx.x * (long long)blockDim.x; base < P; base += nper) {
+    const long long px = base + t;
+    float d[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) d[k] = 0.f;
+    if (px < P) {
+      float z[K];
+      logits_of<C, K>(a + px * C, sW, sb, z);
+      const int64_t y = labels[px];
+      float m = z[0];
+#pragma unroll
+      for (int k = 1; k < K; ++k) m = fmaxf(m, z[k]);
+      float se = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) { z[k] = __expf(z[k] - m); se += z[k]; }
+      const float inv = 1.f / se;
+      if (y != ignore_index) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) d[k] = (z[k] * inv - (k == y ? 1.f : 0.f)) * gs;
+      }
+      // dA = d . Wh
+#pragma unroll
+      for (int c8 = 0; c8 < C; c8 += 8) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float s = 0.f;
+#pragma unroll
+          for (int k = 0; k < K; ++k) s = fmaf(d[k], sW[k * C + c8 + j], s);
+          o[j] = s;
+        }
+        *reinterpret_cast<uint4*>(dA + px * C + c8) = pack8(o);
+      }
+#pragma unroll
+      for (int c8 = 0; c8 < C; c8 += 8)
+        *reinterpret_cast<uint4*>(sA + t * C + c8) = *reinterpret_cast<const uint4*>(a + px * C + c8);
+    } else {
+#pragma unroll
+      for (int c8 = 0; c8 < C; c8 += 8) *reinterpret_cast<uint4*>(sA + t * C + c8) = make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) sD[t * K + k] = d[k];
+    __syncthreads();
+    if (t < K * C) {
+      const int k = t / C, c = t % C;
+      float s = 0.f;
+      for (int i = 0; i < 256; ++i) s = fmaf(bf2f(sA[i * C + c]), sD[i * K + k], s);
+      accw += s;
+    } else if (t < K * C + K) {
+      const int k = t - K * C;
+      float s = 0.f;
+      for (int i = 0; i < 256; ++i) s += sD[i * K + k];
+      accw += s;
+    }
+    __syncthreads();
+  }
+  if (t < K * C + K) dWp[(long long)blockIdx.x * (K * C + K) + t] = accw;
+}
+
+template <int C, int K>
+__global__ void head_logits_kernel(const bf16_t* __restrict__ a, const float* __restrict__ Wh,
+                                   const float* __restrict__ bh, float* __restrict__ out,
+                                   long long P, long long HW) {
+  __shared__ float sW[K * C], sb[K];
+  for (int i = threadIdx.x; i < K * C; i += blockDim.x) sW[i] = Wh[i];
+  if (threadIdx.x < K) sb[threadIdx.x] = bh[threadIdx.x];
+  __syncthreads();
+  for (long long px = blockIdx.x * (long long)blockDim.x + threadIdx.x; px < P;
+       px += (long long)gridDim.x * blockDim.x) {
+    float z[K];
+    logits_of<C, K>(a + px * C, sW, sb, z);
+    const long long n = px / HW, s = px % HW;
+#pragma unroll
+    for (int k = 0; k < K; ++k) out[(n * K + k) * HW + s] = z[k];
+  }
+}
+
+// out[i] (+)= scale * sum_b partial[b][i]   (fixed order -> reproducible)
+__global__ void partial_sum_kernel(const float* __restrict__ partial, int P, int n,
+                                   float* __restrict__ out, float scale, int accumulate) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int b = 0; b < P; ++b) s += partial[(long long)b * n + i];
+    const float v = (float)s * scale;
+    out[i] = accumulate ? out[i] + v : v;
+  }
+}
+
+#define HEAD_SWITCH(C_, K_, ...)                                                  \
+  [&] {                                                                           \
+    if (C_ == 32 && K_ == 6) { constexpr int CC = 32, KK = 6; __VA_ARGS__; }        \
+    else if (C_ == 64 && K_ == 6) { constexpr int CC = 64, KK = 6; __VA_ARGS__; }   \
+    else if (C_ == 16 && K_ == 6) { constexpr int CC = 16, KK = 6; __VA_ARGS__; }   \
+    else if (C_ == 32 && K_ == 2) { constexpr int CC = 32, KK = 2; __VA_ARGS__; }   \
+    else if (C_ == 64 && K_ == 2) { constexpr int CC = 64, KK = 2; __VA_ARGS__; }   \
+    else if (C_ == 16 && K_ == 2) { constexpr int CC = 16, KK = 2; __VA_ARGS__; }   \
+    else if (C_ == 8 && K_ == 2) { constexpr int CC = 8, KK = 2; __VA_ARGS__; }     \
+    else if (C_ == 8 && K_ == 6) { constexpr int CC = 8, KK = 6; __VA_ARGS__; }     \
+    else { return false; }                                                        \
+    return true;                                                                  \
+  }()
+
+}  // namespace
+
+bool head_supported(int C, int K) {
+  return HEAD_SWITCH(C, K, (void)0);
+}
+
+void head_ce_fwd_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
+                        float* partial, float* out3, float* /*unused*/, int nblocks, long long P,
+                        int C, int K, int ignore_index, hipStream_t st) {
+  HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_fwd_kernel<CC, KK>), dim3(nblocks), dim3(256), 0,
+                                       st, a, Wh, bh, labels, partial, P, ignore_index));
+  hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(256), 0, st, partial, nblocks, out3);
+}
+
+void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
+                        const float* gscale, const float* stats3, int /*unused*/, bf16_t* dA,
+                        float* dW_partial, int nblocks, long long P, int C, int K,
+                        int ignore_index, hipStream_t st) {
+  HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK>), dim3(nblocks), dim3(256), 0,
+                                       st, a, Wh, bh, labels, gscale, stats3, dA, dW_partial, P,
+                                       ignore_index));
+}
+
+void head_logits_launch(const bf16_t* a, const float* Wh, const float* bh, float* logits,
+                        long long P, long long HW, int C, int K, hipStream_t st) {
+  const int grid = (int)std::min<long long>((P + 255) / 256, 4096);
+  HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_logits_kernel<CC, KK>), dim3(grid), dim3(256), 0, st,
+                                       a, Wh, bh, logits, P, HW));
+}
+
+void partial_sum_launch(const float* partial, int P, int n, float* out, float scale,
+                        bool accumulate, hipStream_t st) {
+  const int grid = std::max(1, std::min((n + 255) / 256, 1024));
+  hipLaunchKernelGGL(partial_sum_kernel, dim3(grid), dim3(256), 0, st, partial, P, n, out, scale,
+                     accumulate ? 1 : 0);
+}
+
+}  // namespace ddlpc

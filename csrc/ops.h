@@ -1,0 +1,153 @@
+// Kernel launch interfaces (device side lives in *.hip, host glue in bindings.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "common.h"
+
+namespace ddlpc {
+
+// ---------------------------------------------------------------- conv 3x3 fwd / dgrad
+struct ConvFwdArgs {
+  int dims;                       // 2 or 3
+  int N, D, H, W;                 // D = 1 for 2-D
+  int C1, C2, Cin, CinW;          // X1 / X2 channels, Cin = C1 + C2, packed weight stride
+  int Cout, Co1;                  // output channels; [0, Co1) -> Y1, rest -> Y2
+  int taps;                       // 9 or 27
+  const bf16_t* X1;
+  const bf16_t* X2;
+  const float* pscale;            // optional BN-apply + ReLU prologue on X1 (per channel)
+  const float* pshift;
+  const bf16_t* Wt;               // [Cout][taps][CinW]
+  const float* bias;              // optional
+  bf16_t* Y1;
+  bf16_t* Y2;
+  float* stats;                   // optional [nTilesM][2][Cout]
+  int TD, TH, TW;
+  int tilesD, tilesH, tilesW;
+  int nTilesM, nTilesN;
+};
+void conv3_fwd_launch(ConvFwdArgs& a, int bn, hipStream_t st);
+int conv3_fwd_bm(int bn);
+int conv3_halo_cap(int dims);
+
+// ---------------------------------------------------------------- conv 3x3 wgrad
+struct ConvWgradArgs {
+  int dims;
+  int N, D, H, W;
+  int C1, C2, Cin, Cout, taps;
+  const bf16_t* dY;               // [pixels][Cout]
+  const bf16_t* X1;
+  const bf16_t* X2;
+  const float* pscale;
+  const float* pshift;
+  float* partial;                 // [splits][Cout][taps][Cin]
+  int TD, TH, TW;
+  int tilesD, tilesH, tilesW, nTiles;
+  int coTiles, ciChunks, planes, splits;
+};
+void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st);
+void conv3_wgrad_reduce_launch(const float* part, float* dW, int Cout, int taps, int Cin,
+                               int splits, bool accumulate, hipStream_t st);
+int conv3_wgrad_halo_cap(int dims);
+
+// ---------------------------------------------------------------- generic bf16 GEMM (convT)
+// C[M][N] = sum_k A(m, k) * B(n, k)   with k-contiguous operands ("NT"), used by the
+// transposed-conv forward / data-gradient, and a pixel-major ("TN") variant for its
+// weight gradient.  Loader / epilogue modes are selected by `mode`.
+struct GemmArgs {
+  int mode;
+  int M, N, K;
+  const bf16_t* A;
+  const bf16_t* B;
+  const float* bias;
+  void* C;
+  float* partial;
+  int splits;
+  // geometry for the transposed-conv gathers / scatters
+  int dims, Nimg, D, H, W;        // input (low-res) geometry
+  int Cin, Cout;
+  const float* pscale;            // optional BN+ReLU prologue on A (forward of convT)
+  const float* pshift;
+};
+enum GemmMode {
+  GEMM_CONVT_FWD = 0,   // A = x[px][Cin], B = Wt[(sub, co)][Cin] -> scatter to 2x up, + bias
+  GEMM_CONVT_DGRAD = 1, // A = dOut gathered [px][(sub, co)], B = Wd[ci][(sub, co)] -> dx[px][ci]
+  GEMM_CONVT_WGRAD = 2, // TN: dW[ci][(sub, co)] = sum_px x[px][ci] * dOut[up(px, sub)][co]
+};
+void gemm_launch(GemmArgs& a, hipStream_t st);
+void gemm_wgrad_reduce_launch(const float* part, float* dW, float* db, int Cin, int Cout,
+                              int subs, int splits, hipStream_t st);
+
+// ---------------------------------------------------------------- BatchNorm / ReLU / pool
+void bn_finalize_launch(const float* partial, int P, int C, double count, const float* gamma,
+                        const float* beta, float* running_mean, float* running_var,
+                        float momentum, float eps, float* mean, float* invstd, float* scale,
+                        float* shift, bool update_running, int64_t* num_batches_tracked,
+                        hipStream_t st);
+void bn_relu_apply_launch(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
+                          bf16_t* pooled, int dims, int N, int D, int H, int W, int C,
+                          hipStream_t st);
+void bn_bwd_reduce_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y,
+                          const float* scale, const float* shift, const float* mean,
+                          const float* invstd, const float* gscale, float* partial, int nblocks,
+                          int dims, int N, int D, int H, int W, int C, hipStream_t st);
+void bn_bwd_finalize_launch(const float* partial, int P, int C, double count,
+                            const float* gamma, const float* invstd, float* dgamma,
+                            float* dbeta, float* coefs, hipStream_t st);
+void bn_bwd_apply_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y, const float* scale,
+                         const float* shift, const float* mean, const float* invstd,
+                         const float* coefs, const float* gscale, bf16_t* dY, int dims, int N,
+                         int D, int H, int W, int C, hipStream_t st);
+int bn_bwd_reduce_blocks(long long pixels_or_quads);
+
+// ---------------------------------------------------------------- head + cross-entropy
+bool head_supported(int C, int K);
+void head_ce_fwd_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
+                        float* partial, float* out3, float* unused, int nblocks, long long P,
+                        int C, int K, int ignore_index, hipStream_t st);
+void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
+                        const float* gscale, const float* stats3, int unused, bf16_t* dA,
+                        float* dW_partial, int nblocks, long long P, int C, int K,
+                        int ignore_index, hipStream_t st);
+void head_logits_launch(const bf16_t* a, const float* Wh, const float* bh, float* logits_nchw,
+                        long long P, long long HW, int C, int K, hipStream_t st);
+void partial_sum_launch(const float* partial, int P, int n, float* out, float scale,
+                        bool accumulate, hipStream_t st);
+
+// ---------------------------------------------------------------- optimizer / packing
+void adam_launch(float* p, const float* g, float* m, float* v, long long n, float b1, float b2,
+                 float eps, float wd, float step_size, float inv_sqrt_bc2, hipStream_t st);
+struct PackEntry {                 // one conv weight to pack into bf16 kernel layouts
+  const float* src;                // OIHW fp32  (or IOHW for transposed conv)
+  bf16_t* fwd;                     // conv: [co][tap][CinW]; convT: [(sub, co)][Cin]
+  bf16_t* dgrad;                   // conv: [ci][8-tap][CoutW]; convT: [ci][(sub, co)]
+  int kind;                        // 0 = conv3, 1 = convT2
+  int Cout, Cin, taps, CinW, CoutW;
+};
+void weight_pack_launch(const PackEntry* entries_dev, int n_entries, long long max_elems,
+                        hipStream_t st);
+
+// ---------------------------------------------------------------- gradient codec
+void codec_absmax_launch(const float* x, const int64_t* seg, int nseg, float* scales,
+                         hipStream_t st);
+void codec_encode_launch(const float* x, const int64_t* seg, int nseg, const float* scales,
+                         void* out, int codec, long long n, hipStream_t st);
+void codec_decode_sum_launch(float* out, const void* q, const float* scales, const float* w,
+                             const int64_t* seg, int nseg, int world, int codec, long long n,
+                             hipStream_t st);
+
+// ---------------------------------------------------------------- misc
+void bilinear_up2_launch(const bf16_t* x, bf16_t* y, int dims, int N, int D, int H, int W, int C,
+                         bool backward, hipStream_t st);
+void bilinear_up2_bwd_launch(const bf16_t* dy, float* dx_f32, bf16_t* dx, int dims, int N, int D,
+                             int H, int W, int C, hipStream_t st);
+void channel_sum_launch(const bf16_t* x, long long P, int C, float* partial, int nblocks,
+                        hipStream_t st);
+void nchw_to_nhwc_bf16_launch(const void* x, int in_dtype, bf16_t* y, int N, int C,
+                              long long S, hipStream_t st);
+
+}  // namespace ddlpc

@@ -1,0 +1,320 @@
+"""The U-Net forward/backward on the hand-written gfx950 kernels (``torch.ops.ddlpc``).
+
+Execution model (SURVEY.md §2.5 kernel inventory -> fusion plan):
+
+* activations are channel-last bf16 tensors of SHAPE [N, (D,) H, W, C]; parameters stay
+  fp32 in their reference layouts (the flat fp32 master buffer) and are packed to bf16
+  kernel layouts once per optimizer step (``pack_weights``: ONE launch for all convs);
+* a ``DoubleConv`` block is ONE autograd node (``_DoubleConvFn``) with an explicit
+  backward:
+
+      forward   y1,stats = conv3(x [, skip])            (concat = 2 input pointers)
+                s1       = bn_finalize(stats)            (fp64 reduce, running stats)
+                y2,stats = conv3(relu(bn1(y1)))          (BN1+ReLU fused in the prologue)
+                s2       = bn_finalize(stats)
+                a2[,p]   = bn_relu_apply(y2[, pool])     (max-pool fused, encoder only)
+      backward  dY2      = bn_backward(da2 [, dpool])    (unpool + skip-sum + ReLU + BN)
+                dW2      = conv3_wgrad(dY2, relu(bn1(y1)))   (prologue re-applied)
+                dA1      = conv3(dY2, flip(W2)^T)            (data gradient)
+                dY1      = bn_backward(dA1)
+                dW1      = conv3_wgrad(dY1, x [, skip])
+                dx[,dskip] = conv3(dY1, flip(W1)^T) split across the concat inputs
+
+  only x, y1, y2 and the BN statistics are saved; a1 is never materialised and a2 only
+  once (it is the skip tensor / next input);
+* ``ConvTranspose(2, 2)`` is a GEMM with a pixel-shuffle epilogue (``_ConvTFn``);
+* the 1x1 head, softmax cross-entropy, its gradient and the pixel-accuracy count are one
+  fused kernel pair (``_HeadCEFn``): logits never reach HBM in training.
+
+Conv biases feeding a training-mode BatchNorm receive an exactly-zero gradient (the BN
+mean subtraction cancels them); stock PyTorch returns float noise of ~1e-9 there.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import _ext
+
+_F = None
+
+
+def _ops():
+    global _F
+    if _F is None:
+        _F = _ext.ops()
+    return _F
+
+
+def _nhwc_shape_to_nchw(t: torch.Tensor) -> torch.Tensor:
+    """View a channel-last [N,(D,)H,W,C] tensor as NCHW (no copy)."""
+    nd = t.dim()
+    return t.permute(0, nd - 1, *range(1, nd - 1))
+
+
+class _ConvPack:
+    """bf16 kernel-layout copies of one conv / transposed-conv weight."""
+
+    def __init__(self, conv: nn.Module, kind: int, need_dgrad: bool):
+        w = conv.weight
+        self.conv, self.kind = conv, kind
+        dev = w.device
+        if kind == 0:                                  # 3x3(x3) conv, OIHW
+            cout, cin = w.shape[0], w.shape[1]
+            taps = w[0, 0].numel()
+            cinw = (cin + 7) // 8 * 8
+            self.fwd = torch.zeros(cout, taps, cinw, dtype=torch.bfloat16, device=dev)
+            self.dgrad = (torch.zeros(cin, taps, cout, dtype=torch.bfloat16, device=dev)
+                          if need_dgrad else None)
+            self.shape = (cout, cin, taps, cinw, cout)
+        else:                                          # ConvTranspose k2 s2, IOHW
+            cin, cout = w.shape[0], w.shape[1]
+            taps = w[0, 0].numel()                     # 4 or 8 sub-positions
+            self.fwd = torch.zeros(taps * cout, cin, dtype=torch.bfloat16, device=dev)
+            self.dgrad = torch.zeros(cin, taps * cout, dtype=torch.bfloat16, device=dev)
+            self.shape = (cout, cin, taps, cin, cout)
+        self.cout, self.cin, self.taps = self.shape[0], self.shape[1], self.shape[2]
+
+    def entry(self) -> List[int]:
+        w = self.conv.weight
+        assert w.is_contiguous(), "packed weights need contiguous fp32 parameters"
+        cout, cin, taps, cinw, coutw = self.shape
+        return [w.data_ptr(), self.fwd.data_ptr(),
+                self.dgrad.data_ptr() if self.dgrad is not None else 0,
+                (self.kind & 0xffffffff) | (cout << 32), cin | (taps << 32), cinw | (coutw << 32)]
+
+    def numel(self) -> int:
+        return self.cout * self.cin * self.taps
+
+
+class _BNState:
+    def __init__(self, bn: nn.Module):
+        self.bn = bn
+
+    def finalize(self, stats_partial: torch.Tensor, count: float) -> torch.Tensor:
+        bn = self.bn
+        if bn.training:
+            mom = bn.momentum if bn.momentum is not None else 0.1
+            return _ops().bn_finalize(stats_partial, float(count), bn.weight, bn.bias,
+                                      bn.running_mean, bn.running_var, float(mom), float(bn.eps),
+                                      bool(bn.track_running_stats), bn.num_batches_tracked)
+        return self.eval_stats()
+
+    def eval_stats(self) -> torch.Tensor:
+        bn = self.bn
+        inv = torch.rsqrt(bn.running_var.float() + bn.eps)
+        scale = bn.weight * inv
+        shift = bn.bias - bn.running_mean * scale
+        return torch.stack([bn.running_mean.float(), inv, scale, shift]).contiguous()
+
+
+class _DoubleConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x1, x2, w1, b1, g1, be1, w2, b2, g2, be2, blk, pool: bool):
+        F = _ops()
+        p1, p2 = blk.pack1, blk.pack2
+        training = blk.bn1.bn.training
+        c1 = p1.cout
+        y1, _, st1 = F.conv3_fwd(x1, x2, p1.fwd, b1, None, None, c1, 0, training)
+        count = float(y1.numel() // c1)
+        s1 = blk.bn1.finalize(st1, count) if training else blk.bn1.eval_stats()
+        y2, _, st2 = F.conv3_fwd(y1, None, p2.fwd, b2, s1[2], s1[3], p2.cout, 0, training)
+        s2 = blk.bn2.finalize(st2, count) if training else blk.bn2.eval_stats()
+        a2, pooled = F.bn_relu_apply(y2, s2, pool)
+        ctx.blk = blk
+        ctx.pool = pool
+        ctx.has_x2 = x2 is not None
+        ctx.x1_requires_grad = ctx.needs_input_grad[0]
+        ctx.save_for_backward(x1, x2 if x2 is not None else torch.empty(0), y1, y2, s1, s2, g1, g2)
+        ctx.set_materialize_grads(False)
+        if pool:
+            return a2, pooled
+        return a2, None
+
+    @staticmethod
+    def backward(ctx, da2, dpool):
+        F = _ops()
+        x1, x2, y1, y2, s1, s2, g1, g2 = ctx.saved_tensors
+        blk = ctx.blk
+        x2 = x2 if ctx.has_x2 else None
+        if da2 is not None:
+            da2 = da2.contiguous()
+        if dpool is not None:
+            dpool = dpool.contiguous()
+        if da2 is None and dpool is None:
+            return (None,) * 12
+        dy2, dg2, dbe2 = F.bn_backward(da2, dpool, y2, s2, g2, None)
+        dw2 = F.conv3_wgrad(dy2, y1, None, s1[2], s1[3])
+        p1, p2 = blk.pack1, blk.pack2
+        da1, _, _ = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False)
+        dy1, dg1, dbe1 = F.bn_backward(da1, None, y1, s1, g1, None)
+        dw1 = F.conv3_wgrad(dy1, x1, x2, None, None)
+        dx1 = dx2 = None
+        if ctx.needs_input_grad[0] or (x2 is not None and ctx.needs_input_grad[1]):
+            c_x1 = x1.shape[-1]
+            co1 = c_x1 if x2 is not None else 0
+            dx1, dx2, _ = F.conv3_fwd(dy1, None, p1.dgrad, None, None, None, p1.cin, co1, False)
+            if x2 is None:
+                dx2 = None
+        zb1 = torch.zeros_like(dbe1) if ctx.needs_input_grad[3] else None
+        zb2 = torch.zeros_like(dbe2) if ctx.needs_input_grad[7] else None
+        return (dx1, dx2, dw1.view_as(blk.conv1.weight), zb1, dg1, dbe1,
+                dw2.view_as(blk.conv2.weight), zb2, dg2, dbe2, None, None)
+
+
+class _ConvTFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, pack: _ConvPack):
+        out = _ops().convt_fwd(x, pack.fwd, b, pack.cout)
+        ctx.save_for_backward(x)
+        ctx.pack = pack
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        F = _ops()
+        (x,) = ctx.saved_tensors
+        dout = dout.contiguous()
+        dx = F.convt_dgrad(dout, ctx.pack.dgrad, ctx.pack.cin) if ctx.needs_input_grad[0] else None
+        dw, db = F.convt_wgrad(x, dout)
+        return dx, dw.view_as(ctx.pack.conv.weight), db, None
+
+
+class _BilinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return _ops().bilinear_up2(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _ops().bilinear_up2_bwd(dy.contiguous())
+
+
+class _HeadCEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, wh, bh, labels, ignore_index: int):
+        out3 = _ops().head_ce_fwd(a, wh, bh, labels, ignore_index)
+        ctx.save_for_backward(a, wh, bh, labels, out3)
+        ctx.ignore_index = ignore_index
+        loss = out3[0]
+        correct = out3[1]
+        ctx.mark_non_differentiable(correct)
+        return loss, correct
+
+    @staticmethod
+    def backward(ctx, dloss, dcorrect):
+        a, wh, bh, labels, out3 = ctx.saved_tensors
+        gs = dloss.reshape(1).float().contiguous() if dloss is not None else None
+        da, dw, db = _ops().head_ce_bwd(a, wh, bh, labels, out3, gs, ctx.ignore_index)
+        return da, dw, db, None, None
+
+
+class _Block:
+    """Kernel-side view of one DoubleConv: packed weights + BN handles."""
+
+    def __init__(self, dc: nn.Module, first: bool):
+        seq = dc.double_conv
+        self.conv1, self.conv2 = seq[0], seq[3]
+        self.bn1, self.bn2 = _BNState(seq[1]), _BNState(seq[4])
+        self.pack1 = _ConvPack(self.conv1, 0, need_dgrad=not first)
+        self.pack2 = _ConvPack(self.conv2, 0, need_dgrad=True)
+
+    def __call__(self, x1, x2, pool: bool):
+        return _DoubleConvFn.apply(x1, x2, self.conv1.weight, self.conv1.bias,
+                                   self.bn1.bn.weight, self.bn1.bn.bias, self.conv2.weight,
+                                   self.conv2.bias, self.bn2.bn.weight, self.bn2.bn.bias, self,
+                                   pool)
+
+
+class UNetEngine:
+    """Runs a ``models.UNet`` through the HIP kernels (attach with ``UNet.to_hip()``)."""
+
+    def __init__(self, model: nn.Module, strict: bool = True):
+        _ext.load(strict=strict)
+        self.model = model
+        dev = next(model.parameters()).device
+        if dev.type != "cuda":
+            raise RuntimeError("UNetEngine needs the model on the GPU")
+        self.enc = [_Block(b.double_conv, first=(i == 0))
+                    for i, b in enumerate(model.down_blocks())]
+        self.mid = _Block(model.double_conv, first=False)
+        self.dec = []
+        for ub in model.up_blocks():
+            up = ub.up_sample
+            pack = _ConvPack(up, 1, True) if isinstance(up, (nn.ConvTranspose2d, nn.ConvTranspose3d)) else None
+            self.dec.append((ub, pack, _Block(ub.double_conv, first=False)))
+        head = model.conv_last
+        self.head = head
+        self.packs = [p for b in self.enc + [self.mid] for p in (b.pack1, b.pack2)]
+        for _, pk, b in self.dec:
+            self.packs += [pk, b.pack1, b.pack2] if pk is not None else [b.pack1, b.pack2]
+        self._entries = None
+        self._entries_key = None
+        self._version = None
+        self.pack_weights()
+
+    # ------------------------------------------------------------------ weights
+    def _params_version(self):
+        return sum(p.weight._version for p in self.packs)
+
+    def pack_weights(self):
+        key = tuple(p.conv.weight.data_ptr() for p in self.packs)
+        if self._entries is None or key != self._entries_key:
+            rows = [p.entry() for p in self.packs]
+            self._entries = torch.tensor(rows, dtype=torch.int64).to(
+                self.packs[0].fwd.device)
+            self._entries_key = key
+            self._max = max(p.numel() for p in self.packs)
+        _ops().weight_pack(self._entries, len(self.packs), self._max)
+        self._version = self._params_version()
+
+    def _ensure_packed(self):
+        if self._version != self._params_version():
+            self.pack_weights()
+
+    # ------------------------------------------------------------------ layout
+    def to_nhwc(self, x: torch.Tensor) -> torch.Tensor:
+        nd = x.dim()
+        perm = (0,) + tuple(range(2, nd)) + (1,)
+        xt = x.permute(*perm)
+        if xt.is_contiguous() and xt.dtype == torch.bfloat16:
+            return xt                                  # channels_last bf16 input: zero copy
+        return _ops().to_nhwc_bf16(x.contiguous())
+
+    # ------------------------------------------------------------------ graph
+    def features(self, x: torch.Tensor) -> torch.Tensor:
+        """Input (NCHW view) -> last decoder activation, channel-last bf16."""
+        self._ensure_packed()
+        h = self.to_nhwc(x)
+        skips = []
+        for blk in self.enc:
+            skip, h = blk(h, None, True)
+            skips.append(skip)
+        h, _ = self.mid(h, None, False)
+        for (ub, pack, blk), skip in zip(self.dec, reversed(skips)):
+            if pack is not None:
+                up = _ConvTFn.apply(h, ub.up_sample.weight, ub.up_sample.bias, pack)
+            else:
+                up = _BilinearFn.apply(h)
+            h, _ = blk(up, skip, False)
+        return h
+
+    def _head_params(self):
+        w = self.head.weight
+        return w.view(w.shape[0], w.shape[1]), self.head.bias
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        a = self.features(x)
+        wh, bh = self._head_params()
+        if torch.is_grad_enabled() and (wh.requires_grad or a.requires_grad):
+            # differentiable logits (rare: training uses loss_and_correct)
+            logits = torch.einsum("n...c,kc->n...k", a.float(), wh) + bh
+            return _nhwc_shape_to_nchw(logits)
+        return _ops().head_logits(a, wh.detach().contiguous(), bh.detach())
+
+    def loss_and_correct(self, x: torch.Tensor, y: torch.Tensor, ignore_index: int = -100):
+        a = self.features(x)
+        wh, bh = self._head_params()
+        return _HeadCEFn.apply(a, wh, bh, y.contiguous(), ignore_index)

@@ -1,0 +1,280 @@
+"""Numerics of every hand-written HIP kernel against a plain PyTorch fp32 reference.
+
+Each test builds bf16 inputs, runs the gfx950 kernel through ``torch.ops.ddlpc`` and compares
+with the same op computed by stock PyTorch in fp32 on the bf16-valued inputs.  Tolerances
+reflect bf16 OUTPUT rounding (the kernels accumulate in fp32).
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from ddlpc.ops import _ext
+    return _ext.ops()
+
+
+def nhwc(x):           # NCHW(D) -> channel-last shape
+    return x.permute(0, *range(2, x.dim()), 1).contiguous()
+
+
+def nchw(x):
+    return x.permute(0, x.dim() - 1, *range(1, x.dim() - 1))
+
+
+def rel_err(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+
+
+def pack_conv(ops, w, need_dgrad=True):
+    """pack an OIHW fp32 conv weight with the library's packer"""
+    from ddlpc.ops.fused_unet import _ConvPack
+    conv = torch.nn.Module()
+    conv.weight = torch.nn.Parameter(w.contiguous())
+    kind = 0 if w.shape[-1] == 3 else 1
+    pk = _ConvPack(conv, kind, need_dgrad)
+    ent = torch.tensor([pk.entry()], dtype=torch.int64, device=w.device)
+    ops.weight_pack(ent, 1, pk.numel())
+    return pk
+
+
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout", [
+    (2, 16, 16, 32, 0, 32), (2, 32, 32, 64, 0, 64), (1, 16, 16, 64, 64, 128),
+    (2, 8, 8, 256, 0, 256), (2, 32, 32, 3, 0, 32), (1, 16, 16, 64, 32, 96),
+    (2, 24, 20, 32, 0, 64), (1, 64, 64, 32, 64, 32)])
+def test_conv3_fwd(ops, N, H, W, C1, C2, Cout):
+    torch.manual_seed(0)
+    x1 = torch.randn(N, C1, H, W, device=DEV).bfloat16()
+    x2 = torch.randn(N, C2, H, W, device=DEV).bfloat16() if C2 else None
+    w = torch.randn(Cout, C1 + C2, 3, 3, device=DEV) * (1.0 / math.sqrt(9 * (C1 + C2)))
+    b = torch.randn(Cout, device=DEV) * 0.1
+    pk = pack_conv(ops, w)
+    y, _, st = ops.conv3_fwd(nhwc(x1), nhwc(x2) if x2 is not None else None, pk.fwd, b, None,
+                             None, Cout, 0, True)
+    xin = torch.cat([x1, x2], 1) if x2 is not None else x1
+    ref = F.conv2d(xin.float(), w.bfloat16().float(), b, padding=1)
+    assert rel_err(nchw(y), ref) < 1e-2
+    # BN statistics partials: per-channel sum over pixels of the stored bf16 output
+    s = st.sum(0)
+    yf = nchw(y).float()
+    assert torch.allclose(s[0], yf.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(s[1], (yf * yf).sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+
+
+def test_conv3_fwd_prologue(ops):
+    torch.manual_seed(1)
+    N, H, W, C, Cout = 2, 32, 32, 64, 64
+    x = torch.randn(N, C, H, W, device=DEV).bfloat16()
+    scale = torch.rand(C, device=DEV) + 0.5
+    shift = torch.randn(C, device=DEV) * 0.5
+    w = torch.randn(Cout, C, 3, 3, device=DEV) / math.sqrt(9 * C)
+    pk = pack_conv(ops, w)
+    y, _, _ = ops.conv3_fwd(nhwc(x), None, pk.fwd, None, scale, shift, Cout, 0, False)
+    a = torch.relu(x.float() * scale[None, :, None, None] + shift[None, :, None, None]).bfloat16()
+    ref = F.conv2d(a.float(), w.bfloat16().float(), padding=1)
+    assert rel_err(nchw(y), ref) < 1e-2
+
+
+@pytest.mark.parametrize("C1,C2,Cout", [(64, 32, 32), (0, 64, 32), (256, 256, 256)])
+def test_conv3_dgrad_split(ops, C1, C2, Cout):
+    torch.manual_seed(2)
+    if C1 == 0:
+        C1, C2 = C2, 0
+    N, H, W = 2, 16, 16
+    Cin = C1 + C2
+    w = torch.randn(Cout, Cin, 3, 3, device=DEV) / math.sqrt(9 * Cin)
+    dy = torch.randn(N, Cout, H, W, device=DEV).bfloat16()
+    pk = pack_conv(ops, w)
+    dx1, dx2, _ = ops.conv3_fwd(nhwc(dy), None, pk.dgrad, None, None, None, Cin,
+                                C1 if C2 else 0, False)
+    xin = torch.zeros(N, Cin, H, W, device=DEV, requires_grad=True)
+    out = F.conv2d(xin, w.bfloat16().float(), padding=1)
+    (g,) = torch.autograd.grad(out, xin, dy.float())
+    assert rel_err(nchw(dx1), g[:, :C1]) < 1e-2
+    if C2:
+        assert rel_err(nchw(dx2), g[:, C1:]) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout,pro", [
+    (2, 16, 16, 32, 0, 32, False), (2, 32, 32, 64, 0, 64, True), (1, 16, 16, 64, 64, 128, False),
+    (4, 8, 8, 256, 0, 256, True), (2, 32, 32, 3, 0, 32, False), (1, 16, 16, 64, 32, 32, False)])
+def test_conv3_wgrad(ops, N, H, W, C1, C2, Cout, pro):
+    torch.manual_seed(3)
+    x1 = torch.randn(N, C1, H, W, device=DEV).bfloat16()
+    x2 = torch.randn(N, C2, H, W, device=DEV).bfloat16() if C2 else None
+    dy = torch.randn(N, Cout, H, W, device=DEV).bfloat16()
+    scale = shift = None
+    a1 = x1.float()
+    if pro:
+        scale = torch.rand(C1, device=DEV) + 0.5
+        shift = torch.randn(C1, device=DEV) * 0.5
+        a1 = torch.relu(x1.float() * scale[None, :, None, None] + shift[None, :, None, None]).bfloat16().float()
+    xin = torch.cat([a1, x2.float()], 1) if x2 is not None else a1
+    dw = ops.conv3_wgrad(nhwc(dy), nhwc(x1), nhwc(x2) if x2 is not None else None, scale, shift)
+    w = torch.zeros(Cout, C1 + C2, 3, 3, device=DEV, requires_grad=True)
+    out = F.conv2d(xin, w, padding=1)
+    (g,) = torch.autograd.grad(out, w, dy.float())
+    assert dw.shape == g.shape
+    assert rel_err(dw, g) < 5e-3
+
+
+def test_bn_forward_backward(ops):
+    torch.manual_seed(4)
+    N, H, W, C = 4, 16, 16, 64
+    y = (torch.randn(N, C, H, W, device=DEV) * 2 + 0.5).bfloat16()
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    nbt = torch.zeros((), dtype=torch.long, device=DEV)
+    yf = y.float()
+    partial = torch.stack([yf.sum((0, 2, 3)), (yf * yf).sum((0, 2, 3))])[None].contiguous()
+    s4 = ops.bn_finalize(partial, float(N * H * W), gamma, beta, rm, rv, 0.1, 1e-5, True, nbt)
+    bn = torch.nn.BatchNorm2d(C).to(DEV)
+    with torch.no_grad():
+        bn.weight.copy_(gamma)
+        bn.bias.copy_(beta)
+    yr = yf.clone().requires_grad_(True)
+    ar = torch.relu(bn(yr))
+    assert torch.allclose(rm, bn.running_mean, atol=1e-5)
+    assert torch.allclose(rv, bn.running_var, rtol=1e-4, atol=1e-5)
+    assert int(nbt) == 1
+    a, p = ops.bn_relu_apply(nhwc(y), s4, True)
+    assert rel_err(nchw(a), ar) < 5e-3
+    assert rel_err(nchw(p), F.max_pool2d(nchw(a).float(), 2)) < 1e-6
+    # backward through BN + ReLU + max-pool + skip sum
+    dA = torch.randn(N, C, H, W, device=DEV).bfloat16()
+    dP = torch.randn(N, C, H // 2, W // 2, device=DEV).bfloat16()
+    dy, dg, db = ops.bn_backward(nhwc(dA), nhwc(dP), nhwc(y), s4, gamma, None)
+    ar2 = torch.relu(bn(yr))
+    a_bf = ar2.bfloat16().float()
+    pooled = F.max_pool2d(a_bf, 2)
+    loss = (ar2 * dA.float()).sum() + (F.max_pool2d(ar2, 2) * dP.float()).sum()
+    gy, gg, gb = torch.autograd.grad(loss, [yr, bn.weight, bn.bias])
+    assert rel_err(nchw(dy), gy) < 2e-2
+    assert rel_err(dg, gg) < 1e-2
+    assert rel_err(db, gb) < 1e-2
+    del pooled
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 8, 8, 256, 256), (2, 16, 16, 64, 64), (1, 32, 32, 128, 128)])
+def test_convt(ops, N, H, W, Cin, Cout):
+    torch.manual_seed(5)
+    x = torch.randn(N, Cin, H, W, device=DEV).bfloat16()
+    w = torch.randn(Cin, Cout, 2, 2, device=DEV) / math.sqrt(Cin)
+    b = torch.randn(Cout, device=DEV) * 0.1
+    pk = pack_conv(ops, w)
+    out = ops.convt_fwd(nhwc(x), pk.fwd, b, Cout)
+    xr = x.float().requires_grad_(True)
+    wr = w.bfloat16().float().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    ref = F.conv_transpose2d(xr, wr, br, stride=2)
+    assert rel_err(nchw(out), ref) < 1e-2
+    dout = torch.randn_like(ref).bfloat16()
+    gx, gw, gb = torch.autograd.grad(ref, [xr, wr, br], dout.float())
+    dx = ops.convt_dgrad(nhwc(dout), pk.dgrad, Cin)
+    assert rel_err(nchw(dx), gx) < 1e-2
+    dw, db = ops.convt_wgrad(nhwc(x), nhwc(dout))
+    assert rel_err(dw, gw) < 5e-3
+    assert rel_err(db, gb) < 1e-3
+
+
+def test_head_ce(ops):
+    torch.manual_seed(6)
+    N, H, W, C, K = 2, 32, 32, 32, 6
+    a = torch.relu(torch.randn(N, C, H, W, device=DEV)).bfloat16()
+    wh = torch.randn(K, C, device=DEV) * 0.3
+    bh = torch.randn(K, device=DEV) * 0.1
+    y = torch.randint(0, K, (N, H, W), device=DEV)
+    y[0, 0, :5] = -100
+    out3 = ops.head_ce_fwd(nhwc(a), wh, bh, y, -100)
+    ar = a.float().requires_grad_(True)
+    whr = wh.clone().requires_grad_(True)
+    bhr = bh.clone().requires_grad_(True)
+    logits = torch.einsum("nchw,kc->nkhw", ar, whr) + bhr[None, :, None, None]
+    loss = F.cross_entropy(logits, y)
+    assert abs(float(out3[0]) - float(loss)) < 1e-4 * max(1.0, float(loss))
+    assert int(out3[1]) == int((logits.argmax(1) == y).sum())
+    assert int(out3[2]) == int((y != -100).sum())
+    g = torch.tensor([0.5], device=DEV)
+    da, dw, db = ops.head_ce_bwd(nhwc(a), wh, bh, y, out3, g, -100)
+    ga, gw, gb = torch.autograd.grad(loss * 0.5, [ar, whr, bhr])
+    assert rel_err(nchw(da), ga) < 1e-2
+    assert rel_err(dw, gw) < 1e-3
+    assert rel_err(db, gb) < 1e-3
+    lg = ops.head_logits(nhwc(a), wh, bh)
+    assert rel_err(lg, logits) < 1e-5
+
+
+def test_adam_matches_torch(ops):
+    torch.manual_seed(7)
+    n = 10_007
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    pr = p.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pr], lr=1e-3)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    for t in range(1, 4):
+        pr.grad = g.clone()
+        opt.step()
+        bc1, bc2 = 1 - 0.9 ** t, 1 - 0.999 ** t
+        ops.adam_step(p, g, m, v, 0.9, 0.999, 1e-8, 0.0, 1e-3 / bc1, 1 / math.sqrt(bc2))
+    assert torch.allclose(p, pr.detach(), atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("codec", ["fp16_absmax", "int8_absmax"])
+def test_codec_matches_oracle(codec):
+    from ddlpc.ops import codec_ops
+    from ddlpc.parallel import codec as C
+    torch.manual_seed(8)
+    g = torch.randn(100_003, device=DEV) * 1e-3
+    segs = [(0, 50_000), (50_000, 100_003)]
+    q, s = codec_ops.encode_segments(g, segs, codec)
+    qc, sc = C.encode_segments(g.cpu(), segs, codec)
+    assert torch.equal(s.cpu(), sc)
+    assert torch.equal(q.cpu(), qc)
+    out = torch.empty_like(g)
+    codec_ops.decode_sum_segments(out, [q, q], [s, s], segs, codec, [0.25, 0.75])
+    ref = torch.zeros_like(g).cpu()
+    codec_ops.decode_sum_segments(ref, [qc, qc], [sc, sc], segs, codec, [0.25, 0.75])
+    assert torch.allclose(out.cpu(), ref, rtol=1e-6, atol=1e-12)
+
+
+def test_bilinear(ops):
+    torch.manual_seed(9)
+    x = torch.randn(2, 32, 8, 8, device=DEV).bfloat16()
+    y = ops.bilinear_up2(nhwc(x))
+    xr = x.float().requires_grad_(True)
+    ref = F.interpolate(xr, scale_factor=2, mode="bilinear", align_corners=True)
+    assert rel_err(nchw(y), ref) < 1e-2
+    dy = torch.randn_like(ref).bfloat16()
+    (gx,) = torch.autograd.grad(ref, xr, dy.float())
+    dx = ops.bilinear_up2_bwd(nhwc(dy))
+    assert rel_err(nchw(dx), gx) < 1e-2
+
+
+def test_conv3d_fwd_wgrad(ops):
+    torch.manual_seed(10)
+    N, D, H, W, C, Cout = 1, 8, 8, 16, 32, 64
+    x = torch.randn(N, C, D, H, W, device=DEV).bfloat16()
+    w = torch.randn(Cout, C, 3, 3, 3, device=DEV) / math.sqrt(27 * C)
+    pk = pack_conv(ops, w)
+    y, _, _ = ops.conv3_fwd(nhwc(x), None, pk.fwd, None, None, None, Cout, 0, False)
+    ref = F.conv3d(x.float(), w.bfloat16().float(), padding=1)
+    assert rel_err(nchw(y), ref) < 1e-2
+    dy = torch.randn_like(ref).bfloat16()
+    dw = ops.conv3_wgrad(nhwc(dy), nhwc(x), None, None, None)
+    wr = torch.zeros_like(w, requires_grad=True)
+    (g,) = torch.autograd.grad(F.conv3d(x.float(), wr, padding=1), wr, dy.float())
+    assert rel_err(dw, g) < 5e-3
+    dx, _, _ = ops.conv3_fwd(nhwc(dy), None, pk.dgrad, None, None, None, C, 0, False)
+    xr = torch.zeros(N, C, D, H, W, device=DEV, requires_grad=True)
+    (gx,) = torch.autograd.grad(F.conv3d(xr, w.bfloat16().float(), padding=1), xr, dy.float())
+    assert rel_err(nchw(dx), gx) < 1e-2
