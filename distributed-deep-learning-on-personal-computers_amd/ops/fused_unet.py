@@ -257,7 +257,7 @@ class UNetEngine:
 
     # ------------------------------------------------------------------ weights
     def _params_version(self):
-        return sum(p.weight._version for p in self.packs)
+        return sum(p.conv.weight._version for p in self.packs)
 
     def pack_weights(self):
         key = tuple(p.conv.weight.data_ptr() for p in self.packs)
