@@ -14,27 +14,36 @@ def _cos(a, b):
 
 
 @pytest.mark.parametrize("depth,wd,tile,mode,dims", [
-    (5, 2, 64, "conv_transpose", 2), (4, 4, 64, "bilinear", 2), (3, 4, 32, "conv_transpose", 3)])
+    (5, 2, 128, "conv_transpose", 2), (4, 4, 64, "bilinear", 2), (3, 4, 32, "conv_transpose", 3)])
 def test_unet_engine_matches_torch(depth, wd, tile, mode, dims):
+    """HIP bf16 gradients must be as close to the fp32 oracle as stock PyTorch bf16 autocast."""
     from ddlpc.models import UNet
     torch.manual_seed(0)
     ref = UNet(out_classes=6, width_divisor=wd, depth=depth, up_sample_mode=mode, dims=dims).cuda()
+    amp = copy.deepcopy(ref)
     hip = copy.deepcopy(ref).to_hip()
-    N = 2
+    N = 4
     shape = (N, 3) + (tile,) * dims
     x = torch.rand(shape, device="cuda").bfloat16().float()
     y = torch.randint(0, 6, (N,) + (tile,) * dims, device="cuda")
     loss_r = F.cross_entropy(ref(x), y)
     loss_r.backward()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        loss_a = F.cross_entropy(amp(x).float(), y)
+    loss_a.backward()
     loss_h, correct = hip.loss_and_correct(x, y)
     loss_h.backward()
     assert abs(float(loss_h) - float(loss_r)) < 2e-2 * float(loss_r)
-    for (n, pr), (_, ph) in zip(ref.named_parameters(), hip.named_parameters()):
+    worst = []
+    for (n, pr), (_, pa), (_, ph) in zip(ref.named_parameters(), amp.named_parameters(),
+                                          hip.named_parameters()):
         if n.endswith(".bias") and "double_conv.double_conv" in n:
             assert float(ph.grad.abs().max()) == 0.0      # BN-cancelled conv bias
             continue
-        c = _cos(pr.grad, ph.grad)
-        assert c > 0.98, (n, c)
+        ch, ca = _cos(pr.grad, ph.grad), _cos(pr.grad, pa.grad)
+        worst.append((ch - ca, n, ch, ca))
+        assert ch > min(0.98, ca - 0.03), (n, ch, ca)
+    print("worst hip-vs-amp cosine deltas:", sorted(worst)[:4])
     # running statistics updated like nn.BatchNorm
     for (n, br), (_, bh) in zip(ref.named_buffers(), hip.named_buffers()):
         if "running" in n:
