@@ -152,7 +152,8 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
 // ------------------------------------------------------------------------ conv3 wgrad
 at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
                        const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& pscale,
-                       const c10::optional<at::Tensor>& pshift) {
+                       const c10::optional<at::Tensor>& pshift,
+                       const c10::optional<at::Tensor>& out) {
   CHECK_DEV(dy); CHECK_CONTIG(dy); CHECK_BF16(dy); CHECK_CONTIG(x1); CHECK_BF16(x1);
   c10::DeviceGuard guard(dy.device());
   const Geo g = geo_of(x1);
@@ -186,20 +187,27 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   a.coTiles = (a.Cout + bco - 1) / bco;
   a.ciChunks = (a.Cin + 31) / 32;
   a.planes = g.dims == 2 ? 1 : 3;
+  // split-K over pixel tiles: enough blocks to fill the chip, but every block keeps >= 8
+  // tiles so the fp32 partial slab stays small next to the MFMA work
   const int base = a.coTiles * a.ciChunks * a.planes;
-  const int target = 4 * num_cus();
+  const int target = 2 * num_cus();
   int splits = std::max(1, (target + base - 1) / base);
-  splits = std::min(splits, std::max(1, a.nTiles / 2));
+  splits = std::min(splits, std::max(1, a.nTiles / 8));
   a.splits = splits;
   auto part = at::empty({(int64_t)splits * a.Cout * a.taps * a.Cin}, dy.options().dtype(at::kFloat));
   a.partial = part.data_ptr<float>();
   conv3_wgrad_launch(a, bco, cur_stream());
   std::vector<int64_t> wshape = {a.Cout, a.Cin, 3, 3};
   if (g.dims == 3) wshape.push_back(3);
-  at::Tensor dW = at::empty(wshape, dy.options().dtype(at::kFloat));
-  conv3_wgrad_reduce_launch(a.partial, dW.data_ptr<float>(), a.Cout, a.taps, a.Cin, splits, false,
+  const bool into = out.has_value() && out->defined();
+  if (into) {
+    CHECK_F32(*out); CHECK_CONTIG(*out);
+    TORCH_CHECK(out->numel() == (int64_t)a.Cout * a.Cin * a.taps, "dW out size mismatch");
+  }
+  at::Tensor dW = into ? *out : at::empty(wshape, dy.options().dtype(at::kFloat));
+  conv3_wgrad_reduce_launch(a.partial, dW.data_ptr<float>(), a.Cout, a.taps, a.Cin, splits, into,
                             cur_stream());
-  return dW;
+  return into ? at::empty({0}, dy.options().dtype(at::kFloat)) : dW;
 }
 
 // ------------------------------------------------------------------------ BatchNorm
@@ -246,7 +254,9 @@ std::vector<at::Tensor> bn_relu_apply(const at::Tensor& y, const at::Tensor& sta
 std::vector<at::Tensor> bn_backward(const c10::optional<at::Tensor>& dA,
                                     const c10::optional<at::Tensor>& dP, const at::Tensor& y,
                                     const at::Tensor& stats4, const at::Tensor& gamma,
-                                    const c10::optional<at::Tensor>& gscale) {
+                                    const c10::optional<at::Tensor>& gscale,
+                                    const c10::optional<at::Tensor>& dgamma_out,
+                                    const c10::optional<at::Tensor>& dbeta_out) {
   CHECK_DEV(y); CHECK_CONTIG(y); CHECK_BF16(y);
   c10::DeviceGuard guard(y.device());
   const Geo g = geo_of(y);
@@ -269,12 +279,14 @@ std::vector<at::Tensor> bn_backward(const c10::optional<at::Tensor>& dA,
   const bf16_t* pP = hasP ? bptr(*dP) : nullptr;
   bn_bwd_reduce_launch(pA, pP, bptr(y), s + 2 * C, s + 3 * C, s, s + C, gs,
                        partial.data_ptr<float>(), nb, g.dims, g.N, g.D, g.H, g.W, C, cur_stream());
-  at::Tensor dgamma = at::empty({C}, fopts), dbeta = at::empty({C}, fopts);
+  const bool into = dgamma_out.has_value() && dgamma_out->defined();
+  at::Tensor dgamma = into ? *dgamma_out : at::empty({C}, fopts);
+  at::Tensor dbeta = into ? *dbeta_out : at::empty({C}, fopts);
   at::Tensor coefs = at::empty({3, C}, fopts);
   const double count = (double)g.N * g.D * g.H * g.W;
   bn_bwd_finalize_launch(partial.data_ptr<float>(), nb, C, count, gamma.data_ptr<float>(), s + C,
                          dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), coefs.data_ptr<float>(),
-                         cur_stream());
+                         into, cur_stream());
   at::Tensor dY = at::empty_like(y);
   bn_bwd_apply_launch(pA, pP, bptr(y), s + 2 * C, s + 3 * C, s, s + C, coefs.data_ptr<float>(), gs,
                       bptr_mut(dY), g.dims, g.N, g.D, g.H, g.W, C, cur_stream());
@@ -329,7 +341,9 @@ at::Tensor convt_dgrad(const at::Tensor& dout, const at::Tensor& wd, int64_t cin
   return dx;
 }
 
-std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout) {
+std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
+                                    const c10::optional<at::Tensor>& dw_out,
+                                    const c10::optional<at::Tensor>& db_out) {
   CHECK_DEV(x); CHECK_CONTIG(x); CHECK_CONTIG(dout);
   c10::DeviceGuard guard(x.device());
   const Geo g = geo_of(x);
@@ -354,16 +368,18 @@ std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout)
   gemm_launch(a, cur_stream());
   std::vector<int64_t> ws = {g.C, go.C, 2, 2};
   if (g.dims == 3) ws.push_back(2);
-  at::Tensor dW = at::empty(ws, fopts);
-  gemm_wgrad_reduce_launch(a.partial, dW.data_ptr<float>(), nullptr, g.C, go.C, S, splits,
+  const bool into = dw_out.has_value() && dw_out->defined();
+  at::Tensor dW = into ? *dw_out : at::empty(ws, fopts);
+  gemm_wgrad_reduce_launch(a.partial, dW.data_ptr<float>(), nullptr, g.C, go.C, S, splits, into,
                            cur_stream());
   // bias gradient: per-channel sum of dOut
   const long long P = (long long)go.N * go.D * go.H * go.W;
   const int nb = (int)std::max<long long>(1, std::min<long long>((P + 1023) / 1024, 1024));
   at::Tensor cpart = at::empty({nb, go.C}, fopts);
   channel_sum_launch(bptr(dout), P, go.C, cpart.data_ptr<float>(), nb, cur_stream());
-  at::Tensor db = at::empty({go.C}, fopts);
-  partial_sum_launch(cpart.data_ptr<float>(), nb, go.C, db.data_ptr<float>(), 1.f, false, cur_stream());
+  at::Tensor db = into ? *db_out : at::empty({go.C}, fopts);
+  partial_sum_launch(cpart.data_ptr<float>(), nb, go.C, db.data_ptr<float>(), 1.f, into, cur_stream());
+  if (into) return {at::empty({0}, fopts), at::empty({0}, fopts)};
   return {dW, db};
 }
 
@@ -389,7 +405,9 @@ at::Tensor head_ce_fwd(const at::Tensor& a, const at::Tensor& Wh, const at::Tens
 
 std::vector<at::Tensor> head_ce_bwd(const at::Tensor& a, const at::Tensor& Wh, const at::Tensor& bh,
                                     const at::Tensor& labels, const at::Tensor& out3,
-                                    const c10::optional<at::Tensor>& gscale, int64_t ignore_index) {
+                                    const c10::optional<at::Tensor>& gscale, int64_t ignore_index,
+                                    const c10::optional<at::Tensor>& dw_out,
+                                    const c10::optional<at::Tensor>& db_out) {
   CHECK_DEV(a); CHECK_CONTIG(a);
   c10::DeviceGuard guard(a.device());
   const int C = (int)a.size(-1), K = (int)Wh.size(0);
@@ -401,6 +419,17 @@ std::vector<at::Tensor> head_ce_bwd(const at::Tensor& a, const at::Tensor& Wh, c
   head_ce_bwd_launch(bptr(a), Wh.data_ptr<float>(), bh.data_ptr<float>(), labels.data_ptr<int64_t>(),
                      fptr_opt(gscale), out3.data_ptr<float>(), 0, bptr_mut(dA),
                      part.data_ptr<float>(), nb, P, C, K, (int)ignore_index, cur_stream());
+  const bool into = dw_out.has_value() && dw_out->defined();
+  if (into) {
+    // partial rows are [K*C | K]: reduce the two column ranges straight into the grads
+    TORCH_CHECK(dw_out->is_contiguous() && db_out->is_contiguous(), "grad outs must be contiguous");
+    at::Tensor pw = part.narrow(1, 0, K * C).contiguous();
+    at::Tensor pb = part.narrow(1, K * C, K).contiguous();
+    partial_sum_launch(pw.data_ptr<float>(), nb, K * C, dw_out->data_ptr<float>(), 1.f, true, cur_stream());
+    partial_sum_launch(pb.data_ptr<float>(), nb, K, db_out->data_ptr<float>(), 1.f, true, cur_stream());
+    at::Tensor none = at::empty({0}, fopts);
+    return {dA, none, none};
+  }
   at::Tensor red = at::empty({K * C + K}, fopts);
   partial_sum_launch(part.data_ptr<float>(), nb, K * C + K, red.data_ptr<float>(), 1.f, false,
                      cur_stream());
@@ -523,18 +552,18 @@ at::Tensor to_nhwc_bf16(const at::Tensor& x) {
 TORCH_LIBRARY(ddlpc, m) {
   m.def("conv3_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, Tensor? pscale, Tensor? pshift, "
         "int cout, int co1, bool stats) -> Tensor[]");
-  m.def("conv3_wgrad(Tensor dy, Tensor x1, Tensor? x2, Tensor? pscale, Tensor? pshift) -> Tensor");
+  m.def("conv3_wgrad(Tensor dy, Tensor x1, Tensor? x2, Tensor? pscale, Tensor? pshift, Tensor(a!)? out=None) -> Tensor");
   m.def("bn_finalize(Tensor partial, float count, Tensor gamma, Tensor beta, Tensor(a!) running_mean, "
         "Tensor(b!) running_var, float momentum, float eps, bool update_running, Tensor(c!)? nbt) -> Tensor");
   m.def("bn_relu_apply(Tensor y, Tensor stats4, bool pool) -> Tensor[]");
-  m.def("bn_backward(Tensor? dA, Tensor? dP, Tensor y, Tensor stats4, Tensor gamma, Tensor? gscale) "
-        "-> Tensor[]");
+  m.def("bn_backward(Tensor? dA, Tensor? dP, Tensor y, Tensor stats4, Tensor gamma, Tensor? gscale, "
+        "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None) -> Tensor[]");
   m.def("convt_fwd(Tensor x, Tensor wt, Tensor? bias, int cout) -> Tensor");
   m.def("convt_dgrad(Tensor dout, Tensor wd, int cin) -> Tensor");
-  m.def("convt_wgrad(Tensor x, Tensor dout) -> Tensor[]");
+  m.def("convt_wgrad(Tensor x, Tensor dout, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) -> Tensor[]");
   m.def("head_ce_fwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, int ignore_index) -> Tensor");
   m.def("head_ce_bwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, Tensor out3, Tensor? gscale, "
-        "int ignore_index) -> Tensor[]");
+        "int ignore_index, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) -> Tensor[]");
   m.def("head_logits(Tensor a, Tensor Wh, Tensor bh) -> Tensor");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float eps, "
         "float wd, float step_size, float inv_sqrt_bc2) -> ()");

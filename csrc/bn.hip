@@ -244,7 +244,7 @@ __global__ void bn_bwd_kernel(const bf16_t* __restrict__ dA, const bf16_t* __res
 __global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int P, int C,
                                        double count, const float* __restrict__ gamma,
                                        const float* __restrict__ invstd, float* dgamma,
-                                       float* dbeta, float* coefs) {
+                                       float* dbeta, float* coefs, int accumulate) {
   const int c = blockIdx.x;
   double s1 = 0.0, s2 = 0.0;
   for (int p = threadIdx.x; p < P; p += blockDim.x) {
@@ -259,8 +259,8 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int P,
   if (threadIdx.x == 0) {
     double t1 = 0, t2 = 0;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { t1 += r1[w]; t2 += r2[w]; }
-    dbeta[c] = (float)t1;
-    dgamma[c] = (float)t2;
+    dbeta[c] = accumulate ? dbeta[c] + (float)t1 : (float)t1;
+    dgamma[c] = accumulate ? dgamma[c] + (float)t2 : (float)t2;
     coefs[c] = gamma[c] * invstd[c];
     coefs[C + c] = (float)(t1 / count);
     coefs[2 * C + c] = (float)(t2 / count);
@@ -341,9 +341,9 @@ void bn_bwd_reduce_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y,
 
 void bn_bwd_finalize_launch(const float* partial, int P, int C, double count,
                             const float* gamma, const float* invstd, float* dgamma,
-                            float* dbeta, float* coefs, hipStream_t st) {
+                            float* dbeta, float* coefs, bool accumulate, hipStream_t st) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partial, P, C, count,
-                     gamma, invstd, dgamma, dbeta, coefs);
+                     gamma, invstd, dgamma, dbeta, coefs, accumulate ? 1 : 0);
 }
 
 void bn_bwd_apply_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y, const float* scale,

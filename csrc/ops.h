@@ -80,7 +80,7 @@ enum GemmMode {
 };
 void gemm_launch(GemmArgs& a, hipStream_t st);
 void gemm_wgrad_reduce_launch(const float* part, float* dW, float* db, int Cin, int Cout,
-                              int subs, int splits, hipStream_t st);
+                              int subs, int splits, bool accumulate, hipStream_t st);
 
 // ---------------------------------------------------------------- BatchNorm / ReLU / pool
 void bn_finalize_launch(const float* partial, int P, int C, double count, const float* gamma,
@@ -97,7 +97,7 @@ void bn_bwd_reduce_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y,
                           int dims, int N, int D, int H, int W, int C, hipStream_t st);
 void bn_bwd_finalize_launch(const float* partial, int P, int C, double count,
                             const float* gamma, const float* invstd, float* dgamma,
-                            float* dbeta, float* coefs, hipStream_t st);
+                            float* dbeta, float* coefs, bool accumulate, hipStream_t st);
 void bn_bwd_apply_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y, const float* scale,
                          const float* shift, const float* mean, const float* invstd,
                          const float* coefs, const float* gscale, bf16_t* dY, int dims, int N,

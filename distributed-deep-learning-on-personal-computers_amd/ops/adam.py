@@ -78,9 +78,15 @@ class FlatAdam(torch.optim.Optimizer):
             self.exp_avg_sq.mul_(b2).addcmul_(grad, grad, value=1.0 - b2)
             denom = (self.exp_avg_sq.sqrt() * inv_sqrt_bc2).add_(eps)
             P.addcdiv_(self.exp_avg, denom, value=-step_size)
-        for p in self.flat.params:
-            self.state[p]["step"].fill_(float(t))
         return loss
+
+    def _sync_steps(self):
+        for p in self.flat.params:
+            self.state[p]["step"].fill_(float(self.step_count))
+
+    def state_dict(self):
+        self._sync_steps()       # per-parameter step counters are refreshed lazily
+        return super().state_dict()
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)

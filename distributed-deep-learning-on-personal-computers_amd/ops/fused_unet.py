@@ -138,6 +138,7 @@ class _DoubleConvFn(torch.autograd.Function):
         F = _ops()
         x1, x2, y1, y2, s1, s2, g1, g2 = ctx.saved_tensors
         blk = ctx.blk
+        eng = blk.engine
         x2 = x2 if ctx.has_x2 else None
         if da2 is not None:
             da2 = da2.contiguous()
@@ -145,12 +146,28 @@ class _DoubleConvFn(torch.autograd.Function):
             dpool = dpool.contiguous()
         if da2 is None and dpool is None:
             return (None,) * 12
-        dy2, dg2, dbe2 = F.bn_backward(da2, dpool, y2, s2, g2, None)
-        dw2 = F.conv3_wgrad(dy2, y1, None, s1[2], s1[3])
+        bn1, bn2 = blk.bn1.bn, blk.bn2.bn
+        direct = eng.direct_grads
+        # ---- second conv: BN2 + ReLU (+ unpool + skip sum) backward, then its gradients
+        if direct:
+            dy2, _, _ = F.bn_backward(da2, dpool, y2, s2, g2, None, bn2.weight.grad, bn2.bias.grad)
+            F.conv3_wgrad(dy2, y1, None, s1[2], s1[3], blk.conv2.weight.grad)
+            eng.ready(bn2.weight, bn2.bias, blk.conv2.weight, blk.conv2.bias)
+            dg2 = dbe2 = dw2 = None
+        else:
+            dy2, dg2, dbe2 = F.bn_backward(da2, dpool, y2, s2, g2, None)
+            dw2 = F.conv3_wgrad(dy2, y1, None, s1[2], s1[3]).view_as(blk.conv2.weight)
         p1, p2 = blk.pack1, blk.pack2
         da1, _, _ = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False)
-        dy1, dg1, dbe1 = F.bn_backward(da1, None, y1, s1, g1, None)
-        dw1 = F.conv3_wgrad(dy1, x1, x2, None, None)
+        # ---- first conv
+        if direct:
+            dy1, _, _ = F.bn_backward(da1, None, y1, s1, g1, None, bn1.weight.grad, bn1.bias.grad)
+            F.conv3_wgrad(dy1, x1, x2, None, None, blk.conv1.weight.grad)
+            eng.ready(bn1.weight, bn1.bias, blk.conv1.weight, blk.conv1.bias)
+            dg1 = dbe1 = dw1 = None
+        else:
+            dy1, dg1, dbe1 = F.bn_backward(da1, None, y1, s1, g1, None)
+            dw1 = F.conv3_wgrad(dy1, x1, x2, None, None).view_as(blk.conv1.weight)
         dx1 = dx2 = None
         if ctx.needs_input_grad[0] or (x2 is not None and ctx.needs_input_grad[1]):
             c_x1 = x1.shape[-1]
@@ -158,18 +175,19 @@ class _DoubleConvFn(torch.autograd.Function):
             dx1, dx2, _ = F.conv3_fwd(dy1, None, p1.dgrad, None, None, None, p1.cin, co1, False)
             if x2 is None:
                 dx2 = None
-        zb1 = torch.zeros_like(dbe1) if ctx.needs_input_grad[3] else None
-        zb2 = torch.zeros_like(dbe2) if ctx.needs_input_grad[7] else None
-        return (dx1, dx2, dw1.view_as(blk.conv1.weight), zb1, dg1, dbe1,
-                dw2.view_as(blk.conv2.weight), zb2, dg2, dbe2, None, None)
+        # conv biases feeding a training-mode BN have an exactly-zero gradient
+        zb1 = torch.zeros_like(g1) if (not direct and ctx.needs_input_grad[3]) else None
+        zb2 = torch.zeros_like(g2) if (not direct and ctx.needs_input_grad[7]) else None
+        return (dx1, dx2, dw1, zb1, dg1, dbe1, dw2, zb2, dg2, dbe2, None, None)
 
 
 class _ConvTFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, pack: _ConvPack):
+    def forward(ctx, x, w, b, pack: _ConvPack, engine):
         out = _ops().convt_fwd(x, pack.fwd, b, pack.cout)
         ctx.save_for_backward(x)
         ctx.pack = pack
+        ctx.engine = engine
         return out
 
     @staticmethod
@@ -178,8 +196,13 @@ class _ConvTFn(torch.autograd.Function):
         (x,) = ctx.saved_tensors
         dout = dout.contiguous()
         dx = F.convt_dgrad(dout, ctx.pack.dgrad, ctx.pack.cin) if ctx.needs_input_grad[0] else None
+        conv = ctx.pack.conv
+        if ctx.engine.direct_grads:
+            F.convt_wgrad(x, dout, conv.weight.grad, conv.bias.grad)
+            ctx.engine.ready(conv.weight, conv.bias)
+            return dx, None, None, None, None
         dw, db = F.convt_wgrad(x, dout)
-        return dx, dw.view_as(ctx.pack.conv.weight), db, None
+        return dx, dw.view_as(conv.weight), db, None, None
 
 
 class _BilinearFn(torch.autograd.Function):
@@ -194,10 +217,11 @@ class _BilinearFn(torch.autograd.Function):
 
 class _HeadCEFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, wh, bh, labels, ignore_index: int):
+    def forward(ctx, a, wh, bh, labels, ignore_index: int, engine):
         out3 = _ops().head_ce_fwd(a, wh, bh, labels, ignore_index)
         ctx.save_for_backward(a, wh, bh, labels, out3)
         ctx.ignore_index = ignore_index
+        ctx.engine = engine
         loss = out3[0]
         correct = out3[1]
         ctx.mark_non_differentiable(correct)
@@ -207,14 +231,22 @@ class _HeadCEFn(torch.autograd.Function):
     def backward(ctx, dloss, dcorrect):
         a, wh, bh, labels, out3 = ctx.saved_tensors
         gs = dloss.reshape(1).float().contiguous() if dloss is not None else None
+        eng = ctx.engine
+        if eng.direct_grads:
+            head = eng.head
+            da, _, _ = _ops().head_ce_bwd(a, wh, bh, labels, out3, gs, ctx.ignore_index,
+                                          head.weight.grad, head.bias.grad)
+            eng.ready(head.weight, head.bias)
+            return da, None, None, None, None, None
         da, dw, db = _ops().head_ce_bwd(a, wh, bh, labels, out3, gs, ctx.ignore_index)
-        return da, dw, db, None, None
+        return da, dw, db, None, None, None
 
 
 class _Block:
     """Kernel-side view of one DoubleConv: packed weights + BN handles."""
 
-    def __init__(self, dc: nn.Module, first: bool):
+    def __init__(self, dc: nn.Module, first: bool, engine):
+        self.engine = engine
         seq = dc.double_conv
         self.conv1, self.conv2 = seq[0], seq[3]
         self.bn1, self.bn2 = _BNState(seq[1]), _BNState(seq[4])
@@ -237,14 +269,20 @@ class UNetEngine:
         dev = next(model.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("UNetEngine needs the model on the GPU")
-        self.enc = [_Block(b.double_conv, first=(i == 0))
+        # direct_grads: kernels accumulate straight into the (flat) .grad buffers and report
+        # readiness through ``grad_ready`` (the DP reducer's bucket trigger) instead of
+        # returning gradients for autograd to add.  Enabled by the Trainer once parameters
+        # are flattened.
+        self.direct_grads = False
+        self.grad_ready = None
+        self.enc = [_Block(b.double_conv, first=(i == 0), engine=self)
                     for i, b in enumerate(model.down_blocks())]
-        self.mid = _Block(model.double_conv, first=False)
+        self.mid = _Block(model.double_conv, first=False, engine=self)
         self.dec = []
         for ub in model.up_blocks():
             up = ub.up_sample
             pack = _ConvPack(up, 1, True) if isinstance(up, (nn.ConvTranspose2d, nn.ConvTranspose3d)) else None
-            self.dec.append((ub, pack, _Block(ub.double_conv, first=False)))
+            self.dec.append((ub, pack, _Block(ub.double_conv, first=False, engine=self)))
         head = model.conv_last
         self.head = head
         self.packs = [p for b in self.enc + [self.mid] for p in (b.pack1, b.pack2)]
@@ -254,6 +292,18 @@ class UNetEngine:
         self._entries_key = None
         self._version = None
         self.pack_weights()
+
+    def enable_direct_grads(self, grad_ready=None):
+        for p in self.model.parameters():
+            if p.grad is None or not p.grad.is_contiguous():
+                raise RuntimeError("direct grads need persistent contiguous .grad buffers")
+        self.direct_grads = True
+        self.grad_ready = grad_ready
+
+    def ready(self, *params):
+        if self.grad_ready is not None:
+            for p in params:
+                self.grad_ready(p)
 
     # ------------------------------------------------------------------ weights
     def _params_version(self):
@@ -295,7 +345,7 @@ class UNetEngine:
         h, _ = self.mid(h, None, False)
         for (ub, pack, blk), skip in zip(self.dec, reversed(skips)):
             if pack is not None:
-                up = _ConvTFn.apply(h, ub.up_sample.weight, ub.up_sample.bias, pack)
+                up = _ConvTFn.apply(h, ub.up_sample.weight, ub.up_sample.bias, pack, self)
             else:
                 up = _BilinearFn.apply(h)
             h, _ = blk(up, skip, False)
@@ -317,4 +367,4 @@ class UNetEngine:
     def loss_and_correct(self, x: torch.Tensor, y: torch.Tensor, ignore_index: int = -100):
         a = self.features(x)
         wh, bh = self._head_params()
-        return _HeadCEFn.apply(a, wh, bh, y.contiguous(), ignore_index)
+        return _HeadCEFn.apply(a, wh, bh, y.contiguous(), ignore_index, self)

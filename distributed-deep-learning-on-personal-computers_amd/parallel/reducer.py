@@ -121,6 +121,10 @@ class GradBucketReducer:
                 b.launched = False
                 b.payload = b.scales = b.gathered = None
 
+    def mark_ready(self, p):
+        """Readiness notification from kernels that write .grad directly (HIP engine)."""
+        self._on_grad_ready(p)
+
     def _on_grad_ready(self, p):
         if not self._sync or not self.overlap:
             return

@@ -79,6 +79,11 @@ class Trainer:
                                              reduce=cfg.reduce, grad_codec=cfg.grad_codec,
                                              codec_scale=cfg.codec_scale,
                                              overlap=cfg.overlap_comm)
+        if self.impl == "hip":
+            # kernels write gradients straight into the flat grad buffer and trigger the
+            # reducer's buckets themselves (no autograd accumulate pass)
+            model._engine.enable_direct_grads(
+                self.reducer.mark_ready if self.reducer is not None else None)
         self.autocast = (self.device.type == "cuda" and self.impl == "torch"
                          and cfg.dtype == "bf16")
         self.meter = DeviceMeter(self.device)

@@ -31,13 +31,16 @@ class DeviceMeter:
 
     def reset(self):
         self.buf = torch.zeros(4, dtype=torch.float64, device=self.device)
+        self._inc_pixels = None
+        self._inc = None
 
     def add(self, loss: torch.Tensor, correct: torch.Tensor, pixels: int):
-        # [sum loss, sum correct, sum pixels, micro-batches]
-        upd = torch.stack([loss.detach().double(), correct.detach().double(),
-                           torch.tensor(float(pixels), dtype=torch.float64, device=self.device),
-                           torch.ones((), dtype=torch.float64, device=self.device)])
-        self.buf += upd
+        # [sum loss, sum correct, sum pixels, micro-batches]; no host->device copies per step
+        if self._inc_pixels != pixels:
+            self._inc = torch.tensor([float(pixels), 1.0], dtype=torch.float64, device=self.device)
+            self._inc_pixels = pixels
+        self.buf[:2] += torch.stack([loss.detach().double(), correct.detach().double()])
+        self.buf[2:] += self._inc
 
     def reduce(self, group=None) -> Dict[str, float]:
         b = self.buf.clone()
