@@ -18,7 +18,8 @@ for r in rows[lo:hi]:
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     tot += d
     name = r["Kernel_Name"]
-    short = name.split("(")[0].replace("void ", "").replace("ddlpc::(anonymous namespace)::", "")
+    short = name.replace("void ", "").replace("ddlpc::(anonymous namespace)::", "")
+    short = short.split("(")[0] if not short.startswith("(") else short
     short = short[:60]
     agg[short] += d
     if len(sys.argv) > 3:

@@ -1,0 +1,85 @@
+"""Data loaders, sampler and config — CPU."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from ddlpc.config import ModelConfig, TrainConfig, add_config_args, config_from_args
+from ddlpc.data import ShardedSampler, SyntheticTiles, TileDataset, load_files, to_tensors
+
+
+def _write_dir(tmp_path, n=35, size=16):
+    from PIL import Image
+    rng = np.random.default_rng(0)
+    for i in range(n):
+        Image.fromarray(rng.integers(0, 255, (size, size, 3), dtype=np.uint8)).save(
+            tmp_path / f"tile_{i:03d}.png")
+        np.save(tmp_path / f"tile_{i:03d}_label.npy", rng.integers(0, 6, (size, size)))
+    return tmp_path
+
+
+def test_load_files_reference_convention(tmp_path):
+    d = _write_dir(tmp_path)
+    xtr, ytr, xte, yte = load_files(str(d))
+    assert xtr.shape == (5, 16, 16, 3) and xte.shape == (30, 16, 16, 3)   # last 30 held out
+    assert ytr.dtype == np.uint8 and yte.shape == (30, 16, 16)
+    x, y = to_tensors(xtr, ytr)
+    assert x.shape == (5, 3, 16, 16) and x.dtype == torch.float32 and float(x.max()) <= 1.0
+    assert y.dtype == torch.int64
+    # NCHW transpose is the reference's swapaxes(1,3).swapaxes(2,3) (ref.py:737)
+    ref = torch.from_numpy(xtr.astype("float32") / 255).swapaxes(1, 3).swapaxes(2, 3)
+    assert torch.allclose(x, ref)
+    tr, te = TileDataset.from_dir(str(d))
+    assert len(tr) == 5 and len(te) == 30
+
+
+def test_synthetic_deterministic_and_learnable_shape():
+    ds = SyntheticTiles(10, 32, classes=6, seed=3)
+    x1, y1 = ds.get([2, 5])
+    x2, y2 = ds.get([2, 5])
+    assert torch.equal(x1, x2) and torch.equal(y1, y2)
+    assert x1.shape == (2, 3, 32, 32) and y1.shape == (2, 32, 32)
+    assert int(y1.max()) < 6
+    x3, y3 = SyntheticTiles(4, 8, classes=2, dims=3).get([0])
+    assert x3.shape == (1, 3, 8, 8, 8) and y3.shape == (1, 8, 8, 8)
+
+
+def test_sharded_sampler_disjoint_and_replicated():
+    parts = [ShardedSampler(20, r, 4, shard=True, seed=1).indices() for r in range(4)]
+    flat = sorted(i for p in parts for i in p)
+    assert flat == list(range(20))
+    rep = [ShardedSampler(20, r, 4, shard=False, shuffle=False).indices() for r in range(4)]
+    assert all(r == list(range(20)) for r in rep)      # reference replicated mode
+    s = ShardedSampler(20, 0, 2, seed=1)
+    e0 = s.indices()
+    s.set_epoch(1)
+    assert s.indices() != e0
+
+
+def test_config_roundtrip_and_cli(tmp_path):
+    cfg = TrainConfig(model=ModelConfig(depth=4, width_divisor=4), tile=128, accum_steps=50)
+    d = cfg.to_dict()
+    cfg2 = TrainConfig.from_dict(json.loads(json.dumps(d)))
+    assert cfg2.to_dict() == d
+    p = tmp_path / "c.json"
+    cfg.save(str(p))
+    import argparse
+    ap = add_config_args(argparse.ArgumentParser())
+    args = ap.parse_args(["--config", str(p), "--lr", "0.01", "--depth", "5",
+                          "--grad-codec", "int8_absmax", "--shard-data", "false"])
+    c3 = config_from_args(args)
+    assert c3.lr == 0.01 and c3.model.depth == 5 and c3.accum_steps == 50
+    assert c3.grad_codec == "int8_absmax" and c3.shard_data is False
+    with pytest.raises(ValueError):
+        TrainConfig(grad_codec="zip").validate()
+    with pytest.raises(ValueError):
+        TrainConfig.from_dict({"bogus": 1})
+
+
+def test_yaml_config(tmp_path):
+    p = tmp_path / "c.yaml"
+    p.write_text("model:\n  depth: 4\n  out_classes: 2\ntile: 128\nbatch_per_gpu: 2\n")
+    c = TrainConfig.load(str(p))
+    assert c.model.depth == 4 and c.tile == 128 and c.batch_per_gpu == 2
