@@ -53,27 +53,22 @@ std::vector<int64_t> shape_with_c(const Geo& g, int C, int scale = 1) {
 int pow2ceil(int v) { int p = 1; while (p < v) p <<= 1; return p; }
 
 // pixel tile for the 3x3 conv kernels: BM pixels as TD x TH x TW
-void conv_tile(int dims, int BM, int D, int H, int W, int& TD, int& TH, int& TW) {
+void conv_tile(int dims, int BM, int W, int& TD, int& TH, int& TW) {
   if (dims == 2) {
     TD = 1;
-    TW = std::max(8, std::min(16, pow2ceil(W)));
-    if (BM == 256 && W >= 32 && H < 16) TW = 32;
+    TW = W >= 16 ? 16 : 8;
     TH = BM / TW;
   } else {
-    TW = W <= 8 ? 8 : 16;
+    TW = W >= 16 ? 16 : 8;
     TH = 4;
     TD = BM / (TW * TH);
   }
-  (void)D; (void)H;
 }
 
 int pick_bn(int Cout) {
   if (Cout <= 32) return 32;
   if (Cout <= 64) return 64;
-  // minimise padding waste, prefer larger tiles
-  const int w128 = ((Cout + 127) / 128) * 128 - Cout;
-  const int w64 = ((Cout + 63) / 64) * 64 - Cout;
-  return w128 <= w64 ? 128 : 64;
+  return 128;
 }
 
 int num_cus() {
@@ -124,17 +119,25 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   a.pshift = fptr_opt(pshift);
   a.Wt = bptr(w);
   a.bias = fptr_opt(bias);
-  const int bn = pick_bn(a.Cout);
-  const int BM = conv3_fwd_bm(bn);
-  conv_tile(g.dims, BM, g.D, g.H, g.W, a.TD, a.TH, a.TW);
-  TORCH_CHECK(a.TD * a.TH * a.TW == BM, "internal tile error");
-  TORCH_CHECK((a.TD + (g.dims == 3 ? 2 : 0)) * (a.TH + 2) * (a.TW + 2) <= conv3_halo_cap(g.dims),
+  TORCH_CHECK(a.C2 == 0 || a.C1 % 32 == 0, "concat: first input needs C1 % 32 == 0");
+  TORCH_CHECK((a.C1 % 8 == 0) && (a.C2 % 8 == 0), "input channels must be multiples of 8 "
+              "(the engine pads the 3-channel image to 8)");
+  // tile configuration: channel tile from Cout, pixel tile from the image size; the
+  // 128-channel config drops to a 64-pixel tile when the layer would not fill the chip
+  int cfg = a.Cout <= 32 ? 0 : a.Cout <= 64 ? 1 : 2;
+  auto plan = [&](int c) {
+    const int BM = conv3_fwd_cfg_bm(c);
+    conv_tile(g.dims, BM, g.W, a.TD, a.TH, a.TW);
+    a.tilesD = (g.D + a.TD - 1) / a.TD;
+    a.tilesH = (g.H + a.TH - 1) / a.TH;
+    a.tilesW = (g.W + a.TW - 1) / a.TW;
+    a.nTilesM = g.N * a.tilesD * a.tilesH * a.tilesW;
+    a.nTilesN = (a.Cout + conv3_fwd_cfg_bn(c) - 1) / conv3_fwd_cfg_bn(c);
+  };
+  plan(cfg);
+  if (cfg == 2 && a.nTilesM * a.nTilesN < 2 * num_cus()) { cfg = 3; plan(cfg); }
+  TORCH_CHECK((g.dims == 3 ? a.TD + 2 : 1) * (a.TH + 2) * (a.TW + 2) <= conv3_fwd_cfg_halo(g.dims, cfg),
               "halo exceeds LDS capacity");
-  a.tilesD = (g.D + a.TD - 1) / a.TD;
-  a.tilesH = (g.H + a.TH - 1) / a.TH;
-  a.tilesW = (g.W + a.TW - 1) / a.TW;
-  a.nTilesM = g.N * a.tilesD * a.tilesH * a.tilesW;
-  a.nTilesN = (a.Cout + bn - 1) / bn;
   auto opts = x1.options();
   at::Tensor y1 = at::empty(shape_with_c(g, a.Co1), opts);
   at::Tensor y2;
@@ -144,7 +147,7 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   a.Y1 = bptr_mut(y1);
   a.Y2 = y2.defined() ? bptr_mut(y2) : nullptr;
   a.stats = want_stats ? stats.data_ptr<float>() : nullptr;
-  conv3_fwd_launch(a, bn, cur_stream());
+  conv3_fwd_launch(a, cfg, cur_stream());
   at::Tensor none = at::empty({0}, opts);
   return {y1, y2.defined() ? y2 : none, stats.defined() ? stats : none};
 }
@@ -529,19 +532,29 @@ at::Tensor bilinear_up2_bwd(const at::Tensor& dy) {
   return dx;
 }
 
-// NCHW / NCDHW (fp32 or bf16) -> channel-last bf16 [N, (D,) H, W, C]
-at::Tensor to_nhwc_bf16(const at::Tensor& x) {
-  CHECK_DEV(x); CHECK_CONTIG(x);
+// NCHW / NCDHW tensor (fp32 or bf16; contiguous or channels_last memory) -> channel-last bf16
+// [N, (D,) H, W, Cp] with channels zero-padded to a multiple of `cpad`
+at::Tensor to_nhwc_bf16(const at::Tensor& x, int64_t cpad) {
+  CHECK_DEV(x);
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "fp32/bf16 input");
   c10::DeviceGuard guard(x.device());
   const int N = (int)x.size(0), C = (int)x.size(1);
+  const int Cp = (int)((C + cpad - 1) / cpad * cpad);
   const long long S = x.numel() / ((long long)N * C);
+  // supported memory layouts: NCHW-contiguous or channel-last-contiguous
+  long long sC, sS;
+  if (x.is_contiguous()) { sC = S; sS = 1; }
+  else {
+    const auto cl = x.dim() == 4 ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::ChannelsLast3d;
+    TORCH_CHECK(x.is_contiguous(cl), "input must be contiguous or channels-last");
+    sC = 1; sS = C;
+  }
   std::vector<int64_t> shape = {N};
   for (int i = 2; i < x.dim(); ++i) shape.push_back(x.size(i));
-  shape.push_back(C);
+  shape.push_back(Cp);
   at::Tensor y = at::empty(shape, x.options().dtype(at::kBFloat16));
-  nchw_to_nhwc_bf16_launch(x.data_ptr(), x.scalar_type() == at::kFloat ? 0 : 1, bptr_mut(y), N, C,
-                           S, cur_stream());
+  to_nhwc_pad_launch(x.data_ptr(), x.scalar_type() == at::kFloat ? 0 : 1, bptr_mut(y), N, C, Cp, S,
+                     x.stride(0), sC, sS, cur_stream());
   return y;
 }
 
@@ -573,7 +586,7 @@ TORCH_LIBRARY(ddlpc, m) {
   m.def("codec_decode_sum(Tensor(a!) out, Tensor q, Tensor scales, Tensor w, Tensor seg, int codec) -> ()");
   m.def("bilinear_up2(Tensor x) -> Tensor");
   m.def("bilinear_up2_bwd(Tensor dy) -> Tensor");
-  m.def("to_nhwc_bf16(Tensor x) -> Tensor");
+  m.def("to_nhwc_bf16(Tensor x, int cpad=1) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {

@@ -218,18 +218,24 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16_t* __restri
     y[i] = f2bf(x[i]);
 }
 
-// [N][C][S] (fp32 or bf16) -> [N][S][C] bf16
-__global__ void nchw_to_nhwc_kernel(const void* __restrict__ x, int in_dtype, bf16_t* __restrict__ y,
-                                    int N, int C, long long S) {
-  const long long total = (long long)N * C * S;
+// strided [N][C][S] (fp32 or bf16; NCHW or channels-last memory) -> [N][S][Cp] bf16 with the
+// channels zero-padded to Cp (the first conv reads 8-channel, 16-byte pixels)
+__global__ void to_nhwc_pad_kernel(const void* __restrict__ x, int in_dtype, bf16_t* __restrict__ y,
+                                   int N, int C, int Cp, long long S, long long sN, long long sC,
+                                   long long sS) {
+  const long long total = (long long)N * Cp * S;
   for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < total;
        o += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(o % C);
-    const long long s = (o / C) % S;
-    const long long n = o / ((long long)C * S);
-    const long long i = (n * C + c) * S + s;
-    y[o] = in_dtype == 0 ? f2bf(reinterpret_cast<const float*>(x)[i])
-                         : reinterpret_cast<const bf16_t*>(x)[i];
+    const int c = (int)(o % Cp);
+    const long long s = (o / Cp) % S;
+    const long long n = o / ((long long)Cp * S);
+    bf16_t v = 0;
+    if (c < C) {
+      const long long i = n * sN + c * sC + s * sS;
+      v = in_dtype == 0 ? f2bf(reinterpret_cast<const float*>(x)[i])
+                        : reinterpret_cast<const bf16_t*>(x)[i];
+    }
+    y[o] = v;
   }
 }
 
@@ -323,11 +329,12 @@ void bilinear_up2_bwd_launch(const bf16_t* dy, float* dx_f32, bf16_t* dx, int di
   hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(g2), dim3(256), 0, st, dx_f32, dx, nin);
 }
 
-void nchw_to_nhwc_bf16_launch(const void* x, int in_dtype, bf16_t* y, int N, int C, long long S,
-                              hipStream_t st) {
-  const long long total = (long long)N * C * S;
+void to_nhwc_pad_launch(const void* x, int in_dtype, bf16_t* y, int N, int C, int Cp, long long S,
+                        long long sN, long long sC, long long sS, hipStream_t st) {
+  const long long total = (long long)N * Cp * S;
   const int grid = (int)std::min<long long>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid), dim3(256), 0, st, x, in_dtype, y, N, C, S);
+  hipLaunchKernelGGL(to_nhwc_pad_kernel, dim3(grid), dim3(256), 0, st, x, in_dtype, y, N, C, Cp, S,
+                     sN, sC, sS);
 }
 
 void channel_sum_launch(const bf16_t* x, long long P, int C, float* partial, int nblocks,

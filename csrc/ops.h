@@ -30,9 +30,10 @@ struct ConvFwdArgs {
   int tilesD, tilesH, tilesW;
   int nTilesM, nTilesN;
 };
-void conv3_fwd_launch(ConvFwdArgs& a, int bn, hipStream_t st);
-int conv3_fwd_bm(int bn);
-int conv3_halo_cap(int dims);
+void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st);
+int conv3_fwd_cfg_bn(int cfg);
+int conv3_fwd_cfg_bm(int cfg);
+int conv3_fwd_cfg_halo(int dims, int cfg);
 
 // ---------------------------------------------------------------- conv 3x3 wgrad
 struct ConvWgradArgs {
@@ -147,7 +148,7 @@ void bilinear_up2_bwd_launch(const bf16_t* dy, float* dx_f32, bf16_t* dx, int di
                              int H, int W, int C, hipStream_t st);
 void channel_sum_launch(const bf16_t* x, long long P, int C, float* partial, int nblocks,
                         hipStream_t st);
-void nchw_to_nhwc_bf16_launch(const void* x, int in_dtype, bf16_t* y, int N, int C,
-                              long long S, hipStream_t st);
+void to_nhwc_pad_launch(const void* x, int in_dtype, bf16_t* y, int N, int C, int Cp, long long S,
+                        long long sN, long long sC, long long sS, hipStream_t st);
 
 }  // namespace ddlpc

@@ -160,14 +160,20 @@ class _DoubleConvFn(torch.autograd.Function):
         p1, p2 = blk.pack1, blk.pack2
         da1, _, _ = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False)
         # ---- first conv
+        w1 = blk.conv1.weight
+        padded_in = x2 is None and x1.shape[-1] != w1.shape[1]   # first layer: 3 -> 8 ch
         if direct:
             dy1, _, _ = F.bn_backward(da1, None, y1, s1, g1, None, bn1.weight.grad, bn1.bias.grad)
-            F.conv3_wgrad(dy1, x1, x2, None, None, blk.conv1.weight.grad)
-            eng.ready(bn1.weight, bn1.bias, blk.conv1.weight, blk.conv1.bias)
+            if padded_in:
+                w1.grad.add_(F.conv3_wgrad(dy1, x1, None, None, None)[:, :w1.shape[1]])
+            else:
+                F.conv3_wgrad(dy1, x1, x2, None, None, w1.grad)
+            eng.ready(bn1.weight, bn1.bias, w1, blk.conv1.bias)
             dg1 = dbe1 = dw1 = None
         else:
             dy1, dg1, dbe1 = F.bn_backward(da1, None, y1, s1, g1, None)
-            dw1 = F.conv3_wgrad(dy1, x1, x2, None, None).view_as(blk.conv1.weight)
+            dw1 = F.conv3_wgrad(dy1, x1, x2, None, None)
+            dw1 = (dw1[:, :w1.shape[1]] if padded_in else dw1).reshape(w1.shape)
         dx1 = dx2 = None
         if ctx.needs_input_grad[0] or (x2 is not None and ctx.needs_input_grad[1]):
             c_x1 = x1.shape[-1]
@@ -326,12 +332,15 @@ class UNetEngine:
 
     # ------------------------------------------------------------------ layout
     def to_nhwc(self, x: torch.Tensor) -> torch.Tensor:
+        """NCHW-shaped input -> channel-last bf16 with channels padded to 8 (16-byte pixels
+        for the first conv's LDS-DMA).  bf16 channels_last input with C % 8 == 0 is used
+        zero-copy."""
         nd = x.dim()
         perm = (0,) + tuple(range(2, nd)) + (1,)
         xt = x.permute(*perm)
-        if xt.is_contiguous() and xt.dtype == torch.bfloat16:
-            return xt                                  # channels_last bf16 input: zero copy
-        return _ops().to_nhwc_bf16(x.contiguous())
+        if xt.is_contiguous() and xt.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
+            return xt
+        return _ops().to_nhwc_bf16(x, 8)
 
     # ------------------------------------------------------------------ graph
     def features(self, x: torch.Tensor) -> torch.Tensor:

@@ -56,7 +56,8 @@ def test_conv3_fwd(ops, N, H, W, C1, C2, Cout):
     w = torch.randn(Cout, C1 + C2, 3, 3, device=DEV) * (1.0 / math.sqrt(9 * (C1 + C2)))
     b = torch.randn(Cout, device=DEV) * 0.1
     pk = pack_conv(ops, w)
-    y, _, st = ops.conv3_fwd(nhwc(x1), nhwc(x2) if x2 is not None else None, pk.fwd, b, None,
+    xin1 = ops.to_nhwc_bf16(x1, 8) if C1 % 8 else nhwc(x1)     # first layer: 3 -> 8 channels
+    y, _, st = ops.conv3_fwd(xin1, nhwc(x2) if x2 is not None else None, pk.fwd, b, None,
                              None, Cout, 0, True)
     xin = torch.cat([x1, x2], 1) if x2 is not None else x1
     ref = F.conv2d(xin.float(), w.bfloat16().float(), b, padding=1)
@@ -117,7 +118,9 @@ def test_conv3_wgrad(ops, N, H, W, C1, C2, Cout, pro):
         shift = torch.randn(C1, device=DEV) * 0.5
         a1 = torch.relu(x1.float() * scale[None, :, None, None] + shift[None, :, None, None]).bfloat16().float()
     xin = torch.cat([a1, x2.float()], 1) if x2 is not None else a1
-    dw = ops.conv3_wgrad(nhwc(dy), nhwc(x1), nhwc(x2) if x2 is not None else None, scale, shift)
+    xin1 = ops.to_nhwc_bf16(x1, 8) if C1 % 8 else nhwc(x1)
+    dw = ops.conv3_wgrad(nhwc(dy), xin1, nhwc(x2) if x2 is not None else None, scale, shift)
+    dw = dw[:, :C1 + C2]
     w = torch.zeros(Cout, C1 + C2, 3, 3, device=DEV, requires_grad=True)
     out = F.conv2d(xin, w, padding=1)
     (g,) = torch.autograd.grad(out, w, dy.float())
@@ -245,6 +248,15 @@ def test_codec_matches_oracle(codec):
     ref = torch.zeros_like(g).cpu()
     codec_ops.decode_sum_segments(ref, [qc, qc], [sc, sc], segs, codec, [0.25, 0.75])
     assert torch.allclose(out.cpu(), ref, rtol=1e-6, atol=1e-12)
+
+
+def test_to_nhwc_pad(ops):
+    x = torch.randn(2, 3, 8, 8, device=DEV)
+    y = ops.to_nhwc_bf16(x, 8)
+    assert y.shape == (2, 8, 8, 8)
+    assert torch.equal(y[..., :3], nhwc(x).bfloat16()) and not y[..., 3:].any()
+    xc = x.bfloat16().to(memory_format=torch.channels_last)
+    assert torch.equal(ops.to_nhwc_bf16(xc, 8), y)
 
 
 def test_bilinear(ops):
