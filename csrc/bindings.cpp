@@ -143,7 +143,9 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   at::Tensor y2;
   if (a.Co1 < a.Cout) y2 = at::empty(shape_with_c(g, a.Cout - a.Co1), opts);
   at::Tensor stats;
-  if (want_stats) stats = at::empty({a.nTilesM, 2, a.Cout}, opts.dtype(at::kFloat));
+  if (want_stats)
+    stats = at::empty({(int64_t)a.nTilesM * conv3_fwd_cfg_wm(cfg), 2, a.Cout}, opts.dtype(at::kFloat));
+  a.persist_blocks = 2 * num_cus();
   a.Y1 = bptr_mut(y1);
   a.Y2 = y2.defined() ? bptr_mut(y2) : nullptr;
   a.stats = want_stats ? stats.data_ptr<float>() : nullptr;

@@ -74,11 +74,18 @@ struct Cfg {
   static constexpr int B_ITERS = (3 * BN * 4 + 255) / 256;      // DMA instrs / wave / stage
   static constexpr int B_BYTES = B_ITERS * 4 * 1024;            // one weight buffer
   static constexpr int SS_BYTES = 2 * 512 * 4;                  // prologue scale/shift
-  static constexpr int MAIN = 2 * A_BYTES + 2 * B_BYTES;
-  static constexpr int OUT = BM * BN * 2 + 2 * 256 * 4;         // epilogue tile + stats
-  static constexpr int SMEM = SS_BYTES + (MAIN > OUT ? MAIN : OUT);
+  static constexpr int SMEM = SS_BYTES + 2 * A_BYTES + 2 * B_BYTES;
 };
 
+// Persistent workgroups walk (m tile, n tile) items; the stage stream runs across item
+// boundaries, so the next item's first halo and weights are in flight while the current
+// item finishes (and no LDS is needed by the epilogue: results leave straight from the
+// accumulators).
+//
+// Operand roles: the MFMA A operand is the weight tile (rows = output channels) and the B
+// operand the pixel tile, so each lane's accumulator holds 4 CONSECUTIVE channels of one
+// pixel -> 8-byte bf16x4 stores; BN statistics are reduced with 4 lane shuffles and
+// written as one partial row per (m tile, wave row).
 template <int DIMS, int WM, int WN, int MT, int NT, int HALO>
 __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO>;
@@ -97,65 +104,65 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN;
   const int wn = wave % WN;
-
-  // ---- block -> (m tile, n tile); the n tiles of one m tile share an XCD (halo reuse)
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int ntile = bid % p.nTilesN;
-  int mt_id = bid / p.nTilesN;
-  const int mtile = mt_id;
-  const int tw_i = mt_id % p.tilesW; mt_id /= p.tilesW;
-  const int th_i = mt_id % p.tilesH; mt_id /= p.tilesH;
-  const int td_i = mt_id % p.tilesD; mt_id /= p.tilesD;
-  const int n_img = mt_id;
-  const int d0 = td_i * p.TD, h0 = th_i * p.TH, w0 = tw_i * p.TW;
-  const int co0 = ntile * BN;
   const int HW2 = p.TW + 2, HH2 = p.TH + 2;
   const int halo = (DIMS == 3 ? p.TD + 2 : 1) * HH2 * HW2;
+  const long long img_px = (long long)p.D * p.H * p.W;
+  const int n_items = p.nTilesM * p.nTilesN;
+  const int my_items = n_items > (int)blockIdx.x ? (n_items - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int nchunks = (p.Cin + BK - 1) / BK;
+  const int spi = nchunks * NG;                   // stages per item
+  const int S = my_items * spi;
 
   const bool has_pro = p.pscale != nullptr;
   if (has_pro)
     for (int c = tid; c < p.C1; c += 256) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
 
-  // ---- buffer descriptors (per image: 32-bit offsets for any batch size)
-  const long long img_px = (long long)p.D * p.H * p.W;
-  const unsigned x1_bytes = (unsigned)(img_px * p.C1 * 2);
-  const unsigned x2_bytes = (unsigned)(img_px * p.C2 * 2);
-  const auto rX1 = make_rsrc(p.X1 + n_img * img_px * p.C1, x1_bytes);
-  const auto rX2 = make_rsrc(p.C2 > 0 ? p.X2 + n_img * img_px * p.C2 : p.X1, x2_bytes);
   const auto rW = make_rsrc(p.Wt, (unsigned)((long long)p.Cout * p.taps * p.CinW * 2));
 
-  // ---- per-lane DMA geometry (constant over chunks): halo pixel -> source pixel offset
-  int a_pix[C::A_ITERS];   // pixel index within the image, -1 if padding / outside
-  int a_sub[C::A_ITERS];   // source 8-channel sub-chunk (swizzle applied)
-#pragma unroll
-  for (int i = 0; i < C::A_ITERS; ++i) {
-    const int e = (i * 4 + wave) * 64 + lane;
+  struct Item { int mtile, n_img, d0, h0, w0, co0; };
+  auto item_of = [&](int k) {
+    Item it;
+    const int w = (int)blockIdx.x + k * (int)gridDim.x;
+    const int ntile = w % p.nTilesN;
+    int m = w / p.nTilesN;
+    it.mtile = m;
+    const int tw_i = m % p.tilesW; m /= p.tilesW;
+    const int th_i = m % p.tilesH; m /= p.tilesH;
+    const int td_i = m % p.tilesD; m /= p.tilesD;
+    it.n_img = m;
+    it.d0 = td_i * p.TD; it.h0 = th_i * p.TH; it.w0 = tw_i * p.TW;
+    it.co0 = ntile * BN;
+    return it;
+  };
+  // halo element e (16 B) of this lane -> in-image pixel index or -1
+  auto halo_pix = [&](const Item& it, int e) {
     const int px = e >> 2;
-    a_sub[i] = (e & 3) ^ swz(px);
-    a_pix[i] = -1;
-    if (px < halo) {
-      const int hw = px % HW2, hh = (px / HW2) % HH2;
-      const int hd = DIMS == 3 ? px / (HW2 * HH2) : 1;
-      const int gw = w0 + hw - 1, gh = h0 + hh - 1, gd = d0 + hd - 1;
-      if (gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && gd >= 0 && gd < p.D)
-        a_pix[i] = (gd * p.H + gh) * p.W + gw;
-    }
-  }
-  auto issue_A = [&](int chunk, int buf) {
+    if (px >= halo) return -1;
+    const int hw = px % HW2, hh = (px / HW2) % HH2;
+    const int hd = DIMS == 3 ? px / (HW2 * HH2) : 1;
+    const int gw = it.w0 + hw - 1, gh = it.h0 + hh - 1, gd = it.d0 + hd - 1;
+    if (gw < 0 || gw >= p.W || gh < 0 || gh >= p.H || gd < 0 || gd >= p.D) return -1;
+    return (gd * p.H + gh) * p.W + gw;
+  };
+  auto issue_A = [&](int k, int chunk, int buf) {
+    const Item it = item_of(k);
     const int cbase = chunk * BK;
     const bool second = cbase >= p.C1;              // chunk served by X2 (C1 % 32 == 0)
-    const auto r = second ? rX2 : rX1;
     const int Cs = second ? p.C2 : p.C1;
     const int c0 = second ? cbase - p.C1 : cbase;
+    const bf16_t* src = second ? p.X2 : p.X1;
+    const auto r = make_rsrc(src + it.n_img * img_px * Cs, (unsigned)(img_px * Cs * 2));
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
-      const int c8 = c0 + a_sub[i] * 8;
-      const unsigned off = (a_pix[i] >= 0 && c8 < Cs) ? (unsigned)(a_pix[i] * Cs + c8) * 2u : kOOB;
+      const int e = (i * 4 + wave) * 64 + lane;
+      const int pix = halo_pix(it, e);
+      const int c8 = c0 + (((e & 3) ^ swz(e >> 2)) << 3);
+      const unsigned off = (pix >= 0 && c8 < Cs) ? (unsigned)(pix * Cs + c8) * 2u : kOOB;
       dma16(r, sA(buf) + (i * 4 + wave) * 1024, off);
     }
   };
-  auto issue_B = [&](int stage, int buf) {
-    const int chunk = stage / NG, grp = stage % NG;
+  auto issue_B = [&](int k, int chunk, int grp, int buf) {
+    const int co0 = item_of(k).co0;
 #pragma unroll
     for (int i = 0; i < C::B_ITERS; ++i) {
       const int e = (i * 4 + wave) * 64 + lane;
@@ -171,14 +178,15 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
     }
   };
   // prologue BN+ReLU applied in LDS on the landed halo (padding stays zero)
-  auto transform_A = [&](int chunk, int buf) {
+  auto transform_A = [&](int k, int chunk, int buf) {
     const int cbase = chunk * BK;
     if (cbase >= p.C1) return;                      // X2 channels: no prologue
+    const Item it = item_of(k);
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
       const int e = (i * 4 + wave) * 64 + lane;    // same element this lane DMA'd
-      const int c8 = cbase + a_sub[i] * 8;
-      if (a_pix[i] >= 0 && c8 < p.C1) {
+      const int c8 = cbase + (((e & 3) ^ swz(e >> 2)) << 3);
+      if (c8 < p.C1 && halo_pix(it, e) >= 0) {
         uint4* q = reinterpret_cast<uint4*>(sA(buf) + e * 16);
         float f[8];
         unpack8(*q, f);
@@ -189,7 +197,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
     }
   };
 
-  // ---- per-lane fragment geometry
+  // ---- per-lane fragment geometry (item independent)
   const int g = lane >> 4;
   int hp0[MT];
 #pragma unroll
@@ -207,112 +215,114 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int nchunks = (p.Cin + BK - 1) / BK;
-  const int S = nchunks * NG;
-
-  issue_A(0, 0);
-  issue_B(0, 0);
+  if (S > 0) {
+    issue_A(0, 0, 0);
+    issue_B(0, 0, 0, 0);
+  }
   for (int s = 0; s < S; ++s) {
-    const int chunk = s / NG, grp = s % NG;
-    // stage s operands: B(s) (issued during s-1) and, at grp 0, A(chunk).  At grp 1 the
-    // next chunk's halo (issued after B(s) during s-1... see issue order below) may stay
-    // in flight.
-    if (grp == 1 && chunk + 1 < nchunks) dma_wait<C::A_ITERS>();
+    const int k = s / spi, rem = s % spi;
+    const int chunk = rem / NG, grp = rem % NG;
+    const int cseq = k * nchunks + chunk;           // global chunk sequence -> A buffer
+    const bool more_chunks = cseq + 1 < my_items * nchunks;
+    // stage s needs B(s) (issued during s-1) and, at grp 0, A(cseq).  At grp 1 the next
+    // chunk's halo (issued after B(s) during s-1) may stay in flight.
+    if (NG > 1 && grp == 1 && more_chunks) dma_wait<C::A_ITERS>();
     else dma_wait<0>();
     lds_sync();
     if (grp == 0 && has_pro) {
-      transform_A(chunk, chunk & 1);
+      transform_A(k, chunk, cseq & 1);
       lds_sync();
     }
-    if (s + 1 < S) issue_B(s + 1, (s + 1) & 1);
-    if (grp == 0 && chunk + 1 < nchunks) issue_A(chunk + 1, (chunk + 1) & 1);
+    if (s + 1 < S) {
+      const int k1 = (s + 1) / spi, r1 = (s + 1) % spi;
+      issue_B(k1, r1 / NG, r1 % NG, (s + 1) & 1);
+    }
+    if (grp == 0 && more_chunks) {
+      const int k1 = (cseq + 1) / nchunks;
+      issue_A(k1, (cseq + 1) % nchunks, (cseq + 1) & 1);
+    }
     // ---- compute: the 3 taps of kernel row (kd, r)
-    const char* A = sA(chunk & 1);
+    const char* A = sA(cseq & 1);
     const char* B = sB(s & 1);
     const int kd = DIMS == 3 ? grp / 3 : 0;
     const int r = DIMS == 3 ? grp % 3 : grp;
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       const int tapoff = (kd * HH2 + r) * HW2 + t;
-      uint4 af[MT], bfr[NT];
+      uint4 xf[MT], wf[NT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int hp = hp0[mt] + tapoff;
-        af[mt] = *reinterpret_cast<const uint4*>(A + lds_off(hp, g));
+        xf[mt] = *reinterpret_cast<const uint4*>(A + lds_off(hp, g));
       }
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int row = t * BN + wn * (NT * 16) + nt * 16 + (lane & 15);
-        bfr[nt] = *reinterpret_cast<const uint4*>(B + lds_off(row, g));
+        wf[nt] = *reinterpret_cast<const uint4*>(B + lds_off(row, g));
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(af[mt], bfr[nt], acc[mt][nt]);
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[nt], xf[mt], acc[mt][nt]);
     }
-  }
 
-  // ---- epilogue: bias, bf16, stage [BM][BN] in LDS
-  dma_wait<0>();
-  lds_sync();
-  bf16_t* sO = reinterpret_cast<bf16_t*>(base);
+    if (rem == spi - 1) {
+      // ---- epilogue of item k straight from the accumulators:
+      // lane holds channels co..co+3 (co = co0 + wn*NT*16 + nt*16 + 4*(lane>>4)) of pixel
+      // (wm*MT*16 + mt*16 + (lane&15)) of the tile
+      const Item it = item_of(k);
+      float s1[NT][4], s2[NT][4];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int col = wn * (NT * 16) + nt * 16 + (lane & 15);
-    const float b = (p.bias != nullptr && co0 + col < p.Cout) ? p.bias[co0 + col] : 0.0f;
+      for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
+        for (int i = 0; i < 4; ++i) { s1[nt][i] = 0.f; s2[nt][i] = 0.f; }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wm * (MT * 16) + mt * 16 + 4 * (lane >> 4) + i;
-        sO[row * BN + col] = f2bf(acc[mt][nt][i] + b);
-      }
-    }
-  }
-  lds_sync();
-
-  // ---- coalesced 16-B stores (optionally split into Y1 [0, Co1) / Y2 [Co1, Cout))
-  constexpr int CH = BN / 8;
-  for (int e = tid; e < BM * CH; e += 256) {
-    const int row = e / CH, cg = e % CH;
-    const int co = co0 + cg * 8;
-    const int pw = row % p.TW, ph = (row / p.TW) % p.TH;
-    const int pd = DIMS == 3 ? row / (p.TW * p.TH) : 0;
-    const int gw = w0 + pw, gh = h0 + ph, gd = d0 + pd;
-    if (gw >= p.W || gh >= p.H || gd >= p.D || co >= p.Cout) continue;
-    const long long pix = ((long long)(n_img * p.D + gd) * p.H + gh) * p.W + gw;
-    const uint4 v = *reinterpret_cast<const uint4*>(sO + row * BN + cg * 8);
-    if (co < p.Co1) *reinterpret_cast<uint4*>(p.Y1 + pix * p.Co1 + co) = v;
-    else *reinterpret_cast<uint4*>(p.Y2 + pix * (p.Cout - p.Co1) + (co - p.Co1)) = v;
-  }
-
-  // ---- BatchNorm statistics partials over the stored (bf16) values
-  if (p.stats != nullptr) {
-    constexpr int GROUPS = 256 / BN > 0 ? 256 / BN : 1;
-    float* red = reinterpret_cast<float*>(base + BM * BN * 2);
-    for (int c0 = 0; c0 < BN; c0 += 256) {
-      const int col = c0 + tid % (BN < 256 ? BN : 256);
-      const int grp = BN < 256 ? tid / BN : 0;
-      float s1 = 0.f, s2 = 0.f;
-      if (col < BN) {
-        for (int row = grp; row < BM; row += GROUPS) {
-          const int pw = row % p.TW, ph = (row / p.TW) % p.TH;
-          const int pd = DIMS == 3 ? row / (p.TW * p.TH) : 0;
-          if (w0 + pw >= p.W || h0 + ph >= p.H || d0 + pd >= p.D) continue;
-          const float v = bf2f(sO[row * BN + col]);
-          s1 += v;
-          s2 += v * v;
+      for (int mt = 0; mt < MT; ++mt) {
+        const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
+        const int pw = pix % p.TW, ph = (pix / p.TW) % p.TH;
+        const int pd = DIMS == 3 ? pix / (p.TW * p.TH) : 0;
+        const int gw = it.w0 + pw, gh = it.h0 + ph, gd = it.d0 + pd;
+        const bool valid = gw < p.W && gh < p.H && gd < p.D;
+        const long long gpix = ((long long)(it.n_img * p.D + gd) * p.H + gh) * p.W + gw;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const int co = it.co0 + wn * (NT * 16) + nt * 16 + 4 * (lane >> 4);
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float b = (p.bias != nullptr && co + i < p.Cout) ? p.bias[co + i] : 0.0f;
+            v[i] = acc[mt][nt][i] + b;
+          }
+          const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          if (valid && co < p.Cout) {
+            if (co < p.Co1) *reinterpret_cast<uint2*>(p.Y1 + gpix * p.Co1 + co) = pk;
+            else *reinterpret_cast<uint2*>(p.Y2 + gpix * (p.Cout - p.Co1) + (co - p.Co1)) = pk;
+            // statistics of the stored (bf16-rounded) values
+            const float r0 = lo_bf(pk.x), r1 = hi_bf(pk.x), r2 = lo_bf(pk.y), r3 = hi_bf(pk.y);
+            s1[nt][0] += r0; s2[nt][0] += r0 * r0;
+            s1[nt][1] += r1; s2[nt][1] += r1 * r1;
+            s1[nt][2] += r2; s2[nt][2] += r2 * r2;
+            s1[nt][3] += r3; s2[nt][3] += r3 * r3;
+          }
+          acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         }
       }
-      lds_sync();
-      red[tid] = s1;
-      red[256 + tid] = s2;
-      lds_sync();
-      if (grp == 0 && col < BN && co0 + col < p.Cout) {
-        float t1 = 0.f, t2 = 0.f;
-        for (int q = 0; q < GROUPS; ++q) { t1 += red[q * BN + col]; t2 += red[256 + q * BN + col]; }
-        p.stats[(long long)mtile * 2 * p.Cout + co0 + col] = t1;
-        p.stats[(long long)mtile * 2 * p.Cout + p.Cout + co0 + col] = t2;
+      if (p.stats != nullptr) {
+        // reduce over the 16 pixel lanes (lane & 15) sharing the same channels
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float a1 = s1[nt][i], a2 = s2[nt][i];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) { a1 += __shfl_xor(a1, o, 64); a2 += __shfl_xor(a2, o, 64); }
+            const int co = it.co0 + wn * (NT * 16) + nt * 16 + 4 * (lane >> 4) + i;
+            if ((lane & 15) == 0 && co < p.Cout) {
+              float* row = p.stats + ((long long)it.mtile * WM + wm) * 2 * p.Cout;
+              row[co] = a1;
+              row[p.Cout + co] = a2;
+            }
+          }
       }
     }
   }
@@ -321,10 +331,14 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
 template <int DIMS, int WM, int WN, int MT, int NT, int HALO>
 void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO>;
-  const int grid = a.nTilesM * a.nTilesN;
+  const int items = a.nTilesM * a.nTilesN;
+  int grid = items;
+  if (a.persist_blocks > 0 && grid > a.persist_blocks) grid = a.persist_blocks;
   hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO>), dim3(grid), dim3(256),
                      C::SMEM, st, a);
 }
+
+int cfg_wm(int cfg) { return cfg <= 1 ? 4 : cfg == 2 ? 2 : 1; }
 
 }  // namespace
 
@@ -334,6 +348,7 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
 //   2: BN 128, BM 128 (2x2 waves, 4x4 tiles)     2-D 8x16 / 16x8    3-D 2x4x16 / 4x4x8
 //   3: BN 128, BM 64  (1x4 waves, 4x2 tiles)     2-D 4x16 / 8x8     3-D 1x4x16 / 2x4x8
 // (halo capacity = DMA instructions per wave x 64 pixels)
+int conv3_fwd_cfg_wm(int cfg) { return cfg_wm(cfg); }
 int conv3_fwd_cfg_bn(int cfg) { return cfg == 0 ? 32 : cfg == 1 ? 64 : 128; }
 int conv3_fwd_cfg_bm(int cfg) { return cfg <= 1 ? 256 : cfg == 2 ? 128 : 64; }
 int conv3_fwd_cfg_halo(int dims, int cfg) {

@@ -25,12 +25,14 @@ struct ConvFwdArgs {
   const float* bias;              // optional
   bf16_t* Y1;
   bf16_t* Y2;
-  float* stats;                   // optional [nTilesM][2][Cout]
+  float* stats;                   // optional [nTilesM * WM][2][Cout] partial (sum, sum^2)
   int TD, TH, TW;
   int tilesD, tilesH, tilesW;
   int nTilesM, nTilesN;
+  int persist_blocks;             // grid cap (persistent workgroups); 0 = one per item
 };
 void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st);
+int conv3_fwd_cfg_wm(int cfg);
 int conv3_fwd_cfg_bn(int cfg);
 int conv3_fwd_cfg_bm(int cfg);
 int conv3_fwd_cfg_halo(int dims, int cfg);
