@@ -82,6 +82,17 @@ int num_cus() {
   return n;
 }
 
+// fp64 column sums of an fp32 [R][N] partial slab (deterministic two-pass reduction)
+at::Tensor reduce_rows(const at::Tensor& partial, int64_t R, int64_t N) {
+  auto dopts = partial.options().dtype(at::kDouble);
+  at::Tensor sums = at::empty({N}, dopts);
+  const int RC = reduce_rows_chunks((int)R);
+  at::Tensor tmp = RC > 1 ? at::empty({2 * RC * N}, dopts) : sums;
+  reduce_rows_launch(partial.data_ptr<float>(), (int)R, N, tmp.data_ptr<double>(),
+                     sums.data_ptr<double>(), cur_stream());
+  return sums;
+}
+
 // ------------------------------------------------------------------------ conv3 forward
 std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::Tensor>& x2,
                                   const at::Tensor& w, const c10::optional<at::Tensor>& bias,
@@ -210,8 +221,10 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
     TORCH_CHECK(out->numel() == (int64_t)a.Cout * a.Cin * a.taps, "dW out size mismatch");
   }
   at::Tensor dW = into ? *out : at::empty(wshape, dy.options().dtype(at::kFloat));
-  conv3_wgrad_reduce_launch(a.partial, dW.data_ptr<float>(), a.Cout, a.taps, a.Cin, splits, into,
-                            cur_stream());
+  const long long NW = (long long)a.Cout * a.taps * a.Cin;
+  at::Tensor sums = reduce_rows(part, splits, NW);
+  scatter_sums_launch(sums.data_ptr<double>(), NW, dW.data_ptr<float>(), 0, a.Cout, a.taps, a.Cin,
+                      1.f, into, cur_stream());
   return into ? at::empty({0}, dy.options().dtype(at::kFloat)) : dW;
 }
 
@@ -225,14 +238,14 @@ at::Tensor bn_finalize(const at::Tensor& partial, double count, const at::Tensor
   c10::DeviceGuard guard(partial.device());
   const int C = (int)gamma.numel();
   const int P = (int)(partial.numel() / (2 * C));
+  at::Tensor sums = reduce_rows(partial, P, 2 * C);
   at::Tensor st = at::empty({4, C}, partial.options());
-  float* s = st.data_ptr<float>();
-  bn_finalize_launch(partial.data_ptr<float>(), P, C, count, gamma.data_ptr<float>(),
-                     beta.data_ptr<float>(), running_mean.data_ptr<float>(),
-                     running_var.data_ptr<float>(), (float)momentum, (float)eps, s, s + C,
-                     s + 2 * C, s + 3 * C, update_running,
-                     (nbt.has_value() && nbt->defined()) ? nbt->data_ptr<int64_t>() : nullptr,
-                     cur_stream());
+  bn_stats_finalize_launch(sums.data_ptr<double>(), C, count, gamma.data_ptr<float>(),
+                           beta.data_ptr<float>(), running_mean.data_ptr<float>(),
+                           running_var.data_ptr<float>(), (float)momentum, (float)eps,
+                           st.data_ptr<float>(), update_running,
+                           (nbt.has_value() && nbt->defined()) ? nbt->data_ptr<int64_t>() : nullptr,
+                           cur_stream());
   return st;
 }
 
@@ -289,9 +302,10 @@ std::vector<at::Tensor> bn_backward(const c10::optional<at::Tensor>& dA,
   at::Tensor dbeta = into ? *dbeta_out : at::empty({C}, fopts);
   at::Tensor coefs = at::empty({3, C}, fopts);
   const double count = (double)g.N * g.D * g.H * g.W;
-  bn_bwd_finalize_launch(partial.data_ptr<float>(), nb, C, count, gamma.data_ptr<float>(), s + C,
-                         dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), coefs.data_ptr<float>(),
-                         into, cur_stream());
+  at::Tensor sums = reduce_rows(partial, nb, 2 * C);
+  bn_grad_finalize_launch(sums.data_ptr<double>(), C, count, gamma.data_ptr<float>(), s + C,
+                          dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), coefs.data_ptr<float>(),
+                          into, cur_stream());
   at::Tensor dY = at::empty_like(y);
   bn_bwd_apply_launch(pA, pP, bptr(y), s + 2 * C, s + 3 * C, s, s + C, coefs.data_ptr<float>(), gs,
                       bptr_mut(dY), g.dims, g.N, g.D, g.H, g.W, C, cur_stream());
@@ -375,15 +389,19 @@ std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
   if (g.dims == 3) ws.push_back(2);
   const bool into = dw_out.has_value() && dw_out->defined();
   at::Tensor dW = into ? *dw_out : at::empty(ws, fopts);
-  gemm_wgrad_reduce_launch(a.partial, dW.data_ptr<float>(), nullptr, g.C, go.C, S, splits, into,
-                           cur_stream());
+  const long long NW = (long long)a.M * a.N;
+  at::Tensor wsums = reduce_rows(part, splits, NW);
+  scatter_sums_launch(wsums.data_ptr<double>(), NW, dW.data_ptr<float>(), 1, g.C, S, go.C, 1.f,
+                      into, cur_stream());
   // bias gradient: per-channel sum of dOut
   const long long P = (long long)go.N * go.D * go.H * go.W;
   const int nb = (int)std::max<long long>(1, std::min<long long>((P + 1023) / 1024, 1024));
   at::Tensor cpart = at::empty({nb, go.C}, fopts);
   channel_sum_launch(bptr(dout), P, go.C, cpart.data_ptr<float>(), nb, cur_stream());
   at::Tensor db = into ? *db_out : at::empty({go.C}, fopts);
-  partial_sum_launch(cpart.data_ptr<float>(), nb, go.C, db.data_ptr<float>(), 1.f, into, cur_stream());
+  at::Tensor csums = reduce_rows(cpart, nb, go.C);
+  scatter_sums_launch(csums.data_ptr<double>(), go.C, db.data_ptr<float>(), 2, 0, 0, 0, 1.f, into,
+                      cur_stream());
   if (into) return {at::empty({0}, fopts), at::empty({0}, fopts)};
   return {dW, db};
 }
@@ -425,19 +443,19 @@ std::vector<at::Tensor> head_ce_bwd(const at::Tensor& a, const at::Tensor& Wh, c
                      fptr_opt(gscale), out3.data_ptr<float>(), 0, bptr_mut(dA),
                      part.data_ptr<float>(), nb, P, C, K, (int)ignore_index, cur_stream());
   const bool into = dw_out.has_value() && dw_out->defined();
+  at::Tensor sums = reduce_rows(part, nb, K * C + K);   // rows are [dW (K*C) | db (K)]
   if (into) {
-    // partial rows are [K*C | K]: reduce the two column ranges straight into the grads
     TORCH_CHECK(dw_out->is_contiguous() && db_out->is_contiguous(), "grad outs must be contiguous");
-    at::Tensor pw = part.narrow(1, 0, K * C).contiguous();
-    at::Tensor pb = part.narrow(1, K * C, K).contiguous();
-    partial_sum_launch(pw.data_ptr<float>(), nb, K * C, dw_out->data_ptr<float>(), 1.f, true, cur_stream());
-    partial_sum_launch(pb.data_ptr<float>(), nb, K, db_out->data_ptr<float>(), 1.f, true, cur_stream());
+    scatter_sums_launch(sums.data_ptr<double>(), K * C, dw_out->data_ptr<float>(), 2, 0, 0, 0, 1.f,
+                        true, cur_stream());
+    scatter_sums_launch(sums.data_ptr<double>() + K * C, K, db_out->data_ptr<float>(), 2, 0, 0, 0,
+                        1.f, true, cur_stream());
     at::Tensor none = at::empty({0}, fopts);
     return {dA, none, none};
   }
   at::Tensor red = at::empty({K * C + K}, fopts);
-  partial_sum_launch(part.data_ptr<float>(), nb, K * C + K, red.data_ptr<float>(), 1.f, false,
-                     cur_stream());
+  scatter_sums_launch(sums.data_ptr<double>(), K * C + K, red.data_ptr<float>(), 2, 0, 0, 0, 1.f,
+                      false, cur_stream());
   at::Tensor dW = red.narrow(0, 0, K * C).view({K, C});
   at::Tensor db = red.narrow(0, K * C, K);
   return {dA, dW, db};

@@ -22,44 +22,6 @@ namespace ddlpc {
 
 namespace {
 
-// --------------------------------------------------------------------- finalize
-__global__ void bn_finalize_kernel(const float* __restrict__ partial, int P, int C, double count,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                                   float* running_mean, float* running_var, float momentum,
-                                   float eps, float* mean_o, float* invstd_o, float* scale_o,
-                                   float* shift_o, int update_running, int64_t* nbt) {
-  const int c = blockIdx.x;
-  double s1 = 0.0, s2 = 0.0;
-  for (int p = threadIdx.x; p < P; p += blockDim.x) {
-    s1 += partial[(long long)p * 2 * C + c];
-    s2 += partial[(long long)p * 2 * C + C + c];
-  }
-  __shared__ double r1[4], r2[4];
-  s1 = wave_sum_d(s1);
-  s2 = wave_sum_d(s2);
-  if ((threadIdx.x & 63) == 0) { r1[threadIdx.x >> 6] = s1; r2[threadIdx.x >> 6] = s2; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double t1 = 0, t2 = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { t1 += r1[w]; t2 += r2[w]; }
-    const double mean = t1 / count;
-    double var = t2 / count - mean * mean;
-    if (var < 0) var = 0;
-    const float inv = (float)(1.0 / sqrt(var + (double)eps));
-    const float sc = gamma[c] * inv;
-    mean_o[c] = (float)mean;
-    invstd_o[c] = inv;
-    scale_o[c] = sc;
-    shift_o[c] = beta[c] - (float)mean * sc;
-    if (update_running && c == 0 && nbt != nullptr) nbt[0] += 1;
-    if (update_running) {
-      const double unb = count > 1 ? var * count / (count - 1) : var;
-      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-      running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
-    }
-  }
-}
-
 // --------------------------------------------------------------------- apply (+ pool)
 template <int DIMS, bool POOL>
 __global__ void bn_relu_apply_kernel(const bf16_t* __restrict__ y, const float* __restrict__ scale,
@@ -241,32 +203,6 @@ __global__ void bn_bwd_kernel(const bf16_t* __restrict__ dA, const bf16_t* __res
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int P, int C,
-                                       double count, const float* __restrict__ gamma,
-                                       const float* __restrict__ invstd, float* dgamma,
-                                       float* dbeta, float* coefs, int accumulate) {
-  const int c = blockIdx.x;
-  double s1 = 0.0, s2 = 0.0;
-  for (int p = threadIdx.x; p < P; p += blockDim.x) {
-    s1 += partial[(long long)p * 2 * C + c];
-    s2 += partial[(long long)p * 2 * C + C + c];
-  }
-  __shared__ double r1[4], r2[4];
-  s1 = wave_sum_d(s1);
-  s2 = wave_sum_d(s2);
-  if ((threadIdx.x & 63) == 0) { r1[threadIdx.x >> 6] = s1; r2[threadIdx.x >> 6] = s2; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double t1 = 0, t2 = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { t1 += r1[w]; t2 += r2[w]; }
-    dbeta[c] = accumulate ? dbeta[c] + (float)t1 : (float)t1;
-    dgamma[c] = accumulate ? dgamma[c] + (float)t2 : (float)t2;
-    coefs[c] = gamma[c] * invstd[c];
-    coefs[C + c] = (float)(t1 / count);
-    coefs[2 * C + c] = (float)(t2 / count);
-  }
-}
-
 int grid_for(long long items, int per_block) {
   long long g = (items + per_block - 1) / per_block;
   return (int)std::max<long long>(1, std::min<long long>(g, 2048));
@@ -275,15 +211,6 @@ int grid_for(long long items, int per_block) {
 }  // namespace
 
 int bn_bwd_reduce_blocks(long long items) { return grid_for(items, 64); }
-
-void bn_finalize_launch(const float* partial, int P, int C, double count, const float* gamma,
-                        const float* beta, float* running_mean, float* running_var,
-                        float momentum, float eps, float* mean, float* invstd, float* scale,
-                        float* shift, bool update_running, int64_t* nbt, hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, partial, P, C, count, gamma,
-                     beta, running_mean, running_var, momentum, eps, mean, invstd, scale, shift,
-                     update_running ? 1 : 0, nbt);
-}
 
 void bn_relu_apply_launch(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
                           bf16_t* pooled, int dims, int N, int D, int H, int W, int C,
@@ -337,13 +264,6 @@ void bn_bwd_reduce_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y,
   const float* coefs = nullptr;
   bf16_t* dY = nullptr;
   BN_BWD_DISPATCH(0, nblocks);
-}
-
-void bn_bwd_finalize_launch(const float* partial, int P, int C, double count,
-                            const float* gamma, const float* invstd, float* dgamma,
-                            float* dbeta, float* coefs, bool accumulate, hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partial, P, C, count,
-                     gamma, invstd, dgamma, dbeta, coefs, accumulate ? 1 : 0);
 }
 
 void bn_bwd_apply_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y, const float* scale,

@@ -12,7 +12,7 @@
 // row re-reads the same halo.
 //
 // Each workgroup owns (co tile, 32-channel ci chunk, kd plane) and a contiguous range of
-// pixel tiles; it writes an fp32 partial slab that conv3_wgrad_reduce sums over splits in a
+// pixel tiles; it writes an fp32 partial slab that reduce_rows (reduce.hip) sums over splits in a
 // fixed order (bit-reproducible, so all data-parallel ranks stay bit-identical) and
 // accumulates into the fp32 OIHW parameter gradient.
 #include "common.h"
@@ -28,11 +28,14 @@ constexpr int PT = 128;         // pixels per K step tile
 template <int DIMS>
 struct WgHalo { static constexpr int value = DIMS == 2 ? 208 : 448; };
 
+// Wave tiling: every wave holds ALL BCO output channels (NCO = BCO/16 A fragments) and a
+// strided subset of the 18 (tap, ci-half) pairs (5,5,4,4 across the 4 waves), so each dY
+// fragment read feeds up to 5 MFMAs and each input fragment up to NCO: per 32-pixel k-step
+// a wave issues 2*NCO + 2*5 transposed reads for 5*NCO MFMAs.
 template <int DIMS, int BCO>
 struct WgCfg {
-  static constexpr int WAVES_CO = BCO / 16;            // 2 or 4
-  static constexpr int WAVES_CI = 4 / WAVES_CO;        // 2 or 1
-  static constexpr int NCI = 2 / WAVES_CI;             // ci 16-tiles per wave
+  static constexpr int NCO = BCO / 16;                 // 2 or 4
+  static constexpr int NP = 5;                         // max (tap, ci-half) pairs per wave
   static constexpr int HALO = WgHalo<DIMS>::value;
   static constexpr int Y_ROWB = BCO * 2;
   static constexpr int X_ROWB = CI * 2;
@@ -46,16 +49,15 @@ struct WgCfg {
 };
 
 template <int DIMS, int BCO>
-__global__ __launch_bounds__(256, 1) void conv3_wgrad_kernel(ConvWgradArgs p) {
+__global__ __launch_bounds__(256, 2) void conv3_wgrad_kernel(ConvWgradArgs p) {
   using Cfg = WgCfg<DIMS, BCO>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sY = smem;
   char* sX = smem + Cfg::Y_BYTES;
   __shared__ float s_scale[512], s_shift[512];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wco = wave % Cfg::WAVES_CO;
-  const int wci = wave / Cfg::WAVES_CO;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
   // block -> (split, plane, ci chunk, co tile); splits innermost share operand tiles
   int b = blockIdx.x;
@@ -88,11 +90,11 @@ __global__ __launch_bounds__(256, 1) void conv3_wgrad_kernel(ConvWgradArgs p) {
       hp0[ks * 2 + h] = (pd * HH2 + ph) * HW2 + pw;
     }
 
-  f32x4_t acc[9][Cfg::NCI];
+  f32x4_t acc[Cfg::NCO][Cfg::NP];
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int j = 0; j < Cfg::NCO; ++j)
 #pragma unroll
-    for (int j = 0; j < Cfg::NCI; ++j) acc[t][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int q2 = 0; q2 < Cfg::NP; ++q2) acc[j][q2] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   uint4 ry[Cfg::Y_PER_T], rx[Cfg::X_PER_T];
   uint32_t x_valid = 0;
@@ -193,7 +195,6 @@ __global__ __launch_bounds__(256, 1) void conv3_wgrad_kernel(ConvWgradArgs p) {
   if (t_begin < t_end) load(t_begin);
   __syncthreads();
   const int kd = DIMS == 3 ? plane : 0;
-  const int cw = wco * 16;                       // wave's co offset inside the tile
   for (int tile = t_begin; tile < t_end; ++tile) {
     __syncthreads();
     store();
@@ -201,65 +202,49 @@ __global__ __launch_bounds__(256, 1) void conv3_wgrad_kernel(ConvWgradArgs p) {
     if (tile + 1 < t_end) load(tile + 1);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      // A = dY^T fragment (16 co x 32 px): rows = pixels, cols = co
-      uint4 af;
-      {
-        const int r0 = ks * 32 + 8 * g + q;
-        const uint2 lo = lds_read_tr16(sY + r0 * Cfg::Y_ROWB + (cw + 4 * pp) * 2);
-        const uint2 hi = lds_read_tr16(sY + (r0 + 4) * Cfg::Y_ROWB + (cw + 4 * pp) * 2);
-        af = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      // A = dY^T fragments (16 co x 32 px each): rows = pixels, cols = co
+      uint4 af[Cfg::NCO];
+      const int r0 = ks * 32 + 8 * g + q;
+#pragma unroll
+      for (int j = 0; j < Cfg::NCO; ++j) {
+        const uint2 lo = lds_read_tr16(sY + r0 * Cfg::Y_ROWB + (j * 16 + 4 * pp) * 2);
+        const uint2 hi = lds_read_tr16(sY + (r0 + 4) * Cfg::Y_ROWB + (j * 16 + 4 * pp) * 2);
+        af[j] = make_uint4(lo.x, lo.y, hi.x, hi.y);
       }
 #pragma unroll
-      for (int r = 0; r < 3; ++r)
+      for (int pi = 0; pi < Cfg::NP; ++pi) {
+        const int pair = wave + 4 * pi;                 // wave-uniform
+        if (pair < 18) {
+          const int tap = pair >> 1, cih = pair & 1;
+          const int tapoff = (kd * HH2 + tap / 3) * HW2 + tap % 3;
+          const int cc = cih * 16 + 4 * pp;
+          const uint2 lo = lds_read_tr16(sX + (hp0[ks * 2] + tapoff) * Cfg::X_ROWB + cc * 2);
+          const uint2 hi = lds_read_tr16(sX + (hp0[ks * 2 + 1] + tapoff) * Cfg::X_ROWB + cc * 2);
+          const uint4 bfr = make_uint4(lo.x, lo.y, hi.x, hi.y);
 #pragma unroll
-        for (int s = 0; s < 3; ++s) {
-          const int tapoff = (kd * HH2 + r) * HW2 + s;
-#pragma unroll
-          for (int j = 0; j < Cfg::NCI; ++j) {
-            const int cc = (wci * Cfg::NCI + j) * 16 + 4 * pp;
-            const uint2 lo = lds_read_tr16(sX + (hp0[ks * 2] + tapoff) * Cfg::X_ROWB + cc * 2);
-            const uint2 hi = lds_read_tr16(sX + (hp0[ks * 2 + 1] + tapoff) * Cfg::X_ROWB + cc * 2);
-            const uint4 bfr = make_uint4(lo.x, lo.y, hi.x, hi.y);
-            acc[r * 3 + s][j] = mfma16x16x32(af, bfr, acc[r * 3 + s][j]);
-          }
+          for (int j = 0; j < Cfg::NCO; ++j) acc[j][pi] = mfma16x16x32(af[j], bfr, acc[j][pi]);
         }
+      }
     }
   }
 
   // ---- partial slab: part[split][co][tap][ci]   (tap = kd*9 + r*3 + s)
   float* out = p.partial + (long long)split * p.Cout * p.taps * p.Cin;
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int pi = 0; pi < Cfg::NP; ++pi) {
+    const int pair = wave + 4 * pi;
+    if (pair >= 18) continue;
+    const int tap = kd * 9 + (pair >> 1);
+    const int ci = ci0 + (pair & 1) * 16 + (lane & 15);
 #pragma unroll
-    for (int j = 0; j < Cfg::NCI; ++j) {
-      const int ci = ci0 + (wci * Cfg::NCI + j) * 16 + (lane & 15);
-      const int tap = kd * 9 + t;
+    for (int j = 0; j < Cfg::NCO; ++j)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int co = co0 + cw + 4 * (lane >> 4) + i;
-        if (co < p.Cout && ci < p.Cin) out[((long long)co * p.taps + tap) * p.Cin + ci] = acc[t][j][i];
+        const int co = co0 + j * 16 + 4 * (lane >> 4) + i;
+        if (co < p.Cout && ci < p.Cin) out[((long long)co * p.taps + tap) * p.Cin + ci] = acc[j][pi][i];
       }
-    }
-  (void)tiles_per_img;
-}
-
-// sum partial slabs over splits (fixed order), transpose [co][tap][ci] -> OIHW [co][ci][tap]
-// and accumulate into the fp32 parameter gradient.
-__global__ void conv3_wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dW,
-                                          int Cout, int taps, int Cin, int splits, int accumulate) {
-  const long long total = (long long)Cout * Cin * taps;
-  const long long stride = (long long)Cout * taps * Cin;
-  for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < total;
-       o += (long long)gridDim.x * blockDim.x) {
-    // o indexes the slab layout [co][tap][ci] for coalesced reads
-    const int ci = (int)(o % Cin);
-    const int tap = (int)((o / Cin) % taps);
-    const int co = (int)(o / ((long long)Cin * taps));
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += part[k * stride + o];
-    float* dst = dW + ((long long)co * Cin + ci) * taps + tap;
-    *dst = accumulate ? *dst + s : s;
   }
+  (void)tiles_per_img;
 }
 
 template <int DIMS, int BCO>
@@ -277,14 +262,6 @@ void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
   } else {
     if (bco == 32) launch_wg<3, 32>(a, st); else launch_wg<3, 64>(a, st);
   }
-}
-
-void conv3_wgrad_reduce_launch(const float* part, float* dW, int Cout, int taps, int Cin,
-                               int splits, bool accumulate, hipStream_t st) {
-  const long long total = (long long)Cout * Cin * taps;
-  int grid = (int)std::min<long long>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3(grid), dim3(256), 0, st, part, dW, Cout,
-                     taps, Cin, splits, accumulate ? 1 : 0);
 }
 
 int conv3_wgrad_halo_cap(int dims) { return dims == 2 ? WgHalo<2>::value : WgHalo<3>::value; }

@@ -259,22 +259,6 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_wgrad_kernel(GemmArgs p) {
     }
 }
 
-// sum splits; slab [ci][(sub, co)] -> IOHW dW[ci][co][sub] (fp32)
-__global__ void convt_wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dW,
-                                          int Cin, int Cout, int S, int splits, int accumulate) {
-  const long long total = (long long)Cin * S * Cout;
-  for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < total;
-       o += (long long)gridDim.x * blockDim.x) {
-    const int co = (int)(o % Cout);
-    const int sub = (int)((o / Cout) % S);
-    const int ci = (int)(o / ((long long)Cout * S));
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += part[k * total + o];
-    float* d = dW + ((long long)ci * Cout + co) * S + sub;
-    *d = accumulate ? *d + s : s;
-  }
-}
-
 }  // namespace
 
 void gemm_launch(GemmArgs& a, hipStream_t st) {
@@ -288,14 +272,6 @@ void gemm_launch(GemmArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((gemm_nt_kernel<GEMM_CONVT_FWD>), dim3((unsigned)grid), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL((gemm_nt_kernel<GEMM_CONVT_DGRAD>), dim3((unsigned)grid), dim3(256), 0, st, a);
-}
-
-void gemm_wgrad_reduce_launch(const float* part, float* dW, float* /*db*/, int Cin, int Cout,
-                              int subs, int splits, bool accumulate, hipStream_t st) {
-  const long long total = (long long)Cin * subs * Cout;
-  const int grid = (int)std::min<long long>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(convt_wgrad_reduce_kernel, dim3(grid), dim3(256), 0, st, part, dW, Cin, Cout,
-                     subs, splits, accumulate ? 1 : 0);
 }
 
 }  // namespace ddlpc

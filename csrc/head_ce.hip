@@ -195,28 +195,6 @@ __global__ void head_logits_kernel(const bf16_t* __restrict__ a, const float* __
   }
 }
 
-// out[i] (+)= scale * sum_b partial[b][i]   (fixed order -> reproducible)
-// Column tile of 64 per block; the 256 threads split the P rows 4 ways per column (each
-// lane sums a contiguous quarter of the rows), then the 4 quarters are combined in order.
-__global__ void partial_sum_kernel(const float* __restrict__ partial, int P, int n,
-                                   float* __restrict__ out, float scale, int accumulate) {
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int q = threadIdx.x >> 6;
-  const int rows = (P + 3) / 4;
-  const int r0 = q * rows, r1 = min(P, r0 + rows);
-  double s = 0.0;
-  if (col < n)
-    for (int b = r0; b < r1; ++b) s += partial[(long long)b * n + col];
-  __shared__ double red[4][64];
-  red[q][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (q == 0 && col < n) {
-    const double t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    const float v = (float)t * scale;
-    out[col] = accumulate ? out[col] + v : v;
-  }
-}
-
 #define HEAD_SWITCH(C_, K_, ...)                                                  \
   [&] {                                                                           \
     if (C_ == 32 && K_ == 6) { constexpr int CC = 32, KK = 6; __VA_ARGS__; }        \
@@ -259,13 +237,6 @@ void head_logits_launch(const bf16_t* a, const float* Wh, const float* bh, float
   const int grid = (int)std::min<long long>((P + 255) / 256, 4096);
   HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_logits_kernel<CC, KK>), dim3(grid), dim3(256), 0, st,
                                        a, Wh, bh, logits, P, HW));
-}
-
-void partial_sum_launch(const float* partial, int P, int n, float* out, float scale,
-                        bool accumulate, hipStream_t st) {
-  const int grid = std::max(1, (n + 63) / 64);
-  hipLaunchKernelGGL(partial_sum_kernel, dim3(grid), dim3(256), 0, st, partial, P, n, out, scale,
-                     accumulate ? 1 : 0);
 }
 
 }  // namespace ddlpc

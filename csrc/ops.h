@@ -53,8 +53,7 @@ struct ConvWgradArgs {
   int coTiles, ciChunks, planes, splits;
 };
 void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st);
-void conv3_wgrad_reduce_launch(const float* part, float* dW, int Cout, int taps, int Cin,
-                               int splits, bool accumulate, hipStream_t st);
+
 int conv3_wgrad_halo_cap(int dims);
 
 // ---------------------------------------------------------------- generic bf16 GEMM (convT)
@@ -82,15 +81,9 @@ enum GemmMode {
   GEMM_CONVT_WGRAD = 2, // TN: dW[ci][(sub, co)] = sum_px x[px][ci] * dOut[up(px, sub)][co]
 };
 void gemm_launch(GemmArgs& a, hipStream_t st);
-void gemm_wgrad_reduce_launch(const float* part, float* dW, float* db, int Cin, int Cout,
-                              int subs, int splits, bool accumulate, hipStream_t st);
+
 
 // ---------------------------------------------------------------- BatchNorm / ReLU / pool
-void bn_finalize_launch(const float* partial, int P, int C, double count, const float* gamma,
-                        const float* beta, float* running_mean, float* running_var,
-                        float momentum, float eps, float* mean, float* invstd, float* scale,
-                        float* shift, bool update_running, int64_t* num_batches_tracked,
-                        hipStream_t st);
 void bn_relu_apply_launch(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
                           bf16_t* pooled, int dims, int N, int D, int H, int W, int C,
                           hipStream_t st);
@@ -98,9 +91,6 @@ void bn_bwd_reduce_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y,
                           const float* scale, const float* shift, const float* mean,
                           const float* invstd, const float* gscale, float* partial, int nblocks,
                           int dims, int N, int D, int H, int W, int C, hipStream_t st);
-void bn_bwd_finalize_launch(const float* partial, int P, int C, double count,
-                            const float* gamma, const float* invstd, float* dgamma,
-                            float* dbeta, float* coefs, bool accumulate, hipStream_t st);
 void bn_bwd_apply_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y, const float* scale,
                          const float* shift, const float* mean, const float* invstd,
                          const float* coefs, const float* gscale, bf16_t* dY, int dims, int N,
@@ -118,8 +108,7 @@ void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
                         int ignore_index, hipStream_t st);
 void head_logits_launch(const bf16_t* a, const float* Wh, const float* bh, float* logits_nchw,
                         long long P, long long HW, int C, int K, hipStream_t st);
-void partial_sum_launch(const float* partial, int P, int n, float* out, float scale,
-                        bool accumulate, hipStream_t st);
+
 
 // ---------------------------------------------------------------- optimizer / packing
 void adam_launch(float* p, const float* g, float* m, float* v, long long n, float b1, float b2,
@@ -142,6 +131,20 @@ void codec_encode_launch(const float* x, const int64_t* seg, int nseg, const flo
 void codec_decode_sum_launch(float* out, const void* q, const float* scales, const float* w,
                              const int64_t* seg, int nseg, int world, int codec, long long n,
                              hipStream_t st);
+
+// ---------------------------------------------------------------- deterministic reductions
+int reduce_rows_chunks(int R);
+void reduce_rows_launch(const float* in, int R, long long N, double* tmp, double* sums,
+                        hipStream_t st);
+void bn_stats_finalize_launch(const double* sums, int C, double count, const float* gamma,
+                              const float* beta, float* running_mean, float* running_var,
+                              float momentum, float eps, float* out4, bool update_running,
+                              int64_t* nbt, hipStream_t st);
+void bn_grad_finalize_launch(const double* sums, int C, double count, const float* gamma,
+                             const float* invstd, float* dgamma, float* dbeta, float* coefs,
+                             bool accumulate, hipStream_t st);
+void scatter_sums_launch(const double* sums, long long N, float* dst, int mode, int A, int T,
+                         int B, float scale, bool accumulate, hipStream_t st);
 
 // ---------------------------------------------------------------- misc
 void bilinear_up2_launch(const bf16_t* x, bf16_t* y, int dims, int N, int D, int H, int W, int C,

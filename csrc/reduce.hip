@@ -1,0 +1,145 @@
+// Deterministic two-pass row reductions of fp32 partial slabs into fp64 sums, plus the small
+// finishing kernels that consume them (BatchNorm statistics / gradient coefficients, weight
+// gradient transpose + accumulate).
+//
+// Every split-K / per-tile partial in the library (conv and transposed-conv weight-gradient
+// slabs, BatchNorm sum / sum^2 rows, head-gradient rows, channel sums) is reduced here in a
+// FIXED order: pass 1 sums row chunks of 64 (one thread per column, coalesced across the
+// wave), pass 2 sums the chunk results.  No float atomics, so every data-parallel rank
+// computes bit-identical local gradients from identical inputs.
+#include "common.h"
+#include "ops.h"
+
+namespace ddlpc {
+
+namespace {
+
+constexpr int RB = 64;   // rows per chunk
+
+template <typename T>
+__global__ void rows_chunk_sum_kernel(const T* __restrict__ in, int R, long long N,
+                                      double* __restrict__ out) {
+  const long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (j >= N) return;
+  const int r0 = blockIdx.y * RB;
+  const int r1 = min(R, r0 + RB);
+  double s = 0.0;
+#pragma unroll 8
+  for (int r = r0; r < r1; ++r) s += (double)in[(long long)r * N + j];
+  out[(long long)blockIdx.y * N + j] = s;
+}
+
+// mean / invstd / scale / shift + running statistics from fp64 (sum, sum^2)
+__global__ void bn_stats_finalize_kernel(const double* __restrict__ sums, int C, double count,
+                                         const float* __restrict__ gamma,
+                                         const float* __restrict__ beta, float* running_mean,
+                                         float* running_var, float momentum, float eps,
+                                         float* __restrict__ out4, int update_running,
+                                         int64_t* nbt) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && update_running && nbt != nullptr) nbt[0] += 1;
+  if (c >= C) return;
+  const double mean = sums[c] / count;
+  double var = sums[C + c] / count - mean * mean;
+  if (var < 0) var = 0;
+  const float inv = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * inv;
+  out4[c] = (float)mean;
+  out4[C + c] = inv;
+  out4[2 * C + c] = sc;
+  out4[3 * C + c] = beta[c] - (float)mean * sc;
+  if (update_running) {
+    const double unb = count > 1 ? var * count / (count - 1) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+  }
+}
+
+// dgamma, dbeta (accumulated if requested) and dY coefficients from fp64 (sum dyh, sum dyh*xhat)
+__global__ void bn_grad_finalize_kernel(const double* __restrict__ sums, int C, double count,
+                                        const float* __restrict__ gamma,
+                                        const float* __restrict__ invstd, float* dgamma,
+                                        float* dbeta, float* coefs, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double t1 = sums[c], t2 = sums[C + c];
+  dbeta[c] = accumulate ? dbeta[c] + (float)t1 : (float)t1;
+  dgamma[c] = accumulate ? dgamma[c] + (float)t2 : (float)t2;
+  coefs[c] = gamma[c] * invstd[c];
+  coefs[C + c] = (float)(t1 / count);
+  coefs[2 * C + c] = (float)(t2 / count);
+}
+
+// dst[perm(j)] (+)= scale * sums[j]; perm: conv slab [co][tap][ci] -> OIHW [co][ci][tap]
+// (mode 0), convT slab [ci][(sub, co)] -> IOHW [ci][co][sub] (mode 1), identity (mode 2)
+__global__ void scatter_sums_kernel(const double* __restrict__ sums, long long N, float* dst,
+                                    int mode, int A, int T, int B, float scale, int accumulate) {
+  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < N;
+       j += (long long)gridDim.x * blockDim.x) {
+    long long d = j;
+    if (mode == 0) {          // A = Cout, T = taps, B = Cin ; j = (co*T + tap)*B + ci
+      const int ci = (int)(j % B);
+      const int tap = (int)((j / B) % T);
+      const long long co = j / ((long long)B * T);
+      d = (co * B + ci) * T + tap;
+    } else if (mode == 1) {   // A = Cin, T = subs, B = Cout ; j = ci*(T*B) + sub*B + co
+      const int co = (int)(j % B);
+      const int sub = (int)((j / B) % T);
+      const long long ci = j / ((long long)B * T);
+      d = (ci * B + co) * T + sub;
+    }
+    const float v = (float)sums[j] * scale;
+    dst[d] = accumulate ? dst[d] + v : v;
+  }
+}
+
+}  // namespace
+
+int reduce_rows_chunks(int R) { return (R + RB - 1) / RB; }
+
+// sums[N] (fp64) = sum over R rows of in[R][N]; tmp must hold reduce_rows_chunks(R) * N doubles
+void reduce_rows_launch(const float* in, int R, long long N, double* tmp, double* sums,
+                        hipStream_t st) {
+  const int RC = reduce_rows_chunks(R);
+  const unsigned gx = (unsigned)((N + 255) / 256);
+  if (RC == 1) {
+    hipLaunchKernelGGL(rows_chunk_sum_kernel<float>, dim3(gx, 1), dim3(256), 0, st, in, R, N, sums);
+    return;
+  }
+  hipLaunchKernelGGL(rows_chunk_sum_kernel<float>, dim3(gx, RC), dim3(256), 0, st, in, R, N, tmp);
+  int R2 = RC;
+  const double* cur = tmp;
+  while (reduce_rows_chunks(R2) > 1) {       // (only for > 4096 rows)
+    const int RC2 = reduce_rows_chunks(R2);
+    double* nxt = tmp + (long long)RC * N;   // second half of tmp is free scratch
+    hipLaunchKernelGGL(rows_chunk_sum_kernel<double>, dim3(gx, RC2), dim3(256), 0, st, cur, R2, N, nxt);
+    cur = nxt;
+    R2 = RC2;
+  }
+  hipLaunchKernelGGL(rows_chunk_sum_kernel<double>, dim3(gx, 1), dim3(256), 0, st, cur, R2, N, sums);
+}
+
+void bn_stats_finalize_launch(const double* sums, int C, double count, const float* gamma,
+                              const float* beta, float* running_mean, float* running_var,
+                              float momentum, float eps, float* out4, bool update_running,
+                              int64_t* nbt, hipStream_t st) {
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, sums, C,
+                     count, gamma, beta, running_mean, running_var, momentum, eps, out4,
+                     update_running ? 1 : 0, nbt);
+}
+
+void bn_grad_finalize_launch(const double* sums, int C, double count, const float* gamma,
+                             const float* invstd, float* dgamma, float* dbeta, float* coefs,
+                             bool accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(bn_grad_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, sums, C,
+                     count, gamma, invstd, dgamma, dbeta, coefs, accumulate ? 1 : 0);
+}
+
+void scatter_sums_launch(const double* sums, long long N, float* dst, int mode, int A, int T,
+                         int B, float scale, bool accumulate, hipStream_t st) {
+  const int grid = (int)std::max<long long>(1, std::min<long long>((N + 255) / 256, 4096));
+  hipLaunchKernelGGL(scatter_sums_kernel, dim3(grid), dim3(256), 0, st, sums, N, dst, mode, A, T,
+                     B, scale, accumulate ? 1 : 0);
+}
+
+}  // namespace ddlpc
