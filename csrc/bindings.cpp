@@ -154,9 +154,12 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   at::Tensor y2;
   if (a.Co1 < a.Cout) y2 = at::empty(shape_with_c(g, a.Cout - a.Co1), opts);
   at::Tensor stats;
-  if (want_stats)
-    stats = at::empty({(int64_t)a.nTilesM * conv3_fwd_cfg_wm(cfg), 2, a.Cout}, opts.dtype(at::kFloat));
   a.persist_blocks = 2 * num_cus();
+  if (want_stats) {
+    const int items = a.nTilesM * a.nTilesN;
+    const int grid = items > a.persist_blocks ? a.persist_blocks / a.nTilesN * a.nTilesN : items;
+    stats = at::empty({(int64_t)grid, 2, a.Cout}, opts.dtype(at::kFloat));
+  }
   a.Y1 = bptr_mut(y1);
   a.Y2 = y2.defined() ? bptr_mut(y2) : nullptr;
   a.stats = want_stats ? stats.data_ptr<float>() : nullptr;
@@ -222,9 +225,11 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   }
   at::Tensor dW = into ? *out : at::empty(wshape, dy.options().dtype(at::kFloat));
   const long long NW = (long long)a.Cout * a.taps * a.Cin;
-  at::Tensor sums = reduce_rows(part, splits, NW);
-  scatter_sums_launch(sums.data_ptr<double>(), NW, dW.data_ptr<float>(), 0, a.Cout, a.taps, a.Cin,
-                      1.f, into, cur_stream());
+  at::Tensor tmp = splits > 64 ? at::empty({(int64_t)((splits + 63) / 64) * NW},
+                                           dy.options().dtype(at::kDouble))
+                               : at::empty({0}, dy.options().dtype(at::kDouble));
+  reduce_rows_scatter_launch(part.data_ptr<float>(), splits, NW, tmp.data_ptr<double>(),
+                             dW.data_ptr<float>(), 0, a.Cout, a.taps, a.Cin, into, cur_stream());
   return into ? at::empty({0}, dy.options().dtype(at::kFloat)) : dW;
 }
 
@@ -238,14 +243,20 @@ at::Tensor bn_finalize(const at::Tensor& partial, double count, const at::Tensor
   c10::DeviceGuard guard(partial.device());
   const int C = (int)gamma.numel();
   const int P = (int)(partial.numel() / (2 * C));
-  at::Tensor sums = reduce_rows(partial, P, 2 * C);
   at::Tensor st = at::empty({4, C}, partial.options());
+  int64_t* nbp = (nbt.has_value() && nbt->defined()) ? nbt->data_ptr<int64_t>() : nullptr;
+  if (P <= 4096) {
+    bn_stats_finalize_rows_launch(partial.data_ptr<float>(), P, C, count, gamma.data_ptr<float>(),
+                                  beta.data_ptr<float>(), running_mean.data_ptr<float>(),
+                                  running_var.data_ptr<float>(), (float)momentum, (float)eps,
+                                  st.data_ptr<float>(), update_running, nbp, cur_stream());
+    return st;
+  }
+  at::Tensor sums = reduce_rows(partial, P, 2 * C);
   bn_stats_finalize_launch(sums.data_ptr<double>(), C, count, gamma.data_ptr<float>(),
                            beta.data_ptr<float>(), running_mean.data_ptr<float>(),
                            running_var.data_ptr<float>(), (float)momentum, (float)eps,
-                           st.data_ptr<float>(), update_running,
-                           (nbt.has_value() && nbt->defined()) ? nbt->data_ptr<int64_t>() : nullptr,
-                           cur_stream());
+                           st.data_ptr<float>(), update_running, nbp, cur_stream());
   return st;
 }
 
@@ -302,10 +313,9 @@ std::vector<at::Tensor> bn_backward(const c10::optional<at::Tensor>& dA,
   at::Tensor dbeta = into ? *dbeta_out : at::empty({C}, fopts);
   at::Tensor coefs = at::empty({3, C}, fopts);
   const double count = (double)g.N * g.D * g.H * g.W;
-  at::Tensor sums = reduce_rows(partial, nb, 2 * C);
-  bn_grad_finalize_launch(sums.data_ptr<double>(), C, count, gamma.data_ptr<float>(), s + C,
-                          dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), coefs.data_ptr<float>(),
-                          into, cur_stream());
+  bn_grad_finalize_rows_launch(partial.data_ptr<float>(), nb, C, count, gamma.data_ptr<float>(),
+                               s + C, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+                               coefs.data_ptr<float>(), into, cur_stream());
   at::Tensor dY = at::empty_like(y);
   bn_bwd_apply_launch(pA, pP, bptr(y), s + 2 * C, s + 3 * C, s, s + C, coefs.data_ptr<float>(), gs,
                       bptr_mut(dY), g.dims, g.N, g.D, g.H, g.W, C, cur_stream());
@@ -390,18 +400,22 @@ std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
   const bool into = dw_out.has_value() && dw_out->defined();
   at::Tensor dW = into ? *dw_out : at::empty(ws, fopts);
   const long long NW = (long long)a.M * a.N;
-  at::Tensor wsums = reduce_rows(part, splits, NW);
-  scatter_sums_launch(wsums.data_ptr<double>(), NW, dW.data_ptr<float>(), 1, g.C, S, go.C, 1.f,
-                      into, cur_stream());
+  at::Tensor tmp = splits > 64 ? at::empty({(int64_t)((splits + 63) / 64) * NW},
+                                           x.options().dtype(at::kDouble))
+                               : at::empty({0}, x.options().dtype(at::kDouble));
+  reduce_rows_scatter_launch(part.data_ptr<float>(), splits, NW, tmp.data_ptr<double>(),
+                             dW.data_ptr<float>(), 1, g.C, S, go.C, into, cur_stream());
   // bias gradient: per-channel sum of dOut
   const long long P = (long long)go.N * go.D * go.H * go.W;
   const int nb = (int)std::max<long long>(1, std::min<long long>((P + 1023) / 1024, 1024));
   at::Tensor cpart = at::empty({nb, go.C}, fopts);
   channel_sum_launch(bptr(dout), P, go.C, cpart.data_ptr<float>(), nb, cur_stream());
   at::Tensor db = into ? *db_out : at::empty({go.C}, fopts);
-  at::Tensor csums = reduce_rows(cpart, nb, go.C);
-  scatter_sums_launch(csums.data_ptr<double>(), go.C, db.data_ptr<float>(), 2, 0, 0, 0, 1.f, into,
-                      cur_stream());
+  at::Tensor ctmp = nb > 64 ? at::empty({(int64_t)((nb + 63) / 64) * go.C},
+                                        x.options().dtype(at::kDouble))
+                            : at::empty({0}, x.options().dtype(at::kDouble));
+  reduce_rows_scatter_launch(cpart.data_ptr<float>(), nb, go.C, ctmp.data_ptr<double>(),
+                             db.data_ptr<float>(), 2, 0, 0, 0, into, cur_stream());
   if (into) return {at::empty({0}, fopts), at::empty({0}, fopts)};
   return {dW, db};
 }

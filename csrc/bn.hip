@@ -210,7 +210,10 @@ int grid_for(long long items, int per_block) {
 
 }  // namespace
 
-int bn_bwd_reduce_blocks(long long items) { return grid_for(items, 64); }
+int bn_bwd_reduce_blocks(long long items) {
+  // <= 512 partial rows: the per-channel finalize reads them in one kernel
+  return (int)std::max<long long>(1, std::min<long long>((items + 63) / 64, 512));
+}
 
 void bn_relu_apply_launch(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
                           bf16_t* pooled, int dims, int N, int D, int H, int W, int C,

@@ -214,6 +214,13 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // BN statistics accumulate in registers across all items of this workgroup: every item
+  // of a workgroup has the same n tile (grid % nTilesN == 0, enforced by the launcher)
+  float s1[NT][4], s2[NT][4];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { s1[nt][i] = 0.f; s2[nt][i] = 0.f; }
 
   if (S > 0) {
     issue_A(0, 0, 0);
@@ -271,11 +278,6 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
       // lane holds channels co..co+3 (co = co0 + wn*NT*16 + nt*16 + 4*(lane>>4)) of pixel
       // (wm*MT*16 + mt*16 + (lane&15)) of the tile
       const Item it = item_of(k);
-      float s1[NT][4], s2[NT][4];
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { s1[nt][i] = 0.f; s2[nt][i] = 0.f; }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
@@ -307,23 +309,37 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
           acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         }
       }
-      if (p.stats != nullptr) {
-        // reduce over the 16 pixel lanes (lane & 15) sharing the same channels
+    }
+  }
+
+  // ---- one BN-statistics partial row per workgroup: shuffle over the 16 pixel lanes,
+  // LDS float atomics over the wave rows, one coalesced row write
+  if (p.stats != nullptr) {
+    dma_wait<0>();
+    lds_sync();
+    float* red = reinterpret_cast<float*>(base);          // halo buffers are free now
+    const int co0 = my_items > 0 ? item_of(0).co0 : 0;
+    for (int c = tid; c < 2 * BN; c += 256) red[c] = 0.f;
+    lds_sync();
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
+    for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float a1 = s1[nt][i], a2 = s2[nt][i];
+      for (int i = 0; i < 4; ++i) {
+        float a1 = s1[nt][i], a2 = s2[nt][i];
 #pragma unroll
-            for (int o = 1; o < 16; o <<= 1) { a1 += __shfl_xor(a1, o, 64); a2 += __shfl_xor(a2, o, 64); }
-            const int co = it.co0 + wn * (NT * 16) + nt * 16 + 4 * (lane >> 4) + i;
-            if ((lane & 15) == 0 && co < p.Cout) {
-              float* row = p.stats + ((long long)it.mtile * WM + wm) * 2 * p.Cout;
-              row[co] = a1;
-              row[p.Cout + co] = a2;
-            }
-          }
+        for (int o = 1; o < 16; o <<= 1) { a1 += __shfl_xor(a1, o, 64); a2 += __shfl_xor(a2, o, 64); }
+        if ((lane & 15) == 0) {
+          const int col = wn * (NT * 16) + nt * 16 + 4 * (lane >> 4) + i;
+          atomicAdd(red + col, a1);
+          atomicAdd(red + BN + col, a2);
+        }
       }
+    lds_sync();
+    float* row = p.stats + (long long)blockIdx.x * 2 * p.Cout;
+    for (int c = tid; c < p.Cout; c += 256) {      // full row: zeros outside this n tile
+      const bool mine = c >= co0 && c < co0 + BN;
+      row[c] = mine ? red[c - co0] : 0.f;
+      row[p.Cout + c] = mine ? red[BN + c - co0] : 0.f;
     }
   }
 }
@@ -333,7 +349,10 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO>;
   const int items = a.nTilesM * a.nTilesN;
   int grid = items;
-  if (a.persist_blocks > 0 && grid > a.persist_blocks) grid = a.persist_blocks;
+  if (a.persist_blocks > 0 && grid > a.persist_blocks) {
+    grid = a.persist_blocks / a.nTilesN * a.nTilesN;   // keeps each block on one n tile
+  }
+  a.stat_rows = grid;
   hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO>), dim3(grid), dim3(256),
                      C::SMEM, st, a);
 }

@@ -25,11 +25,13 @@ struct ConvFwdArgs {
   const float* bias;              // optional
   bf16_t* Y1;
   bf16_t* Y2;
-  float* stats;                   // optional [nTilesM * WM][2][Cout] partial (sum, sum^2)
+  float* stats;                   // optional [grid][2][Cout] per-workgroup (sum, sum^2); rows of
+                                  // channels outside a workgroup's n tile are not written
   int TD, TH, TW;
   int tilesD, tilesH, tilesW;
   int nTilesM, nTilesN;
   int persist_blocks;             // grid cap (persistent workgroups); 0 = one per item
+  int stat_rows;                  // out: rows written to `stats` (one per workgroup)
 };
 void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st);
 int conv3_fwd_cfg_wm(int cfg);
@@ -143,6 +145,16 @@ void bn_stats_finalize_launch(const double* sums, int C, double count, const flo
 void bn_grad_finalize_launch(const double* sums, int C, double count, const float* gamma,
                              const float* invstd, float* dgamma, float* dbeta, float* coefs,
                              bool accumulate, hipStream_t st);
+// single-kernel variants reading the partial rows directly (P small): one block per channel
+void bn_stats_finalize_rows_launch(const float* partial, int P, int C, double count,
+                                   const float* gamma, const float* beta, float* running_mean,
+                                   float* running_var, float momentum, float eps, float* out4,
+                                   bool update_running, int64_t* nbt, hipStream_t st);
+void bn_grad_finalize_rows_launch(const float* partial, int P, int C, double count,
+                                  const float* gamma, const float* invstd, float* dgamma,
+                                  float* dbeta, float* coefs, bool accumulate, hipStream_t st);
+void reduce_rows_scatter_launch(const float* in, int R, long long N, double* tmp, float* dst,
+                                int mode, int A, int T, int B, bool accumulate, hipStream_t st);
 void scatter_sums_launch(const double* sums, long long N, float* dst, int mode, int A, int T,
                          int B, float scale, bool accumulate, hipStream_t st);
 

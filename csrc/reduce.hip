@@ -93,7 +93,123 @@ __global__ void scatter_sums_kernel(const double* __restrict__ sums, long long N
   }
 }
 
+// one block per channel: fp64 sum of P partial rows, then finalize (P <= a few thousand)
+DDLPC_DEVICE void block_sum2(double& a, double& b) {
+  __shared__ double r1[4], r2[4];
+  a = wave_sum_d(a);
+  b = wave_sum_d(b);
+  if ((threadIdx.x & 63) == 0) { r1[threadIdx.x >> 6] = a; r2[threadIdx.x >> 6] = b; }
+  __syncthreads();
+  a = r1[0] + r1[1] + r1[2] + r1[3];
+  b = r2[0] + r2[1] + r2[2] + r2[3];
+}
+
+__global__ void bn_stats_rows_kernel(const float* __restrict__ partial, int P, int C, double count,
+                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                     float* running_mean, float* running_var, float momentum,
+                                     float eps, float* __restrict__ out4, int update_running,
+                                     int64_t* nbt) {
+  const int c = blockIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int r = threadIdx.x; r < P; r += 256) {
+    a += partial[(long long)r * 2 * C + c];
+    b += partial[(long long)r * 2 * C + C + c];
+  }
+  block_sum2(a, b);
+  if (threadIdx.x != 0) return;
+  if (c == 0 && update_running && nbt != nullptr) nbt[0] += 1;
+  const double mean = a / count;
+  double var = b / count - mean * mean;
+  if (var < 0) var = 0;
+  const float inv = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * inv;
+  out4[c] = (float)mean;
+  out4[C + c] = inv;
+  out4[2 * C + c] = sc;
+  out4[3 * C + c] = beta[c] - (float)mean * sc;
+  if (update_running) {
+    const double unb = count > 1 ? var * count / (count - 1) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+  }
+}
+
+__global__ void bn_grad_rows_kernel(const float* __restrict__ partial, int P, int C, double count,
+                                    const float* __restrict__ gamma,
+                                    const float* __restrict__ invstd, float* dgamma, float* dbeta,
+                                    float* coefs, int accumulate) {
+  const int c = blockIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int r = threadIdx.x; r < P; r += 256) {
+    a += partial[(long long)r * 2 * C + c];
+    b += partial[(long long)r * 2 * C + C + c];
+  }
+  block_sum2(a, b);
+  if (threadIdx.x != 0) return;
+  dbeta[c] = accumulate ? dbeta[c] + (float)a : (float)a;
+  dgamma[c] = accumulate ? dgamma[c] + (float)b : (float)b;
+  coefs[c] = gamma[c] * invstd[c];
+  coefs[C + c] = (float)(a / count);
+  coefs[2 * C + c] = (float)(b / count);
+}
+
+// final pass fused with the scatter/accumulate into the destination gradient
+template <typename T>
+__global__ void rows_sum_scatter_kernel(const T* __restrict__ in, int R, long long N, float* dst,
+                                        int mode, int A, int Tt, int B, int accumulate) {
+  const long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (j >= N) return;
+  double s = 0.0;
+#pragma unroll 8
+  for (int r = 0; r < R; ++r) s += (double)in[(long long)r * N + j];
+  long long d = j;
+  if (mode == 0) {
+    const int ci = (int)(j % B);
+    const int tap = (int)((j / B) % Tt);
+    const long long co = j / ((long long)B * Tt);
+    d = (co * B + ci) * Tt + tap;
+  } else if (mode == 1) {
+    const int co = (int)(j % B);
+    const int sub = (int)((j / B) % Tt);
+    const long long ci = j / ((long long)B * Tt);
+    d = (ci * B + co) * Tt + sub;
+  }
+  const float v = (float)s;
+  dst[d] = accumulate ? dst[d] + v : v;
+}
+
 }  // namespace
+
+void bn_stats_finalize_rows_launch(const float* partial, int P, int C, double count,
+                                   const float* gamma, const float* beta, float* running_mean,
+                                   float* running_var, float momentum, float eps, float* out4,
+                                   bool update_running, int64_t* nbt, hipStream_t st) {
+  hipLaunchKernelGGL(bn_stats_rows_kernel, dim3(C), dim3(256), 0, st, partial, P, C, count, gamma,
+                     beta, running_mean, running_var, momentum, eps, out4, update_running ? 1 : 0,
+                     nbt);
+}
+
+void bn_grad_finalize_rows_launch(const float* partial, int P, int C, double count,
+                                  const float* gamma, const float* invstd, float* dgamma,
+                                  float* dbeta, float* coefs, bool accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(bn_grad_rows_kernel, dim3(C), dim3(256), 0, st, partial, P, C, count, gamma,
+                     invstd, dgamma, dbeta, coefs, accumulate ? 1 : 0);
+}
+
+// dst (+)= permute(sum over rows of in[R][N]); one pass when R <= 64, else chunk sums first
+void reduce_rows_scatter_launch(const float* in, int R, long long N, double* tmp, float* dst,
+                                int mode, int A, int T, int B, bool accumulate, hipStream_t st) {
+  const unsigned gx = (unsigned)((N + 255) / 256);
+  if (R <= 64) {
+    hipLaunchKernelGGL(rows_sum_scatter_kernel<float>, dim3(gx), dim3(256), 0, st, in, R, N, dst,
+                       mode, A, T, B, accumulate ? 1 : 0);
+    return;
+  }
+  const int RC = (R + RB - 1) / RB;
+  hipLaunchKernelGGL(rows_chunk_sum_kernel<float>, dim3(gx, RC), dim3(256), 0, st, in, R, N, tmp);
+  hipLaunchKernelGGL(rows_sum_scatter_kernel<double>, dim3(gx), dim3(256), 0, st, tmp, RC, N, dst,
+                     mode, A, T, B, accumulate ? 1 : 0);
+}
 
 int reduce_rows_chunks(int R) { return (R + RB - 1) / RB; }
 
