@@ -1,0 +1,81 @@
+#!/usr/bin/env python
+"""Per-layer micro-benchmark of the 3x3 conv kernels on the flagship U-Net shapes (B=32, 256^2).
+
+Prints one line per (layer, pass) with time and TFLOP/s; run under rocprofv3 --pmc to get
+counters per kernel.  ``--only`` filters layers by name substring.
+"""
+import argparse
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+LAYERS = [  # name, H, C1, C2, Cout, prologue
+    ("enc1.a", 256, 8, 0, 32, False), ("enc1.b", 256, 32, 0, 32, True),
+    ("enc2.a", 128, 32, 0, 64, False), ("enc2.b", 128, 64, 0, 64, True),
+    ("enc3.a", 64, 64, 0, 128, False), ("enc3.b", 64, 128, 0, 128, True),
+    ("enc4.a", 32, 128, 0, 256, False), ("enc4.b", 32, 256, 0, 256, True),
+    ("enc5.a", 16, 256, 0, 256, False), ("enc5.b", 16, 256, 0, 256, True),
+    ("mid.a", 8, 256, 0, 256, False), ("mid.b", 8, 256, 0, 256, True),
+    ("dec5.a", 16, 256, 256, 256, False), ("dec5.b", 16, 256, 0, 256, True),
+    ("dec4.a", 32, 256, 256, 256, False), ("dec4.b", 32, 256, 0, 256, True),
+    ("dec3.a", 64, 256, 128, 128, False), ("dec3.b", 64, 128, 0, 128, True),
+    ("dec2.a", 128, 128, 64, 64, False), ("dec2.b", 128, 64, 0, 64, True),
+    ("dec1.a", 256, 64, 32, 32, False), ("dec1.b", 256, 32, 0, 32, True),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--passes", default="fwd,dgrad,wgrad")
+    a = ap.parse_args()
+    from ddlpc.ops import _ext
+    from ddlpc.ops.fused_unet import _ConvPack
+    F = _ext.ops()
+    dev = "cuda"
+    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+    for name, H, C1, C2, Co, pro in LAYERS:
+        if a.only and a.only not in name:
+            continue
+        N = a.batch
+        x1 = torch.randn(N, H, H, C1, device=dev).bfloat16()
+        x2 = torch.randn(N, H, H, C2, device=dev).bfloat16() if C2 else None
+        dy = torch.randn(N, H, H, Co, device=dev).bfloat16()
+        conv = torch.nn.Module()
+        conv.weight = torch.nn.Parameter(torch.randn(Co, C1 + C2, 3, 3, device=dev) * 0.05)
+        pk = _ConvPack(conv, 0, True)
+        F.weight_pack(torch.tensor([pk.entry()], dtype=torch.int64, device=dev), 1, pk.numel())
+        sc = torch.rand(C1, device=dev) + 0.5 if pro else None
+        sh = torch.randn(C1, device=dev) * 0.1 if pro else None
+        flops = 2.0 * N * H * H * Co * 9 * (C1 + C2)
+        fns = {
+            "fwd": lambda: F.conv3_fwd(x1, x2, pk.fwd, None, sc, sh, Co, 0, True),
+            "dgrad": lambda: F.conv3_fwd(dy, None, pk.dgrad, None, None, None, C1 + C2,
+                                         C1 if C2 else 0, False),
+            "wgrad": lambda: F.conv3_wgrad(dy, x1, x2, sc, sh),
+        }
+        for ps in a.passes.split(","):
+            if ps == "dgrad" and name == "enc1.a":
+                continue
+            fn = fns[ps]
+            fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                fn()
+            e1.record()
+            e1.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / a.iters
+            tot[ps] += us
+            print(f"{name:8s} {ps:6s} {us:9.1f} us  {flops / us / 1e6:8.1f} TF/s", flush=True)
+    print("totals (us):", {k: round(v, 1) for k, v in tot.items()})
+
+
+if __name__ == "__main__":
+    main()
