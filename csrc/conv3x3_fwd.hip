@@ -134,59 +134,82 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
     it.co0 = ntile * BN;
     return it;
   };
-  // halo element e (16 B) of this lane -> in-image pixel index or -1
-  auto halo_pix = [&](const Item& it, int e) {
+  // ---- per-lane DMA geometry, computed once (no integer division in the stage loop)
+  // A: element e = (i*4 + wave)*64 + lane of a halo buffer -> halo pixel (hd, hh, hw) and
+  //    the swizzled 8-channel sub-chunk it holds
+  int a_dw[C::A_ITERS], a_dh[C::A_ITERS], a_dd[C::A_ITERS], a_sub8[C::A_ITERS];
+  int a_pix[C::A_ITERS];       // in-image pixel of the item last issued, -1 = zero padding
+#pragma unroll
+  for (int i = 0; i < C::A_ITERS; ++i) {
+    const int e = (i * 4 + wave) * 64 + lane;
     const int px = e >> 2;
-    if (px >= halo) return -1;
+    a_sub8[i] = ((e & 3) ^ swz(px)) << 3;
     const int hw = px % HW2, hh = (px / HW2) % HH2;
     const int hd = DIMS == 3 ? px / (HW2 * HH2) : 1;
-    const int gw = it.w0 + hw - 1, gh = it.h0 + hh - 1, gd = it.d0 + hd - 1;
-    if (gw < 0 || gw >= p.W || gh < 0 || gh >= p.H || gd < 0 || gd >= p.D) return -1;
-    return (gd * p.H + gh) * p.W + gw;
+    a_dw[i] = px < halo ? hw - 1 : -(1 << 20);       // outside the halo: always padding
+    a_dh[i] = hh - 1;
+    a_dd[i] = hd - 1;
+    a_pix[i] = -1;
+  }
+  // B: row (tap-in-group, channel) -> byte offset without the (chunk, group) term
+  const int co0_blk = (int)blockIdx.x % p.nTilesN * BN;   // every item of a block: same n tile
+  int b_off[C::B_ITERS], b_sub8[C::B_ITERS];
+#pragma unroll
+  for (int i = 0; i < C::B_ITERS; ++i) {
+    const int e = (i * 4 + wave) * 64 + lane;
+    const int row = e >> 2;
+    const int sub = (e & 3) ^ swz(row);
+    const int tl = row / BN, col = row % BN;
+    const int co = co0_blk + col;
+    b_sub8[i] = sub * 8;
+    b_off[i] = (tl < 3 && co < p.Cout) ? ((co * p.taps + tl) * p.CinW + sub * 8) * 2 : -1;
+  }
+  int a_item = -1;                 // item whose pixels a_pix currently holds
+  int a_nimg = 0;
+  auto set_item_pixels = [&](int k) {
+    const Item it = item_of(k);
+    a_item = k;
+    a_nimg = it.n_img;
+#pragma unroll
+    for (int i = 0; i < C::A_ITERS; ++i) {
+      const int gw = it.w0 + a_dw[i], gh = it.h0 + a_dh[i], gd = it.d0 + a_dd[i];
+      const bool ok = gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && gd >= 0 && gd < p.D;
+      a_pix[i] = ok ? (gd * p.H + gh) * p.W + gw : -1;
+    }
   };
   auto issue_A = [&](int k, int chunk, int buf) {
-    const Item it = item_of(k);
+    if (k != a_item) set_item_pixels(k);
     const int cbase = chunk * BK;
     const bool second = cbase >= p.C1;              // chunk served by X2 (C1 % 32 == 0)
     const int Cs = second ? p.C2 : p.C1;
     const int c0 = second ? cbase - p.C1 : cbase;
     const bf16_t* src = second ? p.X2 : p.X1;
-    const auto r = make_rsrc(src + it.n_img * img_px * Cs, (unsigned)(img_px * Cs * 2));
+    const auto r = make_rsrc(src + a_nimg * img_px * Cs, (unsigned)(img_px * Cs * 2));
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
-      const int e = (i * 4 + wave) * 64 + lane;
-      const int pix = halo_pix(it, e);
-      const int c8 = c0 + (((e & 3) ^ swz(e >> 2)) << 3);
-      const unsigned off = (pix >= 0 && c8 < Cs) ? (unsigned)(pix * Cs + c8) * 2u : kOOB;
+      const int c8 = c0 + a_sub8[i];
+      const unsigned off = (a_pix[i] >= 0 && c8 < Cs) ? (unsigned)(a_pix[i] * Cs + c8) * 2u : kOOB;
       dma16(r, sA(buf) + (i * 4 + wave) * 1024, off);
     }
   };
-  auto issue_B = [&](int k, int chunk, int grp, int buf) {
-    const int co0 = item_of(k).co0;
+  auto issue_B = [&](int chunk, int grp, int buf) {
+    const int soff = (grp * 3 * p.CinW + chunk * BK) * 2;
 #pragma unroll
     for (int i = 0; i < C::B_ITERS; ++i) {
-      const int e = (i * 4 + wave) * 64 + lane;
-      const int row = e >> 2;
-      const int sub = (e & 3) ^ swz(row);
-      const int tl = row / BN, col = row % BN;
-      const int co = co0 + col;
-      const int c8 = chunk * BK + sub * 8;
-      unsigned off = kOOB;
-      if (tl < 3 && co < p.Cout && c8 < p.CinW)
-        off = (unsigned)(((co * p.taps) + grp * 3 + tl) * p.CinW + c8) * 2u;
-      dma16(rW, sB(buf) + (i * 4 + wave) * 1024, off);
+      const bool ok = b_off[i] >= 0 && chunk * BK + b_sub8[i] < p.CinW;
+      dma16(rW, sB(buf) + (i * 4 + wave) * 1024, ok ? (unsigned)(b_off[i] + soff) : kOOB);
     }
   };
-  // prologue BN+ReLU applied in LDS on the landed halo (padding stays zero)
-  auto transform_A = [&](int k, int chunk, int buf) {
+  // prologue BN+ReLU applied in LDS on the landed halo (padding stays zero); a_pix holds
+  // this chunk's item (the next item's pixels are only loaded after this transform)
+  auto transform_A = [&](int chunk, int buf) {
     const int cbase = chunk * BK;
     if (cbase >= p.C1) return;                      // X2 channels: no prologue
-    const Item it = item_of(k);
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
       const int e = (i * 4 + wave) * 64 + lane;    // same element this lane DMA'd
-      const int c8 = cbase + (((e & 3) ^ swz(e >> 2)) << 3);
-      if (c8 < p.C1 && halo_pix(it, e) >= 0) {
+      const int c8 = cbase + a_sub8[i];
+      if (c8 < p.C1 && a_pix[i] >= 0) {
         uint4* q = reinterpret_cast<uint4*>(sA(buf) + e * 16);
         float f[8];
         unpack8(*q, f);
@@ -224,7 +247,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
 
   if (S > 0) {
     issue_A(0, 0, 0);
-    issue_B(0, 0, 0, 0);
+    issue_B(0, 0, 0);
   }
   for (int s = 0; s < S; ++s) {
     const int k = s / spi, rem = s % spi;
@@ -237,12 +260,12 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
     else dma_wait<0>();
     lds_sync();
     if (grp == 0 && has_pro) {
-      transform_A(k, chunk, cseq & 1);
+      transform_A(chunk, cseq & 1);
       lds_sync();
     }
     if (s + 1 < S) {
-      const int k1 = (s + 1) / spi, r1 = (s + 1) % spi;
-      issue_B(k1, r1 / NG, r1 % NG, (s + 1) & 1);
+      const int r1 = (s + 1) % spi;
+      issue_B(r1 / NG, r1 % NG, (s + 1) & 1);
     }
     if (grp == 0 && more_chunks) {
       const int k1 = (cseq + 1) / nchunks;
