@@ -155,15 +155,38 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   if (a.Co1 < a.Cout) y2 = at::empty(shape_with_c(g, a.Cout - a.Co1), opts);
   at::Tensor stats;
   a.persist_blocks = 2 * num_cus();
-  if (want_stats) {
+  a.npix = (long long)g.N * g.D * g.H * g.W;
+  // small layers: split the input-channel chunks across workgroups so the grid fills the
+  // chip; partial sums go through an fp32 buffer and a deterministic finalize
+  const int nchunks_total = (a.Cin + 31) / 32;
+  a.ksplit = 1;
+  {
     const int items = a.nTilesM * a.nTilesN;
-    const int grid = items > a.persist_blocks ? a.persist_blocks / a.nTilesN * a.nTilesN : items;
+    int best = 1;
+    if (items < num_cus())
+      for (int ks = 2; ks <= 8; ++ks)
+        if (nchunks_total % ks == 0 && nchunks_total / ks >= 2 && items * ks <= 2 * num_cus())
+          best = ks;
+    a.ksplit = best;
+  }
+  at::Tensor part;
+  if (a.ksplit > 1) {
+    part = at::empty({(int64_t)a.ksplit * a.npix * a.Cout}, opts.dtype(at::kFloat));
+    a.part = part.data_ptr<float>();
+  }
+  const int fin_grid = (int)std::min<long long>(std::max<long long>(1, a.npix / 64), 512);
+  if (want_stats) {
+    const int items = a.nTilesM * a.nTilesN * a.ksplit;
+    const int q = a.nTilesN * a.ksplit;
+    const int grid = a.ksplit > 1 ? fin_grid
+                                  : (items > a.persist_blocks ? a.persist_blocks / q * q : items);
     stats = at::empty({(int64_t)grid, 2, a.Cout}, opts.dtype(at::kFloat));
   }
   a.Y1 = bptr_mut(y1);
   a.Y2 = y2.defined() ? bptr_mut(y2) : nullptr;
   a.stats = want_stats ? stats.data_ptr<float>() : nullptr;
   conv3_fwd_launch(a, cfg, cur_stream());
+  if (a.ksplit > 1) conv3_splitk_finalize_launch(a, fin_grid, cur_stream());
   at::Tensor none = at::empty({0}, opts);
   return {y1, y2.defined() ? y2 : none, stats.defined() ? stats : none};
 }
@@ -372,7 +395,8 @@ at::Tensor convt_dgrad(const at::Tensor& dout, const at::Tensor& wd, int64_t cin
 
 std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
                                     const c10::optional<at::Tensor>& dw_out,
-                                    const c10::optional<at::Tensor>& db_out) {
+                                    const c10::optional<at::Tensor>& db_out,
+                                    const c10::optional<at::Tensor>& colsum_rows) {
   CHECK_DEV(x); CHECK_CONTIG(x); CHECK_CONTIG(dout);
   c10::DeviceGuard guard(x.device());
   const Geo g = geo_of(x);
@@ -405,17 +429,29 @@ std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
                                : at::empty({0}, x.options().dtype(at::kDouble));
   reduce_rows_scatter_launch(part.data_ptr<float>(), splits, NW, tmp.data_ptr<double>(),
                              dW.data_ptr<float>(), 1, g.C, S, go.C, into, cur_stream());
-  // bias gradient: per-channel sum of dOut
-  const long long P = (long long)go.N * go.D * go.H * go.W;
-  const int nb = (int)std::max<long long>(1, std::min<long long>((P + 1023) / 1024, 1024));
-  at::Tensor cpart = at::empty({nb, go.C}, fopts);
-  channel_sum_launch(bptr(dout), P, go.C, cpart.data_ptr<float>(), nb, cur_stream());
+  // bias gradient: per-channel sum of dOut.  When dOut came out of a conv3 data-gradient
+  // epilogue, its per-workgroup channel sums are already there (rows [R][2][Ctot], sum part
+  // first): reduce those instead of re-reading dOut.
   at::Tensor db = into ? *db_out : at::empty({go.C}, fopts);
-  at::Tensor ctmp = nb > 64 ? at::empty({(int64_t)((nb + 63) / 64) * go.C},
-                                        x.options().dtype(at::kDouble))
-                            : at::empty({0}, x.options().dtype(at::kDouble));
-  reduce_rows_scatter_launch(cpart.data_ptr<float>(), nb, go.C, ctmp.data_ptr<double>(),
-                             db.data_ptr<float>(), 2, 0, 0, 0, into, cur_stream());
+  if (colsum_rows.has_value() && colsum_rows->defined() && colsum_rows->numel() > 0) {
+    const at::Tensor& cr = *colsum_rows;
+    TORCH_CHECK(cr.dim() == 3 && cr.size(1) == 2 && cr.size(2) >= go.C, "colsum rows [R][2][C]");
+    const int R = (int)cr.size(0);
+    at::Tensor ctmp = R > 64 ? at::empty({(int64_t)((R + 63) / 64) * go.C}, x.options().dtype(at::kDouble))
+                             : at::empty({0}, x.options().dtype(at::kDouble));
+    reduce_rows_scatter_launch(cr.data_ptr<float>(), R, go.C, ctmp.data_ptr<double>(),
+                               db.data_ptr<float>(), 2, 0, 0, 0, into, cur_stream(), 2 * cr.size(2));
+  } else {
+    const long long P = (long long)go.N * go.D * go.H * go.W;
+    const int nb = (int)std::max<long long>(1, std::min<long long>((P + 1023) / 1024, 1024));
+    at::Tensor cpart = at::empty({nb, go.C}, fopts);
+    channel_sum_launch(bptr(dout), P, go.C, cpart.data_ptr<float>(), nb, cur_stream());
+    at::Tensor ctmp = nb > 64 ? at::empty({(int64_t)((nb + 63) / 64) * go.C},
+                                          x.options().dtype(at::kDouble))
+                              : at::empty({0}, x.options().dtype(at::kDouble));
+    reduce_rows_scatter_launch(cpart.data_ptr<float>(), nb, go.C, ctmp.data_ptr<double>(),
+                               db.data_ptr<float>(), 2, 0, 0, 0, into, cur_stream());
+  }
   if (into) return {at::empty({0}, fopts), at::empty({0}, fopts)};
   return {dW, db};
 }
@@ -607,7 +643,8 @@ TORCH_LIBRARY(ddlpc, m) {
         "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None) -> Tensor[]");
   m.def("convt_fwd(Tensor x, Tensor wt, Tensor? bias, int cout) -> Tensor");
   m.def("convt_dgrad(Tensor dout, Tensor wd, int cin) -> Tensor");
-  m.def("convt_wgrad(Tensor x, Tensor dout, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) -> Tensor[]");
+  m.def("convt_wgrad(Tensor x, Tensor dout, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, "
+        "Tensor? colsum_rows=None) -> Tensor[]");
   m.def("head_ce_fwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, int ignore_index) -> Tensor");
   m.def("head_ce_bwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, Tensor out3, Tensor? gscale, "
         "int ignore_index, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) -> Tensor[]");

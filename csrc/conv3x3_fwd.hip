@@ -107,9 +107,10 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
   const int HW2 = p.TW + 2, HH2 = p.TH + 2;
   const int halo = (DIMS == 3 ? p.TD + 2 : 1) * HH2 * HW2;
   const long long img_px = (long long)p.D * p.H * p.W;
-  const int n_items = p.nTilesM * p.nTilesN;
+  const int KS = p.ksplit;                        // channel-chunk split (small layers)
+  const int n_items = p.nTilesM * p.nTilesN * KS;
   const int my_items = n_items > (int)blockIdx.x ? (n_items - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-  const int nchunks = (p.Cin + BK - 1) / BK;
+  const int nchunks = ((p.Cin + BK - 1) / BK) / KS;  // chunks per item (KS divides the total)
   const int spi = nchunks * NG;                   // stages per item
   const int S = my_items * spi;
 
@@ -119,10 +120,12 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
 
   const auto rW = make_rsrc(p.Wt, (unsigned)((long long)p.Cout * p.taps * p.CinW * 2));
 
-  struct Item { int mtile, n_img, d0, h0, w0, co0; };
+  struct Item { int mtile, n_img, d0, h0, w0, co0, ks; };
   auto item_of = [&](int k) {
     Item it;
-    const int w = (int)blockIdx.x + k * (int)gridDim.x;
+    int w = (int)blockIdx.x + k * (int)gridDim.x;
+    it.ks = w % KS;
+    w /= KS;
     const int ntile = w % p.nTilesN;
     int m = w / p.nTilesN;
     it.mtile = m;
@@ -152,7 +155,8 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
     a_pix[i] = -1;
   }
   // B: row (tap-in-group, channel) -> byte offset without the (chunk, group) term
-  const int co0_blk = (int)blockIdx.x % p.nTilesN * BN;   // every item of a block: same n tile
+  // every item of a block has the same n tile (launcher: grid % (KS * nTilesN) == 0)
+  const int co0_blk = (int)blockIdx.x / KS % p.nTilesN * BN;
   int b_off[C::B_ITERS], b_sub8[C::B_ITERS];
 #pragma unroll
   for (int i = 0; i < C::B_ITERS; ++i) {
@@ -177,9 +181,10 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
       a_pix[i] = ok ? (gd * p.H + gh) * p.W + gw : -1;
     }
   };
+  auto chunk0_of = [&](int k) { return ((int)blockIdx.x + k * (int)gridDim.x) % KS * nchunks; };
   auto issue_A = [&](int k, int chunk, int buf) {
     if (k != a_item) set_item_pixels(k);
-    const int cbase = chunk * BK;
+    const int cbase = (chunk0_of(k) + chunk) * BK;
     const bool second = cbase >= p.C1;              // chunk served by X2 (C1 % 32 == 0)
     const int Cs = second ? p.C2 : p.C1;
     const int c0 = second ? cbase - p.C1 : cbase;
@@ -192,7 +197,8 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
       dma16(r, sA(buf) + (i * 4 + wave) * 1024, off);
     }
   };
-  auto issue_B = [&](int chunk, int grp, int buf) {
+  auto issue_B = [&](int k, int chunk_local, int grp, int buf) {
+    const int chunk = chunk0_of(k) + chunk_local;
     const int soff = (grp * 3 * p.CinW + chunk * BK) * 2;
 #pragma unroll
     for (int i = 0; i < C::B_ITERS; ++i) {
@@ -202,8 +208,8 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
   };
   // prologue BN+ReLU applied in LDS on the landed halo (padding stays zero); a_pix holds
   // this chunk's item (the next item's pixels are only loaded after this transform)
-  auto transform_A = [&](int chunk, int buf) {
-    const int cbase = chunk * BK;
+  auto transform_A = [&](int k, int chunk, int buf) {
+    const int cbase = (chunk0_of(k) + chunk) * BK;
     if (cbase >= p.C1) return;                      // X2 channels: no prologue
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
@@ -247,7 +253,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
 
   if (S > 0) {
     issue_A(0, 0, 0);
-    issue_B(0, 0, 0);
+    issue_B(0, 0, 0, 0);
   }
   for (int s = 0; s < S; ++s) {
     const int k = s / spi, rem = s % spi;
@@ -260,12 +266,12 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
     else dma_wait<0>();
     lds_sync();
     if (grp == 0 && has_pro) {
-      transform_A(chunk, cseq & 1);
+      transform_A(k, chunk, cseq & 1);
       lds_sync();
     }
     if (s + 1 < S) {
       const int r1 = (s + 1) % spi;
-      issue_B(r1 / NG, r1 % NG, (s + 1) & 1);
+      issue_B((s + 1) / spi, r1 / NG, r1 % NG, (s + 1) & 1);
     }
     if (grp == 0 && more_chunks) {
       const int k1 = (cseq + 1) / nchunks;
@@ -312,6 +318,13 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
           const int co = it.co0 + wn * (NT * 16) + nt * 16 + 4 * (lane >> 4);
+          if (KS > 1) {            // split-K partial: fp32 [ks][pixel][Cout], finalized later
+            if (valid && co < p.Cout)
+              *reinterpret_cast<float4*>(p.part + ((long long)it.ks * p.npix + gpix) * p.Cout + co) =
+                  make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]);
+            acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            continue;
+          }
           float v[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -337,7 +350,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
 
   // ---- one BN-statistics partial row per workgroup: shuffle over the 16 pixel lanes,
   // LDS float atomics over the wave rows, one coalesced row write
-  if (p.stats != nullptr) {
+  if (p.stats != nullptr && KS == 1) {
     dma_wait<0>();
     lds_sync();
     float* red = reinterpret_cast<float*>(base);          // halo buffers are free now
@@ -367,13 +380,66 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
   }
 }
 
+// split-K finalize: sum the KS fp32 partials (fixed order), + bias, bf16 store (optionally
+// split into two outputs), per-workgroup BN statistic rows of the stored values
+__global__ void conv_splitk_finalize_kernel(const float* __restrict__ part, int KS, long long npix,
+                                            int Cout, int Co1, const float* __restrict__ bias,
+                                            bf16_t* __restrict__ Y1, bf16_t* __restrict__ Y2,
+                                            float* __restrict__ stats) {
+  const int G = Cout / 8;
+  const int per = (blockDim.x / G) * G;
+  const int tid = threadIdx.x;
+  const int cg = tid % G;
+  const int c8 = cg * 8;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  if (tid < per) {
+    for (long long px = blockIdx.x * (long long)(per / G) + tid / G; px < npix;
+         px += (long long)gridDim.x * (per / G)) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = bias != nullptr ? bias[c8 + j] : 0.f;
+      for (int k = 0; k < KS; ++k) {
+        const float4* q = reinterpret_cast<const float4*>(part + ((long long)k * npix + px) * Cout + c8);
+        const float4 a = q[0], b = q[1];
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+        v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+      }
+      const uint4 pk = pack8(v);
+      if (c8 < Co1) *reinterpret_cast<uint4*>(Y1 + px * Co1 + c8) = pk;
+      else *reinterpret_cast<uint4*>(Y2 + px * (Cout - Co1) + (c8 - Co1)) = pk;
+      if (stats != nullptr) {
+        float r[8];
+        unpack8(pk, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { s1[j] += r[j]; s2[j] += r[j] * r[j]; }
+      }
+    }
+  }
+  if (stats == nullptr) return;
+  __shared__ float red[256];
+  for (int half = 0; half < 2; ++half)
+    for (int j = 0; j < 8; ++j) {
+      __syncthreads();
+      red[tid] = tid < per ? (half ? s2[j] : s1[j]) : 0.f;
+      __syncthreads();
+      for (int g2 = tid; g2 < G; g2 += blockDim.x) {
+        float t = 0.f;
+        for (int q = g2; q < per; q += G) t += red[q];
+        stats[((long long)blockIdx.x * 2 + half) * Cout + g2 * 8 + j] = t;
+      }
+    }
+}
+
 template <int DIMS, int WM, int WN, int MT, int NT, int HALO>
 void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO>;
-  const int items = a.nTilesM * a.nTilesN;
+  const int items = a.nTilesM * a.nTilesN * a.ksplit;
   int grid = items;
   if (a.persist_blocks > 0 && grid > a.persist_blocks) {
-    grid = a.persist_blocks / a.nTilesN * a.nTilesN;   // keeps each block on one n tile
+    const int q = a.nTilesN * a.ksplit;          // keeps each block on one n tile
+    grid = a.persist_blocks / q * q;
   }
   a.stat_rows = grid;
   hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO>), dim3(grid), dim3(256),
@@ -396,6 +462,11 @@ int conv3_fwd_cfg_bm(int cfg) { return cfg <= 1 ? 256 : cfg == 2 ? 128 : 64; }
 int conv3_fwd_cfg_halo(int dims, int cfg) {
   if (dims == 2) return cfg <= 1 ? 384 : cfg == 2 ? 192 : 128;
   return cfg <= 1 ? 704 : cfg == 2 ? 448 : 384;
+}
+
+void conv3_splitk_finalize_launch(ConvFwdArgs& a, int grid, hipStream_t st) {
+  hipLaunchKernelGGL(conv_splitk_finalize_kernel, dim3(grid), dim3(256), 0, st, a.part, a.ksplit,
+                     a.npix, a.Cout, a.Co1, a.bias, a.Y1, a.Y2, a.stats);
 }
 
 void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st) {

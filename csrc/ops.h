@@ -32,7 +32,11 @@ struct ConvFwdArgs {
   int nTilesM, nTilesN;
   int persist_blocks;             // grid cap (persistent workgroups); 0 = one per item
   int stat_rows;                  // out: rows written to `stats` (one per workgroup)
+  int ksplit;                     // >1: split the channel chunks, fp32 partials to `part`
+  float* part;                    // [ksplit][npix][Cout] fp32 (ksplit > 1)
+  long long npix;                 // N * D * H * W
 };
+void conv3_splitk_finalize_launch(ConvFwdArgs& a, int grid, hipStream_t st);
 void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st);
 int conv3_fwd_cfg_wm(int cfg);
 int conv3_fwd_cfg_bn(int cfg);
@@ -154,7 +158,8 @@ void bn_grad_finalize_rows_launch(const float* partial, int P, int C, double cou
                                   const float* gamma, const float* invstd, float* dgamma,
                                   float* dbeta, float* coefs, bool accumulate, hipStream_t st);
 void reduce_rows_scatter_launch(const float* in, int R, long long N, double* tmp, float* dst,
-                                int mode, int A, int T, int B, bool accumulate, hipStream_t st);
+                                int mode, int A, int T, int B, bool accumulate, hipStream_t st,
+                                long long ld = -1);
 void scatter_sums_launch(const double* sums, long long N, float* dst, int mode, int A, int T,
                          int B, float scale, bool accumulate, hipStream_t st);
 

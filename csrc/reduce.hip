@@ -18,14 +18,15 @@ constexpr int RB = 64;   // rows per chunk
 
 template <typename T>
 __global__ void rows_chunk_sum_kernel(const T* __restrict__ in, int R, long long N,
-                                      double* __restrict__ out) {
+                                      double* __restrict__ out, long long ld = -1) {
   const long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (j >= N) return;
+  if (ld < 0) ld = N;
   const int r0 = blockIdx.y * RB;
   const int r1 = min(R, r0 + RB);
   double s = 0.0;
 #pragma unroll 8
-  for (int r = r0; r < r1; ++r) s += (double)in[(long long)r * N + j];
+  for (int r = r0; r < r1; ++r) s += (double)in[(long long)r * ld + j];
   out[(long long)blockIdx.y * N + j] = s;
 }
 
@@ -156,12 +157,13 @@ __global__ void bn_grad_rows_kernel(const float* __restrict__ partial, int P, in
 // final pass fused with the scatter/accumulate into the destination gradient
 template <typename T>
 __global__ void rows_sum_scatter_kernel(const T* __restrict__ in, int R, long long N, float* dst,
-                                        int mode, int A, int Tt, int B, int accumulate) {
+                                        int mode, int A, int Tt, int B, int accumulate,
+                                        long long ld) {
   const long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (j >= N) return;
   double s = 0.0;
 #pragma unroll 8
-  for (int r = 0; r < R; ++r) s += (double)in[(long long)r * N + j];
+  for (int r = 0; r < R; ++r) s += (double)in[(long long)r * ld + j];
   long long d = j;
   if (mode == 0) {
     const int ci = (int)(j % B);
@@ -198,17 +200,19 @@ void bn_grad_finalize_rows_launch(const float* partial, int P, int C, double cou
 
 // dst (+)= permute(sum over rows of in[R][N]); one pass when R <= 64, else chunk sums first
 void reduce_rows_scatter_launch(const float* in, int R, long long N, double* tmp, float* dst,
-                                int mode, int A, int T, int B, bool accumulate, hipStream_t st) {
+                                int mode, int A, int T, int B, bool accumulate, hipStream_t st,
+                                long long ld) {
   const unsigned gx = (unsigned)((N + 255) / 256);
+  if (ld < 0) ld = N;
   if (R <= 64) {
     hipLaunchKernelGGL(rows_sum_scatter_kernel<float>, dim3(gx), dim3(256), 0, st, in, R, N, dst,
-                       mode, A, T, B, accumulate ? 1 : 0);
+                       mode, A, T, B, accumulate ? 1 : 0, ld);
     return;
   }
   const int RC = (R + RB - 1) / RB;
-  hipLaunchKernelGGL(rows_chunk_sum_kernel<float>, dim3(gx, RC), dim3(256), 0, st, in, R, N, tmp);
+  hipLaunchKernelGGL(rows_chunk_sum_kernel<float>, dim3(gx, RC), dim3(256), 0, st, in, R, N, tmp, ld);
   hipLaunchKernelGGL(rows_sum_scatter_kernel<double>, dim3(gx), dim3(256), 0, st, tmp, RC, N, dst,
-                     mode, A, T, B, accumulate ? 1 : 0);
+                     mode, A, T, B, accumulate ? 1 : 0, N);
 }
 
 int reduce_rows_chunks(int R) { return (R + RB - 1) / RB; }
@@ -219,20 +223,20 @@ void reduce_rows_launch(const float* in, int R, long long N, double* tmp, double
   const int RC = reduce_rows_chunks(R);
   const unsigned gx = (unsigned)((N + 255) / 256);
   if (RC == 1) {
-    hipLaunchKernelGGL(rows_chunk_sum_kernel<float>, dim3(gx, 1), dim3(256), 0, st, in, R, N, sums);
+    hipLaunchKernelGGL(rows_chunk_sum_kernel<float>, dim3(gx, 1), dim3(256), 0, st, in, R, N, sums, -1LL);
     return;
   }
-  hipLaunchKernelGGL(rows_chunk_sum_kernel<float>, dim3(gx, RC), dim3(256), 0, st, in, R, N, tmp);
+  hipLaunchKernelGGL(rows_chunk_sum_kernel<float>, dim3(gx, RC), dim3(256), 0, st, in, R, N, tmp, -1LL);
   int R2 = RC;
   const double* cur = tmp;
   while (reduce_rows_chunks(R2) > 1) {       // (only for > 4096 rows)
     const int RC2 = reduce_rows_chunks(R2);
     double* nxt = tmp + (long long)RC * N;   // second half of tmp is free scratch
-    hipLaunchKernelGGL(rows_chunk_sum_kernel<double>, dim3(gx, RC2), dim3(256), 0, st, cur, R2, N, nxt);
+    hipLaunchKernelGGL(rows_chunk_sum_kernel<double>, dim3(gx, RC2), dim3(256), 0, st, cur, R2, N, nxt, -1LL);
     cur = nxt;
     R2 = RC2;
   }
-  hipLaunchKernelGGL(rows_chunk_sum_kernel<double>, dim3(gx, 1), dim3(256), 0, st, cur, R2, N, sums);
+  hipLaunchKernelGGL(rows_chunk_sum_kernel<double>, dim3(gx, 1), dim3(256), 0, st, cur, R2, N, sums, -1LL);
 }
 
 void bn_stats_finalize_launch(const double* sums, int C, double count, const float* gamma,

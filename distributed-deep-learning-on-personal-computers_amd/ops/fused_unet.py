@@ -178,7 +178,13 @@ class _DoubleConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0] or (x2 is not None and ctx.needs_input_grad[1]):
             c_x1 = x1.shape[-1]
             co1 = c_x1 if x2 is not None else 0
-            dx1, dx2, _ = F.conv3_fwd(dy1, None, p1.dgrad, None, None, None, p1.cin, co1, False)
+            # for a decoder block dx1 is the transposed conv's output gradient: keep the
+            # epilogue's per-channel sums, they are that conv's bias gradient
+            want_sums = x2 is not None and blk.up_is_convt
+            dx1, dx2, sums = F.conv3_fwd(dy1, None, p1.dgrad, None, None, None, p1.cin, co1,
+                                         want_sums)
+            if want_sums:
+                dx1._ddlpc_colsum_rows = sums
             if x2 is None:
                 dx2 = None
         # conv biases feeding a training-mode BN have an exactly-zero gradient
@@ -203,11 +209,12 @@ class _ConvTFn(torch.autograd.Function):
         dout = dout.contiguous()
         dx = F.convt_dgrad(dout, ctx.pack.dgrad, ctx.pack.cin) if ctx.needs_input_grad[0] else None
         conv = ctx.pack.conv
+        rows = getattr(dout, "_ddlpc_colsum_rows", None)
         if ctx.engine.direct_grads:
-            F.convt_wgrad(x, dout, conv.weight.grad, conv.bias.grad)
+            F.convt_wgrad(x, dout, conv.weight.grad, conv.bias.grad, rows)
             ctx.engine.ready(conv.weight, conv.bias)
             return dx, None, None, None, None
-        dw, db = F.convt_wgrad(x, dout)
+        dw, db = F.convt_wgrad(x, dout, None, None, rows)
         return dx, dw.view_as(conv.weight), db, None, None
 
 
@@ -251,8 +258,9 @@ class _HeadCEFn(torch.autograd.Function):
 class _Block:
     """Kernel-side view of one DoubleConv: packed weights + BN handles."""
 
-    def __init__(self, dc: nn.Module, first: bool, engine):
+    def __init__(self, dc: nn.Module, first: bool, engine, up_is_convt: bool = False):
         self.engine = engine
+        self.up_is_convt = up_is_convt
         seq = dc.double_conv
         self.conv1, self.conv2 = seq[0], seq[3]
         self.bn1, self.bn2 = _BNState(seq[1]), _BNState(seq[4])
@@ -288,7 +296,8 @@ class UNetEngine:
         for ub in model.up_blocks():
             up = ub.up_sample
             pack = _ConvPack(up, 1, True) if isinstance(up, (nn.ConvTranspose2d, nn.ConvTranspose3d)) else None
-            self.dec.append((ub, pack, _Block(ub.double_conv, first=False, engine=self)))
+            self.dec.append((ub, pack, _Block(ub.double_conv, first=False, engine=self,
+                                              up_is_convt=pack is not None)))
         head = model.conv_last
         self.head = head
         self.packs = [p for b in self.enc + [self.mid] for p in (b.pack1, b.pack2)]
