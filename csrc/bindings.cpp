@@ -10,6 +10,7 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <cstdlib>
 #include <vector>
 
 #include "ops.h"
@@ -155,6 +156,14 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   if (a.Co1 < a.Cout) y2 = at::empty(shape_with_c(g, a.Cout - a.Co1), opts);
   at::Tensor stats;
   a.persist_blocks = 2 * num_cus();
+  {
+    static const int dbg = [] { const char* e = getenv("DDLPC_CONV_DBG"); return e ? atoi(e) : 0; }();
+    static const int pb = [] { const char* e = getenv("DDLPC_CONV_PERSIST"); return e ? atoi(e) : -1; }();
+    static const int ksx = [] { const char* e = getenv("DDLPC_CONV_KSPLIT"); return e ? atoi(e) : -1; }();
+    a.dbg = dbg;
+    if (pb >= 0) a.persist_blocks = pb * num_cus();
+    (void)ksx;
+  }
   a.npix = (long long)g.N * g.D * g.H * g.W;
   // small layers: split the input-channel chunks across workgroups so the grid fills the
   // chip; partial sums go through an fp32 buffer and a deterministic finalize
@@ -167,6 +176,8 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
       for (int ks = 2; ks <= 8; ++ks)
         if (nchunks_total % ks == 0 && nchunks_total / ks >= 2 && items * ks <= 2 * num_cus())
           best = ks;
+    const char* e = getenv("DDLPC_CONV_KSPLIT");
+    if (e && atoi(e) >= 1 && nchunks_total % atoi(e) == 0) best = atoi(e);
     a.ksplit = best;
   }
   at::Tensor part;

@@ -193,7 +193,8 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
       const int c8 = c0 + a_sub8[i];
-      const unsigned off = (a_pix[i] >= 0 && c8 < Cs) ? (unsigned)(a_pix[i] * Cs + c8) * 2u : kOOB;
+      unsigned off = (a_pix[i] >= 0 && c8 < Cs) ? (unsigned)(a_pix[i] * Cs + c8) * 2u : kOOB;
+      if (p.dbg & 2) off = kOOB;                  // debug: A traffic off
       dma16(r, sA(buf) + (i * 4 + wave) * 1024, off);
     }
   };
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
     const int soff = (grp * 3 * p.CinW + chunk * BK) * 2;
 #pragma unroll
     for (int i = 0; i < C::B_ITERS; ++i) {
-      const bool ok = b_off[i] >= 0 && chunk * BK + b_sub8[i] < p.CinW;
+      const bool ok = b_off[i] >= 0 && chunk * BK + b_sub8[i] < p.CinW && !(p.dbg & 1);
       dma16(rW, sB(buf) + (i * 4 + wave) * 1024, ok ? (unsigned)(b_off[i] + soff) : kOOB);
     }
   };
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
     // chunk's halo (issued after B(s) during s-1) may stay in flight.
     if (NG > 1 && grp == 1 && more_chunks) dma_wait<C::A_ITERS>();
     else dma_wait<0>();
-    lds_sync();
+    if (!(p.dbg & 8)) lds_sync();               // debug 8: no stage barrier (wrong results)
     if (grp == 0 && has_pro) {
       transform_A(k, chunk, cseq & 1);
       lds_sync();
@@ -295,6 +296,13 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
       for (int nt = 0; nt < NT; ++nt) {
         const int row = t * BN + wn * (NT * 16) + nt * 16 + (lane & 15);
         wf[nt] = *reinterpret_cast<const uint4*>(B + lds_off(row, g));
+      }
+      if (p.dbg & 4) {                            // debug: MFMA off (operands kept live)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) asm volatile("" ::"v"(xf[mt]));
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) asm volatile("" ::"v"(wf[nt]));
+        continue;
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
