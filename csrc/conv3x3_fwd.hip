@@ -299,9 +299,11 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
       }
       if (p.dbg & 4) {                            // debug: MFMA off (operands kept live)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) asm volatile("" ::"v"(xf[mt]));
+        for (int mt = 0; mt < MT; ++mt)
+          asm volatile("" ::"v"(xf[mt].x), "v"(xf[mt].y), "v"(xf[mt].z), "v"(xf[mt].w));
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) asm volatile("" ::"v"(wf[nt]));
+        for (int nt = 0; nt < NT; ++nt)
+          asm volatile("" ::"v"(wf[nt].x), "v"(wf[nt].y), "v"(wf[nt].z), "v"(wf[nt].w));
         continue;
       }
 #pragma unroll
