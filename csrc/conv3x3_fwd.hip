@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
       const int c8 = c0 + a_sub8[i];
       unsigned off = (a_pix[i] >= 0 && c8 < Cs) ? (unsigned)(a_pix[i] * Cs + c8) * 2u : kOOB;
       if (p.dbg & 2) off = kOOB;                  // debug: A traffic off
-      dma16(r, sA(buf) + (i * 4 + wave) * 1024, off);
+      if (!(p.dbg & 16)) dma16(r, sA(buf) + (i * 4 + wave) * 1024, off);
     }
   };
   auto issue_B = [&](int k, int chunk_local, int grp, int buf) {
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
 #pragma unroll
     for (int i = 0; i < C::B_ITERS; ++i) {
       const bool ok = b_off[i] >= 0 && chunk * BK + b_sub8[i] < p.CinW && !(p.dbg & 1);
-      dma16(rW, sB(buf) + (i * 4 + wave) * 1024, ok ? (unsigned)(b_off[i] + soff) : kOOB);
+      if (!(p.dbg & 16)) dma16(rW, sB(buf) + (i * 4 + wave) * 1024, ok ? (unsigned)(b_off[i] + soff) : kOOB);
     }
   };
   // prologue BN+ReLU applied in LDS on the landed halo (padding stays zero); a_pix holds
@@ -287,6 +287,12 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
     for (int t = 0; t < 3; ++t) {
       const int tapoff = (kd * HH2 + r) * HW2 + t;
       uint4 xf[MT], wf[NT];
+      if (p.dbg & 32) {                           // debug: fragment LDS reads off
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) xf[mt] = make_uint4(hp0[mt] + tapoff, s, t, lane);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) wf[nt] = make_uint4(nt, s, t, lane);
+      } else {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int hp = hp0[mt] + tapoff;
@@ -296,6 +302,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
       for (int nt = 0; nt < NT; ++nt) {
         const int row = t * BN + wn * (NT * 16) + nt * 16 + (lane & 15);
         wf[nt] = *reinterpret_cast<const uint4*>(B + lds_off(row, g));
+      }
       }
       if (p.dbg & 4) {                            // debug: MFMA off (operands kept live)
 #pragma unroll

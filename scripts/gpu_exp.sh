@@ -5,11 +5,11 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 python scripts/build_ext.py > gpurun_out/build.log 2>&1 || exit 1
-for cfg in "0" "1" "2" "3" "4" "8" "7"; do
+for cfg in ${DBGS:-0 16 32 48 52 60}; do
   echo "== DBG=$cfg"
   DDLPC_CONV_DBG=$cfg timeout -k 10 120 python scripts/conv_micro.py --passes fwd --only "$ONLY" || exit 2
 done
-for pb in 1 2 4; do
+for pb in ${PBS:-}; do
   echo "== PERSIST=$pb"
   DDLPC_CONV_PERSIST=$pb timeout -k 10 120 python scripts/conv_micro.py --passes fwd --only "$ONLY" || exit 2
 done
