@@ -266,7 +266,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
     if (NG > 1 && grp == 1 && more_chunks) dma_wait<C::A_ITERS>();
     else dma_wait<0>();
     if (!(p.dbg & 8)) lds_sync();               // debug 8: no stage barrier (wrong results)
-    if (grp == 0 && has_pro) {
+    if (grp == 0 && has_pro && !(p.dbg & 64)) {
       transform_A(k, chunk, cseq & 1);
       lds_sync();
     }
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[nt], xf[mt], acc[mt][nt]);
     }
 
-    if (rem == spi - 1) {
+    if (rem == spi - 1 && !(p.dbg & 128)) {
       // ---- epilogue of item k straight from the accumulators:
       // lane holds channels co..co+3 (co = co0 + wn*NT*16 + nt*16 + 4*(lane>>4)) of pixel
       // (wm*MT*16 + mt*16 + (lane&15)) of the tile

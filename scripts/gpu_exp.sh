@@ -13,4 +13,4 @@ for pb in ${PBS:-}; do
   echo "== PERSIST=$pb"
   DDLPC_CONV_PERSIST=$pb timeout -k 10 120 python scripts/conv_micro.py --passes fwd --only "$ONLY" || exit 2
 done
-if [ -x tools/dma_latency ]; then timeout -k 10 60 ./tools/dma_latency || exit 3; fi
+if [ -n "$LAT" ] && [ -x tools/dma_latency ]; then timeout -k 10 60 ./tools/dma_latency || exit 3; fi
