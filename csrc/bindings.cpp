@@ -134,6 +134,27 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   TORCH_CHECK(a.C2 == 0 || a.C1 % 32 == 0, "concat: first input needs C1 % 32 == 0");
   TORCH_CHECK((a.C1 % 8 == 0) && (a.C2 % 8 == 0), "input channels must be multiples of 8 "
               "(the engine pads the 3-channel image to 8)");
+  auto opts = x1.options();
+  a.npix = (long long)g.N * g.D * g.H * g.W;
+  {
+    // high-resolution few-channel layers: resident-weight kernel (conv3x3_res.hip)
+    static const int use_res = [] { const char* e = getenv("DDLPC_CONV_RES"); return e ? atoi(e) : 1; }();
+    int grid = 0, smem = 0;
+    const int variant = use_res ? conv3_res_plan(a, num_cus(), grid, smem) : -1;
+    if (variant >= 0) {
+      at::Tensor y1 = at::empty(shape_with_c(g, a.Co1), opts);
+      at::Tensor y2;
+      if (a.Co1 < a.Cout) y2 = at::empty(shape_with_c(g, a.Cout - a.Co1), opts);
+      at::Tensor stats;
+      if (want_stats) stats = at::empty({(int64_t)grid, 2, a.Cout}, opts.dtype(at::kFloat));
+      a.Y1 = bptr_mut(y1);
+      a.Y2 = y2.defined() ? bptr_mut(y2) : nullptr;
+      a.stats = want_stats ? stats.data_ptr<float>() : nullptr;
+      conv3_res_launch(a, variant, grid, smem, cur_stream());
+      at::Tensor none = at::empty({0}, opts);
+      return {y1, y2.defined() ? y2 : none, stats.defined() ? stats : none};
+    }
+  }
   // tile configuration: channel tile from Cout, pixel tile from the image size; the
   // 128-channel config drops to a 64-pixel tile when the layer would not fill the chip
   int cfg = a.Cout <= 32 ? 0 : a.Cout <= 64 ? 1 : 2;
@@ -150,7 +171,6 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   if (cfg == 2 && a.nTilesM * a.nTilesN < 2 * num_cus()) { cfg = 3; plan(cfg); }
   TORCH_CHECK((g.dims == 3 ? a.TD + 2 : 1) * (a.TH + 2) * (a.TW + 2) <= conv3_fwd_cfg_halo(g.dims, cfg),
               "halo exceeds LDS capacity");
-  auto opts = x1.options();
   at::Tensor y1 = at::empty(shape_with_c(g, a.Co1), opts);
   at::Tensor y2;
   if (a.Co1 < a.Cout) y2 = at::empty(shape_with_c(g, a.Cout - a.Co1), opts);
@@ -164,7 +184,6 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
     if (pb >= 0) a.persist_blocks = pb * num_cus();
     (void)ksx;
   }
-  a.npix = (long long)g.N * g.D * g.H * g.W;
   // small layers: split the input-channel chunks across workgroups so the grid fills the
   // chip; partial sums go through an fp32 buffer and a deterministic finalize
   const int nchunks_total = (a.Cin + 31) / 32;

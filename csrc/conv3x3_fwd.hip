@@ -33,37 +33,14 @@
 // The data gradient (K2) is this same kernel run on dY with the flipped, transposed
 // weights W'[ci][8-t][co] (packed by weight_pack).
 #include "common.h"
+#include "conv_lds.h"
 #include "ops.h"
 
 namespace ddlpc {
 
 namespace {
 
-constexpr int BK = 32;                 // channels per K chunk
-constexpr int ROWB = BK * 2;           // bytes per LDS row (one pixel / one weight row)
-constexpr unsigned kOOB = 0x80000000u; // buffer offset that reads as zero
-
-DDLPC_DEVICE int swz(int row) { return ((row >> 2) & 1) << 1; }
-DDLPC_DEVICE int lds_off(int row, int chunk) { return row * ROWB + ((chunk ^ swz(row)) << 4); }
-
-DDLPC_DEVICE void lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-template <int N>
-DDLPC_DEVICE void dma_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-DDLPC_DEVICE __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
-}
-
-DDLPC_DEVICE void dma16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, unsigned voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(
-      r, (__attribute__((address_space(3))) void*)((size_t)lds_wave_base), 16, (int)voff, 0, 0, 0);
-}
+using namespace convlds;
 
 template <int DIMS, int WM, int WN, int MT, int NT, int HALO>
 struct Cfg {

@@ -1,0 +1,382 @@
+// 3x3 2-D convolution (stride 1, pad 1) for the HIGH-RESOLUTION, FEW-CHANNEL U-Net layers
+// (256^2 / 128^2 x 32..96 channels: enc1, enc2, dec2.b, dec1 and their data gradients) —
+// the layers where the streaming kernel (conv3x3_fwd.hip) spends most of its time on
+// per-stage overhead rather than MFMA work.  Reference ops: DoubleConv's nn.Conv2d(k=3,
+// padding=1) (ref.py:579,582) and the first conv on the 3-channel image (ref.py:588).
+//
+// Design (MI355X / gfx950):
+//   * RESIDENT WEIGHTS: every workgroup is persistent and owns ONE output-channel tile, so
+//     all its weights (9 taps x Cin x BN bf16, <= ~74 KB) are DMA'd into LDS once and stay
+//     there; only the input halo streams;
+//   * one pipeline stage = (pixel tile, 32-channel chunk) with ALL 9 taps: 9*MT*NT MFMAs
+//     per wave per stage behind ONE barrier (the streaming kernel: 3 taps per barrier);
+//   * the halo of stage s+1 is in flight (LDS-DMA, double-buffered) while stage s computes;
+//   * the BatchNorm+ReLU prologue of the previous layer is applied in LDS by the lane that
+//     DMA'd each 16-B piece, right after its own DMA lands and BEFORE the stage barrier —
+//     no extra barrier (padding stays zero);
+//   * the epilogue of a tile (bias, bf16, 8-B stores, BN (sum, sum^2) in registers) runs
+//     after the NEXT stage's barrier, just before that stage's DMA is issued, so its stores
+//     drain under the next tile's compute instead of stalling the next vmcnt wait;
+//   * TAP8 (the image layer, Cin <= 8): K packs (tap, channel) as k = 8*tap + c, 12 taps
+//     (3 zero-weight) = 3 MFMA k-steps instead of 9 on a 4x zero-padded chunk; the halo row
+//     is one 16-B pixel.
+// Output / statistics contracts are those of conv3_fwd_kernel (ops.h ConvFwdArgs).
+#include "common.h"
+#include "conv_lds.h"
+#include "ops.h"
+
+namespace ddlpc {
+
+namespace {
+
+using namespace convlds;
+
+template <int WM, int WN, int MT, int NT, int HALO, bool TAP8>
+struct RCfg {
+  static constexpr int NW = WM * WN;
+  static constexpr int NTH = NW * 64;
+  static constexpr int BM = WM * MT * 16;
+  static constexpr int BN = WN * NT * 16;
+  static constexpr int PIECES = TAP8 ? HALO : HALO * 4;   // 16-B pieces per halo buffer
+  static constexpr int INSTR = (PIECES + 63) / 64;         // DMA wave-instructions per halo
+  static constexpr int A_ITERS = (INSTR + NW - 1) / NW;    // ... per wave
+  static constexpr int A_BYTES = INSTR * 1024;
+};
+
+DDLPC_HOST_DEVICE int res_ss_bytes(int C1, bool pro) { return pro ? ((8 * C1 + 15) / 16) * 16 : 0; }
+DDLPC_HOST_DEVICE int res_w_bytes(int Cin, int BN, bool tap8) {
+  return tap8 ? 3 * BN * ROWB : ((Cin + BK - 1) / BK) * 9 * BN * ROWB;
+}
+
+template <int WM, int WN, int MT, int NT, int HALO, bool TAP8>
+__global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_kernel(ConvFwdArgs p) {
+  using C = RCfg<WM, WN, MT, NT, HALO, TAP8>;
+  constexpr int NW = C::NW, BN = C::BN;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const bool has_pro = p.pscale != nullptr;
+  const int ss_bytes = res_ss_bytes(p.C1, has_pro);
+  float* s_scale = reinterpret_cast<float*>(smem);
+  float* s_shift = s_scale + p.C1;
+  char* sW = smem + ss_bytes;
+  char* sA0 = sW + res_w_bytes(p.Cin, BN, TAP8);
+  auto sA = [&](int b) { return sA0 + b * C::A_BYTES; };
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN;
+  const int wn = wave % WN;
+  const int HW2 = p.TW + 2, HH2 = p.TH + 2;
+  const int halo = HH2 * HW2;
+  const long long img_px = (long long)p.H * p.W;
+  const int n_items = p.nTilesM * p.nTilesN;
+  const int my_items = n_items > (int)blockIdx.x ? (n_items - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int nch = TAP8 ? 1 : (p.Cin + BK - 1) / BK;
+  const int S = my_items * nch;
+  // every item of a block has the same n tile (launcher: grid % nTilesN == 0)
+  const int co0 = (int)blockIdx.x % p.nTilesN * BN;
+
+  if (has_pro)
+    for (int c = tid; c < p.C1; c += C::NTH) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
+
+  // ---- resident weights: rows (chunk, tap, col) [TAP8: (k-step, col)], 64 B each
+  {
+    const auto rW = make_rsrc(p.Wt, (unsigned)((long long)p.Cout * 9 * p.CinW * 2));
+    const int pieces = res_w_bytes(p.Cin, BN, TAP8) / 16;
+    for (int b = wave * 64; b < pieces; b += NW * 64) {
+      const int e = b + lane;
+      const int row = e >> 2;
+      const int sub = (e & 3) ^ swz(row);
+      const int col = row % BN;
+      const int co = co0 + col;
+      unsigned off = kOOB;
+      if (TAP8) {
+        const int tap = (row / BN) * 4 + sub;
+        if (tap < 9 && co < p.Cout) off = (unsigned)((co * 9 + tap) * p.CinW) * 2u;
+      } else {
+        const int t = (row / BN) % 9, c = row / (9 * BN);
+        const int ci = c * BK + sub * 8;
+        if (co < p.Cout && ci < p.CinW) off = (unsigned)((co * 9 + t) * p.CinW + ci) * 2u;
+      }
+      dma16(rW, sW + b * 16, off);
+    }
+  }
+
+  struct Item { int n_img, h0, w0; };
+  auto item_of = [&](int k) {
+    Item it;
+    int m = ((int)blockIdx.x + k * (int)gridDim.x) / p.nTilesN;
+    const int tw_i = m % p.tilesW; m /= p.tilesW;
+    const int th_i = m % p.tilesH; m /= p.tilesH;
+    it.n_img = m;
+    it.h0 = th_i * p.TH; it.w0 = tw_i * p.TW;
+    return it;
+  };
+  // ---- per-lane halo DMA geometry (no integer division in the stage loop)
+  int a_dw[C::A_ITERS], a_dh[C::A_ITERS], a_sub8[C::A_ITERS], a_pix[C::A_ITERS];
+#pragma unroll
+  for (int i = 0; i < C::A_ITERS; ++i) {
+    const int e = (i * NW + wave) * 64 + lane;
+    const int px = TAP8 ? e : e >> 2;
+    a_sub8[i] = TAP8 ? 0 : ((e & 3) ^ swz(px)) << 3;
+    a_dw[i] = px < halo ? px % HW2 - 1 : -(1 << 20);    // outside the halo: padding
+    a_dh[i] = px / HW2 - 1;
+    a_pix[i] = -1;
+  }
+  int a_item = -1, a_nimg = 0;
+  auto issue_A = [&](int k, int chunk, int buf) {
+    if (k != a_item) {
+      const Item it = item_of(k);
+      a_item = k;
+      a_nimg = it.n_img;
+#pragma unroll
+      for (int i = 0; i < C::A_ITERS; ++i) {
+        const int gw = it.w0 + a_dw[i], gh = it.h0 + a_dh[i];
+        a_pix[i] = (gw >= 0 && gw < p.W && gh >= 0 && gh < p.H) ? gh * p.W + gw : -1;
+      }
+    }
+    const int cbase = chunk * BK;
+    const bool second = cbase >= p.C1;                 // chunk served by X2 (C1 % 32 == 0)
+    const int Cs = second ? p.C2 : p.C1;
+    const int c0 = second ? cbase - p.C1 : cbase;
+    const bf16_t* src = second ? p.X2 : p.X1;
+    const auto r = make_rsrc(src + a_nimg * img_px * Cs, (unsigned)(img_px * Cs * 2));
+#pragma unroll
+    for (int i = 0; i < C::A_ITERS; ++i) {
+      if ((i * NW + wave) * 64 >= C::PIECES) break;    // wave-uniform
+      const int c8 = c0 + a_sub8[i];
+      const unsigned off = (a_pix[i] >= 0 && c8 < Cs) ? (unsigned)(a_pix[i] * Cs + c8) * 2u : kOOB;
+      dma16(r, sA(buf) + (i * NW + wave) * 1024, off);
+    }
+  };
+  // prologue on the pieces THIS lane DMA'd (a_pix still describes the chunk's item)
+  auto transform_A = [&](int chunk, int buf) {
+    const int cbase = chunk * BK;
+    if (cbase >= p.C1) return;
+#pragma unroll
+    for (int i = 0; i < C::A_ITERS; ++i) {
+      const int e = (i * NW + wave) * 64 + lane;
+      const int c8 = cbase + a_sub8[i];
+      if (e < C::PIECES && c8 < p.C1 && a_pix[i] >= 0) {
+        uint4* q = reinterpret_cast<uint4*>(sA(buf) + e * 16);
+        float f[8];
+        unpack8(*q, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], s_scale[c8 + j], s_shift[c8 + j]), 0.0f);
+        *q = pack8(f);
+      }
+    }
+  };
+
+  // ---- per-lane fragment geometry
+  const int g = lane >> 4;
+  int hp0[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
+    hp0[mt] = (pix / p.TW) * HW2 + pix % p.TW;
+  }
+  int toff8[3];                                        // TAP8: this lane group's tap offsets
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) {
+    const int tap = min(ks * 4 + g, 8);
+    toff8[ks] = (tap / 3) * HW2 + tap % 3;
+  }
+  const int wrow0 = wn * (NT * 16) + (lane & 15);
+
+  f32x4_t acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float s1[NT][4], s2[NT][4];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { s1[nt][i] = 0.f; s2[nt][i] = 0.f; }
+
+  // epilogue of item k straight from the accumulators: lane holds channels co..co+3 of
+  // tile pixel (wm*MT*16 + mt*16 + (lane&15))
+  auto epilogue = [&](int k) {
+    const Item it = item_of(k);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
+      const int gw = it.w0 + pix % p.TW, gh = it.h0 + pix / p.TW;
+      const bool valid = gw < p.W && gh < p.H;
+      const long long gpix = ((long long)it.n_img * p.H + gh) * p.W + gw;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * g;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float b = (p.bias != nullptr && co + i < p.Cout) ? p.bias[co + i] : 0.0f;
+          v[i] = acc[mt][nt][i] + b;
+        }
+        const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        if (valid && co < p.Cout) {
+          if (co < p.Co1) *reinterpret_cast<uint2*>(p.Y1 + gpix * p.Co1 + co) = pk;
+          else *reinterpret_cast<uint2*>(p.Y2 + gpix * (p.Cout - p.Co1) + (co - p.Co1)) = pk;
+          const float r0 = lo_bf(pk.x), r1 = hi_bf(pk.x), r2 = lo_bf(pk.y), r3 = hi_bf(pk.y);
+          s1[nt][0] += r0; s2[nt][0] += r0 * r0;
+          s1[nt][1] += r1; s2[nt][1] += r1 * r1;
+          s1[nt][2] += r2; s2[nt][2] += r2 * r2;
+          s1[nt][3] += r3; s2[nt][3] += r3 * r3;
+        }
+        acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+
+  if (S > 0) issue_A(0, 0, 0);
+  int k = 0, c = 0;
+  for (int s = 0; s < S; ++s) {
+    dma_wait<0>();                                    // this stage's halo (+ weights at s=0)
+    if (!TAP8 && has_pro) transform_A(c, s & 1);
+    lds_sync();
+    if (c == 0 && s > 0) epilogue(k - 1);
+    int k1 = k, c1 = c + 1;
+    if (c1 == nch) { c1 = 0; ++k1; }
+    if (s + 1 < S) issue_A(k1, c1, (s + 1) & 1);
+    // compute: fragments of step j+1 are read while the MFMAs of step j run (register
+    // double buffer; the sched barrier keeps the compiler from hoisting all 9 steps' reads)
+    const char* A = sA(s & 1);
+    const char* Wc = TAP8 ? sW : sW + c * 9 * BN * ROWB;
+    constexpr int KSTEPS = TAP8 ? 3 : 9;
+    auto load_frags = [&](int j, uint4 (&xf)[MT], uint4 (&wf)[NT]) {
+      if (TAP8) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) xf[mt] = lds128(A + (hp0[mt] + toff8[j]) * 16);
+      } else {
+        const int tapoff = (j / 3) * HW2 + j % 3;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) xf[mt] = lds128(A + lds_off(hp0[mt] + tapoff, g));
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) wf[nt] = lds128(Wc + lds_off(j * BN + wrow0 + nt * 16, g));
+    };
+    uint4 xf[2][MT], wf[2][NT];
+    load_frags(0, xf[0], wf[0]);
+#pragma unroll
+    for (int j = 0; j < KSTEPS; ++j) {
+      if (j + 1 < KSTEPS) load_frags(j + 1, xf[(j + 1) & 1], wf[(j + 1) & 1]);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = mfma16x16x32(wf[j & 1][nt], xf[j & 1][mt], acc[mt][nt]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    k = k1; c = c1;
+  }
+  if (S > 0) epilogue(k - 1);
+
+  // ---- one BN-statistics partial row per workgroup (layout of conv3_fwd_kernel)
+  if (p.stats != nullptr) {
+    dma_wait<0>();
+    lds_sync();
+    float* red = reinterpret_cast<float*>(sA0);
+    for (int i = tid; i < 2 * BN; i += C::NTH) red[i] = 0.f;
+    lds_sync();
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float a1 = s1[nt][i], a2 = s2[nt][i];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) { a1 += __shfl_xor(a1, o, 64); a2 += __shfl_xor(a2, o, 64); }
+        if ((lane & 15) == 0) {
+          const int col = wn * (NT * 16) + nt * 16 + 4 * g + i;
+          atomicAdd(red + col, a1);
+          atomicAdd(red + BN + col, a2);
+        }
+      }
+    lds_sync();
+    float* row = p.stats + (long long)blockIdx.x * 2 * p.Cout;
+    for (int i = tid; i < p.Cout; i += C::NTH) {
+      const bool mine = i >= co0 && i < co0 + BN;
+      row[i] = mine ? red[i - co0] : 0.f;
+      row[p.Cout + i] = mine ? red[BN + i - co0] : 0.f;
+    }
+  }
+}
+
+struct ResVariant { int wm, wn, mt, nt, halo; bool tap8; int tw, th; };
+// 0: BM 256 (16x16) BN 32, 4 waves     1: BM 256 BN 64, 4 waves
+// 2: BM 512 (32x16) BN 32, 8 waves     3: BM 256 BN 64, 8 waves (4x2)
+// 4: TAP8 image layer, BM 256 BN 32, 4 waves
+constexpr ResVariant kRes[5] = {
+    {4, 1, 4, 2, 324, false, 16, 16}, {4, 1, 4, 4, 324, false, 16, 16},
+    {8, 1, 4, 2, 612, false, 32, 16}, {4, 2, 4, 2, 324, false, 16, 16},
+    {4, 1, 4, 2, 324, true, 16, 16}};
+
+int res_smem(const ResVariant& v, int Cin, int C1, bool pro) {
+  const int bn = v.wn * v.nt * 16;
+  const int pieces = v.tap8 ? v.halo : v.halo * 4;
+  return res_ss_bytes(C1, pro) + res_w_bytes(Cin, bn, v.tap8) + 2 * ((pieces + 63) / 64) * 1024;
+}
+
+template <int WM, int WN, int MT, int NT, int HALO, bool TAP8>
+void launch_res(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
+  hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8>), dim3(grid), dim3(WM * WN * 64),
+                     smem, st, a);
+}
+
+}  // namespace
+
+// Planner: returns a variant id (and fills tiles / persistent grid) or -1 when the layer
+// belongs to the streaming kernel.  LDS budget: 160 KB per CU; two workgroups per CU when
+// a workgroup needs <= 80 KB.
+int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
+  if (a.dims != 2 || a.W < 16 || a.H < 16) return -1;
+  const bool pro = a.pscale != nullptr;
+  const bool tap8 = a.Cin <= 8 && a.C2 == 0 && a.CinW == 8 && !pro;
+  const int bn = (a.Cout <= 32 || a.Cout % 64 != 0) ? 32 : 64;
+  int cand[2];
+  int nc = 0;
+  if (tap8) {
+    if (bn != 32) return -1;
+    cand[nc++] = 4;
+  } else if (bn == 32) {
+    cand[nc++] = 0; cand[nc++] = 2;
+  } else {
+    cand[nc++] = 3;              // (variant 1, BN 64 on 4 waves, spills: not planned)
+  }
+  for (int i = 0; i < nc; ++i) {
+    const ResVariant& v = kRes[cand[i]];
+    const int sm = res_smem(v, a.Cin, a.C1, pro);
+    const int nw = v.wm * v.wn;
+    // 4-wave blocks need 2 per CU (2 waves / SIMD); 8-wave blocks use ~200 VGPRs: 1 per CU
+    const int bpc = nw == 4 ? (sm <= 80 * 1024 ? 2 : 0) : (sm <= 160 * 1024 ? 1 : 0);
+    if (bpc == 0) continue;
+    a.TD = 1; a.TW = v.tw; a.TH = v.th;
+    a.tilesD = 1;
+    a.tilesH = (a.H + a.TH - 1) / a.TH;
+    a.tilesW = (a.W + a.TW - 1) / a.TW;
+    a.nTilesM = a.N * a.tilesH * a.tilesW;
+    a.nTilesN = (a.Cout + bn - 1) / bn;
+    const int items = a.nTilesM * a.nTilesN;
+    const int cap = bpc * num_cus;
+    if (items < cap) return -1;                         // too small: streaming kernel
+    grid = cap / a.nTilesN * a.nTilesN;
+    smem = sm;
+    a.ksplit = 1;
+    a.persist_blocks = cap;
+    a.stat_rows = grid;
+    return cand[i];
+  }
+  return -1;
+}
+
+void conv3_res_launch(ConvFwdArgs& a, int variant, int grid, int smem, hipStream_t st) {
+  switch (variant) {
+    case 0: launch_res<4, 1, 4, 2, 324, false>(a, grid, smem, st); break;
+    case 1: launch_res<4, 1, 4, 4, 324, false>(a, grid, smem, st); break;
+    case 2: launch_res<8, 1, 4, 2, 612, false>(a, grid, smem, st); break;
+    case 3: launch_res<4, 2, 4, 2, 324, false>(a, grid, smem, st); break;
+    default: launch_res<4, 1, 4, 2, 324, true>(a, grid, smem, st); break;
+  }
+}
+
+}  // namespace ddlpc

@@ -40,6 +40,9 @@ struct ConvFwdArgs {
 void conv3_splitk_finalize_launch(ConvFwdArgs& a, int grid, hipStream_t st);
 void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st);
 int conv3_fwd_cfg_wm(int cfg);
+// resident-weight kernel for high-resolution few-channel layers (conv3x3_res.hip)
+int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem);
+void conv3_res_launch(ConvFwdArgs& a, int variant, int grid, int smem, hipStream_t st);
 int conv3_fwd_cfg_bn(int cfg);
 int conv3_fwd_cfg_bm(int cfg);
 int conv3_fwd_cfg_halo(int dims, int cfg);

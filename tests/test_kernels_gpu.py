@@ -83,6 +83,53 @@ def test_conv3_fwd_prologue(ops):
     assert rel_err(nchw(y), ref) < 1e-2
 
 
+# shapes that take the resident-weight kernel (conv3x3_res.hip): high resolution, few
+# channels, enough 16x16 tiles to fill the chip
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout,pro", [
+    (2, 256, 256, 32, 0, 32, True), (2, 256, 256, 3, 0, 32, False),
+    (2, 256, 256, 64, 32, 32, True), (2, 256, 256, 32, 0, 64, False),
+    (2, 256, 256, 64, 0, 64, True), (3, 200, 232, 32, 0, 32, True),
+    (2, 128, 128, 64, 0, 96, False)])
+def test_conv3_fwd_resident(ops, N, H, W, C1, C2, Cout, pro):
+    torch.manual_seed(4)
+    x1 = torch.randn(N, C1, H, W, device=DEV).bfloat16()
+    x2 = torch.randn(N, C2, H, W, device=DEV).bfloat16() if C2 else None
+    w = torch.randn(Cout, C1 + C2, 3, 3, device=DEV) * (1.0 / math.sqrt(9 * (C1 + C2)))
+    b = torch.randn(Cout, device=DEV) * 0.1
+    scale = torch.rand(C1, device=DEV) + 0.5 if pro else None
+    shift = torch.randn(C1, device=DEV) * 0.5 if pro else None
+    pk = pack_conv(ops, w)
+    xin1 = ops.to_nhwc_bf16(x1, 8) if C1 % 8 else nhwc(x1)
+    y, _, st = ops.conv3_fwd(xin1, nhwc(x2) if x2 is not None else None, pk.fwd, b, scale,
+                             shift, Cout, 0, True)
+    a1 = x1.float()
+    if pro:
+        a1 = torch.relu(a1 * scale[None, :, None, None] + shift[None, :, None, None]).bfloat16().float()
+    xin = torch.cat([a1, x2.float()], 1) if x2 is not None else a1
+    ref = F.conv2d(xin, w.bfloat16().float(), b, padding=1)
+    assert rel_err(nchw(y), ref) < 1e-2
+    s = st.sum(0)
+    yf = nchw(y).float()
+    assert torch.allclose(s[0], yf.sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+    assert torch.allclose(s[1], (yf * yf).sum((0, 2, 3)), rtol=1e-3, atol=1.0)
+
+
+@pytest.mark.parametrize("C1,C2,Cout", [(64, 32, 32), (32, 0, 32), (64, 128, 64)])
+def test_conv3_dgrad_resident(ops, C1, C2, Cout):
+    torch.manual_seed(5)
+    N, H, W = 2, 256, 256
+    Cin = C1 + C2
+    w = torch.randn(Cout, Cin, 3, 3, device=DEV) / math.sqrt(9 * Cin)
+    dy = torch.randn(N, Cout, H, W, device=DEV).bfloat16()
+    pk = pack_conv(ops, w)
+    dx1, dx2, _ = ops.conv3_fwd(nhwc(dy), None, pk.dgrad, None, None, None, Cin,
+                                C1 if C2 else 0, False)
+    ref = F.conv_transpose2d(dy.float(), w.bfloat16().float(), padding=1)
+    assert rel_err(nchw(dx1), ref[:, :C1]) < 1e-2
+    if C2:
+        assert rel_err(nchw(dx2), ref[:, C1:]) < 1e-2
+
+
 @pytest.mark.parametrize("C1,C2,Cout", [(64, 32, 32), (0, 64, 32), (256, 256, 256)])
 def test_conv3_dgrad_split(ops, C1, C2, Cout):
     torch.manual_seed(2)
