@@ -177,10 +177,8 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   at::Tensor stats;
   a.persist_blocks = 2 * num_cus();
   {
-    static const int dbg = [] { const char* e = getenv("DDLPC_CONV_DBG"); return e ? atoi(e) : 0; }();
     static const int pb = [] { const char* e = getenv("DDLPC_CONV_PERSIST"); return e ? atoi(e) : -1; }();
     static const int ksx = [] { const char* e = getenv("DDLPC_CONV_KSPLIT"); return e ? atoi(e) : -1; }();
-    a.dbg = dbg;
     if (pb >= 0) a.persist_blocks = pb * num_cus();
     (void)ksx;
   }

@@ -171,8 +171,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
     for (int i = 0; i < C::A_ITERS; ++i) {
       const int c8 = c0 + a_sub8[i];
       unsigned off = (a_pix[i] >= 0 && c8 < Cs) ? (unsigned)(a_pix[i] * Cs + c8) * 2u : kOOB;
-      if (p.dbg & 2) off = kOOB;                  // debug: A traffic off
-      if (!(p.dbg & 16)) dma16(r, sA(buf) + (i * 4 + wave) * 1024, off);
+      dma16(r, sA(buf) + (i * 4 + wave) * 1024, off);
     }
   };
   auto issue_B = [&](int k, int chunk_local, int grp, int buf) {
@@ -180,8 +179,8 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
     const int soff = (grp * 3 * p.CinW + chunk * BK) * 2;
 #pragma unroll
     for (int i = 0; i < C::B_ITERS; ++i) {
-      const bool ok = b_off[i] >= 0 && chunk * BK + b_sub8[i] < p.CinW && !(p.dbg & 1);
-      if (!(p.dbg & 16)) dma16(rW, sB(buf) + (i * 4 + wave) * 1024, ok ? (unsigned)(b_off[i] + soff) : kOOB);
+      const bool ok = b_off[i] >= 0 && chunk * BK + b_sub8[i] < p.CinW;
+      dma16(rW, sB(buf) + (i * 4 + wave) * 1024, ok ? (unsigned)(b_off[i] + soff) : kOOB);
     }
   };
   // prologue BN+ReLU applied in LDS on the landed halo (padding stays zero); a_pix holds
@@ -229,6 +228,79 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) { s1[nt][i] = 0.f; s2[nt][i] = 0.f; }
 
+  // bias of this block's channel tile, loaded once (a global load inside the epilogue would
+  // make the compiler wait vmcnt(0) — on in-flight stores and DMA — before every use)
+  float bias_r[NT][4];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co0_blk + wn * (NT * 16) + nt * 16 + 4 * g + i;
+      bias_r[nt][i] = (p.bias != nullptr && co < p.Cout) ? p.bias[co] : 0.0f;
+    }
+
+  // ---- epilogue of item k straight from the accumulators:
+  // lane holds channels co..co+3 (co = co0 + wn*NT*16 + nt*16 + 4*(lane>>4)) of pixel
+  // (wm*MT*16 + mt*16 + (lane&15)) of the tile
+  auto epilogue = [&](int k) {
+    const Item it = item_of(k);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
+      const int pw = pix % p.TW, ph = (pix / p.TW) % p.TH;
+      const int pd = DIMS == 3 ? pix / (p.TW * p.TH) : 0;
+      const int gw = it.w0 + pw, gh = it.h0 + ph, gd = it.d0 + pd;
+      const bool valid = gw < p.W && gh < p.H && gd < p.D;
+      const long long gpix = ((long long)(it.n_img * p.D + gd) * p.H + gh) * p.W + gw;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int co = it.co0 + wn * (NT * 16) + nt * 16 + 4 * g;
+        if (KS > 1) {            // split-K partial: fp32 [ks][pixel][Cout], finalized later
+          if (valid && co < p.Cout)
+            *reinterpret_cast<float4*>(p.part + ((long long)it.ks * p.npix + gpix) * p.Cout + co) =
+                make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]);
+          acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+          continue;
+        }
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bias_r[nt][i];
+        const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        if (valid && co < p.Cout) {
+          if (co < p.Co1) *reinterpret_cast<uint2*>(p.Y1 + gpix * p.Co1 + co) = pk;
+          else *reinterpret_cast<uint2*>(p.Y2 + gpix * (p.Cout - p.Co1) + (co - p.Co1)) = pk;
+          // statistics of the stored (bf16-rounded) values
+          const float r0 = lo_bf(pk.x), r1 = hi_bf(pk.x), r2 = lo_bf(pk.y), r3 = hi_bf(pk.y);
+          s1[nt][0] += r0; s2[nt][0] += r0 * r0;
+          s1[nt][1] += r1; s2[nt][1] += r1 * r1;
+          s1[nt][2] += r2; s2[nt][2] += r2 * r2;
+          s1[nt][3] += r3; s2[nt][3] += r3 * r3;
+        }
+        acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+
+  // ---- compute one stage: the 3 taps of kernel row (kd, r).  The operand pointers are
+  // restrict-qualified so the LDS reads carry alias scopes and the compiler does not make
+  // them wait (vmcnt) for the NEXT stage's in-flight LDS-DMA; vmcnt is managed by hand.
+  auto compute = [&](const char* __restrict__ A, const char* __restrict__ B, int kd, int r) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int tapoff = (kd * HH2 + r) * HW2 + t;
+      uint4 xf[MT], wf[NT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) xf[mt] = lds128(A + lds_off(hp0[mt] + tapoff, g));
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        wf[nt] = lds128(B + lds_off(t * BN + wn * (NT * 16) + nt * 16 + (lane & 15), g));
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[nt], xf[mt], acc[mt][nt]);
+    }
+  };
+
   if (S > 0) {
     issue_A(0, 0, 0);
     issue_B(0, 0, 0, 0);
@@ -242,11 +314,14 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
     // chunk's halo (issued after B(s) during s-1) may stay in flight.
     if (NG > 1 && grp == 1 && more_chunks) dma_wait<C::A_ITERS>();
     else dma_wait<0>();
-    if (!(p.dbg & 8)) lds_sync();               // debug 8: no stage barrier (wrong results)
-    if (grp == 0 && has_pro && !(p.dbg & 64)) {
+    lds_sync();
+    if (grp == 0 && has_pro) {
       transform_A(k, chunk, cseq & 1);
       lds_sync();
     }
+    // the previous item's epilogue runs here, BEFORE this stage's DMA is issued, so its
+    // stores drain under this stage's compute (vmcnt retires in order)
+    if (rem == 0 && s > 0) epilogue(k - 1);
     if (s + 1 < S) {
       const int r1 = (s + 1) % spi;
       issue_B((s + 1) / spi, r1 / NG, r1 % NG, (s + 1) & 1);
@@ -255,92 +330,9 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
       const int k1 = (cseq + 1) / nchunks;
       issue_A(k1, (cseq + 1) % nchunks, (cseq + 1) & 1);
     }
-    // ---- compute: the 3 taps of kernel row (kd, r)
-    const char* A = sA(cseq & 1);
-    const char* B = sB(s & 1);
-    const int kd = DIMS == 3 ? grp / 3 : 0;
-    const int r = DIMS == 3 ? grp % 3 : grp;
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const int tapoff = (kd * HH2 + r) * HW2 + t;
-      uint4 xf[MT], wf[NT];
-      if (p.dbg & 32) {                           // debug: fragment LDS reads off
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) xf[mt] = make_uint4(hp0[mt] + tapoff, s, t, lane);
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) wf[nt] = make_uint4(nt, s, t, lane);
-      } else {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int hp = hp0[mt] + tapoff;
-        xf[mt] = *reinterpret_cast<const uint4*>(A + lds_off(hp, g));
-      }
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const int row = t * BN + wn * (NT * 16) + nt * 16 + (lane & 15);
-        wf[nt] = *reinterpret_cast<const uint4*>(B + lds_off(row, g));
-      }
-      }
-      if (p.dbg & 4) {                            // debug: MFMA off (operands kept live)
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-          asm volatile("" ::"v"(xf[mt].x), "v"(xf[mt].y), "v"(xf[mt].z), "v"(xf[mt].w));
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-          asm volatile("" ::"v"(wf[nt].x), "v"(wf[nt].y), "v"(wf[nt].z), "v"(wf[nt].w));
-        continue;
-      }
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[nt], xf[mt], acc[mt][nt]);
-    }
-
-    if (rem == spi - 1 && !(p.dbg & 128)) {
-      // ---- epilogue of item k straight from the accumulators:
-      // lane holds channels co..co+3 (co = co0 + wn*NT*16 + nt*16 + 4*(lane>>4)) of pixel
-      // (wm*MT*16 + mt*16 + (lane&15)) of the tile
-      const Item it = item_of(k);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
-        const int pw = pix % p.TW, ph = (pix / p.TW) % p.TH;
-        const int pd = DIMS == 3 ? pix / (p.TW * p.TH) : 0;
-        const int gw = it.w0 + pw, gh = it.h0 + ph, gd = it.d0 + pd;
-        const bool valid = gw < p.W && gh < p.H && gd < p.D;
-        const long long gpix = ((long long)(it.n_img * p.D + gd) * p.H + gh) * p.W + gw;
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          const int co = it.co0 + wn * (NT * 16) + nt * 16 + 4 * (lane >> 4);
-          if (KS > 1) {            // split-K partial: fp32 [ks][pixel][Cout], finalized later
-            if (valid && co < p.Cout)
-              *reinterpret_cast<float4*>(p.part + ((long long)it.ks * p.npix + gpix) * p.Cout + co) =
-                  make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]);
-            acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            continue;
-          }
-          float v[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float b = (p.bias != nullptr && co + i < p.Cout) ? p.bias[co + i] : 0.0f;
-            v[i] = acc[mt][nt][i] + b;
-          }
-          const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-          if (valid && co < p.Cout) {
-            if (co < p.Co1) *reinterpret_cast<uint2*>(p.Y1 + gpix * p.Co1 + co) = pk;
-            else *reinterpret_cast<uint2*>(p.Y2 + gpix * (p.Cout - p.Co1) + (co - p.Co1)) = pk;
-            // statistics of the stored (bf16-rounded) values
-            const float r0 = lo_bf(pk.x), r1 = hi_bf(pk.x), r2 = lo_bf(pk.y), r3 = hi_bf(pk.y);
-            s1[nt][0] += r0; s2[nt][0] += r0 * r0;
-            s1[nt][1] += r1; s2[nt][1] += r1 * r1;
-            s1[nt][2] += r2; s2[nt][2] += r2 * r2;
-            s1[nt][3] += r3; s2[nt][3] += r3 * r3;
-          }
-          acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        }
-      }
-    }
+    compute(sA(cseq & 1), sB(s & 1), DIMS == 3 ? grp / 3 : 0, DIMS == 3 ? grp % 3 : grp);
   }
+  if (S > 0) epilogue(my_items - 1);
 
   // ---- one BN-statistics partial row per workgroup: shuffle over the 16 pixel lanes,
   // LDS float atomics over the wave rows, one coalesced row write

@@ -195,6 +195,16 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
 #pragma unroll
     for (int i = 0; i < 4; ++i) { s1[nt][i] = 0.f; s2[nt][i] = 0.f; }
 
+  // bias of this block's channel tile, loaded once (a global load inside the epilogue would
+  // make the compiler wait vmcnt(0) — on this tile's stores — before every use)
+  float bias_r[NT][4];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * g + i;
+      bias_r[nt][i] = (p.bias != nullptr && co < p.Cout) ? p.bias[co] : 0.0f;
+    }
   // epilogue of item k straight from the accumulators: lane holds channels co..co+3 of
   // tile pixel (wm*MT*16 + mt*16 + (lane&15))
   auto epilogue = [&](int k) {
@@ -210,10 +220,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
         const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * g;
         float v[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float b = (p.bias != nullptr && co + i < p.Cout) ? p.bias[co + i] : 0.0f;
-          v[i] = acc[mt][nt][i] + b;
-        }
+        for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bias_r[nt][i];
         const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         if (valid && co < p.Cout) {
           if (co < p.Co1) *reinterpret_cast<uint2*>(p.Y1 + gpix * p.Co1 + co) = pk;
@@ -241,8 +248,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     if (s + 1 < S) issue_A(k1, c1, (s + 1) & 1);
     // compute: fragments of step j+1 are read while the MFMAs of step j run (register
     // double buffer; the sched barrier keeps the compiler from hoisting all 9 steps' reads)
-    const char* A = sA(s & 1);
-    const char* Wc = TAP8 ? sW : sW + c * 9 * BN * ROWB;
+    // (restrict-qualified operand pointers give the LDS reads alias scopes, so the compiler
+    // does not make them wait for the next stage's in-flight LDS-DMA: vmcnt is managed by
+    // hand above)
+    auto compute = [&](const char* __restrict__ A, const char* __restrict__ Wc) {
     constexpr int KSTEPS = TAP8 ? 3 : 9;
     auto load_frags = [&](int j, uint4 (&xf)[MT], uint4 (&wf)[NT]) {
       if (TAP8) {
@@ -268,6 +277,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
           acc[mt][nt] = mfma16x16x32(wf[j & 1][nt], xf[j & 1][mt], acc[mt][nt]);
       __builtin_amdgcn_sched_barrier(0);
     }
+    };
+    compute(sA(s & 1), TAP8 ? sW : sW + c * 9 * BN * ROWB);
     k = k1; c = c1;
   }
   if (S > 0) epilogue(k - 1);

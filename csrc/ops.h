@@ -35,7 +35,6 @@ struct ConvFwdArgs {
   int ksplit;                     // >1: split the channel chunks, fp32 partials to `part`
   float* part;                    // [ksplit][npix][Cout] fp32 (ksplit > 1)
   long long npix;                 // N * D * H * W
-  int dbg;                        // perf experiments only (env DDLPC_CONV_DBG); 0 in production
 };
 void conv3_splitk_finalize_launch(ConvFwdArgs& a, int grid, hipStream_t st);
 void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st);
