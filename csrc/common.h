@@ -32,22 +32,32 @@ DDLPC_HOST_DEVICE float bf2f(bf16_t h) {
   return v.f;
 }
 
-// round-to-nearest-even (NaN kept quiet)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+// round-to-nearest-even (NaN kept quiet).  Device code: the gfx950 hardware conversion
+// (v_cvt_pk_bf16_f32, RNE); host code: the same rounding in integer arithmetic.
 DDLPC_HOST_DEVICE bf16_t f2bf(float f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_bit_cast(bf16_t, (__bf16)f);
+#else
   union { uint32_t u; float f; } v;
   v.f = f;
   uint32_t u = v.u;
   if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return static_cast<bf16_t>((u >> 16) | 0x40);
   u += 0x7fffu + ((u >> 16) & 1u);
   return static_cast<bf16_t>(u >> 16);
+#endif
 }
 
+// two floats -> packed bf16x2 in ONE v_cvt_pk_bf16_f32
 DDLPC_DEVICE uint32_t pack2(float a, float b) {
-  return static_cast<uint32_t>(f2bf(a)) | (static_cast<uint32_t>(f2bf(b)) << 16);
+  const f32x2_t f = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2_t));
 }
 
-DDLPC_DEVICE float lo_bf(uint32_t w) { return bf2f(static_cast<bf16_t>(w & 0xffffu)); }
-DDLPC_DEVICE float hi_bf(uint32_t w) { return bf2f(static_cast<bf16_t>(w >> 16)); }
+DDLPC_DEVICE float lo_bf(uint32_t w) { return __builtin_bit_cast(float, w << 16); }
+DDLPC_DEVICE float hi_bf(uint32_t w) { return __builtin_bit_cast(float, w & 0xffff0000u); }
 
 // 16-byte (8 x bf16) vector <-> 8 floats
 DDLPC_DEVICE void unpack8(const uint4& v, float (&f)[8]) {
