@@ -245,10 +245,13 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   a.pshift = fptr_opt(pshift);
   if (a.pscale) TORCH_CHECK(a.C1 <= 512, "prologue supports C1 <= 512");
   const int bco = a.Cout <= 32 ? 32 : 64;
-  // 128-pixel tiles
-  if (g.dims == 2) { a.TD = 1; a.TW = g.W >= 16 ? 16 : 8; a.TH = 128 / a.TW; }
+  static const int use_v2 = [] { const char* e = getenv("DDLPC_WGRAD_V2"); return e ? atoi(e) : 1; }();
+  const bool v2 = use_v2 && g.dims == 2 && g.W >= 16 && (a.C2 == 0 || a.C1 % 32 == 0);
+  // 128-pixel tiles (v2: 16 x conv3_wgrad2_pt/16)
+  if (v2) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad2_pt(bco) / 16; }
+  else if (g.dims == 2) { a.TD = 1; a.TW = g.W >= 16 ? 16 : 8; a.TH = 128 / a.TW; }
   else { a.TW = g.W >= 16 ? 16 : 8; a.TH = 4; a.TD = 128 / (a.TW * a.TH); }
-  TORCH_CHECK((a.TD + (g.dims == 3 ? 2 : 0)) * (a.TH + 2) * (a.TW + 2) <= conv3_wgrad_halo_cap(g.dims),
+  TORCH_CHECK(v2 || (a.TD + (g.dims == 3 ? 2 : 0)) * (a.TH + 2) * (a.TW + 2) <= conv3_wgrad_halo_cap(g.dims),
               "wgrad halo exceeds LDS capacity");
   a.tilesD = (g.D + a.TD - 1) / a.TD;
   a.tilesH = (g.H + a.TH - 1) / a.TH;
@@ -266,7 +269,8 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   a.splits = splits;
   auto part = at::empty({(int64_t)splits * a.Cout * a.taps * a.Cin}, dy.options().dtype(at::kFloat));
   a.partial = part.data_ptr<float>();
-  conv3_wgrad_launch(a, bco, cur_stream());
+  if (v2) conv3_wgrad2_launch(a, bco, cur_stream());
+  else conv3_wgrad_launch(a, bco, cur_stream());
   std::vector<int64_t> wshape = {a.Cout, a.Cin, 3, 3};
   if (g.dims == 3) wshape.push_back(3);
   const bool into = out.has_value() && out->defined();

@@ -93,9 +93,9 @@ DDLPC_DEVICE float wave_max(float v) {
 // lane i receives column i of the 4 rows (row q in element q).  EXEC must be all ones.
 DDLPC_DEVICE uint2 lds_read_tr16(const void* lds_ptr) {
   typedef short v4s __attribute__((ext_vector_type(4)));
-  v4s r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) v4s*)(
-          (__attribute__((address_space(3))) char*)((size_t)lds_ptr)));
+  // address-space cast (not an integer round trip) keeps pointer provenance, so the read
+  // inherits the alias scope of a restrict-qualified LDS operand pointer
+  v4s r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(lds_ptr));
   return __builtin_bit_cast(uint2, r);
 }
 

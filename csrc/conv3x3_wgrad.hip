@@ -16,6 +16,7 @@
 // fixed order (bit-reproducible, so all data-parallel ranks stay bit-identical) and
 // accumulates into the fp32 OIHW parameter gradient.
 #include "common.h"
+#include "conv_lds.h"
 #include "ops.h"
 
 namespace ddlpc {
@@ -247,6 +248,219 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad_kernel(ConvWgradArgs p) {
   (void)tiles_per_img;
 }
 
+// ============================================================================ 2-D, v2
+// Same GEMM and partial-slab contract, restructured like the forward kernels:
+//   * both operands arrive by LDS-DMA into DOUBLE-BUFFERED LDS (no VGPR round trip, no
+//     integer division in the tile loop: per-lane source geometry is tile independent);
+//     the tile t+1 DMA is in flight while tile t computes, ONE barrier per tile;
+//   * the prologue (BN-apply + ReLU) runs in LDS on the pieces each lane DMA'd, before the
+//     barrier;
+//   * dY rows carry an XOR swizzle on 32-B segments so the transposed A reads are bank-
+//     conflict free (x = row bit 1 | row bit 3 << 1 for 128-B rows, row bit 3 for 64-B);
+//     the swizzle is lane-constant, so every read address folds into the offset field;
+//   * X halo rows stay linear (tap offsets fold into immediates; the B reads are 2-way).
+template <int BCO, int PT>
+struct Wg2Cfg {
+  static constexpr int NCO = BCO / 16;
+  static constexpr int NP = 5;
+  static constexpr int TH = PT / 16;
+  static constexpr int HALO = (TH + 2) * 18;
+  static constexpr int Y_ROWB = BCO * 2;
+  static constexpr int Y_PIECES = PT * BCO / 8;
+  static constexpr int Y_INSTR = Y_PIECES / 64;
+  static constexpr int Y_ITERS = (Y_INSTR + 3) / 4;
+  static constexpr int Y_BYTES = Y_INSTR * 1024;
+  static constexpr int X_PIECES = HALO * 4;
+  static constexpr int X_INSTR = (X_PIECES + 63) / 64;
+  static constexpr int X_ITERS = (X_INSTR + 3) / 4;
+  static constexpr int X_BYTES = X_INSTR * 1024;
+  static constexpr int SS_BYTES = 2 * 512 * 4;
+  static constexpr int SMEM = SS_BYTES + 2 * (Y_BYTES + X_BYTES);
+  static constexpr int KSTEPS = PT / 32;
+};
+
+template <int BCO>
+DDLPC_DEVICE int wg2_yswz(int row) {             // XOR on the 16-B piece index
+  return BCO == 64 ? ((((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1) : (((row >> 3) & 1) << 1);
+}
+
+template <int BCO, int PT>
+__global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
+  using namespace convlds;
+  using Cfg = Wg2Cfg<BCO, PT>;
+  constexpr int TH = Cfg::TH, HW2 = 18;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* s_scale = reinterpret_cast<float*>(smem);
+  float* s_shift = s_scale + 512;
+  char* base = smem + Cfg::SS_BYTES;
+  auto sY = [&](int b) { return base + b * (Cfg::Y_BYTES + Cfg::X_BYTES); };
+  auto sX = [&](int b) { return base + b * (Cfg::Y_BYTES + Cfg::X_BYTES) + Cfg::Y_BYTES; };
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int b = blockIdx.x;
+  const int split = b % p.splits; b /= p.splits;
+  const int cic = b % p.ciChunks; b /= p.ciChunks;
+  const int co0 = b * BCO, ci0 = cic * BK;
+
+  const bool has_pro = p.pscale != nullptr;
+  if (has_pro)
+    for (int c = tid; c < p.C1; c += 256) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
+  const int t_begin = (int)((long long)p.nTiles * split / p.splits);
+  const int t_end = (int)((long long)p.nTiles * (split + 1) / p.splits);
+  const long long img_px = (long long)p.H * p.W;
+
+  // ---- tile-independent per-lane DMA geometry
+  int y_pw[Cfg::Y_ITERS], y_ph[Cfg::Y_ITERS], y_rel[Cfg::Y_ITERS];
+#pragma unroll
+  for (int i = 0; i < Cfg::Y_ITERS; ++i) {
+    const int e = (i * 4 + wave) * 64 + lane;
+    const int row = e / (BCO / 8), pc = e % (BCO / 8);
+    const int sp = pc ^ wg2_yswz<BCO>(row);        // source piece stored at LDS piece pc
+    y_pw[i] = row % 16;
+    y_ph[i] = row / 16;
+    const int co = co0 + sp * 8;
+    y_rel[i] = co < p.Cout ? (y_ph[i] * p.W + y_pw[i]) * p.Cout + co : -1;
+  }
+  int x_dw[Cfg::X_ITERS], x_dh[Cfg::X_ITERS], x_pix[Cfg::X_ITERS];
+#pragma unroll
+  for (int i = 0; i < Cfg::X_ITERS; ++i) {
+    const int e = (i * 4 + wave) * 64 + lane;
+    const int px = e >> 2;
+    x_dw[i] = px < Cfg::HALO ? px % HW2 - 1 : -(1 << 20);
+    x_dh[i] = px / HW2 - 1;
+    x_pix[i] = -1;
+  }
+  const int c8l = ci0 + (lane & 3) * 8;              // this lane's X channel group
+  const bool second = ci0 >= p.C1;                   // chunk served by X2 (C1 % 32 == 0)
+  const int Cs = second ? p.C2 : p.C1;
+  const int cs0 = second ? c8l - p.C1 : c8l;
+  const bf16_t* xsrc = second ? p.X2 : p.X1;
+  const bool xch_ok = cs0 < Cs;
+
+  auto issue = [&](int tile, int buf) {
+    int t = tile;
+    const int tw_i = t % p.tilesW; t /= p.tilesW;
+    const int th_i = t % p.tilesH; t /= p.tilesH;
+    const int n = t;
+    const int h0 = th_i * TH, w0 = tw_i * 16;
+    const auto ry = make_rsrc(p.dY + n * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
+    const int ybase = (h0 * p.W + w0) * p.Cout;
+#pragma unroll
+    for (int i = 0; i < Cfg::Y_ITERS; ++i) {
+      if ((i * 4 + wave) >= Cfg::Y_INSTR) break;
+      const bool ok = y_rel[i] >= 0 && w0 + y_pw[i] < p.W && h0 + y_ph[i] < p.H;
+      dma16(ry, sY(buf) + (i * 4 + wave) * 1024, ok ? (unsigned)(ybase + y_rel[i]) * 2u : kOOB);
+    }
+    const auto rx = make_rsrc(xsrc + n * img_px * Cs, (unsigned)(img_px * Cs * 2));
+#pragma unroll
+    for (int i = 0; i < Cfg::X_ITERS; ++i) {
+      if ((i * 4 + wave) >= Cfg::X_INSTR) break;
+      const int gw = w0 + x_dw[i], gh = h0 + x_dh[i];
+      x_pix[i] = (gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && xch_ok) ? gh * p.W + gw : -1;
+      dma16(rx, sX(buf) + (i * 4 + wave) * 1024, x_pix[i] >= 0 ? (unsigned)(x_pix[i] * Cs + cs0) * 2u : kOOB);
+    }
+  };
+  auto transform = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < Cfg::X_ITERS; ++i) {
+      const int e = (i * 4 + wave) * 64 + lane;
+      if ((i * 4 + wave) < Cfg::X_INSTR && x_pix[i] >= 0) {
+        uint4* q = reinterpret_cast<uint4*>(sX(buf) + e * 16);
+        float f[8];
+        unpack8(*q, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = min(c8l + j, p.C1 - 1);
+          f[j] = fmaxf(fmaf(f[j], s_scale[c], s_shift[c]), 0.0f);
+        }
+        *q = pack8(f);
+      }
+    }
+  };
+
+  // ---- per-lane transposed-read geometry
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  // A (dY): rows ks*32 + 8g + 4h + q; swizzle depends only on (g, h, q)
+  int ya[2][Cfg::NCO];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < Cfg::NCO; ++j) {
+      const int row = 8 * g + 4 * h + q;
+      const int pc = 2 * j + (pp >> 1);
+      ya[h][j] = row * Cfg::Y_ROWB + ((pc ^ wg2_yswz<BCO>(row)) << 4) + (pp & 1) * 8;
+    }
+  // B (X): tile pixel ks*32 + 8g + 4h + q -> halo row; + tap offset
+  int xb[Cfg::KSTEPS][2];
+#pragma unroll
+  for (int ks = 0; ks < Cfg::KSTEPS; ++ks)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int pix = ks * 32 + 8 * g + 4 * h + q;
+      xb[ks][h] = ((pix / 16) * HW2 + pix % 16) * 64 + (pp >> 1) * 16 + (pp & 1) * 8;
+    }
+
+  f32x4_t acc[Cfg::NCO][Cfg::NP];
+#pragma unroll
+  for (int j = 0; j < Cfg::NCO; ++j)
+#pragma unroll
+    for (int q2 = 0; q2 < Cfg::NP; ++q2) acc[j][q2] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](const char* __restrict__ Y, const char* __restrict__ X) {
+#pragma unroll
+    for (int ks = 0; ks < Cfg::KSTEPS; ++ks) {
+      uint4 af[Cfg::NCO];
+#pragma unroll
+      for (int j = 0; j < Cfg::NCO; ++j) {
+        const uint2 lo = lds_read_tr16(Y + ks * 32 * Cfg::Y_ROWB + ya[0][j]);
+        const uint2 hi = lds_read_tr16(Y + ks * 32 * Cfg::Y_ROWB + ya[1][j]);
+        af[j] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+#pragma unroll
+      for (int pi = 0; pi < Cfg::NP; ++pi) {
+        const int pair = wave + 4 * pi;                 // wave-uniform
+        if (pair < 18) {
+          const int tap = pair >> 1, cih = pair & 1;
+          const int toff = ((tap / 3) * HW2 + tap % 3) * 64 + cih * 32;
+          const uint2 lo = lds_read_tr16(X + xb[ks][0] + toff);
+          const uint2 hi = lds_read_tr16(X + xb[ks][1] + toff);
+          const uint4 bfr = make_uint4(lo.x, lo.y, hi.x, hi.y);
+#pragma unroll
+          for (int j = 0; j < Cfg::NCO; ++j) acc[j][pi] = mfma16x16x32(af[j], bfr, acc[j][pi]);
+        }
+      }
+    }
+  };
+
+  if (t_begin < t_end) issue(t_begin, 0);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int buf = (tile - t_begin) & 1;
+    dma_wait<0>();
+    if (has_pro && !second) transform(buf);
+    lds_sync();
+    if (tile + 1 < t_end) issue(tile + 1, buf ^ 1);
+    compute(sY(buf), sX(buf));
+  }
+
+  // ---- partial slab: part[split][co][tap][ci]
+  float* out = p.partial + (long long)split * p.Cout * 9 * p.Cin;
+#pragma unroll
+  for (int pi = 0; pi < Cfg::NP; ++pi) {
+    const int pair = wave + 4 * pi;
+    if (pair >= 18) continue;
+    const int tap = pair >> 1;
+    const int ci = ci0 + (pair & 1) * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < Cfg::NCO; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = co0 + j * 16 + 4 * g + i;
+        if (co < p.Cout && ci < p.Cin) out[((long long)co * 9 + tap) * p.Cin + ci] = acc[j][pi][i];
+      }
+  }
+}
+
 template <int DIMS, int BCO>
 void launch_wg(ConvWgradArgs& a, hipStream_t st) {
   using Cfg = WgCfg<DIMS, BCO>;
@@ -255,6 +469,15 @@ void launch_wg(ConvWgradArgs& a, hipStream_t st) {
 }
 
 }  // namespace
+
+void conv3_wgrad2_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
+  const int grid = a.coTiles * a.ciChunks * a.splits;
+  if (bco == 32)
+    hipLaunchKernelGGL((conv3_wgrad2_kernel<32, 256>), dim3(grid), dim3(256), (Wg2Cfg<32, 256>::SMEM), st, a);
+  else
+    hipLaunchKernelGGL((conv3_wgrad2_kernel<64, 128>), dim3(grid), dim3(256), (Wg2Cfg<64, 128>::SMEM), st, a);
+}
+int conv3_wgrad2_pt(int bco) { return bco == 32 ? 256 : 128; }
 
 void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
   if (a.dims == 2) {

@@ -152,7 +152,9 @@ def test_conv3_dgrad_split(ops, C1, C2, Cout):
 
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout,pro", [
     (2, 16, 16, 32, 0, 32, False), (2, 32, 32, 64, 0, 64, True), (1, 16, 16, 64, 64, 128, False),
-    (4, 8, 8, 256, 0, 256, True), (2, 32, 32, 3, 0, 32, False), (1, 16, 16, 64, 32, 32, False)])
+    (4, 8, 8, 256, 0, 256, True), (2, 32, 32, 3, 0, 32, False), (1, 16, 16, 64, 32, 32, False),
+    (2, 64, 64, 64, 32, 32, True), (2, 72, 40, 32, 0, 64, True), (1, 128, 128, 128, 64, 64, False),
+    (2, 48, 48, 128, 0, 96, True)])
 def test_conv3_wgrad(ops, N, H, W, C1, C2, Cout, pro):
     torch.manual_seed(3)
     x1 = torch.randn(N, C1, H, W, device=DEV).bfloat16()
