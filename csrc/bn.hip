@@ -203,6 +203,133 @@ __global__ void bn_bwd_kernel(const bf16_t* __restrict__ dA, const bf16_t* __res
   }
 }
 
+// 2-D backward, v2: fully coalesced and unrolled.  A thread keeps one 8-channel group
+// (constants in registers); consecutive lanes walk consecutive 16-B pieces of memory:
+//   no pool: unit = pixel, lanes (cg) cover the pixel's C channels;
+//   pool:    unit = 2x2 window, lanes (kw, cg) cover the window's top-row pixel pair
+//            contiguously and each lane also handles the pixel below it; the window arg-max
+//            is completed with the kw partner lane (lane ^ G) — first maximum wins in
+//            PyTorch's (kh, kw) scan order.
+// Requires G = C/8 a power of two (pool: G <= 32) and even H, W for pool.
+template <bool POOL, int MODE>
+__global__ __launch_bounds__(256) void bn_bwd2_kernel(
+    const bf16_t* __restrict__ dA, const bf16_t* __restrict__ dP, const bf16_t* __restrict__ y,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ coefs, const float* __restrict__ gscale,
+    float* __restrict__ partial, bf16_t* __restrict__ dY, int N, int H, int W, int C) {
+  constexpr int UNROLL = 2;
+  const int G = C / 8;
+  const int L = POOL ? 2 * G : G;                 // lanes per unit (divides 256)
+  const int tid = threadIdx.x;
+  const int cg = tid % G, c8 = cg * 8;
+  const int kw = POOL ? (tid / G) & 1 : 0;
+  const int upb = 256 / L;                        // units per block per step
+  const int Wo = W / 2;
+  const int units = POOL ? N * (H / 2) * Wo : N * H * W;
+  const int stride = gridDim.x * upb;
+  const float gs = gscale != nullptr ? gscale[0] : 1.0f;
+  float sc[8], sh[8], is[8], nm[8], k1[8], m1[8], m2[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = scale[c8 + j]; sh[j] = shift[c8 + j];
+    is[j] = invstd[c8 + j]; nm[j] = -mean[c8 + j] * is[j];
+    if (MODE == 1) { k1[j] = coefs[c8 + j]; m1[j] = coefs[C + c8 + j]; m2[j] = coefs[2 * C + c8 + j]; }
+    s1[j] = 0.f; s2[j] = 0.f;
+  }
+  constexpr int NK = POOL ? 2 : 1;                // pixels per lane per unit (kh)
+  for (int u0 = blockIdx.x * upb + tid / L; u0 < units; u0 += UNROLL * stride) {
+    uint4 vy[UNROLL][NK], vd[UNROLL][NK], vp[UNROLL];
+    long long off[UNROLL][NK];
+    bool ok[UNROLL];
+#pragma unroll
+    for (int r = 0; r < UNROLL; ++r) {            // all loads first (memory-level parallelism)
+      const int u = u0 + r * stride;
+      ok[r] = u < units;
+      const int uu = ok[r] ? u : u0;
+      if (POOL) {
+        const int rr = uu / Wo, wo = uu - rr * Wo;
+        const long long pix0 = (long long)rr * 2 * W + 2 * wo + kw;
+        off[r][0] = pix0 * C + c8;
+        off[r][NK - 1] = (pix0 + W) * C + c8;
+        vp[r] = *reinterpret_cast<const uint4*>(dP + (long long)uu * C + c8);
+      } else {
+        off[r][0] = (long long)uu * C + c8;
+      }
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        vy[r][k] = *reinterpret_cast<const uint4*>(y + off[r][k]);
+        vd[r][k] = dA != nullptr ? *reinterpret_cast<const uint4*>(dA + off[r][k]) : make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < UNROLL; ++r) {
+      float fy[NK][8], fd[NK][8], fp[8];
+      int bestk[8];
+#pragma unroll
+      for (int k = 0; k < NK; ++k) { unpack8(vy[r][k], fy[k]); unpack8(vd[r][k], fd[k]); }
+      if (POOL) {
+        unpack8(vp[r], fp);
+        // bf16-rounded activations of my two pixels, partner's via lane ^ G
+        float a[2][8];
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            const uint32_t w2 = pack2(fmaxf(fmaf(fy[k][j], sc[j], sh[j]), 0.f),
+                                      fmaxf(fmaf(fy[k][j + 1], sc[j + 1], sh[j + 1]), 0.f));
+            a[k][j] = lo_bf(w2); a[k][j + 1] = hi_bf(w2);
+          }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float p0 = __shfl_xor(a[0][j], G, 64), p1 = __shfl_xor(a[1][j], G, 64);
+          // window values in scan order w = 2*kh + kw
+          const float v0 = kw ? p0 : a[0][j], v1 = kw ? a[0][j] : p0;
+          const float v2 = kw ? p1 : a[1][j], v3 = kw ? a[1][j] : p1;
+          int best = 0;
+          float bv = v0;
+          if (v1 > bv) { bv = v1; best = 1; }
+          if (v2 > bv) { bv = v2; best = 2; }
+          if (v3 > bv) { best = 3; }
+          bestk[j] = best;                        // routed to (kh, kw) = (best >> 1, best & 1)
+        }
+      }
+      if (!ok[r]) continue;
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float a = fmaf(fy[k][j], sc[j], sh[j]);
+          float dt = fd[k][j];
+          if (POOL && bestk[j] == 2 * k + kw) dt += fp[j];
+          const float dyh = a > 0.f ? dt * gs : 0.f;
+          const float xh = fmaf(fy[k][j], is[j], nm[j]);
+          if (MODE == 0) { s1[j] += dyh; s2[j] = fmaf(dyh, xh, s2[j]); }
+          else o[j] = k1[j] * (dyh - m1[j] - xh * m2[j]);
+        }
+        if (MODE == 1) *reinterpret_cast<uint4*>(dY + off[r][k]) = pack8(o);
+      }
+    }
+  }
+  if (MODE == 0) {
+    // block reduction: threads with equal cg hold the same channels
+    __shared__ float red[256 * 8];
+    for (int half = 0; half < 2; ++half) {
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[j * 256 + tid] = half ? s2[j] : s1[j];
+      __syncthreads();
+      for (int c = tid; c < C; c += 256) {
+        const int g2 = c / 8, j = c % 8;
+        float t = 0.f;
+        for (int k = g2; k < 256; k += G) t += red[j * 256 + k];
+        partial[(long long)blockIdx.x * 2 * C + half * C + c] = t;
+      }
+    }
+  }
+}
+
 int grid_for(long long items, int per_block) {
   long long g = (items + per_block - 1) / per_block;
   return (int)std::max<long long>(1, std::min<long long>(g, 2048));
@@ -211,9 +338,19 @@ int grid_for(long long items, int per_block) {
 }  // namespace
 
 int bn_bwd_reduce_blocks(long long items) {
-  // <= 512 partial rows: the per-channel finalize reads them in one kernel
-  return (int)std::max<long long>(1, std::min<long long>((items + 63) / 64, 512));
+  // <= 2048 partial rows (the per-channel finalize reads them in one kernel): enough
+  // workgroups to keep HBM busy
+  return (int)std::max<long long>(1, std::min<long long>((items + 63) / 64, 2048));
 }
+
+namespace {
+bool bn_bwd2_ok(int dims, bool pool, int H, int W, int C) {
+  const int G = C / 8;
+  if (dims != 2 || C % 8 != 0 || (G & (G - 1)) != 0 || G > 256) return false;
+  if (pool && (G > 32 || H % 2 != 0 || W % 2 != 0)) return false;
+  return true;
+}
+}  // namespace
 
 void bn_relu_apply_launch(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
                           bf16_t* pooled, int dims, int N, int D, int H, int W, int C,
@@ -266,6 +403,13 @@ void bn_bwd_reduce_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y,
   const bool pool = dP != nullptr;
   const float* coefs = nullptr;
   bf16_t* dY = nullptr;
+  if (bn_bwd2_ok(dims, pool, H, W, C)) {
+    if (pool) hipLaunchKernelGGL((bn_bwd2_kernel<true, 0>), dim3(nblocks), dim3(256), 0, st, dA, dP, y,
+                                 scale, shift, mean, invstd, coefs, gscale, partial, dY, N, H, W, C);
+    else hipLaunchKernelGGL((bn_bwd2_kernel<false, 0>), dim3(nblocks), dim3(256), 0, st, dA, dP, y,
+                            scale, shift, mean, invstd, coefs, gscale, partial, dY, N, H, W, C);
+    return;
+  }
   BN_BWD_DISPATCH(0, nblocks);
 }
 
@@ -279,6 +423,15 @@ void bn_bwd_apply_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y, co
   const long long items = (long long)N * (pool ? (dims == 3 ? D / 2 : 1) * (H / 2) * (W / 2)
                                                 : (long long)D * H * W);
   const int per = std::max(1, 256 / G);
+  if (bn_bwd2_ok(dims, pool, H, W, C)) {
+    const int upb = 256 / (pool ? 2 * G : G);
+    const int grid2 = (int)std::max<long long>(1, std::min<long long>((items + 2 * upb - 1) / (2 * upb), 8192));
+    if (pool) hipLaunchKernelGGL((bn_bwd2_kernel<true, 1>), dim3(grid2), dim3(256), 0, st, dA, dP, y,
+                                 scale, shift, mean, invstd, coefs, gscale, partial, dY, N, H, W, C);
+    else hipLaunchKernelGGL((bn_bwd2_kernel<false, 1>), dim3(grid2), dim3(256), 0, st, dA, dP, y,
+                            scale, shift, mean, invstd, coefs, gscale, partial, dY, N, H, W, C);
+    return;
+  }
   const int grid = std::min(grid_for(items, per), 16384);
   BN_BWD_DISPATCH(1, grid);
 }
