@@ -34,6 +34,7 @@ DDLPC_HOST_DEVICE float bf2f(bf16_t h) {
 
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef short i16x2_t __attribute__((ext_vector_type(2)));
 
 // round-to-nearest-even (NaN kept quiet).  Device code: the gfx950 hardware conversion
 // (v_cvt_pk_bf16_f32, RNE); host code: the same rounding in integer arithmetic.

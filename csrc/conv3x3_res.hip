@@ -112,44 +112,59 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     it.h0 = th_i * p.TH; it.w0 = tw_i * p.TW;
     return it;
   };
-  // ---- per-lane halo DMA geometry (no integer division in the stage loop)
-  int a_dw[C::A_ITERS], a_dh[C::A_ITERS], a_sub8[C::A_ITERS], a_pix[C::A_ITERS];
+  // ---- per-lane halo DMA geometry (no integer division in the stage loop).  Interior
+  // tiles (the common case) need no bounds checks: pixel = tile base + a_rel.
+  int a_dw[C::A_ITERS], a_dh[C::A_ITERS], a_sub8[C::A_ITERS], a_rel[C::A_ITERS];
+  uint32_t a_inhalo = 0;
 #pragma unroll
   for (int i = 0; i < C::A_ITERS; ++i) {
     const int e = (i * NW + wave) * 64 + lane;
     const int px = TAP8 ? e : e >> 2;
     a_sub8[i] = TAP8 ? 0 : ((e & 3) ^ swz(px)) << 3;
-    a_dw[i] = px < halo ? px % HW2 - 1 : -(1 << 20);    // outside the halo: padding
+    a_dw[i] = px % HW2 - 1;
     a_dh[i] = px / HW2 - 1;
-    a_pix[i] = -1;
+    a_rel[i] = a_dh[i] * p.W + a_dw[i];
+    if (px < halo && e < C::PIECES) a_inhalo |= 1u << i;
   }
-  int a_item = -1, a_nimg = 0;
+  uint32_t a_valid = 0;            // pieces of the current item inside the image
+  int a_item = -1, a_nimg = 0, a_base = 0;
   auto issue_A = [&](int k, int chunk, int buf) {
     if (k != a_item) {
       const Item it = item_of(k);
       a_item = k;
       a_nimg = it.n_img;
+      a_base = it.h0 * p.W + it.w0;
+      const bool interior = it.w0 >= 1 && it.h0 >= 1 && it.w0 + p.TW < p.W && it.h0 + p.TH < p.H;
+      if (interior) {
+        a_valid = a_inhalo;
+      } else {
+        a_valid = 0;
 #pragma unroll
-      for (int i = 0; i < C::A_ITERS; ++i) {
-        const int gw = it.w0 + a_dw[i], gh = it.h0 + a_dh[i];
-        a_pix[i] = (gw >= 0 && gw < p.W && gh >= 0 && gh < p.H) ? gh * p.W + gw : -1;
+        for (int i = 0; i < C::A_ITERS; ++i) {
+          const int gw = it.w0 + a_dw[i], gh = it.h0 + a_dh[i];
+          if (gw >= 0 && gw < p.W && gh >= 0 && gh < p.H) a_valid |= 1u << i;
+        }
+        a_valid &= a_inhalo;
       }
     }
     const int cbase = chunk * BK;
     const bool second = cbase >= p.C1;                 // chunk served by X2 (C1 % 32 == 0)
     const int Cs = second ? p.C2 : p.C1;
     const int c0 = second ? cbase - p.C1 : cbase;
+    const bool full = c0 + BK <= Cs;                   // wave-uniform: no channel check
     const bf16_t* src = second ? p.X2 : p.X1;
     const auto r = make_rsrc(src + a_nimg * img_px * Cs, (unsigned)(img_px * Cs * 2));
+    const int s0 = a_base * Cs + c0;                   // scalar part of the element offset
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
       if ((i * NW + wave) * 64 >= C::PIECES) break;    // wave-uniform
-      const int c8 = c0 + a_sub8[i];
-      const unsigned off = (a_pix[i] >= 0 && c8 < Cs) ? (unsigned)(a_pix[i] * Cs + c8) * 2u : kOOB;
+      const bool ok = ((a_valid >> i) & 1u) && (full || c0 + a_sub8[i] < Cs);
+      const unsigned off = ok ? (unsigned)(a_rel[i] * Cs + a_sub8[i] + s0) * 2u : kOOB;
       dma16(r, sA(buf) + (i * NW + wave) * 1024, off);
     }
   };
-  // prologue on the pieces THIS lane DMA'd (a_pix still describes the chunk's item)
+  // prologue on the pieces THIS lane DMA'd (a_valid still describes the chunk's item):
+  // packed fp32 FMA, bf16 rounding, ReLU as a packed signed-16-bit max on the bf16 bits
   auto transform_A = [&](int chunk, int buf) {
     const int cbase = chunk * BK;
     if (cbase >= p.C1) return;
@@ -157,13 +172,27 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     for (int i = 0; i < C::A_ITERS; ++i) {
       const int e = (i * NW + wave) * 64 + lane;
       const int c8 = cbase + a_sub8[i];
-      if (e < C::PIECES && c8 < p.C1 && a_pix[i] >= 0) {
+      if (((a_valid >> i) & 1u) && c8 < p.C1) {
         uint4* q = reinterpret_cast<uint4*>(sA(buf) + e * 16);
-        float f[8];
-        unpack8(*q, f);
+        const uint4 v = *q;
+        const float4* scp = reinterpret_cast<const float4*>(s_scale + c8);
+        const float4* shp = reinterpret_cast<const float4*>(s_shift + c8);
+        const float4 sa = scp[0], sb = scp[1], ha = shp[0], hb = shp[1];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        const float scf[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+        const float shf[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
+        uint32_t o[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], s_scale[c8 + j], s_shift[c8 + j]), 0.0f);
-        *q = pack8(f);
+        for (int j = 0; j < 4; ++j) {
+          const f32x2_t x = {lo_bf(w[j]), hi_bf(w[j])};
+          const f32x2_t sc2 = {scf[2 * j], scf[2 * j + 1]};
+          const f32x2_t sh2 = {shf[2 * j], shf[2 * j + 1]};
+          const f32x2_t y2 = __builtin_elementwise_fma(x, sc2, sh2);
+          const uint32_t pk = __builtin_bit_cast(uint32_t, __builtin_convertvector(y2, bf16x2_t));
+          const i16x2_t m = __builtin_elementwise_max(__builtin_bit_cast(i16x2_t, pk), i16x2_t{0, 0});
+          o[j] = __builtin_bit_cast(uint32_t, m);
+        }
+        *q = make_uint4(o[0], o[1], o[2], o[3]);
       }
     }
   };
@@ -209,27 +238,39 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   // tile pixel (wm*MT*16 + mt*16 + (lane&15))
   auto epilogue = [&](int k) {
     const Item it = item_of(k);
+    const bool split = p.Co1 < p.Cout;                 // dgrad of a concat conv (rare)
+    bf16_t* y1img = p.Y1 + (long long)it.n_img * img_px * p.Co1;
+    bf16_t* y2img = split ? p.Y2 + (long long)it.n_img * img_px * (p.Cout - p.Co1) : nullptr;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
       const int gw = it.w0 + pix % p.TW, gh = it.h0 + pix / p.TW;
       const bool valid = gw < p.W && gh < p.H;
-      const long long gpix = ((long long)it.n_img * p.H + gh) * p.W + gw;
+      const int lp = gh * p.W + gw;                     // pixel within the image (32-bit)
+      bf16_t* row1 = y1img + lp * p.Co1;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * g;
-        float v[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bias_r[nt][i];
-        const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        const f32x2_t v01 = f32x2_t{acc[mt][nt][0], acc[mt][nt][1]} + f32x2_t{bias_r[nt][0], bias_r[nt][1]};
+        const f32x2_t v23 = f32x2_t{acc[mt][nt][2], acc[mt][nt][3]} + f32x2_t{bias_r[nt][2], bias_r[nt][3]};
+        const uint2 pk = make_uint2(__builtin_bit_cast(uint32_t, __builtin_convertvector(v01, bf16x2_t)),
+                                    __builtin_bit_cast(uint32_t, __builtin_convertvector(v23, bf16x2_t)));
         if (valid && co < p.Cout) {
-          if (co < p.Co1) *reinterpret_cast<uint2*>(p.Y1 + gpix * p.Co1 + co) = pk;
-          else *reinterpret_cast<uint2*>(p.Y2 + gpix * (p.Cout - p.Co1) + (co - p.Co1)) = pk;
-          const float r0 = lo_bf(pk.x), r1 = hi_bf(pk.x), r2 = lo_bf(pk.y), r3 = hi_bf(pk.y);
-          s1[nt][0] += r0; s2[nt][0] += r0 * r0;
-          s1[nt][1] += r1; s2[nt][1] += r1 * r1;
-          s1[nt][2] += r2; s2[nt][2] += r2 * r2;
-          s1[nt][3] += r3; s2[nt][3] += r3 * r3;
+          if (!split) {
+            *reinterpret_cast<uint2*>(row1 + co) = pk;
+          } else {                                     // wave-uniform branch
+            bf16_t* dst = co < p.Co1 ? row1 + co : y2img + lp * (p.Cout - p.Co1) + (co - p.Co1);
+            *reinterpret_cast<uint2*>(dst) = pk;
+          }
+          // statistics of the stored (bf16-rounded) values
+          const f32x2_t r01 = {lo_bf(pk.x), hi_bf(pk.x)}, r23 = {lo_bf(pk.y), hi_bf(pk.y)};
+          f32x2_t a01 = {s1[nt][0], s1[nt][1]}, a23 = {s1[nt][2], s1[nt][3]};
+          f32x2_t q01 = {s2[nt][0], s2[nt][1]}, q23 = {s2[nt][2], s2[nt][3]};
+          a01 += r01; a23 += r23;
+          q01 = __builtin_elementwise_fma(r01, r01, q01);
+          q23 = __builtin_elementwise_fma(r23, r23, q23);
+          s1[nt][0] = a01.x; s1[nt][1] = a01.y; s1[nt][2] = a23.x; s1[nt][3] = a23.y;
+          s2[nt][0] = q01.x; s2[nt][1] = q01.y; s2[nt][2] = q23.x; s2[nt][3] = q23.y;
         }
         acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       }
