@@ -23,6 +23,13 @@ typedef short i16x8_t __attribute__((ext_vector_type(8)));
 typedef short i16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+
+// 8-byte store of 4 bf16 (an ext-vector type carries its 8-byte alignment, so this is one
+// global_store_dwordx2 — a HIP uint2 store through a computed pointer can be split)
+DDLPC_DEVICE void store_bf16x4(bf16_t* dst, uint32_t lo, uint32_t hi) {
+  *reinterpret_cast<u32x2_t*>(dst) = u32x2_t{lo, hi};
+}
 
 constexpr int kWave = 64;
 

@@ -267,8 +267,8 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
         for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bias_r[nt][i];
         const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         if (valid && co < p.Cout) {
-          if (co < p.Co1) *reinterpret_cast<uint2*>(p.Y1 + gpix * p.Co1 + co) = pk;
-          else *reinterpret_cast<uint2*>(p.Y2 + gpix * (p.Cout - p.Co1) + (co - p.Co1)) = pk;
+          if (co < p.Co1) store_bf16x4(p.Y1 + gpix * p.Co1 + co, pk.x, pk.y);
+          else store_bf16x4(p.Y2 + gpix * (p.Cout - p.Co1) + (co - p.Co1), pk.x, pk.y);
           // statistics of the stored (bf16-rounded) values
           const float r0 = lo_bf(pk.x), r1 = hi_bf(pk.x), r2 = lo_bf(pk.y), r3 = hi_bf(pk.y);
           s1[nt][0] += r0; s2[nt][0] += r0 * r0;

@@ -257,10 +257,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
                                     __builtin_bit_cast(uint32_t, __builtin_convertvector(v23, bf16x2_t)));
         if (valid && co < p.Cout) {
           if (!split) {
-            *reinterpret_cast<uint2*>(row1 + co) = pk;
+            store_bf16x4(row1 + co, pk.x, pk.y);
           } else {                                     // wave-uniform branch
             bf16_t* dst = co < p.Co1 ? row1 + co : y2img + lp * (p.Cout - p.Co1) + (co - p.Co1);
-            *reinterpret_cast<uint2*>(dst) = pk;
+            store_bf16x4(dst, pk.x, pk.y);
           }
           // statistics of the stored (bf16-rounded) values
           const f32x2_t r01 = {lo_bf(pk.x), hi_bf(pk.x)}, r23 = {lo_bf(pk.y), hi_bf(pk.y)};
