@@ -148,12 +148,13 @@ class TrainConfig:
 
 
 def _flag_type(tp, default):
-    if tp in ("bool", bool) or isinstance(default, bool):
+    t = str(tp)                          # annotations are strings (postponed evaluation)
+    if t in ("bool", "<class 'bool'>") or isinstance(default, bool):
         return lambda s: str(s).lower() in ("1", "true", "yes", "on")
-    if isinstance(default, float):
+    if isinstance(default, float) or t in ("float", "Optional[float]"):
         return float
-    if isinstance(default, int):
-        return int
+    if isinstance(default, int) or t in ("int", "Optional[int]"):
+        return lambda s: None if s in ("", "none", "None") else int(s)
     if isinstance(default, tuple):
         return lambda s: tuple(float(x) for x in s.split(","))
     return lambda s: None if s in ("", "none", "None") else s
