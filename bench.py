@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=8.0)
     ap.add_argument("--codec", default="none")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--hip-graph", type=int, default=int(os.environ.get("DDLPC_HIP_GRAPH", "0")),
+                    help="1: replay the single-GPU train step as one hipGraph")
     args = ap.parse_args()
 
     from ddlpc.config import ModelConfig, TrainConfig
@@ -66,7 +68,7 @@ def main():
                                         width_divisor=args.width_divisor),
                       tile=args.tile, batch_per_gpu=args.batch, accum_steps=args.accum,
                       num_samples=1, test_holdout=0, impl=args.impl, bucket_mb=args.bucket_mb,
-                      grad_codec=args.codec, log_dir=None)
+                      grad_codec=args.codec, log_dir=None, hip_graph=bool(args.hip_graph))
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     tr = Trainer(cfg, device=dev)
     world, rank = tr.world, tr.rank

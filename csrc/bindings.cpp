@@ -569,6 +569,20 @@ void adam_step(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, do
               (float)inv_sqrt_bc2, cur_stream());
 }
 
+// graph-capturable step: scal = device float[3] (t, step_size, inv_sqrt_bc2), advanced on
+// the device by this call
+void adam_step_dev(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, at::Tensor scal,
+                   double lr, double b1, double b2, double eps, double wd) {
+  CHECK_DEV(p); CHECK_F32(p); CHECK_F32(g); CHECK_F32(m); CHECK_F32(v); CHECK_F32(scal);
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "size");
+  TORCH_CHECK(scal.numel() >= 3 && scal.is_contiguous(), "scal must be float[3]");
+  c10::DeviceGuard guard(p.device());
+  adam_scalars_launch(scal.data_ptr<float>(), lr, b1, b2, cur_stream());
+  adam_launch(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+              p.numel(), (float)b1, (float)b2, (float)eps, (float)wd, 0.f, 1.f, cur_stream(),
+              scal.data_ptr<float>());
+}
+
 void weight_pack(const at::Tensor& entries, int64_t n, int64_t max_elems) {
   CHECK_DEV(entries);
   TORCH_CHECK(entries.scalar_type() == at::kLong && entries.numel() == n * 6,
@@ -683,6 +697,8 @@ TORCH_LIBRARY(ddlpc, m) {
   m.def("head_logits(Tensor a, Tensor Wh, Tensor bh) -> Tensor");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float eps, "
         "float wd, float step_size, float inv_sqrt_bc2) -> ()");
+  m.def("adam_step_dev(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!) scal, "
+        "float lr, float b1, float b2, float eps, float wd) -> ()");
   m.def("weight_pack(Tensor entries, int n, int max_elems) -> ()");
   m.def("codec_absmax(Tensor x, Tensor seg) -> Tensor");
   m.def("codec_encode(Tensor x, Tensor seg, Tensor scales, int codec) -> Tensor");
@@ -705,6 +721,7 @@ TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
   m.impl("head_ce_bwd", &ddlpc::head_ce_bwd);
   m.impl("head_logits", &ddlpc::head_logits);
   m.impl("adam_step", &ddlpc::adam_step);
+  m.impl("adam_step_dev", &ddlpc::adam_step_dev);
   m.impl("weight_pack", &ddlpc::weight_pack);
   m.impl("codec_absmax", &ddlpc::codec_absmax);
   m.impl("codec_encode", &ddlpc::codec_encode);

@@ -13,9 +13,13 @@ namespace ddlpc {
 
 namespace {
 
+// dscal (optional, hipGraph replays): device [t, step_size, inv_sqrt_bc2] written by
+// adam_scalars_kernel in the same graph, overriding the host-side scalars
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                             float* __restrict__ m, float* __restrict__ v, long long n, float b1,
-                            float b2, float eps, float wd, float step_size, float inv_sqrt_bc2) {
+                            float b2, float eps, float wd, float step_size, float inv_sqrt_bc2,
+                            const float* __restrict__ dscal) {
+  if (dscal != nullptr) { step_size = dscal[1]; inv_sqrt_bc2 = dscal[2]; }
   const long long n4 = n / 4;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
        i += (long long)gridDim.x * blockDim.x) {
@@ -272,10 +276,25 @@ __global__ void channel_sum_kernel(const bf16_t* __restrict__ x, long long P, in
 }  // namespace
 
 void adam_launch(float* p, const float* g, float* m, float* v, long long n, float b1, float b2,
-                 float eps, float wd, float step_size, float inv_sqrt_bc2, hipStream_t st) {
+                 float eps, float wd, float step_size, float inv_sqrt_bc2, hipStream_t st,
+                 const float* dscal) {
   const int grid = (int)std::min<long long>((n / 4 + 255) / 256 + 1, 2048);
   hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, st, p, g, m, v, n, b1, b2, eps, wd,
-                     step_size, inv_sqrt_bc2);
+                     step_size, inv_sqrt_bc2, dscal);
+}
+
+// one thread: t += 1, step_size = lr / (1 - b1^t), inv_sqrt_bc2 = 1 / sqrt(1 - b2^t) in
+// double (the host path's arithmetic), so a captured optimizer step stays correct on replay
+__global__ void adam_scalars_kernel(float* s, double lr, double b1, double b2) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const double t = (double)s[0] + 1.0;
+  s[0] = (float)t;
+  s[1] = (float)(lr / (1.0 - pow(b1, t)));
+  s[2] = (float)(1.0 / sqrt(1.0 - pow(b2, t)));
+}
+
+void adam_scalars_launch(float* s, double lr, double b1, double b2, hipStream_t st) {
+  hipLaunchKernelGGL(adam_scalars_kernel, dim3(1), dim3(64), 0, st, s, lr, b1, b2);
 }
 
 void weight_pack_launch(const PackEntry* entries_dev, int n_entries, long long max_elems,

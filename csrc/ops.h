@@ -124,7 +124,9 @@ void head_logits_launch(const bf16_t* a, const float* Wh, const float* bh, float
 
 // ---------------------------------------------------------------- optimizer / packing
 void adam_launch(float* p, const float* g, float* m, float* v, long long n, float b1, float b2,
-                 float eps, float wd, float step_size, float inv_sqrt_bc2, hipStream_t st);
+                 float eps, float wd, float step_size, float inv_sqrt_bc2, hipStream_t st,
+                 const float* dscal = nullptr);
+void adam_scalars_launch(float* s, double lr, double b1, double b2, hipStream_t st);
 struct PackEntry {                 // one conv weight to pack into bf16 kernel layouts
   const float* src;                // OIHW fp32  (or IOHW for transposed conv)
   bf16_t* fwd;                     // conv: [co][tap][CinW]; convT: [(sub, co)][Cin]

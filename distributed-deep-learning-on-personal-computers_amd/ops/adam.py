@@ -40,6 +40,7 @@ class FlatAdam(torch.optim.Optimizer):
         self.step_count = 0
         self._bind_state()
         self.weight_pack = None          # set by ops.fused_unet (bf16 conv-weight copies)
+        self._dev_scal = None            # device [t, step_size, inv_sqrt_bc2] (hipGraph mode)
         self._use_hip = (dev.type == "cuda") if use_hip is None else use_hip
         if self._use_hip:
             _ext.ops()                   # fail loudly if the kernel library is missing
@@ -52,6 +53,18 @@ class FlatAdam(torch.optim.Optimizer):
             st["exp_avg"] = self.flat._view(self.exp_avg, a, p)
             st["exp_avg_sq"] = self.flat._view(self.exp_avg_sq, a, p)
 
+    def enable_device_scalars(self):
+        """Bias corrections computed ON the device (adam_step_dev), so a captured step
+        replays correctly: no host scalar is baked into the graph."""
+        if not self._use_hip:
+            raise RuntimeError("device-side Adam scalars need the HIP kernel library")
+        self._dev_scal = torch.tensor([float(self.step_count), 0.0, 0.0],
+                                      dtype=torch.float32, device=self.flat.param_buf.device)
+
+    def note_replayed_step(self):
+        """Host mirror of a step executed by a graph replay."""
+        self.step_count += 1
+
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero_grad()
 
@@ -61,12 +74,18 @@ class FlatAdam(torch.optim.Optimizer):
         g = self.param_groups[0]
         lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
         self.step_count += 1
+        P, G = self.flat.param_buf, self.flat.grad_buf
+        if self._dev_scal is not None:
+            _ext.ops().adam_step_dev(P, G, self.exp_avg, self.exp_avg_sq, self._dev_scal,
+                                     float(lr), float(b1), float(b2), float(eps), float(wd))
+            if self.weight_pack is not None:
+                self.weight_pack()
+            return loss
         t = self.step_count
         bc1 = 1.0 - b1 ** t
         bc2 = 1.0 - b2 ** t
         step_size = lr / bc1
         inv_sqrt_bc2 = 1.0 / math.sqrt(bc2)
-        P, G = self.flat.param_buf, self.flat.grad_buf
         if self._use_hip:
             _ext.ops().adam_step(P, G, self.exp_avg, self.exp_avg_sq, float(b1), float(b2),
                                  float(eps), float(wd), float(step_size), float(inv_sqrt_bc2))
@@ -101,6 +120,8 @@ class FlatAdam(torch.optim.Optimizer):
                 if "step" in st:
                     steps.append(int(float(st["step"])))
         self.step_count = max(steps) if steps else 0
+        if self._dev_scal is not None:
+            self._dev_scal[0] = float(self.step_count)
         self._bind_state()
         if self.weight_pack is not None:
             self.weight_pack()

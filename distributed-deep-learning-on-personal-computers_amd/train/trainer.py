@@ -90,6 +90,9 @@ class Trainer:
         self.logger = RunLogger(cfg.log_dir, self.rank, cfg.grad_codec)
         self.step_count = 0
         self.micro_count = 0
+        self._graph = None               # hipGraph of the train step (cfg.hip_graph)
+        self._graph_warm = 0
+        self._static = None
         self.epoch = 0
         self.train_set, self.test_set = self._build_data()
         self.sampler = ShardedSampler(len(self.train_set), self.rank, self.world,
@@ -133,8 +136,57 @@ class Trainer:
         self.micro_count += 1
         return loss
 
+    # ------------------------------------------------------------------ hipGraph step
+    def _graph_ok(self, n_micro: int) -> bool:
+        return (self.cfg.hip_graph and self.impl == "hip" and self.device.type == "cuda"
+                and self.reducer is None and n_micro == 1 and not self.cfg.broadcast_buffers
+                and not self.cfg.check_consistency_every)
+
+    def _graph_body(self):
+        x, y = self._static
+        loss, correct = self.model.loss_and_correct(x, y)
+        loss.backward()
+        self.meter.add(loss, correct, y.numel())
+        self.optimizer.step()
+        self.optimizer.zero_grad()
+
+    def _graph_step(self, x: torch.Tensor, y: torch.Tensor):
+        """Single-GPU step as ONE hipGraph replay (~250 kernel launches -> 1): the batch
+        is copied into static buffers, the first ``GRAPH_WARMUP`` steps run eagerly on a
+        side stream (allocator + lazy state warm-up), then forward + backward + Adam (with
+        device-side bias corrections) + weight re-pack are captured once and replayed."""
+        self.model.train()
+        if self._static is None:
+            self._static = (torch.empty_like(x), torch.empty_like(y))
+            self.optimizer.enable_device_scalars()
+        self._static[0].copy_(x)
+        self._static[1].copy_(y)
+        if self._graph is None:
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):
+                self._graph_body()
+            torch.cuda.current_stream(self.device).wait_stream(side)
+            self._graph_warm += 1
+            if self._graph_warm >= self.GRAPH_WARMUP:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._graph_body()
+                self.optimizer.step_count -= 1       # capture ran step() once in Python
+                self._graph = g
+                # the capture itself executed nothing: the step above was the real one
+        else:
+            self._graph.replay()
+            self.optimizer.note_replayed_step()
+        self.micro_count += 1
+        self.step_count += 1
+
+    GRAPH_WARMUP = 3
+
     def train_step(self, micro_batches: List[Tuple[torch.Tensor, torch.Tensor]]):
         """One optimizer step over ``len(micro_batches)`` accumulated micro-batches."""
+        if self._graph_ok(len(micro_batches)):
+            return self._graph_step(*micro_batches[0])
         self.model.train()
         n = len(micro_batches)
         for i, (x, y) in enumerate(micro_batches):

@@ -30,9 +30,14 @@ class DeviceMeter:
         self.reset()
 
     def reset(self):
-        self.buf = torch.zeros(4, dtype=torch.float64, device=self.device)
-        self._inc_pixels = None
-        self._inc = None
+        # in place once allocated: a captured train step (hipGraph) keeps accumulating into
+        # the same buffer
+        if getattr(self, "buf", None) is None:
+            self.buf = torch.zeros(4, dtype=torch.float64, device=self.device)
+            self._inc_pixels = None
+            self._inc = None
+        else:
+            self.buf.zero_()
 
     def add(self, loss: torch.Tensor, correct: torch.Tensor, pixels: int):
         # [sum loss, sum correct, sum pixels, micro-batches]; no host->device copies per step

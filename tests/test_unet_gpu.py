@@ -73,3 +73,33 @@ def test_trainer_hip_step_decreases_loss():
         tr.meter.reset()
     assert losses[-1] < losses[0]
     tr.close()
+
+
+def test_trainer_hip_graph_matches_eager():
+    """cfg.hip_graph: the captured/replayed step reproduces the eager step (same kernels,
+    device-side Adam bias corrections) — parameters, optimizer state and metrics."""
+    from ddlpc.config import ModelConfig, TrainConfig
+    from ddlpc.data import device_random_batch
+    from ddlpc.train.trainer import Trainer
+    batches = None
+    out = []
+    for graph in (False, True):
+        cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=4,
+                          num_samples=1, test_holdout=0, impl="hip", hip_graph=graph)
+        tr = Trainer(cfg, device="cuda")
+        if batches is None:
+            batches = [device_random_batch(4, 64, 6, tr.device, seed=s) for s in range(3)]
+        losses = []
+        for i in range(7):                       # 3 eager warm-up + capture, then replays
+            tr.train_step([batches[i % 3]])
+            losses.append(tr.meter.reduce()["loss"])
+            tr.meter.reset()
+        if graph:
+            assert tr._graph is not None, "step was not captured"
+        assert tr.optimizer.step_count == 7 and tr.step_count == 7
+        out.append((tr.flat.param_buf.clone(), tr.optimizer.exp_avg_sq.clone(), losses))
+        tr.close()
+    (p0, v0, l0), (p1, v1, l1) = out
+    assert torch.allclose(p0, p1, rtol=0, atol=1e-6), float((p0 - p1).abs().max())
+    assert torch.allclose(v0, v1, rtol=1e-6, atol=0)
+    assert max(abs(a - b) for a, b in zip(l0, l1)) < 1e-5
