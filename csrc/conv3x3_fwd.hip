@@ -335,14 +335,12 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
   if (S > 0) epilogue(my_items - 1);
 
   // ---- one BN-statistics partial row per workgroup: shuffle over the 16 pixel lanes,
-  // LDS float atomics over the wave rows, one coalesced row write
+  // per-wave-row LDS slots summed in a fixed order (bit-reproducible), one row write
   if (p.stats != nullptr && KS == 1) {
     dma_wait<0>();
     lds_sync();
     float* red = reinterpret_cast<float*>(base);          // halo buffers are free now
     const int co0 = my_items > 0 ? item_of(0).co0 : 0;
-    for (int c = tid; c < 2 * BN; c += 256) red[c] = 0.f;
-    lds_sync();
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -352,16 +350,19 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
         for (int o = 1; o < 16; o <<= 1) { a1 += __shfl_xor(a1, o, 64); a2 += __shfl_xor(a2, o, 64); }
         if ((lane & 15) == 0) {
           const int col = wn * (NT * 16) + nt * 16 + 4 * (lane >> 4) + i;
-          atomicAdd(red + col, a1);
-          atomicAdd(red + BN + col, a2);
+          red[(2 * wm) * BN + col] = a1;           // one writer per (wave row, column)
+          red[(2 * wm + 1) * BN + col] = a2;
         }
       }
     lds_sync();
     float* row = p.stats + (long long)blockIdx.x * 2 * p.Cout;
     for (int c = tid; c < p.Cout; c += 256) {      // full row: zeros outside this n tile
       const bool mine = c >= co0 && c < co0 + BN;
-      row[c] = mine ? red[c - co0] : 0.f;
-      row[p.Cout + c] = mine ? red[BN + c - co0] : 0.f;
+      float t1 = 0.f, t2 = 0.f;                    // fixed-order sum over wave rows
+      if (mine)
+        for (int r = 0; r < WM; ++r) { t1 += red[(2 * r) * BN + c - co0]; t2 += red[(2 * r + 1) * BN + c - co0]; }
+      row[c] = t1;
+      row[p.Cout + c] = t2;
     }
   }
 }

@@ -329,8 +329,6 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     dma_wait<0>();
     lds_sync();
     float* red = reinterpret_cast<float*>(sA0);
-    for (int i = tid; i < 2 * BN; i += C::NTH) red[i] = 0.f;
-    lds_sync();
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -340,16 +338,19 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
         for (int o = 1; o < 16; o <<= 1) { a1 += __shfl_xor(a1, o, 64); a2 += __shfl_xor(a2, o, 64); }
         if ((lane & 15) == 0) {
           const int col = wn * (NT * 16) + nt * 16 + 4 * g + i;
-          atomicAdd(red + col, a1);
-          atomicAdd(red + BN + col, a2);
+          red[(2 * wm) * BN + col] = a1;           // one writer per (wave row, column)
+          red[(2 * wm + 1) * BN + col] = a2;
         }
       }
     lds_sync();
     float* row = p.stats + (long long)blockIdx.x * 2 * p.Cout;
     for (int i = tid; i < p.Cout; i += C::NTH) {
       const bool mine = i >= co0 && i < co0 + BN;
-      row[i] = mine ? red[i - co0] : 0.f;
-      row[p.Cout + i] = mine ? red[BN + i - co0] : 0.f;
+      float t1 = 0.f, t2 = 0.f;                    // fixed-order sum over wave rows
+      if (mine)
+        for (int r = 0; r < WM; ++r) { t1 += red[(2 * r) * BN + i - co0]; t2 += red[(2 * r + 1) * BN + i - co0]; }
+      row[i] = t1;
+      row[p.Cout + i] = t2;
     }
   }
 }

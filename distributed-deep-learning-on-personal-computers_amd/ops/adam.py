@@ -44,6 +44,9 @@ class FlatAdam(torch.optim.Optimizer):
         self._use_hip = (dev.type == "cuda") if use_hip is None else use_hip
         if self._use_hip:
             _ext.ops()                   # fail loudly if the kernel library is missing
+            # bias corrections on the device: identical arithmetic for eager and hipGraph
+            # steps, and nothing step-dependent is baked into a captured graph
+            self.enable_device_scalars()
 
     def _bind_state(self):
         for p in self.flat.params:

@@ -158,7 +158,6 @@ class Trainer:
         self.model.train()
         if self._static is None:
             self._static = (torch.empty_like(x), torch.empty_like(y))
-            self.optimizer.enable_device_scalars()
         self._static[0].copy_(x)
         self._static[1].copy_(y)
         if self._graph is None:

@@ -285,6 +285,24 @@ def test_adam_matches_torch(ops):
     assert torch.allclose(p, pr.detach(), atol=1e-6, rtol=1e-5)
 
 
+def test_adam_device_scalars_match_torch(ops):
+    """adam_step_dev: bias corrections advanced on the device (graph-capturable)."""
+    torch.manual_seed(7)
+    n = 10_007
+    p = torch.randn(n, device=DEV)
+    pr = p.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pr], lr=1e-3, weight_decay=0.01)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    scal = torch.zeros(3, device=DEV)
+    for t in range(1, 6):
+        g = torch.randn(n, device=DEV)
+        pr.grad = g.clone()
+        opt.step()
+        ops.adam_step_dev(p, g, m, v, scal, 1e-3, 0.9, 0.999, 1e-8, 0.01)
+    assert float(scal[0]) == 5.0
+    assert torch.allclose(p, pr.detach(), atol=1e-6, rtol=1e-5)
+
+
 @pytest.mark.parametrize("codec", ["fp16_absmax", "int8_absmax"])
 def test_codec_matches_oracle(codec):
     from ddlpc.ops import codec_ops

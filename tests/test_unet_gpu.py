@@ -100,6 +100,7 @@ def test_trainer_hip_graph_matches_eager():
         out.append((tr.flat.param_buf.clone(), tr.optimizer.exp_avg_sq.clone(), losses))
         tr.close()
     (p0, v0, l0), (p1, v1, l1) = out
-    assert torch.allclose(p0, p1, rtol=0, atol=1e-6), float((p0 - p1).abs().max())
-    assert torch.allclose(v0, v1, rtol=1e-6, atol=0)
-    assert max(abs(a - b) for a, b in zip(l0, l1)) < 1e-5
+    # every kernel is deterministic (no float atomics on this path), so replay == eager
+    assert torch.equal(p0, p1), float((p0 - p1).abs().max())
+    assert torch.equal(v0, v1)
+    assert l0 == l1
