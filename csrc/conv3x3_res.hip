@@ -251,10 +251,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * g;
-        const f32x2_t v01 = f32x2_t{acc[mt][nt][0], acc[mt][nt][1]} + f32x2_t{bias_r[nt][0], bias_r[nt][1]};
-        const f32x2_t v23 = f32x2_t{acc[mt][nt][2], acc[mt][nt][3]} + f32x2_t{bias_r[nt][2], bias_r[nt][3]};
-        const uint2 pk = make_uint2(__builtin_bit_cast(uint32_t, __builtin_convertvector(v01, bf16x2_t)),
-                                    __builtin_bit_cast(uint32_t, __builtin_convertvector(v23, bf16x2_t)));
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bias_r[nt][i];
+        const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         if (valid && co < p.Cout) {
           if (!split) {
             store_bf16x4(row1 + co, pk.x, pk.y);
@@ -263,14 +263,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
             store_bf16x4(dst, pk.x, pk.y);
           }
           // statistics of the stored (bf16-rounded) values
-          const f32x2_t r01 = {lo_bf(pk.x), hi_bf(pk.x)}, r23 = {lo_bf(pk.y), hi_bf(pk.y)};
-          f32x2_t a01 = {s1[nt][0], s1[nt][1]}, a23 = {s1[nt][2], s1[nt][3]};
-          f32x2_t q01 = {s2[nt][0], s2[nt][1]}, q23 = {s2[nt][2], s2[nt][3]};
-          a01 += r01; a23 += r23;
-          q01 = __builtin_elementwise_fma(r01, r01, q01);
-          q23 = __builtin_elementwise_fma(r23, r23, q23);
-          s1[nt][0] = a01.x; s1[nt][1] = a01.y; s1[nt][2] = a23.x; s1[nt][3] = a23.y;
-          s2[nt][0] = q01.x; s2[nt][1] = q01.y; s2[nt][2] = q23.x; s2[nt][3] = q23.y;
+          const float r0 = lo_bf(pk.x), r1 = hi_bf(pk.x), r2 = lo_bf(pk.y), r3 = hi_bf(pk.y);
+          s1[nt][0] += r0; s2[nt][0] += r0 * r0;
+          s1[nt][1] += r1; s2[nt][1] += r1 * r1;
+          s1[nt][2] += r2; s2[nt][2] += r2 * r2;
+          s1[nt][3] += r3; s2[nt][3] += r3 * r3;
         }
         acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       }
