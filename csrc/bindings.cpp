@@ -168,6 +168,11 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
     a.nTilesN = (a.Cout + conv3_fwd_cfg_bn(c) - 1) / conv3_fwd_cfg_bn(c);
   };
   plan(cfg);
+  if (cfg == 2 && g.dims == 2) {                // 256-pixel tiles on 8 waves if they fill the chip
+    plan(4);
+    if (a.nTilesM * a.nTilesN >= num_cus()) cfg = 4;
+    else plan(cfg);
+  }
   if (cfg == 2 && a.nTilesM * a.nTilesN < 2 * num_cus()) { cfg = 3; plan(cfg); }
   TORCH_CHECK((g.dims == 3 ? a.TD + 2 : 1) * (a.TH + 2) * (a.TW + 2) <= conv3_fwd_cfg_halo(g.dims, cfg),
               "halo exceeds LDS capacity");
@@ -175,7 +180,7 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   at::Tensor y2;
   if (a.Co1 < a.Cout) y2 = at::empty(shape_with_c(g, a.Cout - a.Co1), opts);
   at::Tensor stats;
-  a.persist_blocks = 2 * num_cus();
+  a.persist_blocks = (cfg == 4 ? 1 : 2) * num_cus();   // cfg 4: one 8-wave workgroup per CU
   {
     static const int pb = [] { const char* e = getenv("DDLPC_CONV_PERSIST"); return e ? atoi(e) : -1; }();
     static const int ksx = [] { const char* e = getenv("DDLPC_CONV_KSPLIT"); return e ? atoi(e) : -1; }();

@@ -4,7 +4,7 @@
 //
 // GEMM view:  M = output pixels, N = output channels, K = taps x input channels.
 //
-// Tiling (one 256-thread workgroup = 4 waves as WM x WN):
+// Tiling (one workgroup = 4 or 8 waves as WM x WN):
 //   * output tile BM pixels (a TD x TH x TW box) x BN channels; each wave owns
 //     (16*MT) px x (16*NT) ch = MT x NT tiles of v_mfma_f32_16x16x32_bf16;
 //   * K runs over 32-channel chunks; per chunk the (TD+2)(TH+2)(TW+2) input HALO is staged
@@ -44,12 +44,14 @@ using namespace convlds;
 
 template <int DIMS, int WM, int WN, int MT, int NT, int HALO>
 struct Cfg {
+  static constexpr int NW = WM * WN;                            // waves per workgroup (4 or 8)
+  static constexpr int NTH = NW * 64;
   static constexpr int BM = WM * MT * 16;
   static constexpr int BN = WN * NT * 16;
-  static constexpr int A_ITERS = (HALO + 63) / 64;              // DMA instrs / wave / chunk
-  static constexpr int A_BYTES = A_ITERS * 4 * 1024;            // one halo buffer
-  static constexpr int B_ITERS = (3 * BN * 4 + 255) / 256;      // DMA instrs / wave / stage
-  static constexpr int B_BYTES = B_ITERS * 4 * 1024;            // one weight buffer
+  static constexpr int A_ITERS = (HALO / 16 + NW - 1) / NW;     // DMA instrs / wave / chunk
+  static constexpr int A_BYTES = A_ITERS * NW * 1024;           // one halo buffer
+  static constexpr int B_ITERS = (3 * BN * 4 / 64 + NW - 1) / NW;  // DMA instrs / wave / stage
+  static constexpr int B_BYTES = B_ITERS * NW * 1024;           // one weight buffer
   static constexpr int SS_BYTES = 2 * 512 * 4;                  // prologue scale/shift
   static constexpr int SMEM = SS_BYTES + 2 * A_BYTES + 2 * B_BYTES;
 };
@@ -64,7 +66,7 @@ struct Cfg {
 // pixel -> 8-byte bf16x4 stores; BN statistics are reduced with 4 lane shuffles and
 // written as one partial row per (m tile, wave row).
 template <int DIMS, int WM, int WN, int MT, int NT, int HALO>
-__global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
+__global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_kernel(ConvFwdArgs p) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO>;
   constexpr int BM = C::BM, BN = C::BN;
   constexpr int NG = DIMS == 2 ? 3 : 9;           // (kd, r) kernel rows per chunk
@@ -93,7 +95,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
 
   const bool has_pro = p.pscale != nullptr;
   if (has_pro)
-    for (int c = tid; c < p.C1; c += 256) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
+    for (int c = tid; c < p.C1; c += C::NTH) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
 
   const auto rW = make_rsrc(p.Wt, (unsigned)((long long)p.Cout * p.taps * p.CinW * 2));
 
@@ -121,7 +123,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
   int a_pix[C::A_ITERS];       // in-image pixel of the item last issued, -1 = zero padding
 #pragma unroll
   for (int i = 0; i < C::A_ITERS; ++i) {
-    const int e = (i * 4 + wave) * 64 + lane;
+    const int e = (i * C::NW + wave) * 64 + lane;
     const int px = e >> 2;
     a_sub8[i] = ((e & 3) ^ swz(px)) << 3;
     const int hw = px % HW2, hh = (px / HW2) % HH2;
@@ -137,7 +139,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
   int b_off[C::B_ITERS], b_sub8[C::B_ITERS];
 #pragma unroll
   for (int i = 0; i < C::B_ITERS; ++i) {
-    const int e = (i * 4 + wave) * 64 + lane;
+    const int e = (i * C::NW + wave) * 64 + lane;
     const int row = e >> 2;
     const int sub = (e & 3) ^ swz(row);
     const int tl = row / BN, col = row % BN;
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
     for (int i = 0; i < C::A_ITERS; ++i) {
       const int c8 = c0 + a_sub8[i];
       unsigned off = (a_pix[i] >= 0 && c8 < Cs) ? (unsigned)(a_pix[i] * Cs + c8) * 2u : kOOB;
-      dma16(r, sA(buf) + (i * 4 + wave) * 1024, off);
+      dma16(r, sA(buf) + (i * C::NW + wave) * 1024, off);
     }
   };
   auto issue_B = [&](int k, int chunk_local, int grp, int buf) {
@@ -180,7 +182,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
 #pragma unroll
     for (int i = 0; i < C::B_ITERS; ++i) {
       const bool ok = b_off[i] >= 0 && chunk * BK + b_sub8[i] < p.CinW;
-      dma16(rW, sB(buf) + (i * 4 + wave) * 1024, ok ? (unsigned)(b_off[i] + soff) : kOOB);
+      dma16(rW, sB(buf) + (i * C::NW + wave) * 1024, ok ? (unsigned)(b_off[i] + soff) : kOOB);
     }
   };
   // prologue BN+ReLU applied in LDS on the landed halo (padding stays zero); a_pix holds
@@ -190,7 +192,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
     if (cbase >= p.C1) return;                      // X2 channels: no prologue
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
-      const int e = (i * 4 + wave) * 64 + lane;    // same element this lane DMA'd
+      const int e = (i * C::NW + wave) * 64 + lane;    // same element this lane DMA'd
       const int c8 = cbase + a_sub8[i];
       if (c8 < p.C1 && a_pix[i] >= 0) {
         uint4* q = reinterpret_cast<uint4*>(sA(buf) + e * 16);
@@ -356,7 +358,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(ConvFwdArgs p) {
       }
     lds_sync();
     float* row = p.stats + (long long)blockIdx.x * 2 * p.Cout;
-    for (int c = tid; c < p.Cout; c += 256) {      // full row: zeros outside this n tile
+    for (int c = tid; c < p.Cout; c += C::NTH) {   // full row: zeros outside this n tile
       const bool mine = c >= co0 && c < co0 + BN;
       float t1 = 0.f, t2 = 0.f;                    // fixed-order sum over wave rows
       if (mine)
@@ -429,11 +431,11 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
     grid = a.persist_blocks / q * q;
   }
   a.stat_rows = grid;
-  hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO>), dim3(grid), dim3(256),
+  hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO>), dim3(grid), dim3(C::NTH),
                      C::SMEM, st, a);
 }
 
-int cfg_wm(int cfg) { return cfg <= 1 ? 4 : cfg == 2 ? 2 : 1; }
+int cfg_wm(int cfg) { return cfg <= 1 || cfg == 4 ? 4 : cfg == 2 ? 2 : 1; }
 
 }  // namespace
 
@@ -442,12 +444,14 @@ int cfg_wm(int cfg) { return cfg <= 1 ? 4 : cfg == 2 ? 2 : 1; }
 //   1: BN 64,  BM 256 (4x1 waves, 4x4 tiles)     2-D 16x16 / 32x8   3-D 4x4x16 / 8x4x8
 //   2: BN 128, BM 128 (2x2 waves, 4x4 tiles)     2-D 8x16 / 16x8    3-D 2x4x16 / 4x4x8
 //   3: BN 128, BM 64  (1x4 waves, 4x2 tiles)     2-D 4x16 / 8x8     3-D 1x4x16 / 2x4x8
+//   4: BN 128, BM 256 (4x2 waves = 512 threads, 4x4 tiles; 2-D only) 16x16 / 32x8: half the
+//      weight-stream traffic per MFMA of cfg 2 (one workgroup per CU)
 // (halo capacity = DMA instructions per wave x 64 pixels)
 int conv3_fwd_cfg_wm(int cfg) { return cfg_wm(cfg); }
 int conv3_fwd_cfg_bn(int cfg) { return cfg == 0 ? 32 : cfg == 1 ? 64 : 128; }
-int conv3_fwd_cfg_bm(int cfg) { return cfg <= 1 ? 256 : cfg == 2 ? 128 : 64; }
+int conv3_fwd_cfg_bm(int cfg) { return cfg <= 1 || cfg == 4 ? 256 : cfg == 2 ? 128 : 64; }
 int conv3_fwd_cfg_halo(int dims, int cfg) {
-  if (dims == 2) return cfg <= 1 ? 384 : cfg == 2 ? 192 : 128;
+  if (dims == 2) return cfg <= 1 || cfg == 4 ? 384 : cfg == 2 ? 192 : 128;
   return cfg <= 1 ? 704 : cfg == 2 ? 448 : 384;
 }
 
@@ -462,6 +466,7 @@ void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st) {
       case 0: launch_cfg<2, 4, 1, 4, 2, 384>(a, st); break;
       case 1: launch_cfg<2, 4, 1, 4, 4, 384>(a, st); break;
       case 2: launch_cfg<2, 2, 2, 4, 4, 192>(a, st); break;
+      case 4: launch_cfg<2, 4, 2, 4, 4, 384>(a, st); break;
       default: launch_cfg<2, 1, 4, 4, 2, 128>(a, st); break;
     }
   } else {

@@ -89,7 +89,9 @@ def test_conv3_fwd_prologue(ops):
     (2, 256, 256, 32, 0, 32, True), (2, 256, 256, 3, 0, 32, False),
     (2, 256, 256, 64, 32, 32, True), (2, 256, 256, 32, 0, 64, False),
     (2, 256, 256, 64, 0, 64, True), (3, 200, 232, 32, 0, 32, True),
-    (2, 128, 128, 64, 0, 96, False)])
+    (2, 128, 128, 64, 0, 96, False),
+    # streaming kernel, 8-wave 256x128 tiles (cfg 4)
+    (16, 64, 64, 128, 0, 128, True), (8, 64, 64, 128, 64, 256, False)])
 def test_conv3_fwd_resident(ops, N, H, W, C1, C2, Cout, pro):
     torch.manual_seed(4)
     x1 = torch.randn(N, C1, H, W, device=DEV).bfloat16()
@@ -114,7 +116,7 @@ def test_conv3_fwd_resident(ops, N, H, W, C1, C2, Cout, pro):
     assert torch.allclose(s[1], (yf * yf).sum((0, 2, 3)), rtol=1e-3, atol=1.0)
 
 
-@pytest.mark.parametrize("C1,C2,Cout", [(64, 32, 32), (32, 0, 32), (64, 128, 64)])
+@pytest.mark.parametrize("C1,C2,Cout", [(64, 32, 32), (32, 0, 32), (64, 128, 64), (128, 0, 128)])
 def test_conv3_dgrad_resident(ops, C1, C2, Cout):
     torch.manual_seed(5)
     N, H, W = 2, 256, 256
