@@ -31,7 +31,7 @@ namespace {
 
 using namespace convlds;
 
-template <int WM, int WN, int MT, int NT, int HALO, bool TAP8>
+template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF>
 struct RCfg {
   static constexpr int NW = WM * WN;
   static constexpr int NTH = NW * 64;
@@ -39,18 +39,24 @@ struct RCfg {
   static constexpr int BN = WN * NT * 16;
   static constexpr int PIECES = TAP8 ? HALO : HALO * 4;   // 16-B pieces per halo buffer
   static constexpr int INSTR = (PIECES + 63) / 64;         // DMA wave-instructions per halo
-  static constexpr int A_ITERS = (INSTR + NW - 1) / NW;    // ... per wave
-  static constexpr int A_BYTES = INSTR * 1024;
+  // EVERY wave issues exactly A_ITERS DMA instructions per stage (surplus ones land
+  // zeros past the halo), so the counted vmcnt waits below are exact
+  static constexpr int A_ITERS = (INSTR + NW - 1) / NW;
+  static constexpr int A_BYTES = A_ITERS * NW * 1024;
 };
+
+template <int N>
+DDLPC_DEVICE void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
 DDLPC_HOST_DEVICE int res_ss_bytes(int C1, bool pro) { return pro ? ((8 * C1 + 15) / 16) * 16 : 0; }
 DDLPC_HOST_DEVICE int res_w_bytes(int Cin, int BN, bool tap8) {
   return tap8 ? 3 * BN * ROWB : ((Cin + BK - 1) / BK) * 9 * BN * ROWB;
 }
 
-template <int WM, int WN, int MT, int NT, int HALO, bool TAP8>
+template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF, bool SPLIT>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_kernel(ConvFwdArgs p) {
-  using C = RCfg<WM, WN, MT, NT, HALO, TAP8>;
+  using C = RCfg<WM, WN, MT, NT, HALO, TAP8, NBUF>;
+  static_assert(NBUF == 2 || NBUF == 3, "halo ring depth");
   constexpr int NW = C::NW, BN = C::BN;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bool has_pro = p.pscale != nullptr;
@@ -79,6 +85,20 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   if (has_pro)
     for (int c = tid; c < p.C1; c += C::NTH) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
 
+  // bias of this block's channel tile, loaded once (a global load inside the epilogue would
+  // make the compiler wait vmcnt(0) — on this tile's stores — before every use); loaded
+  // BEFORE any DMA is issued, so no later wait of ours is affected by it
+  float bias_r[NT][4];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * (lane >> 4) + i;
+      bias_r[nt][i] = (p.bias != nullptr && co < p.Cout) ? p.bias[co] : 0.0f;
+    }
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)                     // consume now: the compiler's wait
+    asm volatile("" ::"v"(bias_r[nt][0]), "v"(bias_r[nt][1]), "v"(bias_r[nt][2]), "v"(bias_r[nt][3]));
   // ---- resident weights: rows (chunk, tap, col) [TAP8: (k-step, col)], 64 B each
   {
     const auto rW = make_rsrc(p.Wt, (unsigned)((long long)p.Cout * 9 * p.CinW * 2));
@@ -126,7 +146,15 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     a_rel[i] = a_dh[i] * p.W + a_dw[i];
     if (px < halo && e < C::PIECES) a_inhalo |= 1u << i;
   }
-  uint32_t a_valid = 0;            // pieces of the current item inside the image
+  uint32_t a_valid = 0;            // pieces of the item last issued that are inside the image
+  // a_valid of the stage held by each ring slot, 8 bits per slot in one register (a
+  // runtime-indexed array would live in scratch: vm ops that break the counted waits)
+  static_assert(C::A_ITERS <= 8, "valid mask packing");
+  uint32_t vmasks = 0;
+  auto set_vmask = [&](int buf, uint32_t m) {
+    vmasks = (vmasks & ~(0xffu << (8 * buf))) | (m << (8 * buf));
+  };
+  auto get_vmask = [&](int buf) { return (vmasks >> (8 * buf)) & 0xffu; };
   int a_item = -1, a_nimg = 0, a_base = 0;
   auto issue_A = [&](int k, int chunk, int buf) {
     if (k != a_item) {
@@ -153,11 +181,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     const int c0 = second ? cbase - p.C1 : cbase;
     const bool full = c0 + BK <= Cs;                   // wave-uniform: no channel check
     const bf16_t* src = second ? p.X2 : p.X1;
+    set_vmask(buf, a_valid);
     const auto r = make_rsrc(src + a_nimg * img_px * Cs, (unsigned)(img_px * Cs * 2));
     const int s0 = a_base * Cs + c0;                   // scalar part of the element offset
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
-      if ((i * NW + wave) * 64 >= C::PIECES) break;    // wave-uniform
       const bool ok = ((a_valid >> i) & 1u) && (full || c0 + a_sub8[i] < Cs);
       const unsigned off = ok ? (unsigned)(a_rel[i] * Cs + a_sub8[i] + s0) * 2u : kOOB;
       dma16(r, sA(buf) + (i * NW + wave) * 1024, off);
@@ -165,18 +193,17 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   };
   // prologue on the pieces THIS lane DMA'd (a_valid still describes the chunk's item):
   // packed fp32 FMA, bf16 rounding, ReLU as a packed signed-16-bit max on the bf16 bits
-  auto transform_A = [&](int chunk, int buf) {
-    const int cbase = chunk * BK;
-    if (cbase >= p.C1) return;
+  auto transform_body = [&](char* __restrict__ Ab, const float* __restrict__ scl,
+                            const float* __restrict__ shf_, int cbase, uint32_t vm) {
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
       const int e = (i * NW + wave) * 64 + lane;
       const int c8 = cbase + a_sub8[i];
-      if (((a_valid >> i) & 1u) && c8 < p.C1) {
-        uint4* q = reinterpret_cast<uint4*>(sA(buf) + e * 16);
+      if (((vm >> i) & 1u) && c8 < p.C1) {
+        uint4* q = reinterpret_cast<uint4*>(Ab + e * 16);
         const uint4 v = *q;
-        const float4* scp = reinterpret_cast<const float4*>(s_scale + c8);
-        const float4* shp = reinterpret_cast<const float4*>(s_shift + c8);
+        const float4* scp = reinterpret_cast<const float4*>(scl + c8);
+        const float4* shp = reinterpret_cast<const float4*>(shf_ + c8);
         const float4 sa = scp[0], sb = scp[1], ha = shp[0], hb = shp[1];
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
         const float scf[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
@@ -195,6 +222,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
         *q = make_uint4(o[0], o[1], o[2], o[3]);
       }
     }
+  };
+  // (restrict-qualified LDS pointers: alias scopes keep the compiler from waiting on the
+  // in-flight halo DMAs of later ring slots before these reads)
+  auto transform_A = [&](int chunk, int buf) {
+    const int cbase = chunk * BK;
+    if (cbase >= p.C1) return;
+    transform_body(sA(buf), s_scale, s_shift, cbase, get_vmask(buf));
   };
 
   // ---- per-lane fragment geometry
@@ -224,30 +258,23 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
 #pragma unroll
     for (int i = 0; i < 4; ++i) { s1[nt][i] = 0.f; s2[nt][i] = 0.f; }
 
-  // bias of this block's channel tile, loaded once (a global load inside the epilogue would
-  // make the compiler wait vmcnt(0) — on this tile's stores — before every use)
-  float bias_r[NT][4];
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * g + i;
-      bias_r[nt][i] = (p.bias != nullptr && co < p.Cout) ? p.bias[co] : 0.0f;
-    }
   // epilogue of item k straight from the accumulators: lane holds channels co..co+3 of
   // tile pixel (wm*MT*16 + mt*16 + (lane&15))
+  // Stores are buffer stores with an out-of-range offset for masked lanes: every wave
+  // issues exactly EPI_STORES of them per epilogue (no exec branches), which keeps the
+  // counted vmcnt waits exact.
+  constexpr int EPI_STORES = MT * NT * (SPLIT ? 2 : 1);
   auto epilogue = [&](int k) {
     const Item it = item_of(k);
-    const bool split = p.Co1 < p.Cout;                 // dgrad of a concat conv (rare)
-    bf16_t* y1img = p.Y1 + (long long)it.n_img * img_px * p.Co1;
-    bf16_t* y2img = split ? p.Y2 + (long long)it.n_img * img_px * (p.Cout - p.Co1) : nullptr;
+    const int Co2 = p.Cout - p.Co1;
+    const auto r1 = make_rsrc(p.Y1 + (long long)it.n_img * img_px * p.Co1, (unsigned)(img_px * p.Co1 * 2));
+    const auto r2 = SPLIT ? make_rsrc(p.Y2 + (long long)it.n_img * img_px * Co2, (unsigned)(img_px * Co2 * 2)) : r1;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
       const int gw = it.w0 + pix % p.TW, gh = it.h0 + pix / p.TW;
       const bool valid = gw < p.W && gh < p.H;
       const int lp = gh * p.W + gw;                     // pixel within the image (32-bit)
-      bf16_t* row1 = y1img + lp * p.Co1;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * g;
@@ -255,35 +282,78 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bias_r[nt][i];
         const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        if (valid && co < p.Cout) {
-          if (!split) {
-            store_bf16x4(row1 + co, pk.x, pk.y);
-          } else {                                     // wave-uniform branch
-            bf16_t* dst = co < p.Co1 ? row1 + co : y2img + lp * (p.Cout - p.Co1) + (co - p.Co1);
-            store_bf16x4(dst, pk.x, pk.y);
-          }
-          // statistics of the stored (bf16-rounded) values
-          const float r0 = lo_bf(pk.x), r1 = hi_bf(pk.x), r2 = lo_bf(pk.y), r3 = hi_bf(pk.y);
-          s1[nt][0] += r0; s2[nt][0] += r0 * r0;
-          s1[nt][1] += r1; s2[nt][1] += r1 * r1;
-          s1[nt][2] += r2; s2[nt][2] += r2 * r2;
-          s1[nt][3] += r3; s2[nt][3] += r3 * r3;
+        const bool ok = valid && co < p.Cout;
+        const u32x2_t d = u32x2_t{pk.x, pk.y};
+        // the offsets go through an opaque asm so the compiler cannot turn the masked
+        // store into a branch around it (the store COUNT must not depend on the data)
+        if (!SPLIT) {
+          unsigned o1 = ok ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
+          asm volatile("" : "+v"(o1));
+          __builtin_amdgcn_raw_buffer_store_b64(d, r1, o1, 0, 0);
+        } else {
+          const bool in1 = co < p.Co1;
+          unsigned o1 = (ok && in1) ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
+          unsigned o2 = (ok && !in1) ? (unsigned)(lp * Co2 + co - p.Co1) * 2u : kOOB;
+          asm volatile("" : "+v"(o1), "+v"(o2));
+          __builtin_amdgcn_raw_buffer_store_b64(d, r1, o1, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(d, r2, o2, 0, 0);
         }
+        // statistics of the stored (bf16-rounded) values; masked lanes add zeros
+        const float r0 = ok ? lo_bf(pk.x) : 0.f, q1 = ok ? hi_bf(pk.x) : 0.f;
+        const float q2 = ok ? lo_bf(pk.y) : 0.f, q3 = ok ? hi_bf(pk.y) : 0.f;
+        s1[nt][0] += r0; s2[nt][0] += r0 * r0;
+        s1[nt][1] += q1; s2[nt][1] += q1 * q1;
+        s1[nt][2] += q2; s2[nt][2] += q2 * q2;
+        s1[nt][3] += q3; s2[nt][3] += q3 * q3;
         acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       }
     }
   };
 
-  if (S > 0) issue_A(0, 0, 0);
+  // ---- pipeline: the halo of stage s+NBUF-1 is issued at stage s (ring of NBUF buffers).
+  // Per stage a wave issues: [epilogue stores of the previous item] then [A_ITERS DMAs],
+  // so at stage s the ops younger than DMA(s) are exactly those of stage s-1 (NBUF = 3)
+  // or none (NBUF = 2) plus the prologue's extra DMA at s = 0.
+  auto next_of = [&](int k0, int c0, int& k1, int& c1) {
+    k1 = k0; c1 = c0 + 1;
+    if (c1 == nch) { c1 = 0; ++k1; }
+  };
+  int kp = 0, cp = 0;                                 // stage whose halo is issued next
+  for (int j = 0; j < NBUF - 1 && j < S; ++j) {
+    issue_A(kp, cp, j % NBUF);
+    int k1, c1;
+    next_of(kp, cp, k1, c1);
+    kp = k1; cp = c1;
+  }
   int k = 0, c = 0;
+  bool epi_prev = false;                              // stage s-1 ran an epilogue
   for (int s = 0; s < S; ++s) {
-    dma_wait<0>();                                    // this stage's halo (+ weights at s=0)
-    if (!TAP8 && has_pro) transform_A(c, s & 1);
+    if (NBUF == 2) {
+      vm_wait<0>();                                   // DMA(s) is the youngest op
+    } else {
+      // younger than DMA(s): s == 0 -> DMA(1); s >= 1 -> [stores(s-1)] + [DMA(s+1)]
+      const bool dma_next = s + 1 < S;
+      if (s == 0) {
+        if (dma_next) vm_wait<C::A_ITERS>(); else vm_wait<0>();
+      } else if (epi_prev) {
+        if (dma_next) vm_wait<C::A_ITERS + EPI_STORES>(); else vm_wait<EPI_STORES>();
+      } else {
+        if (dma_next) vm_wait<C::A_ITERS>(); else vm_wait<0>();
+      }
+    }
+    const int buf = s % NBUF;
+    if (!TAP8 && has_pro) transform_A(c, buf);
     lds_sync();
-    if (c == 0 && s > 0) epilogue(k - 1);
+    epi_prev = (c == 0 && s > 0);
+    if (epi_prev) epilogue(k - 1);
+    if (s + NBUF - 1 < S) {
+      issue_A(kp, cp, (s + NBUF - 1) % NBUF);
+      int k1, c1;
+      next_of(kp, cp, k1, c1);
+      kp = k1; cp = c1;
+    }
     int k1 = k, c1 = c + 1;
     if (c1 == nch) { c1 = 0; ++k1; }
-    if (s + 1 < S) issue_A(k1, c1, (s + 1) & 1);
     // compute: fragments of step j+1 are read while the MFMAs of step j run (register
     // double buffer; the sched barrier keeps the compiler from hoisting all 9 steps' reads)
     // (restrict-qualified operand pointers give the LDS reads alias scopes, so the compiler
@@ -316,7 +386,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
       __builtin_amdgcn_sched_barrier(0);
     }
     };
-    compute(sA(s & 1), TAP8 ? sW : sW + c * 9 * BN * ROWB);
+    compute(sA(buf), TAP8 ? sW : sW + c * 9 * BN * ROWB);
     k = k1; c = c1;
   }
   if (S > 0) epilogue(k - 1);
@@ -352,25 +422,33 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   }
 }
 
-struct ResVariant { int wm, wn, mt, nt, halo; bool tap8; int tw, th; };
-// 0: BM 256 (16x16) BN 32, 4 waves     1: BM 256 BN 64, 4 waves
-// 2: BM 512 (32x16) BN 32, 8 waves     3: BM 256 BN 64, 8 waves (4x2)
-// 4: TAP8 image layer, BM 256 BN 32, 4 waves
-constexpr ResVariant kRes[5] = {
-    {4, 1, 4, 2, 324, false, 16, 16}, {4, 1, 4, 4, 324, false, 16, 16},
-    {8, 1, 4, 2, 612, false, 32, 16}, {4, 2, 4, 2, 324, false, 16, 16},
-    {4, 1, 4, 2, 324, true, 16, 16}};
+struct ResVariant { int wm, wn, mt, nt, halo; bool tap8; int tw, th, nbuf; };
+// BN 32 = 4x2 16x16 MFMA tiles per wave column, BN 64 = two wave columns; NBUF = halo ring
+constexpr ResVariant kRes[7] = {
+    {4, 1, 4, 2, 324, false, 16, 16, 2},   // 0: BM 256 BN 32, 4 waves, 2-deep (2 WG / CU)
+    {8, 1, 4, 2, 612, false, 32, 16, 3},   // 1: BM 512 BN 32, 8 waves, 3-deep
+    {4, 2, 4, 2, 324, false, 16, 16, 3},   // 2: BM 256 BN 64, 8 waves, 3-deep
+    {4, 1, 4, 2, 324, true, 16, 16, 2},    // 3: image layer (TAP8), 4 waves, 2-deep
+    {8, 1, 4, 2, 612, true, 32, 16, 3},    // 4: image layer (TAP8), 8 waves, 3-deep
+    {8, 1, 4, 2, 612, false, 32, 16, 2},   // 5: BM 512 BN 32, 8 waves, 2-deep (large Cin)
+    {4, 2, 4, 2, 324, false, 16, 16, 2}};  // 6: BM 256 BN 64, 8 waves, 2-deep (large Cin)
 
 int res_smem(const ResVariant& v, int Cin, int C1, bool pro) {
   const int bn = v.wn * v.nt * 16;
-  const int pieces = v.tap8 ? v.halo : v.halo * 4;
-  return res_ss_bytes(C1, pro) + res_w_bytes(Cin, bn, v.tap8) + 2 * ((pieces + 63) / 64) * 1024;
+  const int nw = v.wm * v.wn;
+  const int instr = ((v.tap8 ? v.halo : v.halo * 4) + 63) / 64;
+  const int a_bytes = (instr + nw - 1) / nw * nw * 1024;
+  return res_ss_bytes(C1, pro) + res_w_bytes(Cin, bn, v.tap8) + v.nbuf * a_bytes;
 }
 
-template <int WM, int WN, int MT, int NT, int HALO, bool TAP8>
+template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF>
 void launch_res(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
-  hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8>), dim3(grid), dim3(WM * WN * 64),
-                     smem, st, a);
+  if (a.Co1 < a.Cout)
+    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, true>), dim3(grid),
+                       dim3(WM * WN * 64), smem, st, a);
+  else
+    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, false>), dim3(grid),
+                       dim3(WM * WN * 64), smem, st, a);
 }
 
 }  // namespace
@@ -383,15 +461,19 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
   const bool pro = a.pscale != nullptr;
   const bool tap8 = a.Cin <= 8 && a.C2 == 0 && a.CinW == 8 && !pro;
   const int bn = (a.Cout <= 32 || a.Cout % 64 != 0) ? 32 : 64;
-  int cand[2];
+  // preference: 3-deep halo rings (latency hiding) first; DDLPC_RES_DEPTH=2 prefers the
+  // 2-deep, two-workgroups-per-CU variants (A/B experiments)
+  static const int depth = [] { const char* e = getenv("DDLPC_RES_DEPTH"); return e ? atoi(e) : 3; }();
+  int cand[3];
   int nc = 0;
   if (tap8) {
     if (bn != 32) return -1;
-    cand[nc++] = 4;
+    if (depth == 2) { cand[nc++] = 3; } else { cand[nc++] = 4; cand[nc++] = 3; }
   } else if (bn == 32) {
-    cand[nc++] = 0; cand[nc++] = 2;
+    if (depth == 2) { cand[nc++] = 0; cand[nc++] = 5; }
+    else { cand[nc++] = 1; cand[nc++] = 5; cand[nc++] = 0; }
   } else {
-    cand[nc++] = 3;              // (variant 1, BN 64 on 4 waves, spills: not planned)
+    if (depth == 2) { cand[nc++] = 6; } else { cand[nc++] = 2; cand[nc++] = 6; }
   }
   for (int i = 0; i < nc; ++i) {
     const ResVariant& v = kRes[cand[i]];
@@ -421,11 +503,13 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
 
 void conv3_res_launch(ConvFwdArgs& a, int variant, int grid, int smem, hipStream_t st) {
   switch (variant) {
-    case 0: launch_res<4, 1, 4, 2, 324, false>(a, grid, smem, st); break;
-    case 1: launch_res<4, 1, 4, 4, 324, false>(a, grid, smem, st); break;
-    case 2: launch_res<8, 1, 4, 2, 612, false>(a, grid, smem, st); break;
-    case 3: launch_res<4, 2, 4, 2, 324, false>(a, grid, smem, st); break;
-    default: launch_res<4, 1, 4, 2, 324, true>(a, grid, smem, st); break;
+    case 0: launch_res<4, 1, 4, 2, 324, false, 2>(a, grid, smem, st); break;
+    case 1: launch_res<8, 1, 4, 2, 612, false, 3>(a, grid, smem, st); break;
+    case 2: launch_res<4, 2, 4, 2, 324, false, 3>(a, grid, smem, st); break;
+    case 3: launch_res<4, 1, 4, 2, 324, true, 2>(a, grid, smem, st); break;
+    case 4: launch_res<8, 1, 4, 2, 612, true, 3>(a, grid, smem, st); break;
+    case 5: launch_res<8, 1, 4, 2, 612, false, 2>(a, grid, smem, st); break;
+    default: launch_res<4, 2, 4, 2, 324, false, 2>(a, grid, smem, st); break;
   }
 }
 
