@@ -29,12 +29,16 @@ import torch.distributed as dist  # noqa: E402
 BASELINE_IMG_S = None   # set from BASELINE.json "inhouse_baseline" if present
 
 
-def _baseline():
+def _baseline(args):
+    """In-house MIOpen baseline (BASELINE.json) for the SAME config, else None."""
+    if args.dims != 2 or args.tile != 256 or args.depth != 5 or args.width_divisor != 2 \
+            or args.classes != 6 or args.accum != 1:
+        return None
     p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "BASELINE.json")
     try:
         with open(p) as f:
-            b = json.load(f)
-        v = b.get("inhouse_baseline", {}).get("images_per_sec_per_gpu")
+            b = json.load(f).get("inhouse_baseline", {})
+        v = {32: b.get("images_per_sec_per_gpu"), 64: b.get("batch_64_images_per_sec")}.get(args.batch)
         return float(v) if v else None
     except Exception:
         return None
@@ -51,6 +55,7 @@ def main():
     ap.add_argument("--width-divisor", type=int, default=2)
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--classes", type=int, default=6)
+    ap.add_argument("--dims", type=int, default=2, help="2 = images, 3 = volumes (3-D U-Net)")
     ap.add_argument("--impl", default=os.environ.get("DDLPC_IMPL", "hip"),
                     choices=["hip", "torch"])
     ap.add_argument("--bucket-mb", type=float, default=8.0)
@@ -65,7 +70,7 @@ def main():
     from ddlpc.train.trainer import Trainer
 
     cfg = TrainConfig(model=ModelConfig(out_classes=args.classes, depth=args.depth,
-                                        width_divisor=args.width_divisor),
+                                        width_divisor=args.width_divisor, dims=args.dims),
                       tile=args.tile, batch_per_gpu=args.batch, accum_steps=args.accum,
                       num_samples=1, test_holdout=0, impl=args.impl, bucket_mb=args.bucket_mb,
                       grad_codec=args.codec, log_dir=None, hip_graph=bool(args.hip_graph))
@@ -79,7 +84,7 @@ def main():
     pool = []
     for i in range(4):
         x, y = device_random_batch(args.batch, args.tile, args.classes, device,
-                                   seed=1000 * rank + i,
+                                   seed=1000 * rank + i, dims=args.dims,
                                    dtype=torch.bfloat16 if dev == "cuda" else torch.float32,
                                    channels_last=(dev == "cuda"))
         if tr.impl == "torch":
@@ -113,22 +118,32 @@ def main():
     ms = dt / args.steps * 1e3
     imgs = args.batch * args.accum * world * args.steps
     value = imgs / dt
-    base = _baseline()
+    base = _baseline(args)
     loss = tr.meter.reduce()
+    if args.dims == 2:
+        metric = f"images/sec (whole node), U-Net {args.tile}x{args.tile} {args.classes}-class tiles"
+        data_desc = (f"synthetic (Vaihingen-shape {args.tile}x{args.tile} RGB tiles, "
+                     f"{args.classes} classes, random-init weights)")
+    else:
+        metric = (f"volumes/sec (whole node), 3-D U-Net {args.tile}^3 {args.classes}-class volumes")
+        data_desc = (f"synthetic ({args.tile}^3 3-channel volumes, {args.classes} classes, "
+                     "random-init weights)")
     if rank == 0:
         rec = {
-            "metric": "images/sec (whole node), U-Net 256x256 6-class tiles",
-            "value": round(value, 2), "unit": "images/s", "n_gpus": world,
+            "metric": metric,
+            "value": round(value, 2), "unit": "images/s" if args.dims == 2 else "volumes/s",
+            "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": (round(value / (base * world), 3) if base else None),
             "dtype": "bf16" if dev == "cuda" else "fp32",
-            "data": "synthetic (Vaihingen-shape 256x256 RGB tiles, 6 classes, random-init weights)",
+            "data": data_desc,
             "config": {"model": f"UNet depth{args.depth} width/{args.width_divisor} "
                                 f"conv_transpose ({sum(p.numel() for p in tr.model.parameters())} params)",
                        "global_batch": args.batch * args.accum * world,
                        "per_gpu_batch": args.batch, "accum_steps": args.accum,
-                       "seq_len": None, "tile": args.tile, "classes": args.classes,
+                       "seq_len": None, "tile": args.tile, "dims": args.dims,
+                       "classes": args.classes,
                        "parallelism": f"dp{world}", "impl": tr.impl,
                        "optimizer": "Adam(lr=1e-3)", "loss": "CrossEntropy",
                        "train_loss_mean": round(loss["loss"], 4)},
