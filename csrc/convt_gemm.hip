@@ -25,21 +25,19 @@ constexpr int BK = 32;
 DDLPC_DEVICE int swz(int row, int chunk) { return chunk ^ (((row >> 2) & 1) << 1); }
 DDLPC_DEVICE int lds_off(int row, int chunk) { return row * 64 + (swz(row, chunk) << 4); }
 
-// output (high-res) pixel of input pixel m and sub-position sub
-DDLPC_DEVICE long long up_pixel(long long m, int sub, int dims, int D, int H, int W) {
-  const int w = (int)(m % W);
-  long long q = m / W;
-  const int h = (int)(q % H);
-  q /= H;
+// output (high-res) pixel of input pixel m and sub-position sub, in 32-bit arithmetic
+// (pixel counts < 2^31): with q = m / W (= n*H + h for 2-D), the 2x up-sampled pixel is
+// (2q + i) * 2W + 2w + j — one integer division for 2-D, two for 3-D
+DDLPC_DEVICE int up_pixel(int m, int sub, int dims, int D, int H, int W) {
+  const int q = m / W, w = m - q * W;
   if (dims == 2) {
-    const long long n = q;
     const int i = sub >> 1, j = sub & 1;
-    return (n * (2 * H) + 2 * h + i) * (2 * W) + 2 * w + j;
+    return (2 * q + i) * (2 * W) + 2 * w + j;
   }
-  const int d = (int)(q % D);
-  const long long n = q / D;
+  const int q2 = q / H, h = q - q2 * H;           // q2 = n*D + d
   const int kd = sub >> 2, i = (sub >> 1) & 1, j = sub & 1;
-  return ((n * (2 * D) + 2 * d + kd) * (2 * H) + 2 * h + i) * (2 * W) + 2 * w + j;
+  (void)D;
+  return ((2 * q2 + kd) * (2 * H) + 2 * h + i) * (2 * W) + 2 * w + j;
 }
 
 template <int MODE>
@@ -64,16 +62,16 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs p) {
     for (int i = 0; i < 2; ++i) {
       const int e = tid + 256 * i;
       const int row = e >> 2, cq = e & 3;
-      const long long m = m0 + row;
+      const int m = (int)m0 + row;
       const int k8 = kc * BK + cq * 8;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (m < p.M && k8 < p.K) {
         if (MODE == GEMM_CONVT_FWD) {
-          v = *reinterpret_cast<const uint4*>(p.A + m * p.K + k8);
+          v = *reinterpret_cast<const uint4*>(p.A + (long long)m * p.K + k8);
         } else {   // DGRAD: k = sub*Cout + co gathered from the high-res gradient
           const int sub = k8 / p.Cout, co = k8 % p.Cout;
-          const long long up = up_pixel(m, sub, p.dims, p.D, p.H, p.W);
-          v = *reinterpret_cast<const uint4*>(p.A + up * p.Cout + co);
+          const int up = up_pixel(m, sub, p.dims, p.D, p.H, p.W);
+          v = *reinterpret_cast<const uint4*>(p.A + (long long)up * p.Cout + co);
         }
       }
       ra[i] = v;
@@ -140,16 +138,16 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs p) {
   bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
   for (int e = tid; e < BM * (BN / 8); e += 256) {
     const int row = e / (BN / 8), cg = e % (BN / 8);
-    const long long m = m0 + row;
+    const int m = (int)m0 + row;
     const int n = n0 + cg * 8;
     if (m >= p.M || n >= p.N) continue;
     const uint4 v = *reinterpret_cast<const uint4*>(sO + row * BN + cg * 8);
     if (MODE == GEMM_CONVT_FWD) {
       const int sub = n / p.Cout, co = n % p.Cout;
-      const long long up = up_pixel(m, sub, p.dims, p.D, p.H, p.W);
-      *reinterpret_cast<uint4*>(C + up * p.Cout + co) = v;
+      const int up = up_pixel(m, sub, p.dims, p.D, p.H, p.W);
+      *reinterpret_cast<uint4*>(C + (long long)up * p.Cout + co) = v;
     } else {
-      *reinterpret_cast<uint4*>(C + m * p.N + n) = v;
+      *reinterpret_cast<uint4*>(C + (long long)m * p.N + n) = v;
     }
   }
   (void)S;
@@ -197,8 +195,8 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_wgrad_kernel(GemmArgs p) {
         const int n = n0 + cg * 8;
         if (n < p.N) {
           const int sub = n / p.Cout, co = n % p.Cout;
-          const long long up = up_pixel(px, sub, p.dims, p.D, p.H, p.W);
-          vb = *reinterpret_cast<const uint4*>(p.B + up * p.Cout + co);
+          const int up = up_pixel((int)px, sub, p.dims, p.D, p.H, p.W);
+          vb = *reinterpret_cast<const uint4*>(p.B + (long long)up * p.Cout + co);
         }
       }
       ra[i] = va;

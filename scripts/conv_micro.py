@@ -60,6 +60,8 @@ def main():
             "wgrad": lambda: F.conv3_wgrad(dy, x1, x2, sc, sh),
         }
         for ps in a.passes.split(","):
+            if ps.startswith("t"):
+                continue
             if ps == "dgrad" and name == "enc1.a":
                 continue
             fn = fns[ps]
@@ -74,6 +76,38 @@ def main():
             us = e0.elapsed_time(e1) * 1e3 / a.iters
             tot[ps] += us
             print(f"{name:8s} {ps:6s} {us:9.1f} us  {flops / us / 1e6:8.1f} TF/s", flush=True)
+    # transposed-conv up-sampling (2x2 stride 2), channels preserved: (name, Hin, C)
+    UPS = [("up5", 8, 256), ("up4", 16, 256), ("up3", 32, 256), ("up2", 64, 128), ("up1", 128, 64)]
+    tpasses = [p for p in a.passes.split(",") if p.startswith("t")]
+    for name, H, C in UPS:
+        if not tpasses or (a.only and a.only not in name):
+            continue
+        N = a.batch
+        x = torch.randn(N, H, H, C, device=dev).bfloat16()
+        dout = torch.randn(N, 2 * H, 2 * H, C, device=dev).bfloat16()
+        up = torch.nn.Module()
+        up.weight = torch.nn.Parameter(torch.randn(C, C, 2, 2, device=dev) * 0.05)
+        pk = _ConvPack(up, 1, True)
+        F.weight_pack(torch.tensor([pk.entry()], dtype=torch.int64, device=dev), 1, pk.numel())
+        b = torch.zeros(C, device=dev)
+        flops = 2.0 * N * H * H * C * 4 * C
+        fns = {"tfwd": lambda: F.convt_fwd(x, pk.fwd, b, C),
+               "tdgrad": lambda: F.convt_dgrad(dout, pk.dgrad, C),
+               "twgrad": lambda: F.convt_wgrad(x, dout)}
+        for ps in tpasses:
+            fn = fns[ps]
+            fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                fn()
+            e1.record()
+            e1.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / a.iters
+            tot[ps] = tot.get(ps, 0.0) + us
+            gbs = (x.numel() + dout.numel()) * 2 / us / 1e3
+            print(f"{name:8s} {ps:6s} {us:9.1f} us  {flops / us / 1e6:8.1f} TF/s  {gbs:7.1f} GB/s", flush=True)
     print("totals (us):", {k: round(v, 1) for k, v in tot.items()})
 
 
