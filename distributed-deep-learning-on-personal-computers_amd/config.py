@@ -92,6 +92,11 @@ class TrainConfig:
     png_dir: Optional[str] = None        # prediction/label/image dumps (ref.py:785-790)
     png_count: int = 5
     log_every: int = 10
+    # ---- tracing --------------------------------------------------
+    trace_ranges: bool = False           # roctx ranges around the step phases
+    phase_timers: bool = True            # hipEvent phase times (fwd+bwd, comm wait, optim)
+    profile_dir: Optional[str] = None    # torch.profiler Chrome traces per rank
+    profile_steps: int = 5               # active profiler steps (after 2 wait + 2 warm-up)
     # ---- execution -----------------------------------------------------------------
     impl: str = "auto"                   # auto | hip | torch   (hip = hand-written kernels)
     hip_graph: bool = False              # capture the train step in a hipGraph

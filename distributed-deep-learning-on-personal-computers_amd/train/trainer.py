@@ -37,6 +37,7 @@ from ..ops.adam import FlatAdam
 from ..parallel import (GradBucketReducer, assert_replicas_identical, broadcast_buffers,
                         broadcast_module, flatten_module, init_distributed)
 from ..utils.metrics import DeviceMeter, RunLogger, StepTimer, dump_pngs, iou_per_class
+from ..utils.tracing import PhaseTimer, StepProfiler, enable_ranges, trace_range
 from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
 
 
@@ -88,6 +89,10 @@ class Trainer:
                          and cfg.dtype == "bf16")
         self.meter = DeviceMeter(self.device)
         self.logger = RunLogger(cfg.log_dir, self.rank, cfg.grad_codec)
+        if cfg.trace_ranges:
+            enable_ranges(True)
+        self.phases = PhaseTimer(self.device) if cfg.phase_timers else None
+        self.profiler = StepProfiler(cfg.profile_dir, self.rank, active=cfg.profile_steps)
         self.step_count = 0
         self.micro_count = 0
         self._graph = None               # hipGraph of the train step (cfg.hip_graph)
@@ -179,6 +184,7 @@ class Trainer:
             self.optimizer.note_replayed_step()
         self.micro_count += 1
         self.step_count += 1
+        self.profiler.step()
 
     GRAPH_WARMUP = 3
 
@@ -188,12 +194,26 @@ class Trainer:
             return self._graph_step(*micro_batches[0])
         self.model.train()
         n = len(micro_batches)
-        for i, (x, y) in enumerate(micro_batches):
-            self._micro(x, y, sync=(i == n - 1))
+        ph = self.phases
+        if ph is not None:
+            ph.mark("start")
+        with trace_range("ddlpc.fwd_bwd"):
+            for i, (x, y) in enumerate(micro_batches):
+                self._micro(x, y, sync=(i == n - 1))
+        if ph is not None:
+            ph.mark("fwd_bwd")
         if self.reducer is not None:
-            self.reducer.finish()
-        self.optimizer.step()
-        self.optimizer.zero_grad()
+            with trace_range("ddlpc.grad_sync"):
+                self.reducer.finish()
+            if ph is not None:
+                ph.mark("comm_wait")          # exposed (non-overlapped) all-reduce time
+        with trace_range("ddlpc.optimizer"):
+            self.optimizer.step()
+            self.optimizer.zero_grad()
+        if ph is not None:
+            ph.mark("optimizer")
+            ph.end_step()
+        self.profiler.step()
         if self.cfg.broadcast_buffers:
             broadcast_buffers(self.model)
         self.step_count += 1
@@ -206,6 +226,7 @@ class Trainer:
         self.logger.header(c.batch_per_gpu, self.world, c.accum_steps, c.model.width_divisor)
         last = {}
         t_start = time.perf_counter()
+        log_t, log_step = t_start, self.step_count
         while self.epoch < c.epochs:
             self.sampler.set_epoch(self.epoch)
             self.meter.reset()
@@ -220,9 +241,15 @@ class Trainer:
                 pending = []
                 steps_this_epoch += 1
                 if c.log_every and self.step_count % c.log_every == 0:
-                    m = self.meter.reduce()
+                    m = self.meter.reduce()       # synchronises: phase events are complete
+                    now = time.perf_counter()
+                    imgs = (self.step_count - log_step) * c.batch_per_gpu * c.accum_steps * self.world
                     rec = {"epoch": self.epoch, "step": self.step_count, **m,
-                           "elapsed_s": time.perf_counter() - t_start}
+                           "images_per_s": imgs / max(now - log_t, 1e-9),
+                           "elapsed_s": now - t_start}
+                    if self.phases is not None:
+                        rec.update(self.phases.read())
+                    log_t, log_step = now, self.step_count
                     self.logger.log(rec)
                 if c.ckpt_dir and c.ckpt_every and self.step_count % c.ckpt_every == 0:
                     self.save()
@@ -310,6 +337,7 @@ class Trainer:
         return blob
 
     def close(self):
+        self.profiler.close()
         self.logger.close()
         if self.reducer is not None:
             self.reducer.remove_hooks()
