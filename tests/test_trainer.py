@@ -56,6 +56,29 @@ def test_validate_from_checkpoint(tmp_path):
     assert abs(v["val_pixel_acc"] - tr.validate()["val_pixel_acc"]) < 1e-9
 
 
+def test_profiler_trace_and_throughput_metrics(tmp_path):
+    cfg = _cfg(tmp_path, epochs=2, max_steps=6, profile_dir=str(tmp_path / "prof"),
+               profile_steps=1, trace_ranges=True)
+    train(cfg, device="cpu")
+    assert os.path.exists(tmp_path / "prof" / "trace_rank0.json")
+    trace = json.load(open(tmp_path / "prof" / "trace_rank0.json"))
+    names = {e.get("name") for e in trace.get("traceEvents", [])}
+    assert any(n and "conv" in n for n in names)
+    lines = [json.loads(l) for l in open(tmp_path / "logs" / "metrics.jsonl")]
+    steps = [l for l in lines if "step" in l and "epoch_end" not in l]
+    assert steps and all(l["images_per_s"] > 0 for l in steps)
+
+
+def test_phase_timer_reads_on_cpu_are_empty():
+    from ddlpc.utils.tracing import PhaseTimer, trace_range
+    pt = PhaseTimer(torch.device("cpu"))
+    pt.mark("start")
+    with trace_range("x"):
+        pt.mark("a")
+    pt.end_step()
+    assert pt.read() == {}
+
+
 def test_bench_cpu_json_contract():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--impl", "torch",
@@ -67,3 +90,26 @@ def test_bench_cpu_json_contract():
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in rec
     assert rec["n_gpus"] == 1 and rec["steps"] == 1 and rec["value"] > 0
+
+
+def test_bench_torchrun_two_ranks_gloo():
+    """The driver's N>1 launch line (torch.distributed.run, 127.0.0.1) on CPU/gloo: one JSON
+    line from rank 0 with the whole-job aggregate."""
+    import socket
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                          "--master-port", str(port), os.path.join(root, "bench.py"),
+                          "--gpus", "2", "--impl", "torch", "--steps", "2", "--warmup", "1",
+                          "--batch", "2", "--tile", "64", "--width-divisor", "16"],
+                         capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.strip().splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
+    assert rec["config"]["global_batch"] == 4 and rec["value"] > 0
