@@ -60,12 +60,13 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad_kernel(ConvWgradArgs p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-  // block -> (split, plane, ci chunk, co tile); splits innermost share operand tiles
-  int b = blockIdx.x;
-  const int split = b % p.splits; b /= p.splits;
+  // block -> (plane, ci chunk, co tile, split), the first three innermost in XCD-contiguous
+  // order: workgroups streaming the same pixel range share one XCD's L2
+  int b = xcd_remap(blockIdx.x, gridDim.x);
   const int plane = b % p.planes; b /= p.planes;
   const int cic = b % p.ciChunks; b /= p.ciChunks;
-  const int cot = b;
+  const int cot = b % p.coTiles; b /= p.coTiles;
+  const int split = b;
   const int co0 = cot * BCO, ci0 = cic * CI;
 
   const bool has_pro = p.pscale != nullptr;
@@ -298,10 +299,14 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int b = blockIdx.x;
-  const int split = b % p.splits; b /= p.splits;
+  // (ci chunk, co tile) innermost in the XCD-contiguous logical order: the workgroups that
+  // stream the SAME pixel range (same dY and X tiles) run together on one XCD and share its
+  // L2 instead of each re-reading the operands from HBM
+  int b = xcd_remap(blockIdx.x, gridDim.x);
   const int cic = b % p.ciChunks; b /= p.ciChunks;
-  const int co0 = b * BCO, ci0 = cic * BK;
+  const int cot = b % p.coTiles; b /= p.coTiles;
+  const int split = b;
+  const int co0 = cot * BCO, ci0 = cic * BK;
 
   const bool has_pro = p.pscale != nullptr;
   if (has_pro)

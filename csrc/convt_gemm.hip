@@ -163,17 +163,17 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_wgrad_kernel(GemmArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int nTilesN = (p.N + BN - 1) / BN, nTilesM = (p.M + BM - 1) / BM;
-  int b = blockIdx.x;
-  const int split = b % p.splits; b /= p.splits;
+  // tiles of one pixel range innermost in XCD-contiguous order (shared operands hit L2)
+  int b = xcd_remap(blockIdx.x, gridDim.x);
   const int ntile = b % nTilesN; b /= nTilesN;
-  const int mtile = b;
+  const int mtile = b % nTilesM; b /= nTilesM;
+  const int split = b;
   const int m0 = mtile * BM, n0 = ntile * BN;
   const long long npx = (long long)p.K;
   const long long per = (npx + p.splits - 1) / p.splits;
   const long long k_begin = per * split;
   const long long k_end = k_begin + per < npx ? k_begin + per : npx;
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  (void)nTilesM;
 
   f32x4_t acc[2][2];
 #pragma unroll

@@ -31,6 +31,8 @@ mean subtraction cancels them); stock PyTorch returns float noise of ~1e-9 there
 """
 from __future__ import annotations
 
+import contextlib
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -151,8 +153,9 @@ class _DoubleConvFn(torch.autograd.Function):
         # ---- second conv: BN2 + ReLU (+ unpool + skip sum) backward, then its gradients
         if direct:
             dy2, _, _ = F.bn_backward(da2, dpool, y2, s2, g2, None, bn2.weight.grad, bn2.bias.grad)
-            F.conv3_wgrad(dy2, y1, None, s1[2], s1[3], blk.conv2.weight.grad)
-            eng.ready(bn2.weight, bn2.bias, blk.conv2.weight, blk.conv2.bias)
+            with eng.wgrad_stream(dy2, y1, s1):
+                F.conv3_wgrad(dy2, y1, None, s1[2], s1[3], blk.conv2.weight.grad)
+                eng.ready(bn2.weight, bn2.bias, blk.conv2.weight, blk.conv2.bias)
             dg2 = dbe2 = dw2 = None
         else:
             dy2, dg2, dbe2 = F.bn_backward(da2, dpool, y2, s2, g2, None)
@@ -164,11 +167,12 @@ class _DoubleConvFn(torch.autograd.Function):
         padded_in = x2 is None and x1.shape[-1] != w1.shape[1]   # first layer: 3 -> 8 ch
         if direct:
             dy1, _, _ = F.bn_backward(da1, None, y1, s1, g1, None, bn1.weight.grad, bn1.bias.grad)
-            if padded_in:
-                w1.grad.add_(F.conv3_wgrad(dy1, x1, None, None, None)[:, :w1.shape[1]])
-            else:
-                F.conv3_wgrad(dy1, x1, x2, None, None, w1.grad)
-            eng.ready(bn1.weight, bn1.bias, w1, blk.conv1.bias)
+            with eng.wgrad_stream(dy1, x1, x2):
+                if padded_in:
+                    w1.grad.add_(F.conv3_wgrad(dy1, x1, None, None, None)[:, :w1.shape[1]])
+                else:
+                    F.conv3_wgrad(dy1, x1, x2, None, None, w1.grad)
+                eng.ready(bn1.weight, bn1.bias, w1, blk.conv1.bias)
             dg1 = dbe1 = dw1 = None
         else:
             dy1, dg1, dbe1 = F.bn_backward(da1, None, y1, s1, g1, None)
@@ -187,6 +191,8 @@ class _DoubleConvFn(torch.autograd.Function):
                 dx1._ddlpc_colsum_rows = sums
             if x2 is None:
                 dx2 = None
+        if blk.first:
+            eng.join()                   # last backward node: main stream waits for wgrads
         # conv biases feeding a training-mode BN have an exactly-zero gradient
         zb1 = torch.zeros_like(g1) if (not direct and ctx.needs_input_grad[3]) else None
         zb2 = torch.zeros_like(g2) if (not direct and ctx.needs_input_grad[7]) else None
@@ -210,9 +216,11 @@ class _ConvTFn(torch.autograd.Function):
         dx = F.convt_dgrad(dout, ctx.pack.dgrad, ctx.pack.cin) if ctx.needs_input_grad[0] else None
         conv = ctx.pack.conv
         rows = getattr(dout, "_ddlpc_colsum_rows", None)
-        if ctx.engine.direct_grads:
-            F.convt_wgrad(x, dout, conv.weight.grad, conv.bias.grad, rows)
-            ctx.engine.ready(conv.weight, conv.bias)
+        eng = ctx.engine
+        if eng.direct_grads:
+            with eng.wgrad_stream(x, dout, rows):
+                F.convt_wgrad(x, dout, conv.weight.grad, conv.bias.grad, rows)
+                eng.ready(conv.weight, conv.bias)
             return dx, None, None, None, None
         dw, db = F.convt_wgrad(x, dout, None, None, rows)
         return dx, dw.view_as(conv.weight), db, None, None
@@ -249,7 +257,8 @@ class _HeadCEFn(torch.autograd.Function):
             head = eng.head
             da, _, _ = _ops().head_ce_bwd(a, wh, bh, labels, out3, gs, ctx.ignore_index,
                                           head.weight.grad, head.bias.grad)
-            eng.ready(head.weight, head.bias)
+            with eng.wgrad_stream():
+                eng.ready(head.weight, head.bias)
             return da, None, None, None, None, None
         da, dw, db = _ops().head_ce_bwd(a, wh, bh, labels, out3, gs, ctx.ignore_index)
         return da, dw, db, None, None, None
@@ -261,6 +270,7 @@ class _Block:
     def __init__(self, dc: nn.Module, first: bool, engine, up_is_convt: bool = False):
         self.engine = engine
         self.up_is_convt = up_is_convt
+        self.first = first
         seq = dc.double_conv
         self.conv1, self.conv2 = seq[0], seq[3]
         self.bn1, self.bn2 = _BNState(seq[1]), _BNState(seq[4])
@@ -289,6 +299,13 @@ class UNetEngine:
         # are flattened.
         self.direct_grads = False
         self.grad_ready = None
+        # weight gradients (3x3 wgrad + its split-K reduction, convT wgrad) run on a side
+        # HIP stream, concurrently with the data-gradient chain on the compute stream: the
+        # two chains are independent until the optimizer step, and the small deep-layer
+        # kernels of one fill the CUs the other leaves idle.  DDLPC_WGRAD_STREAM=0 disables.
+        use_side = os.environ.get("DDLPC_WGRAD_STREAM", "1") != "0"
+        self.side = torch.cuda.Stream(dev) if use_side else None
+        self._side_used = False
         self.enc = [_Block(b.double_conv, first=(i == 0), engine=self)
                     for i, b in enumerate(model.down_blocks())]
         self.mid = _Block(model.double_conv, first=False, engine=self)
@@ -315,7 +332,32 @@ class UNetEngine:
         self.direct_grads = True
         self.grad_ready = grad_ready
 
+    def wgrad_stream(self, *tensors):
+        """Context for weight-gradient work: the side stream first waits for everything
+        queued so far on the compute stream; tensors allocated there and read on the side
+        stream are marked so the caching allocator does not recycle them early."""
+        if self.side is None or not self.direct_grads:
+            return contextlib.nullcontext()
+        cur = torch.cuda.current_stream(self.side.device)
+        self.side.wait_stream(cur)
+        # (inside a hipGraph capture the allocator defers reuse of such blocks to the end
+        # of the capture, so the replayed graph cannot race on them either)
+        for t in tensors:
+            if isinstance(t, torch.Tensor) and t.numel() and t.is_cuda:
+                t.record_stream(self.side)
+        self._side_used = True
+        return torch.cuda.stream(self.side)
+
+    def join(self):
+        """Compute stream waits for all queued weight-gradient work."""
+        if self.side is not None and self._side_used:
+            torch.cuda.current_stream(self.side.device).wait_stream(self.side)
+            self._side_used = False
+
     def ready(self, *params):
+        """Gradients of ``params`` are complete once the queued work finishes.  Called on
+        the side stream (after it joined the compute stream), so a bucket collective the
+        reducer launches here is ordered after every gradient write of either stream."""
         if self.grad_ready is not None:
             for p in params:
                 self.grad_ready(p)

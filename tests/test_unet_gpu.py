@@ -104,3 +104,25 @@ def test_trainer_hip_graph_matches_eager():
     assert torch.equal(p0, p1), float((p0 - p1).abs().max())
     assert torch.equal(v0, v1)
     assert l0 == l1
+
+
+def test_wgrad_side_stream_matches_serial(monkeypatch):
+    """Weight gradients on the side HIP stream (default) give bit-identical training to the
+    fully serial schedule (DDLPC_WGRAD_STREAM=0): same kernels, only the overlap differs."""
+    from ddlpc.config import ModelConfig, TrainConfig
+    from ddlpc.data import device_random_batch
+    from ddlpc.train.trainer import Trainer
+    out = []
+    for side in ("0", "1"):
+        monkeypatch.setenv("DDLPC_WGRAD_STREAM", side)
+        cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=4,
+                          num_samples=1, test_holdout=0, impl="hip", accum_steps=2)
+        tr = Trainer(cfg, device="cuda")
+        assert (tr.model._engine.side is not None) == (side == "1")
+        batches = [device_random_batch(4, 64, 6, tr.device, seed=s) for s in range(4)]
+        for i in range(3):
+            tr.train_step([batches[i % 4], batches[(i + 1) % 4]])
+        torch.cuda.synchronize()
+        out.append(tr.flat.param_buf.clone())
+        tr.close()
+    assert torch.equal(out[0], out[1]), float((out[0] - out[1]).abs().max())
