@@ -304,7 +304,10 @@ class UNetEngine:
         # two chains are independent until the optimizer step, and the small deep-layer
         # kernels of one fill the CUs the other leaves idle.  DDLPC_WGRAD_STREAM=0 disables.
         use_side = os.environ.get("DDLPC_WGRAD_STREAM", "1") != "0"
-        self.side = torch.cuda.Stream(dev) if use_side else None
+        # low priority: when both streams have work queued, the critical data-gradient
+        # chain is dispatched first and the weight gradients fill what is left
+        prio = int(os.environ.get("DDLPC_SIDE_PRIORITY", "1"))
+        self.side = torch.cuda.Stream(dev, priority=prio) if use_side else None
         self._side_used = False
         self.enc = [_Block(b.double_conv, first=(i == 0), engine=self)
                     for i, b in enumerate(model.down_blocks())]
