@@ -61,6 +61,7 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=8.0)
     ap.add_argument("--codec", default="none")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--verbose", type=int, default=0, help="1: progress lines on stderr")
     ap.add_argument("--hip-graph", type=int, default=int(os.environ.get("DDLPC_HIP_GRAPH", "0")),
                     help="1: replay the single-GPU train step as one hipGraph")
     args = ap.parse_args()
@@ -105,6 +106,8 @@ def main():
 
     for i in range(args.warmup):
         step(i)
+        if args.verbose and rank == 0:
+            print(f"warmup step {i} done", file=sys.stderr, flush=True)
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):

@@ -50,29 +50,53 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
   }
 }
 
+// Destination-ordered: consecutive lanes write consecutive bf16 of a packed layout (the
+// innermost packed index is the fastest-varying thread index), reads gather from the small
+// fp32 source (L2 / Infinity-Cache resident).  Packing pads (ci >= Cin) were zeroed at
+// allocation and are never written.
 __global__ void weight_pack_kernel(const PackEntry* __restrict__ ents) {
   const PackEntry e = ents[blockIdx.y];
   const long long total = (long long)e.Cout * e.Cin * e.taps;
-  for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < total;
-       o += (long long)gridDim.x * blockDim.x) {
-    if (e.kind == 0) {
-      // src OIHW [co][ci][tap]
-      const int tap = (int)(o % e.taps);
-      const int ci = (int)((o / e.taps) % e.Cin);
-      const int co = (int)(o / ((long long)e.taps * e.Cin));
-      const bf16_t w = f2bf(e.src[o]);
-      e.fwd[((long long)co * e.taps + tap) * e.CinW + ci] = w;
-      if (e.dgrad != nullptr)
-        e.dgrad[((long long)ci * e.taps + (e.taps - 1 - tap)) * e.CoutW + co] = w;
-    } else {
-      // src IOHW [ci][co][sub]  (taps = S sub-positions)
-      const int sub = (int)(o % e.taps);
-      const int co = (int)((o / e.taps) % e.Cout);
-      const int ci = (int)(o / ((long long)e.taps * e.Cout));
-      const bf16_t w = f2bf(e.src[o]);
-      e.fwd[((long long)sub * e.Cout + co) * e.Cin + ci] = w;
-      if (e.dgrad != nullptr) e.dgrad[(long long)ci * e.taps * e.Cout + sub * e.Cout + co] = w;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long t0 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (e.kind == 0) {
+    // src OIHW [co][ci][tap]  ->  fwd [co][tap][CinW] (ci fastest)
+    for (long long o = t0; o < total; o += stride) {
+      const int ci = (int)(o % e.Cin);
+      const long long r = o / e.Cin;
+      const int tap = (int)(r % e.taps);
+      const int co = (int)(r / e.taps);
+      e.fwd[((long long)co * e.taps + tap) * e.CinW + ci] =
+          f2bf(e.src[((long long)co * e.Cin + ci) * e.taps + tap]);
     }
+    // -> dgrad [ci][tap'][CoutW] (co fastest), tap' = taps-1-tap (flipped filter)
+    if (e.dgrad != nullptr)
+      for (long long o = t0; o < total; o += stride) {
+        const int co = (int)(o % e.Cout);
+        const long long r = o / e.Cout;
+        const int tp = (int)(r % e.taps);
+        const int ci = (int)(r / e.taps);
+        e.dgrad[((long long)ci * e.taps + tp) * e.CoutW + co] =
+            f2bf(e.src[((long long)co * e.Cin + ci) * e.taps + (e.taps - 1 - tp)]);
+      }
+  } else {
+    // src IOHW [ci][co][sub]  ->  fwd [(sub, co)][Cin] (ci fastest)
+    for (long long o = t0; o < total; o += stride) {
+      const int ci = (int)(o % e.Cin);
+      const long long r = o / e.Cin;             // = sub * Cout + co
+      const int co = (int)(r % e.Cout);
+      const int sub = (int)(r / e.Cout);
+      e.fwd[o] = f2bf(e.src[((long long)ci * e.Cout + co) * e.taps + sub]);
+    }
+    // -> dgrad [ci][(sub, co)] (co fastest)
+    if (e.dgrad != nullptr)
+      for (long long o = t0; o < total; o += stride) {
+        const int co = (int)(o % e.Cout);
+        const long long r = o / e.Cout;
+        const int sub = (int)(r % e.taps);
+        const int ci = (int)(r / e.taps);
+        e.dgrad[o] = f2bf(e.src[((long long)ci * e.Cout + co) * e.taps + sub]);
+      }
   }
 }
 
