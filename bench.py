@@ -49,7 +49,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32, help="per-GPU batch (images)")
+    ap.add_argument("--batch", type=int, default=64,
+                    help="per-GPU batch (images); 64 = the largest batch with a measured in-house baseline")
     ap.add_argument("--accum", type=int, default=1)
     ap.add_argument("--tile", type=int, default=256)
     ap.add_argument("--width-divisor", type=int, default=2)

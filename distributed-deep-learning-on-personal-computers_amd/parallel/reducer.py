@@ -52,7 +52,7 @@ class _Bucket:
 class GradBucketReducer:
     def __init__(self, flat: FlatParams, group=None, bucket_mb: float = 8.0,
                  reduce: str = "mean", grad_codec: str = "none", codec_scale: str = "bucket",
-                 overlap: bool = True):
+                 overlap: bool = True, use_hooks: bool = True):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -74,8 +74,14 @@ class GradBucketReducer:
             for p in b.params:
                 self._bucket_of[id(p)] = b
         self._sync = True
+        self._seen = set()
         self._hooks = []
-        if self.world > 1:
+        # readiness: autograd post-accumulate hooks (stock PyTorch modules), or — with
+        # use_hooks=False — ONLY explicit mark_ready() calls from kernels that write .grad
+        # directly (the HIP engine).  Never both: autograd still runs the AccumulateGrad
+        # nodes of such parameters (with no gradient), which would count them twice and
+        # launch a bucket before its last gradient is written.
+        if self.world > 1 and use_hooks:
             for p in flat.order:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
         self.stats = {"buckets": len(self.buckets), "launched_in_backward": 0}
@@ -115,6 +121,7 @@ class GradBucketReducer:
         """Call before each micro-batch backward: ``sync`` only on the last one."""
         self._sync = sync
         if sync:
+            self._seen = set()
             for b in self.buckets:
                 b.pending = len(b.params)
                 b.work = None
@@ -129,8 +136,9 @@ class GradBucketReducer:
         if not self._sync or not self.overlap:
             return
         b = self._bucket_of.get(id(p))
-        if b is None:
+        if b is None or id(p) in self._seen:       # a parameter counts once per step
             return
+        self._seen.add(id(p))
         b.pending -= 1
         if b.pending == 0 and not b.launched:
             self._launch(b)

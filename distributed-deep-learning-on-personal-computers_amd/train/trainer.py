@@ -79,7 +79,8 @@ class Trainer:
             self.reducer = GradBucketReducer(self.flat, bucket_mb=cfg.bucket_mb,
                                              reduce=cfg.reduce, grad_codec=cfg.grad_codec,
                                              codec_scale=cfg.codec_scale,
-                                             overlap=cfg.overlap_comm)
+                                             overlap=cfg.overlap_comm,
+                                             use_hooks=(self.impl != "hip"))
         if self.impl == "hip":
             # kernels write gradients straight into the flat grad buffer and trigger the
             # reducer's buckets themselves (no autograd accumulate pass)

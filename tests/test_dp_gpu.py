@@ -1,0 +1,75 @@
+"""Data parallel on the HIP engine: 2 ranks share the box's one GPU over gloo (RCCL refuses
+two ranks on one device; the 8-GPU RCCL run is the driver's).  Exercises the kernels'
+direct-to-flat-buffer gradients, readiness callbacks from the weight-gradient side stream
+launching bucket all-reduces during backward, and replica identity."""
+import pytest
+import torch
+
+from dist_utils import run
+
+pytestmark = pytest.mark.gpu
+
+
+def _dp_rank(rank, world, bucket_mb, side, overlap):
+    import os
+    os.environ["LOCAL_RANK"] = "0"              # both ranks on the box's single GPU
+    os.environ["DDLPC_WGRAD_STREAM"] = side
+    import torch.distributed as dist
+    from ddlpc.config import ModelConfig, TrainConfig
+    from ddlpc.data import device_random_batch
+    from ddlpc.train.trainer import Trainer
+    cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=2,
+                      num_samples=1, test_holdout=0, impl="hip", backend="gloo",
+                      bucket_mb=bucket_mb, overlap_comm=overlap)
+    tr = Trainer(cfg, device="cuda")
+    red = tr.reducer
+    x, y = device_random_batch(2, 64, 6, tr.device, seed=10 + rank)
+    # local gradient (no communication)
+    red.prepare(sync=False)
+    loss, _ = tr.model.loss_and_correct(x, y)
+    loss.backward()
+    torch.cuda.synchronize()
+    g_local = tr.flat.grad_buf.clone()
+    tr.optimizer.zero_grad()
+    # same micro-batch with the bucketed all-reduce overlapped with backward
+    red.prepare(sync=True)
+    loss, _ = tr.model.loss_and_correct(x, y)
+    loss.backward()
+    launched = red.stats["launched_in_backward"]
+    red.finish()
+    torch.cuda.synchronize()
+    g_red = tr.flat.grad_buf.clone()
+    tr.optimizer.zero_grad()
+    gl = [torch.empty_like(g_local) for _ in range(world)]
+    dist.all_gather(gl, g_local)
+    mean = sum(gl) / world
+    for i in range(3):
+        xb, yb = device_random_batch(2, 64, 6, tr.device, seed=100 * i + rank)
+        tr.train_step([(xb, yb)])
+    torch.cuda.synchronize()
+    p = tr.flat.param_buf.clone()
+    ps = [torch.empty_like(p) for _ in range(world)]
+    dist.all_gather(ps, p)
+    bad = []
+    for n, q in tr.model.named_parameters():
+        a, b = tr.flat.span(q)
+        e = float((g_red[a:b] - mean[a:b]).abs().max())
+        if e > 1e-6:
+            bad.append((n, e, float(mean[a:b].abs().max()), float(g_red[a:b].abs().max()),
+                        float(gl[rank][a:b].abs().max())))
+    out = {"max_err": float((g_red - mean).abs().max()), "scale": float(mean.abs().max()),
+           "bad": bad[:12],
+           "launched": launched, "buckets": len(red.buckets),
+           "replicas_equal": all(torch.equal(ps[0], q) for q in ps)}
+    tr.close()
+    return out
+
+
+@pytest.mark.parametrize("side,overlap", [("1", True), ("0", True), ("1", False), ("0", False)])
+def test_dp_two_ranks_hip_engine_gloo(side, overlap):
+    res = run(_dp_rank, 2, (1.0, side, overlap), timeout=150)
+    for r in (0, 1):
+        o = res[r]
+        assert o["buckets"] > 1 and o["launched"] == (o["buckets"] if overlap else 0), o
+        assert o["max_err"] <= 1e-6 * max(o["scale"], 1.0), o
+        assert o["replicas_equal"], o
