@@ -18,7 +18,7 @@ def _batch(seed, n=2, tile=16):
     return torch.rand(n, 3, tile, tile, generator=g), torch.randint(0, 3, (n, tile, tile), generator=g)
 
 
-def _reducer_vs_big_batch(rank, world, codec, reduce):
+def _reducer_vs_big_batch(rank, world, codec, reduce, double_report=False):
     import torch.distributed as dist
     import torch.nn.functional as F
     from ddlpc.parallel import GradBucketReducer, broadcast_module, flatten_module, init_distributed
@@ -27,6 +27,9 @@ def _reducer_vs_big_batch(rank, world, codec, reduce):
     flat = flatten_module(m)
     broadcast_module(m)
     red = GradBucketReducer(flat, bucket_mb=0.01, reduce=reduce, grad_codec=codec)
+    if double_report:           # a second readiness source (as kernels writing .grad directly)
+        for q in flat.order:
+            q.register_post_accumulate_grad_hook(red.mark_ready)
     x, y = _batch(100 + rank)
     red.prepare(sync=True)
     F.cross_entropy(m(x), y).backward()
@@ -50,9 +53,10 @@ def _single_process_grads(world, reduce):
     return flat.grad_buf.clone()
 
 
-@pytest.mark.parametrize("reduce", ["mean", "sum", "reference"])
-def test_bucketed_allreduce_equals_big_batch(reduce):
-    res = run(_reducer_vs_big_batch, 2, ("none", reduce))
+@pytest.mark.parametrize("reduce,double", [("mean", False), ("sum", False), ("reference", False),
+                                           ("mean", True)])
+def test_bucketed_allreduce_equals_big_batch(reduce, double):
+    res = run(_reducer_vs_big_batch, 2, ("none", reduce, double))
     ref = _single_process_grads(2, "mean" if reduce == "mean" else "sum")
     for r in (0, 1):
         assert res[r]["all_same"]
