@@ -40,59 +40,81 @@ DDLPC_DEVICE int up_pixel(int m, int sub, int dims, int D, int H, int W) {
   return ((2 * q2 + kd) * (2 * H) + 2 * h + i) * (2 * W) + 2 * w + j;
 }
 
-template <int MODE>
-__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs p) {
+// NT GEMM, KC 32-wide k chunks per pipeline step: every thread has 2*KC A pieces and KC B
+// pieces (16 B each) in flight while the previous step's 8*KC MFMAs per wave run, so a
+// block exposes the memory latency once per 32*KC of K instead of once per 32 (these GEMMs
+// are skinny — K or N is 64..1024 against M up to millions of pixels — and memory bound).
+// The dgrad gather addresses are formed without division in the k loop: a step's chunk
+// sits inside one sub-position (Cout % 32 == 0), whose up-sampled pixel is the row's base
+// pixel plus a per-sub offset.
+template <int MODE, int KC>
+__global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
   constexpr int BM = 128, BN = 64;
-  __shared__ __attribute__((aligned(16))) char smem[(BM + BN) * 64 > BM * BN * 2 ? (BM + BN) * 64 : BM * BN * 2];
-  char* sA = smem;
-  char* sB = smem + BM * 64;
+  constexpr int A_BYTES = KC * BM * 64, B_BYTES = KC * BN * 64;
+  constexpr int SMEM = A_BYTES + B_BYTES > BM * BN * 2 ? A_BYTES + B_BYTES : BM * BN * 2;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  char* sA = smem;                       // [KC][BM rows][64 B]
+  char* sB = smem + A_BYTES;             // [KC][BN rows][64 B]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int nTilesN = (p.N + BN - 1) / BN;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int ntile = bid % nTilesN, mtile = bid / nTilesN;
-  const long long m0 = (long long)mtile * BM;
+  const int m0 = mtile * BM;
   const int n0 = ntile * BN;
-  const int S = p.dims == 2 ? 4 : 8;
   const int g = lane >> 4;
 
-  uint4 ra[2], rb[1];
-  auto load = [&](int kc) {
+  // per-thread rows: A rows (tid>>2) and (tid>>2)+64, B row tid>>2; 8-channel piece tid&3
+  const int cq = tid & 3;
+  int arow_off[2];                       // FWD: m*K ; DGRAD: up-pixel base * Cout (-1: none)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = tid + 256 * i;
-      const int row = e >> 2, cq = e & 3;
-      const int m = (int)m0 + row;
-      const int k8 = kc * BK + cq * 8;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (m < p.M && k8 < p.K) {
-        if (MODE == GEMM_CONVT_FWD) {
-          v = *reinterpret_cast<const uint4*>(p.A + (long long)m * p.K + k8);
-        } else {   // DGRAD: k = sub*Cout + co gathered from the high-res gradient
-          const int sub = k8 / p.Cout, co = k8 % p.Cout;
-          const int up = up_pixel(m, sub, p.dims, p.D, p.H, p.W);
-          v = *reinterpret_cast<const uint4*>(p.A + (long long)up * p.Cout + co);
-        }
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + (tid >> 2) + 64 * i;
+    if (m >= p.M) { arow_off[i] = -1; continue; }
+    if (MODE == GEMM_CONVT_FWD) arow_off[i] = m * p.K;
+    else arow_off[i] = up_pixel(m, 0, p.dims, p.D, p.H, p.W) * p.Cout;
+  }
+  const int n_b = n0 + (tid >> 2);
+  const int brow_off = n_b < p.N ? n_b * p.K : -1;
+  const int W2 = 2 * p.W, HW4 = 4 * p.H * p.W;
+  auto sub_off = [&](int sub) {          // up-pixel offset of sub-position sub (x Cout)
+    const int o = (p.dims == 2 ? (sub >> 1) * W2 + (sub & 1)
+                               : (sub >> 2) * HW4 + ((sub >> 1) & 1) * W2 + (sub & 1));
+    return o * p.Cout;
+  };
+
+  uint4 ra[KC][2], rb[KC];
+  auto load = [&](int it) {
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      const int kb = (it * KC + j) * BK;           // chunk base (uniform)
+      const int k8 = kb + cq * 8;
+      int aoff;                                    // element offset added to the row base
+      if (MODE == GEMM_CONVT_FWD) aoff = k8;
+      else {
+        const int sub = kb / p.Cout;               // uniform per chunk
+        aoff = sub_off(sub) + (kb - sub * p.Cout) + cq * 8;
       }
-      ra[i] = v;
-    }
-    {
-      const int e = tid;
-      const int row = e >> 2, cq = e & 3;
-      const int n = n0 + row;
-      const int k8 = kc * BK + cq * 8;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (arow_off[i] >= 0 && k8 < p.K)
+          v = *reinterpret_cast<const uint4*>(p.A + (long long)arow_off[i] + aoff);
+        ra[j][i] = v;
+      }
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (n < p.N && k8 < p.K) v = *reinterpret_cast<const uint4*>(p.B + (long long)n * p.K + k8);
-      rb[0] = v;
+      if (brow_off >= 0 && k8 < p.K) v = *reinterpret_cast<const uint4*>(p.B + (long long)brow_off + k8);
+      rb[j] = v;
     }
   };
   auto store = [&]() {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = tid + 256 * i;
-      *reinterpret_cast<uint4*>(sA + lds_off(e >> 2, e & 3)) = ra[i];
+    for (int j = 0; j < KC; ++j) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        *reinterpret_cast<uint4*>(sA + j * BM * 64 + lds_off((tid >> 2) + 64 * i, cq)) = ra[j][i];
+      *reinterpret_cast<uint4*>(sB + j * BN * 64 + lds_off(tid >> 2, cq)) = rb[j];
     }
-    *reinterpret_cast<uint4*>(sB + lds_off(tid >> 2, tid & 3)) = rb[0];
   };
 
   f32x4_t acc[4][2];
@@ -101,24 +123,27 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (p.K + BK - 1) / BK;
+  const int nit = (p.K + BK * KC - 1) / (BK * KC);
   load(0);
-  for (int kc = 0; kc < nk; ++kc) {
+  for (int it = 0; it < nit; ++it) {
     __syncthreads();
     store();
     __syncthreads();
-    if (kc + 1 < nk) load(kc + 1);
-    uint4 af[4], bfr[2];
+    if (it + 1 < nit) load(it + 1);
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-      af[mt] = *reinterpret_cast<const uint4*>(sA + lds_off(wm * 64 + mt * 16 + (lane & 15), g));
+    for (int j = 0; j < KC; ++j) {
+      uint4 af[4], bfr[2];
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-      bfr[nt] = *reinterpret_cast<const uint4*>(sB + lds_off(wn * 32 + nt * 16 + (lane & 15), g));
+      for (int mt = 0; mt < 4; ++mt)
+        af[mt] = *reinterpret_cast<const uint4*>(sA + j * BM * 64 + lds_off(wm * 64 + mt * 16 + (lane & 15), g));
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+      for (int nt = 0; nt < 2; ++nt)
+        bfr[nt] = *reinterpret_cast<const uint4*>(sB + j * BN * 64 + lds_off(wn * 32 + nt * 16 + (lane & 15), g));
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma16x16x32(af[mt], bfr[nt], acc[mt][nt]);
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma16x16x32(af[mt], bfr[nt], acc[mt][nt]);
+    }
   }
 
   __syncthreads();
@@ -138,7 +163,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs p) {
   bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
   for (int e = tid; e < BM * (BN / 8); e += 256) {
     const int row = e / (BN / 8), cg = e % (BN / 8);
-    const int m = (int)m0 + row;
+    const int m = m0 + row;
     const int n = n0 + cg * 8;
     if (m >= p.M || n >= p.N) continue;
     const uint4 v = *reinterpret_cast<const uint4*>(sO + row * BN + cg * 8);
@@ -150,7 +175,6 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs p) {
       *reinterpret_cast<uint4*>(C + (long long)m * p.N + n) = v;
     }
   }
-  (void)S;
 }
 
 // ---------------------------------------------------------------- TN (weight gradient)
@@ -266,10 +290,18 @@ void gemm_launch(GemmArgs& a, hipStream_t st) {
     return;
   }
   const long long grid = ((a.M + 127) / 128) * (long long)((a.N + 63) / 64);
-  if (a.mode == GEMM_CONVT_FWD)
-    hipLaunchKernelGGL((gemm_nt_kernel<GEMM_CONVT_FWD>), dim3((unsigned)grid), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((gemm_nt_kernel<GEMM_CONVT_DGRAD>), dim3((unsigned)grid), dim3(256), 0, st, a);
+  // measured (B=64 U-Net shapes): the gathered data-gradient A operand gains from wide
+  // steps; the forward (contiguous A, K = Cin) runs best at one chunk per step
+  const int kc = a.mode == GEMM_CONVT_FWD ? 1 : a.K <= 64 ? 2 : 4;
+#define DDLPC_GEMM_NT(MODE)                                                                  \
+  switch (kc) {                                                                             \
+    case 1: hipLaunchKernelGGL((gemm_nt_kernel<MODE, 1>), dim3((unsigned)grid), dim3(256), 0, st, a); break; \
+    case 2: hipLaunchKernelGGL((gemm_nt_kernel<MODE, 2>), dim3((unsigned)grid), dim3(256), 0, st, a); break; \
+    default: hipLaunchKernelGGL((gemm_nt_kernel<MODE, 4>), dim3((unsigned)grid), dim3(256), 0, st, a); break; \
+  }
+  if (a.mode == GEMM_CONVT_FWD) { DDLPC_GEMM_NT(GEMM_CONVT_FWD) }
+  else { DDLPC_GEMM_NT(GEMM_CONVT_DGRAD) }
+#undef DDLPC_GEMM_NT
 }
 
 }  // namespace ddlpc
