@@ -339,13 +339,16 @@ std::vector<at::Tensor> bn_relu_apply(const at::Tensor& y, const at::Tensor& sta
   return {a, p.defined() ? p : at::empty({0}, y.options())};
 }
 
+static bool gscale_is_none(const c10::optional<at::Tensor>& g) { return !(g.has_value() && g->defined()); }
+
 // dY, dgamma, dbeta from dA (+ unpool(dP)) through ReLU and BN
 std::vector<at::Tensor> bn_backward(const c10::optional<at::Tensor>& dA,
                                     const c10::optional<at::Tensor>& dP, const at::Tensor& y,
                                     const at::Tensor& stats4, const at::Tensor& gamma,
                                     const c10::optional<at::Tensor>& gscale,
                                     const c10::optional<at::Tensor>& dgamma_out,
-                                    const c10::optional<at::Tensor>& dbeta_out) {
+                                    const c10::optional<at::Tensor>& dbeta_out,
+                                    const c10::optional<at::Tensor>& partial_in) {
   CHECK_DEV(y); CHECK_CONTIG(y); CHECK_BF16(y);
   c10::DeviceGuard guard(y.device());
   const Geo g = geo_of(y);
@@ -361,30 +364,58 @@ std::vector<at::Tensor> bn_backward(const c10::optional<at::Tensor>& dA,
   const float* gs = fptr_opt(gscale);
   const long long items = (long long)g.N * (hasP ? (g.dims == 3 ? g.D / 2 : 1) * (g.H / 2) * (g.W / 2)
                                                  : (long long)g.D * g.H * g.W);
-  const int nb = bn_bwd_reduce_blocks(items);
   auto fopts = y.options().dtype(at::kFloat);
-  at::Tensor partial = at::empty({nb, 2, C}, fopts);
   const bf16_t* pA = hasA ? bptr(*dA) : nullptr;
   const bf16_t* pP = hasP ? bptr(*dP) : nullptr;
-  bn_bwd_reduce_launch(pA, pP, bptr(y), s + 2 * C, s + 3 * C, s, s + C, gs,
-                       partial.data_ptr<float>(), nb, g.dims, g.N, g.D, g.H, g.W, C, cur_stream());
+  // partial_in: (sum dyh, sum dyh*xhat) rows [R][2][C] already produced by the kernel that
+  // wrote dA (deferred-BN epilogues); otherwise one reduction pass over dA (+dP) and y
+  const bool pre = partial_in.has_value() && partial_in->defined() && partial_in->numel() > 0;
+  int nb;
+  at::Tensor partial;
+  if (pre) {
+    TORCH_CHECK(!hasP && gscale_is_none(gscale), "precomputed BN partials: no pool / grad scale");
+    CHECK_F32(*partial_in); CHECK_CONTIG(*partial_in);
+    TORCH_CHECK(partial_in->numel() % (2 * C) == 0, "partial rows must be [R][2][C]");
+    partial = *partial_in;
+    nb = (int)(partial.numel() / (2 * C));
+  } else {
+    nb = bn_bwd_reduce_blocks(items);
+    partial = at::empty({nb, 2, C}, fopts);
+    bn_bwd_reduce_launch(pA, pP, bptr(y), s + 2 * C, s + 3 * C, s, s + C, gs,
+                         partial.data_ptr<float>(), nb, g.dims, g.N, g.D, g.H, g.W, C, cur_stream());
+  }
   const bool into = dgamma_out.has_value() && dgamma_out->defined();
   at::Tensor dgamma = into ? *dgamma_out : at::empty({C}, fopts);
   at::Tensor dbeta = into ? *dbeta_out : at::empty({C}, fopts);
   at::Tensor coefs = at::empty({3, C}, fopts);
   const double count = (double)g.N * g.D * g.H * g.W;
-  bn_grad_finalize_rows_launch(partial.data_ptr<float>(), nb, C, count, gamma.data_ptr<float>(),
-                               s + C, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
-                               coefs.data_ptr<float>(), into, cur_stream());
+  if (nb <= 2048) {
+    bn_grad_finalize_rows_launch(partial.data_ptr<float>(), nb, C, count, gamma.data_ptr<float>(),
+                                 s + C, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+                                 coefs.data_ptr<float>(), into, cur_stream());
+  } else {   // many rows (per-tile epilogue partials): coalesced two-pass fp64 reduction
+    at::Tensor sums = reduce_rows(partial, nb, 2 * C);
+    bn_grad_finalize_launch(sums.data_ptr<double>(), C, count, gamma.data_ptr<float>(), s + C,
+                            dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+                            coefs.data_ptr<float>(), into, cur_stream());
+  }
   at::Tensor dY = at::empty_like(y);
   bn_bwd_apply_launch(pA, pP, bptr(y), s + 2 * C, s + 3 * C, s, s + C, coefs.data_ptr<float>(), gs,
                       bptr_mut(dY), g.dims, g.N, g.D, g.H, g.W, C, cur_stream());
   return {dY, dgamma, dbeta};
 }
 
+static const float* bn4_ptr(const c10::optional<at::Tensor>& bn4, int C) {
+  if (!(bn4.has_value() && bn4->defined())) return nullptr;
+  CHECK_F32(*bn4); CHECK_CONTIG(*bn4);
+  TORCH_CHECK(bn4->numel() == 4 * C, "bn4 must be [4][C] (mean, invstd, scale, shift)");
+  TORCH_CHECK(C <= 512, "deferred BatchNorm supports C <= 512");
+  return bn4->data_ptr<float>();
+}
+
 // ------------------------------------------------------------------------ transposed conv
 at::Tensor convt_fwd(const at::Tensor& x, const at::Tensor& wt, const c10::optional<at::Tensor>& bias,
-                     int64_t cout) {
+                     int64_t cout, const c10::optional<at::Tensor>& bn4) {
   CHECK_DEV(x); CHECK_CONTIG(x); CHECK_BF16(x); CHECK_BF16(wt);
   c10::DeviceGuard guard(x.device());
   const Geo g = geo_of(x);
@@ -401,6 +432,7 @@ at::Tensor convt_fwd(const at::Tensor& x, const at::Tensor& wt, const c10::optio
   a.bias = fptr_opt(bias);
   a.dims = g.dims; a.Nimg = g.N; a.D = g.D; a.H = g.H; a.W = g.W;
   a.Cin = g.C; a.Cout = (int)cout;
+  a.bn4 = bn4_ptr(bn4, g.C);
   TORCH_CHECK((int64_t)a.M * std::max(a.K, a.N) < (int64_t)INT32_MAX, "convT: tensor too large for 32-bit offsets");
   at::Tensor out = at::empty(shape_with_c(g, (int)cout, 2), x.options());
   a.C = out.data_ptr();
@@ -408,7 +440,9 @@ at::Tensor convt_fwd(const at::Tensor& x, const at::Tensor& wt, const c10::optio
   return out;
 }
 
-at::Tensor convt_dgrad(const at::Tensor& dout, const at::Tensor& wd, int64_t cin) {
+std::vector<at::Tensor> convt_dgrad(const at::Tensor& dout, const at::Tensor& wd, int64_t cin,
+                                    const c10::optional<at::Tensor>& bny,
+                                    const c10::optional<at::Tensor>& bn4) {
   CHECK_DEV(dout); CHECK_CONTIG(dout); CHECK_BF16(dout); CHECK_BF16(wd);
   c10::DeviceGuard guard(dout.device());
   const Geo go = geo_of(dout);
@@ -428,14 +462,26 @@ at::Tensor convt_dgrad(const at::Tensor& dout, const at::Tensor& wd, int64_t cin
   TORCH_CHECK((int64_t)a.M * std::max(a.K, a.N) < (int64_t)INT32_MAX, "convT: tensor too large for 32-bit offsets");
   at::Tensor dx = at::empty(shape_with_c(g, (int)cin), dout.options());
   a.C = dx.data_ptr();
+  at::Tensor bnpart = at::empty({0}, dout.options().dtype(at::kFloat));
+  a.bn4 = bn4_ptr(bn4, (int)cin);
+  if (a.bn4 != nullptr) {
+    TORCH_CHECK(bny.has_value() && bny->defined() && bny->is_contiguous() &&
+                bny->numel() == dx.numel() && bny->scalar_type() == at::kBFloat16,
+                "convt_dgrad: bny must be the deferred pre-BN input (shape of dx, bf16)");
+    a.bny = bptr(*bny);
+    const long long grid = ((a.M + 127) / 128) * (long long)((a.N + 63) / 64);
+    bnpart = at::empty({(int64_t)grid, 2, (int64_t)cin}, dout.options().dtype(at::kFloat));
+    a.bnpart = bnpart.data_ptr<float>();
+  }
   gemm_launch(a, cur_stream());
-  return dx;
+  return {dx, bnpart};
 }
 
 std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
                                     const c10::optional<at::Tensor>& dw_out,
                                     const c10::optional<at::Tensor>& db_out,
-                                    const c10::optional<at::Tensor>& colsum_rows) {
+                                    const c10::optional<at::Tensor>& colsum_rows,
+                                    const c10::optional<at::Tensor>& bn4) {
   CHECK_DEV(x); CHECK_CONTIG(x); CHECK_CONTIG(dout);
   c10::DeviceGuard guard(x.device());
   const Geo g = geo_of(x);
@@ -450,6 +496,7 @@ std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
   a.B = bptr(dout);
   a.dims = g.dims; a.Nimg = g.N; a.D = g.D; a.H = g.H; a.W = g.W;
   a.Cin = g.C; a.Cout = go.C;
+  a.bn4 = bn4_ptr(bn4, g.C);
   const int base = ((a.M + 63) / 64) * ((a.N + 63) / 64);
   int splits = std::max(1, (4 * num_cus() + base - 1) / base);
   splits = std::min(splits, std::max(1, a.K / 256));
@@ -497,7 +544,8 @@ std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
 
 // ------------------------------------------------------------------------ head + CE
 at::Tensor head_ce_fwd(const at::Tensor& a, const at::Tensor& Wh, const at::Tensor& bh,
-                       const at::Tensor& labels, int64_t ignore_index) {
+                       const at::Tensor& labels, int64_t ignore_index,
+                       const c10::optional<at::Tensor>& bn4) {
   CHECK_DEV(a); CHECK_CONTIG(a); CHECK_BF16(a); CHECK_F32(Wh); CHECK_CONTIG(Wh);
   TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous(), "labels must be int64");
   c10::DeviceGuard guard(a.device());
@@ -510,7 +558,7 @@ at::Tensor head_ce_fwd(const at::Tensor& a, const at::Tensor& Wh, const at::Tens
   at::Tensor partial = at::empty({nb, 3}, fopts);
   at::Tensor out3 = at::empty({3}, fopts);
   head_ce_fwd_launch(bptr(a), Wh.data_ptr<float>(), bh.data_ptr<float>(), labels.data_ptr<int64_t>(),
-                     partial.data_ptr<float>(), out3.data_ptr<float>(), nullptr, nb, P, C, K,
+                     partial.data_ptr<float>(), out3.data_ptr<float>(), bn4_ptr(bn4, C), nb, P, C, K,
                      (int)ignore_index, cur_stream());
   return out3;
 }
@@ -519,18 +567,22 @@ std::vector<at::Tensor> head_ce_bwd(const at::Tensor& a, const at::Tensor& Wh, c
                                     const at::Tensor& labels, const at::Tensor& out3,
                                     const c10::optional<at::Tensor>& gscale, int64_t ignore_index,
                                     const c10::optional<at::Tensor>& dw_out,
-                                    const c10::optional<at::Tensor>& db_out) {
+                                    const c10::optional<at::Tensor>& db_out,
+                                    const c10::optional<at::Tensor>& bn4) {
   CHECK_DEV(a); CHECK_CONTIG(a);
   c10::DeviceGuard guard(a.device());
   const int C = (int)a.size(-1), K = (int)Wh.size(0);
+  const float* pbn = bn4_ptr(bn4, C);
   const long long P = a.numel() / C;
   const int nb = (int)std::max<long long>(1, std::min<long long>((P + 255) / 256, 1024));
   auto fopts = a.options().dtype(at::kFloat);
   at::Tensor dA = at::empty_like(a);
   at::Tensor part = at::empty({nb, K * C + K}, fopts);
+  at::Tensor bnpart = at::empty({0}, fopts);         // (no fused BN-backward partials)
   head_ce_bwd_launch(bptr(a), Wh.data_ptr<float>(), bh.data_ptr<float>(), labels.data_ptr<int64_t>(),
                      fptr_opt(gscale), out3.data_ptr<float>(), 0, bptr_mut(dA),
-                     part.data_ptr<float>(), nb, P, C, K, (int)ignore_index, cur_stream());
+                     part.data_ptr<float>(), nb, P, C, K, (int)ignore_index, pbn, nullptr,
+                     cur_stream());
   const bool into = dw_out.has_value() && dw_out->defined();
   at::Tensor sums = reduce_rows(part, nb, K * C + K);   // rows are [dW (K*C) | db (K)]
   if (into) {
@@ -540,17 +592,18 @@ std::vector<at::Tensor> head_ce_bwd(const at::Tensor& a, const at::Tensor& Wh, c
     scatter_sums_launch(sums.data_ptr<double>() + K * C, K, db_out->data_ptr<float>(), 2, 0, 0, 0,
                         1.f, true, cur_stream());
     at::Tensor none = at::empty({0}, fopts);
-    return {dA, none, none};
+    return {dA, none, none, bnpart};
   }
   at::Tensor red = at::empty({K * C + K}, fopts);
   scatter_sums_launch(sums.data_ptr<double>(), K * C + K, red.data_ptr<float>(), 2, 0, 0, 0, 1.f,
                       false, cur_stream());
   at::Tensor dW = red.narrow(0, 0, K * C).view({K, C});
   at::Tensor db = red.narrow(0, K * C, K);
-  return {dA, dW, db};
+  return {dA, dW, db, bnpart};
 }
 
-at::Tensor head_logits(const at::Tensor& a, const at::Tensor& Wh, const at::Tensor& bh) {
+at::Tensor head_logits(const at::Tensor& a, const at::Tensor& Wh, const at::Tensor& bh,
+                       const c10::optional<at::Tensor>& bn4) {
   CHECK_DEV(a); CHECK_CONTIG(a);
   c10::DeviceGuard guard(a.device());
   const Geo g = geo_of(a);
@@ -561,7 +614,7 @@ at::Tensor head_logits(const at::Tensor& a, const at::Tensor& Wh, const at::Tens
                                         : std::vector<int64_t>{g.N, K, g.D, g.H, g.W};
   at::Tensor out = at::empty(os, a.options().dtype(at::kFloat));
   head_logits_launch(bptr(a), Wh.data_ptr<float>(), bh.data_ptr<float>(), out.data_ptr<float>(),
-                     (long long)g.N * HW, HW, C, K, cur_stream());
+                     (long long)g.N * HW, HW, C, K, bn4_ptr(bn4, C), cur_stream());
   return out;
 }
 
@@ -693,15 +746,15 @@ TORCH_LIBRARY(ddlpc, m) {
         "Tensor(b!) running_var, float momentum, float eps, bool update_running, Tensor(c!)? nbt) -> Tensor");
   m.def("bn_relu_apply(Tensor y, Tensor stats4, bool pool) -> Tensor[]");
   m.def("bn_backward(Tensor? dA, Tensor? dP, Tensor y, Tensor stats4, Tensor gamma, Tensor? gscale, "
-        "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None) -> Tensor[]");
-  m.def("convt_fwd(Tensor x, Tensor wt, Tensor? bias, int cout) -> Tensor");
-  m.def("convt_dgrad(Tensor dout, Tensor wd, int cin) -> Tensor");
+        "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None, Tensor? partial=None) -> Tensor[]");
+  m.def("convt_fwd(Tensor x, Tensor wt, Tensor? bias, int cout, Tensor? bn4=None) -> Tensor");
+  m.def("convt_dgrad(Tensor dout, Tensor wd, int cin, Tensor? bny=None, Tensor? bn4=None) -> Tensor[]");
   m.def("convt_wgrad(Tensor x, Tensor dout, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, "
-        "Tensor? colsum_rows=None) -> Tensor[]");
-  m.def("head_ce_fwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, int ignore_index) -> Tensor");
+        "Tensor? colsum_rows=None, Tensor? bn4=None) -> Tensor[]");
+  m.def("head_ce_fwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, int ignore_index, Tensor? bn4=None) -> Tensor");
   m.def("head_ce_bwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, Tensor out3, Tensor? gscale, "
-        "int ignore_index, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) -> Tensor[]");
-  m.def("head_logits(Tensor a, Tensor Wh, Tensor bh) -> Tensor");
+        "int ignore_index, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, Tensor? bn4=None) -> Tensor[]");
+  m.def("head_logits(Tensor a, Tensor Wh, Tensor bh, Tensor? bn4=None) -> Tensor");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float eps, "
         "float wd, float step_size, float inv_sqrt_bc2) -> ()");
   m.def("adam_step_dev(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!) scal, "

@@ -51,11 +51,27 @@ template <int MODE, int KC>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
   constexpr int BM = 128, BN = 64;
   constexpr int A_BYTES = KC * BM * 64, B_BYTES = KC * BN * 64;
-  constexpr int SMEM = A_BYTES + B_BYTES > BM * BN * 2 ? A_BYTES + B_BYTES : BM * BN * 2;
+  // deferred-BN constants live in otherwise idle LDS: FWD (scale|shift, 2 x 512 floats)
+  // behind the operand tiles, used in the k loop; DGRAD (scale|shift|mean|invstd) behind the
+  // 16 KB output staging tile, used in the epilogue only
+  constexpr int BN_OFF = MODE == GEMM_CONVT_FWD ? A_BYTES + B_BYTES : BM * BN * 2;
+  constexpr int BN_BYTES = MODE == GEMM_CONVT_FWD ? 2 * 512 * 4 : 4 * 512 * 4;
+  constexpr int SMEM0 = A_BYTES + B_BYTES > BM * BN * 2 ? A_BYTES + B_BYTES : BM * BN * 2;
+  constexpr int SMEM = SMEM0 > BN_OFF + BN_BYTES ? SMEM0 : BN_OFF + BN_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  float* s_bn = reinterpret_cast<float*>(smem + BN_OFF);
   char* sA = smem;                       // [KC][BM rows][64 B]
   char* sB = smem + A_BYTES;             // [KC][BN rows][64 B]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Cbn = MODE == GEMM_CONVT_FWD ? p.K : p.N;   // channels of the deferred tensor
+  const bool bn = p.bn4 != nullptr;
+  if (bn && MODE == GEMM_CONVT_FWD) {
+    for (int i = tid; i < Cbn; i += 256) {
+      s_bn[i] = p.bn4[2 * Cbn + i];              // scale
+      s_bn[512 + i] = p.bn4[3 * Cbn + i];        // shift
+    }
+    __syncthreads();
+  }
   const int wm = wave >> 1, wn = wave & 1;
   const int nTilesN = (p.N + BN - 1) / BN;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -84,7 +100,9 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
   };
 
   uint4 ra[KC][2], rb[KC];
+  int kcur = 0;                          // k base of the step held in ra (FWD prologue)
   auto load = [&](int it) {
+    kcur = it * KC * BK;
 #pragma unroll
     for (int j = 0; j < KC; ++j) {
       const int kb = (it * KC + j) * BK;           // chunk base (uniform)
@@ -111,8 +129,18 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < KC; ++j) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        *reinterpret_cast<uint4*>(sA + j * BM * 64 + lds_off((tid >> 2) + 64 * i, cq)) = ra[j][i];
+      for (int i = 0; i < 2; ++i) {
+        uint4 v = ra[j][i];
+        const int k8 = kcur + j * BK + cq * 8;
+        if (MODE == GEMM_CONVT_FWD && bn && arow_off[i] >= 0 && k8 < p.K) {
+          float f[8];                    // deferred BN + ReLU of the input activation
+          unpack8(v, f);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) f[q] = fmaxf(fmaf(f[q], s_bn[k8 + q], s_bn[512 + k8 + q]), 0.f);
+          v = pack8(f);
+        }
+        *reinterpret_cast<uint4*>(sA + j * BM * 64 + lds_off((tid >> 2) + 64 * i, cq)) = v;
+      }
       *reinterpret_cast<uint4*>(sB + j * BN * 64 + lds_off(tid >> 2, cq)) = rb[j];
     }
   };
@@ -159,8 +187,19 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
       for (int i = 0; i < 4; ++i)
         sO[(wm * 64 + mt * 16 + 4 * (lane >> 4) + i) * BN + col] = f2bf(acc[mt][nt][i] + b);
   }
+  const bool bnst = MODE == GEMM_CONVT_DGRAD && p.bnpart != nullptr;
+  if (bnst)
+    for (int i = tid; i < Cbn; i += 256) {
+      s_bn[i] = p.bn4[2 * Cbn + i];              // scale
+      s_bn[512 + i] = p.bn4[3 * Cbn + i];        // shift
+      s_bn[1024 + i] = p.bn4[i];                 // mean
+      s_bn[1536 + i] = p.bn4[Cbn + i];           // invstd
+    }
   __syncthreads();
   bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+  float s1[8], s2[8];                    // BN-backward partials of this thread's 8 channels
+#pragma unroll
+  for (int q = 0; q < 8; ++q) { s1[q] = 0.f; s2[q] = 0.f; }
   for (int e = tid; e < BM * (BN / 8); e += 256) {
     const int row = e / (BN / 8), cg = e % (BN / 8);
     const int m = m0 + row;
@@ -173,6 +212,37 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
       *reinterpret_cast<uint4*>(C + (long long)up * p.Cout + co) = v;
     } else {
       *reinterpret_cast<uint4*>(C + (long long)m * p.N + n) = v;
+      if (bnst) {                        // dyh = dx [y*scale+shift > 0], xhat = (y-mean)*invstd
+        float dx[8], yv[8];
+        unpack8(v, dx);
+        unpack8(*reinterpret_cast<const uint4*>(p.bny + (long long)m * p.N + n), yv);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int c = n + q;
+          const float dyh = fmaf(yv[q], s_bn[c], s_bn[512 + c]) > 0.f ? dx[q] : 0.f;
+          s1[q] += dyh;
+          s2[q] = fmaf(dyh, (yv[q] - s_bn[1024 + c]) * s_bn[1536 + c], s2[q]);
+        }
+      }
+    }
+  }
+  if (bnst) {
+    // threads with equal tid % (BN/8) hold the same channels: fixed-order LDS reduction,
+    // then one full-width row per workgroup (zeros outside this channel tile)
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);     // [2][8][256]
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { red[q * 256 + tid] = s1[q]; red[2048 + q * 256 + tid] = s2[q]; }
+    __syncthreads();
+    float* row = p.bnpart + (long long)blockIdx.x * 2 * p.N;
+    for (int c = tid; c < 2 * p.N; c += 256) {
+      const int half = c / p.N, ch = c - half * p.N;
+      float t = 0.f;
+      if (ch >= n0 && ch < n0 + BN) {
+        const int cg = (ch - n0) >> 3, q = (ch - n0) & 7;
+        for (int k = cg; k < 256; k += BN / 8) t += red[half * 2048 + q * 256 + k];
+      }
+      row[c] = t;
     }
   }
 }
@@ -182,9 +252,14 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
 __global__ __launch_bounds__(256, 2) void gemm_tn_wgrad_kernel(GemmArgs p) {
   constexpr int BM = 64, BN = 64, KT = 64;
   __shared__ __attribute__((aligned(16))) char smem[2 * KT * 128];
+  __shared__ float s_bn[2 * 512];
   char* sA = smem;               // [KT px][BM ci]   128-B rows
   char* sB = smem + KT * 128;    // [KT px][BN n]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (p.bn4 != nullptr) {
+    for (int i = tid; i < p.M; i += 256) { s_bn[i] = p.bn4[2 * p.M + i]; s_bn[512 + i] = p.bn4[3 * p.M + i]; }
+    __syncthreads();
+  }
   const int wm = wave >> 1, wn = wave & 1;
   const int nTilesN = (p.N + BN - 1) / BN, nTilesM = (p.M + BM - 1) / BM;
   // tiles of one pixel range innermost in XCD-contiguous order (shared operands hit L2)
@@ -240,6 +315,20 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_wgrad_kernel(GemmArgs p) {
   if (k_begin < k_end) load(k_begin);
   for (long long k0 = k_begin; k0 < k_end; k0 += KT) {
     __syncthreads();
+    if (p.bn4 != nullptr) {               // deferred BN + ReLU of x (valid pieces only)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int e = tid + 256 * i;
+        const int row = e >> 3, ci = m0 + (e & 7) * 8;
+        if (k0 + row < k_end && ci < p.M) {
+          float f[8];
+          unpack8(ra[i], f);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) f[q] = fmaxf(fmaf(f[q], s_bn[ci + q], s_bn[512 + ci + q]), 0.f);
+          ra[i] = pack8(f);
+        }
+      }
+    }
     store();
     __syncthreads();
     if (k0 + KT < k_end) load(k0 + KT);

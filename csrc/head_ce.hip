@@ -18,14 +18,33 @@ namespace {
 
 constexpr int MAXC = 64, MAXK = 16;
 
-template <int C, int K>
-DDLPC_DEVICE void logits_of(const bf16_t* ap, const float* sW, const float* sb, float (&z)[K]) {
+// The head's input activation, 8 channels at c8.  With a deferred BatchNorm (sBN != null:
+// scale [C] | shift [C] in LDS) the tensor holds the block's PRE-BN conv output y and the
+// activation relu(y*scale + shift) is formed here, rounded to bf16 exactly as a
+// materialised activation would be — the last decoder block never writes it to HBM.
+template <int C, bool DEFER>
+DDLPC_DEVICE void act8(const bf16_t* ap, int c8, const float* sBN, float (&f)[8]) {
+  const uint4 v = *reinterpret_cast<const uint4*>(ap + c8);
+  unpack8(v, f);
+  if (DEFER) {
+    // volatile LDS-broadcast reads: the compiler would otherwise hoist all 2*C constants out
+    // of the pixel loop into live registers and halve the kernel's occupancy
+    const volatile float* vb = sBN;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], vb[c8 + j], vb[C + c8 + j]), 0.f);
+    unpack8(pack8(f), f);
+  }
+}
+
+template <int C, int K, bool DEFER>
+DDLPC_DEVICE void logits_of(const bf16_t* ap, const float* sW, const float* sb, const float* sBN,
+                            float (&z)[K]) {
 #pragma unroll
   for (int k = 0; k < K; ++k) z[k] = sb[k];
 #pragma unroll
   for (int c8 = 0; c8 < C; c8 += 8) {
     float f[8];
-    unpack8(*reinterpret_cast<const uint4*>(ap + c8), f);
+    act8<C, DEFER>(ap, c8, sBN, f);
 #pragma unroll
     for (int k = 0; k < K; ++k)
 #pragma unroll
@@ -33,20 +52,32 @@ DDLPC_DEVICE void logits_of(const bf16_t* ap, const float* sW, const float* sb, 
   }
 }
 
-template <int C, int K>
+// bn4 = [mean | invstd | scale | shift] (C each) -> LDS: scale, shift (+ mean, invstd)
+template <int C>
+DDLPC_DEVICE const float* load_bn(const float* bn4, float* sBN, bool need_stats) {
+  if (bn4 == nullptr) return nullptr;
+  for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) sBN[i] = bn4[2 * C + i];
+  if (need_stats)
+    for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) sBN[2 * C + i] = bn4[i];
+  return sBN;
+}
+
+template <int C, int K, bool DEFER>
 __global__ __launch_bounds__(256) void head_ce_fwd_kernel(
     const bf16_t* __restrict__ a, const float* __restrict__ Wh, const float* __restrict__ bh,
     const int64_t* __restrict__ labels, float* __restrict__ partial, long long P,
-    int ignore_index) {
+    int ignore_index, const float* __restrict__ bn4) {
+  __shared__ __attribute__((aligned(16))) float sBNm[4 * C];
   __shared__ float sW[K * C], sb[K];
   for (int i = threadIdx.x; i < K * C; i += blockDim.x) sW[i] = Wh[i];
   if (threadIdx.x < K) sb[threadIdx.x] = bh[threadIdx.x];
+  const float* sBN = DEFER ? load_bn<C>(bn4, sBNm, false) : nullptr;
   __syncthreads();
   float loss = 0.f, correct = 0.f, count = 0.f;
   for (long long px = blockIdx.x * (long long)blockDim.x + threadIdx.x; px < P;
        px += (long long)gridDim.x * blockDim.x) {
     float z[K];
-    logits_of<C, K>(a + px * C, sW, sb, z);
+    logits_of<C, K, DEFER>(a + px * C, sW, sb, sBN, z);
     const int64_t y = labels[px];
     float m = z[0];
     int am = 0;
@@ -101,17 +132,22 @@ __global__ void ce_finalize_kernel(const float* __restrict__ partial, int nb, fl
   }
 }
 
-template <int C, int K>
+// bn4 != null: deferred BatchNorm of the last decoder block (see act8).  (Its backward
+// partial sums are NOT reduced here: 2*C per-thread accumulators cost the kernel its
+// occupancy — measured slower than the separate reduction pass.)
+template <int C, int K, bool DEFER>
 __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
     const bf16_t* __restrict__ a, const float* __restrict__ Wh, const float* __restrict__ bh,
     const int64_t* __restrict__ labels, const float* __restrict__ gscale,
     const float* __restrict__ stats3, bf16_t* __restrict__ dA, float* __restrict__ dWp,
-    long long P, int ignore_index) {
+    long long P, int ignore_index, const float* __restrict__ bn4) {
+  __shared__ __attribute__((aligned(16))) float sBNm[4 * C];
   __shared__ float sW[K * C], sb[K];
   __shared__ __attribute__((aligned(16))) bf16_t sA[256 * C];
   __shared__ float sD[256 * K];
   for (int i = threadIdx.x; i < K * C; i += blockDim.x) sW[i] = Wh[i];
   if (threadIdx.x < K) sb[threadIdx.x] = bh[threadIdx.x];
+  const float* sBN = DEFER ? load_bn<C>(bn4, sBNm, false) : nullptr;
   __syncthreads();
   const float cnt = stats3[2];
   const float gs = (gscale != nullptr ? gscale[0] : 1.0f) / (cnt > 0.f ? cnt : 1.f);
@@ -125,7 +161,7 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
     for (int k = 0; k < K; ++k) d[k] = 0.f;
     if (px < P) {
       float z[K];
-      logits_of<C, K>(a + px * C, sW, sb, z);
+      logits_of<C, K, DEFER>(a + px * C, sW, sb, sBN, z);
       const int64_t y = labels[px];
       float m = z[0];
 #pragma unroll
@@ -152,8 +188,11 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
         *reinterpret_cast<uint4*>(dA + px * C + c8) = pack8(o);
       }
 #pragma unroll
-      for (int c8 = 0; c8 < C; c8 += 8)
-        *reinterpret_cast<uint4*>(sA + t * C + c8) = *reinterpret_cast<const uint4*>(a + px * C + c8);
+      for (int c8 = 0; c8 < C; c8 += 8) {
+        float f[8];
+        act8<C, DEFER>(a + px * C, c8, sBN, f);
+        *reinterpret_cast<uint4*>(sA + t * C + c8) = pack8(f);
+      }
     } else {
 #pragma unroll
       for (int c8 = 0; c8 < C; c8 += 8) *reinterpret_cast<uint4*>(sA + t * C + c8) = make_uint4(0, 0, 0, 0);
@@ -177,18 +216,20 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
   if (t < K * C + K) dWp[(long long)blockIdx.x * (K * C + K) + t] = accw;
 }
 
-template <int C, int K>
+template <int C, int K, bool DEFER>
 __global__ void head_logits_kernel(const bf16_t* __restrict__ a, const float* __restrict__ Wh,
                                    const float* __restrict__ bh, float* __restrict__ out,
-                                   long long P, long long HW) {
+                                   long long P, long long HW, const float* __restrict__ bn4) {
+  __shared__ __attribute__((aligned(16))) float sBNm[4 * C];
   __shared__ float sW[K * C], sb[K];
   for (int i = threadIdx.x; i < K * C; i += blockDim.x) sW[i] = Wh[i];
   if (threadIdx.x < K) sb[threadIdx.x] = bh[threadIdx.x];
+  const float* sBN = DEFER ? load_bn<C>(bn4, sBNm, false) : nullptr;
   __syncthreads();
   for (long long px = blockIdx.x * (long long)blockDim.x + threadIdx.x; px < P;
        px += (long long)gridDim.x * blockDim.x) {
     float z[K];
-    logits_of<C, K>(a + px * C, sW, sb, z);
+    logits_of<C, K, DEFER>(a + px * C, sW, sb, sBN, z);
     const long long n = px / HW, s = px % HW;
 #pragma unroll
     for (int k = 0; k < K; ++k) out[(n * K + k) * HW + s] = z[k];
@@ -216,27 +257,41 @@ bool head_supported(int C, int K) {
 }
 
 void head_ce_fwd_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
-                        float* partial, float* out3, float* /*unused*/, int nblocks, long long P,
+                        float* partial, float* out3, const float* bn4, int nblocks, long long P,
                         int C, int K, int ignore_index, hipStream_t st) {
-  HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_fwd_kernel<CC, KK>), dim3(nblocks), dim3(256), 0,
-                                       st, a, Wh, bh, labels, partial, P, ignore_index));
+  if (bn4 != nullptr)
+    HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_fwd_kernel<CC, KK, true>), dim3(nblocks), dim3(256), 0,
+                                         st, a, Wh, bh, labels, partial, P, ignore_index, bn4));
+  else
+    HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_fwd_kernel<CC, KK, false>), dim3(nblocks), dim3(256), 0,
+                                         st, a, Wh, bh, labels, partial, P, ignore_index, bn4));
   hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(256), 0, st, partial, nblocks, out3);
 }
 
 void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
                         const float* gscale, const float* stats3, int /*unused*/, bf16_t* dA,
                         float* dW_partial, int nblocks, long long P, int C, int K,
-                        int ignore_index, hipStream_t st) {
-  HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK>), dim3(nblocks), dim3(256), 0,
-                                       st, a, Wh, bh, labels, gscale, stats3, dA, dW_partial, P,
-                                       ignore_index));
+                        int ignore_index, const float* bn4, float* /*bnpart: unused*/,
+                        hipStream_t st) {
+  if (bn4 != nullptr)
+    HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK, true>), dim3(nblocks), dim3(256), 0,
+                                         st, a, Wh, bh, labels, gscale, stats3, dA, dW_partial, P,
+                                         ignore_index, bn4));
+  else
+    HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK, false>), dim3(nblocks), dim3(256), 0,
+                                         st, a, Wh, bh, labels, gscale, stats3, dA, dW_partial, P,
+                                         ignore_index, bn4));
 }
 
 void head_logits_launch(const bf16_t* a, const float* Wh, const float* bh, float* logits,
-                        long long P, long long HW, int C, int K, hipStream_t st) {
+                        long long P, long long HW, int C, int K, const float* bn4, hipStream_t st) {
   const int grid = (int)std::min<long long>((P + 255) / 256, 4096);
-  HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_logits_kernel<CC, KK>), dim3(grid), dim3(256), 0, st,
-                                       a, Wh, bh, logits, P, HW));
+  if (bn4 != nullptr)
+    HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_logits_kernel<CC, KK, true>), dim3(grid), dim3(256), 0, st,
+                                         a, Wh, bh, logits, P, HW, bn4));
+  else
+    HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_logits_kernel<CC, KK, false>), dim3(grid), dim3(256), 0, st,
+                                         a, Wh, bh, logits, P, HW, bn4));
 }
 
 }  // namespace ddlpc

@@ -84,8 +84,15 @@ struct GemmArgs {
   // geometry for the transposed-conv gathers / scatters
   int dims, Nimg, D, H, W;        // input (low-res) geometry
   int Cin, Cout;
-  const float* pscale;            // optional BN+ReLU prologue on A (forward of convT)
+  const float* pscale;            // unused (kept for layout)
   const float* pshift;
+  // deferred BatchNorm of the convT INPUT tensor (bn4 = [mean|invstd|scale|shift] x Cin):
+  //   FWD / WGRAD: x holds the pre-BN conv output; relu(x*scale+shift) is formed on load
+  //   DGRAD: bny = that pre-BN tensor; the epilogue emits BN-backward partial rows
+  //          bnpart[block][2][Cin] of the stored dx (zeros outside the block's channel tile)
+  const float* bn4;
+  const bf16_t* bny;
+  float* bnpart;
 };
 enum GemmMode {
   GEMM_CONVT_FWD = 0,   // A = x[px][Cin], B = Wt[(sub, co)][Cin] -> scatter to 2x up, + bias
@@ -111,15 +118,18 @@ int bn_bwd_reduce_blocks(long long pixels_or_quads);
 
 // ---------------------------------------------------------------- head + cross-entropy
 bool head_supported(int C, int K);
+// bn4 (optional, [mean | invstd | scale | shift] x C): the input holds a PRE-BatchNorm
+// conv output whose BN + ReLU is applied on load (deferred activation)
 void head_ce_fwd_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
-                        float* partial, float* out3, float* unused, int nblocks, long long P,
+                        float* partial, float* out3, const float* bn4, int nblocks, long long P,
                         int C, int K, int ignore_index, hipStream_t st);
+// bnpart (with bn4): per-workgroup [2][C] BatchNorm-backward partial sums of the stored dA
 void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
                         const float* gscale, const float* stats3, int unused, bf16_t* dA,
                         float* dW_partial, int nblocks, long long P, int C, int K,
-                        int ignore_index, hipStream_t st);
+                        int ignore_index, const float* bn4, float* bnpart, hipStream_t st);
 void head_logits_launch(const bf16_t* a, const float* Wh, const float* bh, float* logits_nchw,
-                        long long P, long long HW, int C, int K, hipStream_t st);
+                        long long P, long long HW, int C, int K, const float* bn4, hipStream_t st);
 
 
 // ---------------------------------------------------------------- optimizer / packing

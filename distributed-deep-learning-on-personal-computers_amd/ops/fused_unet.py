@@ -114,7 +114,7 @@ class _BNState:
 
 class _DoubleConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x1, x2, w1, b1, g1, be1, w2, b2, g2, be2, blk, pool: bool):
+    def forward(ctx, x1, x2, w1, b1, g1, be1, w2, b2, g2, be2, blk, pool: bool, defer: bool):
         F = _ops()
         p1, p2 = blk.pack1, blk.pack2
         training = blk.bn1.bn.training
@@ -124,19 +124,31 @@ class _DoubleConvFn(torch.autograd.Function):
         s1 = blk.bn1.finalize(st1, count) if training else blk.bn1.eval_stats()
         y2, _, st2 = F.conv3_fwd(y1, None, p2.fwd, b2, s1[2], s1[3], p2.cout, 0, training)
         s2 = blk.bn2.finalize(st2, count) if training else blk.bn2.eval_stats()
-        a2, pooled = F.bn_relu_apply(y2, s2, pool)
         ctx.blk = blk
         ctx.pool = pool
+        ctx.defer = defer
+        if defer:
+            # deferred activation: the block hands out its PRE-BN output y2 with the BN
+            # statistics s2; the consumer (transposed conv / head kernels) applies BN + ReLU
+            # on load and returns dL/da2 with BN-backward partial sums attached
+            ctx.has_x2 = x2 is not None
+            ctx.x1_requires_grad = ctx.needs_input_grad[0]
+            ctx.save_for_backward(x1, x2 if x2 is not None else torch.empty(0), y1, y2, s1, s2,
+                                  g1, g2)
+            ctx.set_materialize_grads(False)
+            ctx.mark_non_differentiable(s2)
+            return y2, None, s2
+        a2, pooled = F.bn_relu_apply(y2, s2, pool)
         ctx.has_x2 = x2 is not None
         ctx.x1_requires_grad = ctx.needs_input_grad[0]
         ctx.save_for_backward(x1, x2 if x2 is not None else torch.empty(0), y1, y2, s1, s2, g1, g2)
         ctx.set_materialize_grads(False)
         if pool:
-            return a2, pooled
-        return a2, None
+            return a2, pooled, None
+        return a2, None, None
 
     @staticmethod
-    def backward(ctx, da2, dpool):
+    def backward(ctx, da2, dpool, _ds2):
         F = _ops()
         x1, x2, y1, y2, s1, s2, g1, g2 = ctx.saved_tensors
         blk = ctx.blk
@@ -147,18 +159,21 @@ class _DoubleConvFn(torch.autograd.Function):
         if dpool is not None:
             dpool = dpool.contiguous()
         if da2 is None and dpool is None:
-            return (None,) * 12
+            return (None,) * 13
+        # BN-backward partial sums already reduced by the consumer's kernel (deferred BN)
+        part2 = getattr(da2, "_ddlpc_bn_partial", None) if ctx.defer else None
         bn1, bn2 = blk.bn1.bn, blk.bn2.bn
         direct = eng.direct_grads
         # ---- second conv: BN2 + ReLU (+ unpool + skip sum) backward, then its gradients
         if direct:
-            dy2, _, _ = F.bn_backward(da2, dpool, y2, s2, g2, None, bn2.weight.grad, bn2.bias.grad)
+            dy2, _, _ = F.bn_backward(da2, dpool, y2, s2, g2, None, bn2.weight.grad, bn2.bias.grad,
+                                      part2)
             with eng.wgrad_stream(dy2, y1, s1):
                 F.conv3_wgrad(dy2, y1, None, s1[2], s1[3], blk.conv2.weight.grad)
                 eng.ready(bn2.weight, bn2.bias, blk.conv2.weight, blk.conv2.bias)
             dg2 = dbe2 = dw2 = None
         else:
-            dy2, dg2, dbe2 = F.bn_backward(da2, dpool, y2, s2, g2, None)
+            dy2, dg2, dbe2 = F.bn_backward(da2, dpool, y2, s2, g2, None, None, None, part2)
             dw2 = F.conv3_wgrad(dy2, y1, None, s1[2], s1[3]).view_as(blk.conv2.weight)
         p1, p2 = blk.pack1, blk.pack2
         da1, _, _ = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False)
@@ -196,14 +211,16 @@ class _DoubleConvFn(torch.autograd.Function):
         # conv biases feeding a training-mode BN have an exactly-zero gradient
         zb1 = torch.zeros_like(g1) if (not direct and ctx.needs_input_grad[3]) else None
         zb2 = torch.zeros_like(g2) if (not direct and ctx.needs_input_grad[7]) else None
-        return (dx1, dx2, dw1, zb1, dg1, dbe1, dw2, zb2, dg2, dbe2, None, None)
+        return (dx1, dx2, dw1, zb1, dg1, dbe1, dw2, zb2, dg2, dbe2, None, None, None)
 
 
 class _ConvTFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, pack: _ConvPack, engine):
-        out = _ops().convt_fwd(x, pack.fwd, b, pack.cout)
-        ctx.save_for_backward(x)
+    def forward(ctx, x, w, b, pack: _ConvPack, engine, bn: Optional[torch.Tensor] = None):
+        # bn: statistics of a deferred-BN input (x = pre-BN y2 of the previous block)
+        out = _ops().convt_fwd(x, pack.fwd, b, pack.cout, bn)
+        ctx.save_for_backward(x, bn if bn is not None else torch.empty(0))
+        ctx.has_bn = bn is not None
         ctx.pack = pack
         ctx.engine = engine
         return out
@@ -211,19 +228,25 @@ class _ConvTFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         F = _ops()
-        (x,) = ctx.saved_tensors
+        x, bn = ctx.saved_tensors
+        bn = bn if ctx.has_bn else None
         dout = dout.contiguous()
-        dx = F.convt_dgrad(dout, ctx.pack.dgrad, ctx.pack.cin) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx, part = F.convt_dgrad(dout, ctx.pack.dgrad, ctx.pack.cin, x if bn is not None else None,
+                                     bn)
+            if bn is not None:
+                dx._ddlpc_bn_partial = part
         conv = ctx.pack.conv
         rows = getattr(dout, "_ddlpc_colsum_rows", None)
         eng = ctx.engine
         if eng.direct_grads:
-            with eng.wgrad_stream(x, dout, rows):
-                F.convt_wgrad(x, dout, conv.weight.grad, conv.bias.grad, rows)
+            with eng.wgrad_stream(x, dout, rows, bn):
+                F.convt_wgrad(x, dout, conv.weight.grad, conv.bias.grad, rows, bn)
                 eng.ready(conv.weight, conv.bias)
-            return dx, None, None, None, None
-        dw, db = F.convt_wgrad(x, dout, None, None, rows)
-        return dx, dw.view_as(conv.weight), db, None, None
+            return dx, None, None, None, None, None
+        dw, db = F.convt_wgrad(x, dout, None, None, rows, bn)
+        return dx, dw.view_as(conv.weight), db, None, None, None
 
 
 class _BilinearFn(torch.autograd.Function):
@@ -238,9 +261,11 @@ class _BilinearFn(torch.autograd.Function):
 
 class _HeadCEFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, wh, bh, labels, ignore_index: int, engine):
-        out3 = _ops().head_ce_fwd(a, wh, bh, labels, ignore_index)
-        ctx.save_for_backward(a, wh, bh, labels, out3)
+    def forward(ctx, a, wh, bh, labels, ignore_index: int, engine,
+                bn: Optional[torch.Tensor] = None):
+        out3 = _ops().head_ce_fwd(a, wh, bh, labels, ignore_index, bn)
+        ctx.save_for_backward(a, wh, bh, labels, out3, bn if bn is not None else torch.empty(0))
+        ctx.has_bn = bn is not None
         ctx.ignore_index = ignore_index
         ctx.engine = engine
         loss = out3[0]
@@ -250,18 +275,23 @@ class _HeadCEFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dloss, dcorrect):
-        a, wh, bh, labels, out3 = ctx.saved_tensors
+        a, wh, bh, labels, out3, bn = ctx.saved_tensors
+        bn = bn if ctx.has_bn else None
         gs = dloss.reshape(1).float().contiguous() if dloss is not None else None
         eng = ctx.engine
         if eng.direct_grads:
             head = eng.head
-            da, _, _ = _ops().head_ce_bwd(a, wh, bh, labels, out3, gs, ctx.ignore_index,
-                                          head.weight.grad, head.bias.grad)
+            da, _, _, part = _ops().head_ce_bwd(a, wh, bh, labels, out3, gs, ctx.ignore_index,
+                                                head.weight.grad, head.bias.grad, bn)
             with eng.wgrad_stream():
                 eng.ready(head.weight, head.bias)
-            return da, None, None, None, None, None
-        da, dw, db = _ops().head_ce_bwd(a, wh, bh, labels, out3, gs, ctx.ignore_index)
-        return da, dw, db, None, None, None
+            dw = db = None
+        else:
+            da, dw, db, part = _ops().head_ce_bwd(a, wh, bh, labels, out3, gs, ctx.ignore_index,
+                                                  None, None, bn)
+        if bn is not None:
+            da._ddlpc_bn_partial = part
+        return da, dw, db, None, None, None, None
 
 
 class _Block:
@@ -277,11 +307,12 @@ class _Block:
         self.pack1 = _ConvPack(self.conv1, 0, need_dgrad=not first)
         self.pack2 = _ConvPack(self.conv2, 0, need_dgrad=True)
 
-    def __call__(self, x1, x2, pool: bool):
+    def __call__(self, x1, x2, pool: bool, defer: bool = False):
+        """-> (activation, pooled | None, None) or, deferred, (pre-BN y2, None, stats s2)."""
         return _DoubleConvFn.apply(x1, x2, self.conv1.weight, self.conv1.bias,
                                    self.bn1.bn.weight, self.bn1.bn.bias, self.conv2.weight,
                                    self.conv2.bias, self.bn2.bn.weight, self.bn2.bn.bias, self,
-                                   pool)
+                                   pool, defer)
 
 
 class UNetEngine:
@@ -309,6 +340,8 @@ class UNetEngine:
         prio = int(os.environ.get("DDLPC_SIDE_PRIORITY", "1"))
         self.side = torch.cuda.Stream(dev, priority=prio) if use_side else None
         self._side_used = False
+        # deferred BatchNorm activations (see ``features``): DDLPC_DEFER_BN=all|convt|none
+        self.defer_mode = os.environ.get("DDLPC_DEFER_BN", "all")
         self.enc = [_Block(b.double_conv, first=(i == 0), engine=self)
                     for i, b in enumerate(model.down_blocks())]
         self.mid = _Block(model.double_conv, first=False, engine=self)
@@ -356,6 +389,8 @@ class UNetEngine:
         if self.side is not None and self._side_used:
             torch.cuda.current_stream(self.side.device).wait_stream(self.side)
             self._side_used = False
+        # deferred BatchNorm activations (see ``features``): DDLPC_DEFER_BN=all|convt|none
+        self.defer_mode = os.environ.get("DDLPC_DEFER_BN", "all")
 
     def ready(self, *params):
         """Gradients of ``params`` are complete once the queued work finishes.  Called on
@@ -397,37 +432,50 @@ class UNetEngine:
         return _ops().to_nhwc_bf16(x, 8)
 
     # ------------------------------------------------------------------ graph
-    def features(self, x: torch.Tensor) -> torch.Tensor:
-        """Input (NCHW view) -> last decoder activation, channel-last bf16."""
+    def features(self, x: torch.Tensor, defer_last: bool = False):
+        """Input (NCHW view) -> (last decoder activation, None), channel-last bf16, or with
+        ``defer_last`` (pre-BN output, BN statistics) for the fused head kernels.
+
+        A block whose only consumer is one of this engine's transposed convolutions (or the
+        head) defers its final BatchNorm + ReLU into that consumer's loads: the activation
+        is never materialised, and the consumer's backward kernel also reduces the
+        BatchNorm-backward partial sums (SURVEY.md §2.5 K4/K5 fusion)."""
         self._ensure_packed()
         h = self.to_nhwc(x)
         skips = []
         for blk in self.enc:
-            skip, h = blk(h, None, True)
+            skip, h, _ = blk(h, None, True)
             skips.append(skip)
-        h, _ = self.mid(h, None, False)
-        for (ub, pack, blk), skip in zip(self.dec, reversed(skips)):
+        n = len(self.dec)
+        mode = self.defer_mode                       # "all" | "convt" | "none"
+        feeds_convt = [pack is not None and mode != "none" for _, pack, _ in self.dec]
+        defer_last = defer_last and mode == "all"
+        h, _, s = self.mid(h, None, False, defer=n > 0 and feeds_convt[0])
+        for i, ((ub, pack, blk), skip) in enumerate(zip(self.dec, reversed(skips))):
             if pack is not None:
-                up = _ConvTFn.apply(h, ub.up_sample.weight, ub.up_sample.bias, pack, self)
+                up = _ConvTFn.apply(h, ub.up_sample.weight, ub.up_sample.bias, pack, self, s)
             else:
                 up = _BilinearFn.apply(h)
-            h, _ = blk(up, skip, False)
-        return h
+            defer = feeds_convt[i + 1] if i + 1 < n else defer_last
+            h, _, s = blk(up, skip, False, defer=defer)
+        return h, s
 
     def _head_params(self):
         w = self.head.weight
         return w.view(w.shape[0], w.shape[1]), self.head.bias
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        a = self.features(x)
         wh, bh = self._head_params()
-        if torch.is_grad_enabled() and (wh.requires_grad or a.requires_grad):
+        if torch.is_grad_enabled() and (wh.requires_grad or x.requires_grad or
+                                        any(p.requires_grad for p in self.model.parameters())):
             # differentiable logits (rare: training uses loss_and_correct)
+            a, _ = self.features(x)
             logits = torch.einsum("n...c,kc->n...k", a.float(), wh) + bh
             return _nhwc_shape_to_nchw(logits)
-        return _ops().head_logits(a, wh.detach().contiguous(), bh.detach())
+        a, s = self.features(x, defer_last=True)
+        return _ops().head_logits(a, wh.detach().contiguous(), bh.detach(), s)
 
     def loss_and_correct(self, x: torch.Tensor, y: torch.Tensor, ignore_index: int = -100):
-        a = self.features(x)
+        a, s = self.features(x, defer_last=True)
         wh, bh = self._head_params()
-        return _HeadCEFn.apply(a, wh, bh, y.contiguous(), ignore_index, self)
+        return _HeadCEFn.apply(a, wh, bh, y.contiguous(), ignore_index, self, s)

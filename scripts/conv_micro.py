@@ -92,7 +92,7 @@ def main():
         b = torch.zeros(C, device=dev)
         flops = 2.0 * N * H * H * C * 4 * C
         fns = {"tfwd": lambda: F.convt_fwd(x, pk.fwd, b, C),
-               "tdgrad": lambda: F.convt_dgrad(dout, pk.dgrad, C),
+               "tdgrad": lambda: F.convt_dgrad(dout, pk.dgrad, C)[0],
                "twgrad": lambda: F.convt_wgrad(x, dout)}
         for ps in tpasses:
             fn = fns[ps]

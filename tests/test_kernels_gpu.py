@@ -236,7 +236,7 @@ def test_convt(ops, N, H, W, Cin, Cout):
     assert rel_err(nchw(out), ref) < 1e-2
     dout = torch.randn_like(ref).bfloat16()
     gx, gw, gb = torch.autograd.grad(ref, [xr, wr, br], dout.float())
-    dx = ops.convt_dgrad(nhwc(dout), pk.dgrad, Cin)
+    dx = ops.convt_dgrad(nhwc(dout), pk.dgrad, Cin)[0]
     assert rel_err(nchw(dx), gx) < 1e-2
     dw, db = ops.convt_wgrad(nhwc(x), nhwc(dout))
     assert rel_err(dw, gw) < 5e-3
@@ -261,7 +261,7 @@ def test_head_ce(ops):
     assert int(out3[1]) == int((logits.argmax(1) == y).sum())
     assert int(out3[2]) == int((y != -100).sum())
     g = torch.tensor([0.5], device=DEV)
-    da, dw, db = ops.head_ce_bwd(nhwc(a), wh, bh, y, out3, g, -100)
+    da, dw, db, _ = ops.head_ce_bwd(nhwc(a), wh, bh, y, out3, g, -100)
     ga, gw, gb = torch.autograd.grad(loss * 0.5, [ar, whr, bhr])
     assert rel_err(nchw(da), ga) < 1e-2
     assert rel_err(dw, gw) < 1e-3
@@ -363,3 +363,60 @@ def test_conv3d_fwd_wgrad(ops):
     xr = torch.zeros(N, C, D, H, W, device=DEV, requires_grad=True)
     (gx,) = torch.autograd.grad(F.conv3d(xr, w.bfloat16().float(), padding=1), xr, dy.float())
     assert rel_err(nchw(dx), gx) < 1e-2
+
+
+def _bn4(C, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    mean = torch.randn(C, device=DEV, generator=g) * 0.2
+    invstd = torch.rand(C, device=DEV, generator=g) + 0.5
+    scale = torch.randn(C, device=DEV, generator=g)
+    shift = torch.randn(C, device=DEV, generator=g) * 0.3
+    return torch.stack([mean, invstd, scale, shift]).contiguous()
+
+
+def test_deferred_bn_consumers_match_materialised(ops):
+    """Deferred BatchNorm activations (engine: block output kept pre-BN, BN + ReLU applied
+    on load by the transposed-conv / head kernels) equal the materialised path bit for bit,
+    and the BN-backward partial sums emitted by the consumers' backward epilogues give the
+    same BatchNorm backward as the standalone reduction pass."""
+    torch.manual_seed(11)
+    N, H, W, C = 2, 16, 16, 64
+    y = torch.randn(N, H, W, C, device=DEV).bfloat16()
+    bn4 = _bn4(C, 1)
+    a = ops.bn_relu_apply(y, bn4, False)[0]                     # materialised activation
+    w = torch.randn(C, C, 2, 2, device=DEV) / math.sqrt(C)
+    b = torch.randn(C, device=DEV) * 0.1
+    pk = pack_conv(ops, w)
+    assert torch.equal(ops.convt_fwd(y, pk.fwd, b, C, bn4), ops.convt_fwd(a, pk.fwd, b, C))
+    dout = torch.randn(N, 2 * H, 2 * W, C, device=DEV).bfloat16()
+    dw1, db1 = ops.convt_wgrad(y, dout, None, None, None, bn4)
+    dw2, db2 = ops.convt_wgrad(a, dout)
+    assert torch.equal(dw1, dw2) and torch.equal(db1, db2)
+    dx1, part = ops.convt_dgrad(dout, pk.dgrad, C, y, bn4)
+    dx2, _ = ops.convt_dgrad(dout, pk.dgrad, C)
+    assert torch.equal(dx1, dx2) and part.dim() == 3 and part.shape[1:] == (2, C)
+    gamma = torch.rand(C, device=DEV) + 0.5
+    r_pre = ops.bn_backward(dx1, None, y, bn4, gamma, None, None, None, part)
+    r_ref = ops.bn_backward(dx1, None, y, bn4, gamma, None)
+    for u, v in zip(r_pre, r_ref):
+        assert rel_err(u, v) < 2e-3
+    # head: C = 32, K = 6
+    Ch, K = 32, 6
+    yh = torch.randn(N, H, W, Ch, device=DEV).bfloat16()
+    bnh = _bn4(Ch, 2)
+    ah = ops.bn_relu_apply(yh, bnh, False)[0]
+    wh = torch.randn(K, Ch, device=DEV) * 0.3
+    bh = torch.randn(K, device=DEV) * 0.1
+    lab = torch.randint(0, K, (N, H, W), device=DEV)
+    o1 = ops.head_ce_fwd(yh, wh, bh, lab, -100, bnh)
+    o2 = ops.head_ce_fwd(ah, wh, bh, lab, -100)
+    assert torch.equal(o1, o2)
+    da1, dwh1, dbh1, hpart = ops.head_ce_bwd(yh, wh, bh, lab, o1, None, -100, None, None, bnh)
+    da2, dwh2, dbh2, _ = ops.head_ce_bwd(ah, wh, bh, lab, o2, None, -100)
+    assert torch.equal(da1, da2) and torch.equal(dwh1, dwh2) and torch.equal(dbh1, dbh2)
+    gh = torch.rand(Ch, device=DEV) + 0.5
+    h_pre = ops.bn_backward(da1, None, yh, bnh, gh, None, None, None, hpart)
+    h_ref = ops.bn_backward(da1, None, yh, bnh, gh, None)
+    for u, v in zip(h_pre, h_ref):
+        assert rel_err(u, v) < 2e-3
+    assert torch.equal(ops.head_logits(yh, wh, bh, bnh), ops.head_logits(ah, wh, bh))
