@@ -412,6 +412,11 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
 #pragma unroll
     for (int q2 = 0; q2 < Cfg::NP; ++q2) acc[j][q2] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  // input chunks with at most 16 valid channels (the 8-channel padded image layer): only
+  // the first 16-channel half carries data, so the 9 (tap, half 0) pairs are spread over
+  // the waves instead of 18 pairs of which half are all-zero
+  const bool half_only = p.Cin - ci0 <= 16;
+  const int npairs = half_only ? 9 : 18;
   auto compute = [&](const char* __restrict__ Y, const char* __restrict__ X) {
 #pragma unroll
     for (int ks = 0; ks < Cfg::KSTEPS; ++ks) {
@@ -425,8 +430,8 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
 #pragma unroll
       for (int pi = 0; pi < Cfg::NP; ++pi) {
         const int pair = wave + 4 * pi;                 // wave-uniform
-        if (pair < 18) {
-          const int tap = pair >> 1, cih = pair & 1;
+        if (pair < npairs) {
+          const int tap = half_only ? pair : pair >> 1, cih = half_only ? 0 : pair & 1;
           const int toff = ((tap / 3) * HW2 + tap % 3) * 64 + cih * 32;
           const uint2 lo = lds_read_tr16(X + xb[ks][0] + toff);
           const uint2 hi = lds_read_tr16(X + xb[ks][1] + toff);
@@ -453,9 +458,9 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
 #pragma unroll
   for (int pi = 0; pi < Cfg::NP; ++pi) {
     const int pair = wave + 4 * pi;
-    if (pair >= 18) continue;
-    const int tap = pair >> 1;
-    const int ci = ci0 + (pair & 1) * 16 + (lane & 15);
+    if (pair >= npairs) continue;
+    const int tap = half_only ? pair : pair >> 1;
+    const int ci = ci0 + (half_only ? 0 : (pair & 1) * 16) + (lane & 15);
 #pragma unroll
     for (int j = 0; j < Cfg::NCO; ++j)
 #pragma unroll
