@@ -150,7 +150,9 @@ def main():
                        "classes": args.classes,
                        "parallelism": f"dp{world}", "impl": tr.impl,
                        "optimizer": "Adam(lr=1e-3)", "loss": "CrossEntropy",
-                       "train_loss_mean": round(loss["loss"], 4)},
+                       "train_loss_mean": round(loss["loss"], 4),
+                       "peak_mem_gb": (round(torch.cuda.max_memory_allocated(device) / 2**30, 2)
+                                       if dev == "cuda" else None)},
         }
         print(json.dumps(rec), flush=True)
     tr.close()

@@ -433,7 +433,7 @@ at::Tensor convt_fwd(const at::Tensor& x, const at::Tensor& wt, const c10::optio
   a.dims = g.dims; a.Nimg = g.N; a.D = g.D; a.H = g.H; a.W = g.W;
   a.Cin = g.C; a.Cout = (int)cout;
   a.bn4 = bn4_ptr(bn4, g.C);
-  TORCH_CHECK((int64_t)a.M * std::max(a.K, a.N) < (int64_t)INT32_MAX, "convT: tensor too large for 32-bit offsets");
+  TORCH_CHECK((int64_t)a.M * (g.dims == 2 ? 4 : 8) < (int64_t)INT32_MAX, "convT: too many pixels for 32-bit pixel indices");
   at::Tensor out = at::empty(shape_with_c(g, (int)cout, 2), x.options());
   a.C = out.data_ptr();
   gemm_launch(a, cur_stream());
@@ -459,7 +459,7 @@ std::vector<at::Tensor> convt_dgrad(const at::Tensor& dout, const at::Tensor& wd
   a.dims = g.dims; a.Nimg = g.N; a.D = g.D; a.H = g.H; a.W = g.W;
   a.Cin = (int)cin; a.Cout = go.C;
   TORCH_CHECK(go.C % 32 == 0, "convT dgrad needs Cout % 32 == 0");
-  TORCH_CHECK((int64_t)a.M * std::max(a.K, a.N) < (int64_t)INT32_MAX, "convT: tensor too large for 32-bit offsets");
+  TORCH_CHECK((int64_t)a.M * (g.dims == 2 ? 4 : 8) < (int64_t)INT32_MAX, "convT: too many pixels for 32-bit pixel indices");
   at::Tensor dx = at::empty(shape_with_c(g, (int)cin), dout.options());
   a.C = dx.data_ptr();
   at::Tensor bnpart = at::empty({0}, dout.options().dtype(at::kFloat));

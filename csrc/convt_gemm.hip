@@ -82,13 +82,13 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
 
   // per-thread rows: A rows (tid>>2) and (tid>>2)+64, B row tid>>2; 8-channel piece tid&3
   const int cq = tid & 3;
-  int arow_off[2];                       // FWD: m*K ; DGRAD: up-pixel base * Cout (-1: none)
+  long long arow_off[2];                 // FWD: m*K ; DGRAD: up-pixel base * Cout (-1: none)
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int m = m0 + (tid >> 2) + 64 * i;
     if (m >= p.M) { arow_off[i] = -1; continue; }
-    if (MODE == GEMM_CONVT_FWD) arow_off[i] = m * p.K;
-    else arow_off[i] = up_pixel(m, 0, p.dims, p.D, p.H, p.W) * p.Cout;
+    if (MODE == GEMM_CONVT_FWD) arow_off[i] = (long long)m * p.K;
+    else arow_off[i] = (long long)up_pixel(m, 0, p.dims, p.D, p.H, p.W) * p.Cout;
   }
   const int n_b = n0 + (tid >> 2);
   const int brow_off = n_b < p.N ? n_b * p.K : -1;
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
       for (int i = 0; i < 2; ++i) {
         uint4 v = make_uint4(0, 0, 0, 0);
         if (arow_off[i] >= 0 && k8 < p.K)
-          v = *reinterpret_cast<const uint4*>(p.A + (long long)arow_off[i] + aoff);
+          v = *reinterpret_cast<const uint4*>(p.A + arow_off[i] + aoff);
         ra[j][i] = v;
       }
       uint4 v = make_uint4(0, 0, 0, 0);
