@@ -50,53 +50,67 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
   }
 }
 
-// Destination-ordered: consecutive lanes write consecutive bf16 of a packed layout (the
-// innermost packed index is the fastest-varying thread index), reads gather from the small
-// fp32 source (L2 / Infinity-Cache resident).  Packing pads (ci >= Cin) were zeroed at
-// allocation and are never written.
-__global__ void weight_pack_kernel(const PackEntry* __restrict__ ents) {
+// LDS-tiled transposes: a workgroup loads one (32 x 32-channel) tile of the fp32 source
+// with coalesced reads, then writes every packed layout from LDS as contiguous 64-B runs
+// (both sides coalesced; all weights of the model in one launch, blockIdx.y = entry).
+//   conv3 (OIHW [co][ci][tap]):  tile = 32 co x (32 ci x taps)   (10 ci for 27 taps)
+//     fwd   [co][tap][CinW]      runs of 32 ci
+//     dgrad [ci][taps-1-tap][CoutW] runs of 32 co
+//   convT (IOHW [ci][co][sub]):  tile = 32 ci x (32 co x S)
+//     fwd   [(sub, co)][Cin]     runs of 32 ci
+//     dgrad [ci][(sub, co)]      runs of 32 co
+// Packing pads (ci >= Cin) were zeroed at allocation and are never written.
+constexpr int PT = 32;
+__global__ __launch_bounds__(256) void weight_pack_kernel(const PackEntry* __restrict__ ents) {
+  __shared__ float tile[PT][PT * 9 + 1];
   const PackEntry e = ents[blockIdx.y];
-  const long long total = (long long)e.Cout * e.Cin * e.taps;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  const long long t0 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  if (e.kind == 0) {
-    // src OIHW [co][ci][tap]  ->  fwd [co][tap][CinW] (ci fastest)
-    for (long long o = t0; o < total; o += stride) {
-      const int ci = (int)(o % e.Cin);
-      const long long r = o / e.Cin;
-      const int tap = (int)(r % e.taps);
-      const int co = (int)(r / e.taps);
-      e.fwd[((long long)co * e.taps + tap) * e.CinW + ci] =
-          f2bf(e.src[((long long)co * e.Cin + ci) * e.taps + tap]);
+  const int T = e.taps;
+  const int NC = min(PT, PT * 9 / T);                 // tile columns: 32, or 10 for 27 taps
+  // tile grid: conv3 rows = co, cols = ci; convT rows = ci, cols = co
+  const int R = e.kind == 0 ? e.Cout : e.Cin, Cc = e.kind == 0 ? e.Cin : e.Cout;
+  const int tr = (R + PT - 1) / PT, tc = (Cc + NC - 1) / NC;
+  const int tid = threadIdx.x;
+  for (int t = blockIdx.x; t < tr * tc; t += gridDim.x) {
+    const int r0 = (t / tc) * PT, c0 = (t % tc) * NC;
+    const int nr = min(PT, R - r0), nc = min(NC, Cc - c0);
+    __syncthreads();
+    // load: row r, the nc*T contiguous floats of columns [c0, c0+nc)
+    for (int i = tid; i < PT * NC * T; i += 256) {
+      const int r = i / (NC * T), j = i % (NC * T);
+      if (r < nr && j < nc * T)
+        tile[r][j] = e.src[((long long)(r0 + r) * Cc + c0) * T + j];
     }
-    // -> dgrad [ci][tap'][CoutW] (co fastest), tap' = taps-1-tap (flipped filter)
-    if (e.dgrad != nullptr)
-      for (long long o = t0; o < total; o += stride) {
-        const int co = (int)(o % e.Cout);
-        const long long r = o / e.Cout;
-        const int tp = (int)(r % e.taps);
-        const int ci = (int)(r / e.taps);
-        e.dgrad[((long long)ci * e.taps + tp) * e.CoutW + co] =
-            f2bf(e.src[((long long)co * e.Cin + ci) * e.taps + (e.taps - 1 - tp)]);
+    __syncthreads();
+    if (e.kind == 0) {
+      // fwd: [co = r0+r][tap][ci = c0 + c]
+      for (int i = tid; i < PT * T * NC; i += 256) {
+        const int c = i % NC, rt = i / NC, tap = rt % T, r = rt / T;
+        if (r < nr && c < nc)
+          e.fwd[((long long)(r0 + r) * T + tap) * e.CinW + c0 + c] = f2bf(tile[r][c * T + tap]);
       }
-  } else {
-    // src IOHW [ci][co][sub]  ->  fwd [(sub, co)][Cin] (ci fastest)
-    for (long long o = t0; o < total; o += stride) {
-      const int ci = (int)(o % e.Cin);
-      const long long r = o / e.Cin;             // = sub * Cout + co
-      const int co = (int)(r % e.Cout);
-      const int sub = (int)(r / e.Cout);
-      e.fwd[o] = f2bf(e.src[((long long)ci * e.Cout + co) * e.taps + sub]);
+      // dgrad: [ci = c0 + c][tp][co = r0 + r], source tap = T-1-tp
+      if (e.dgrad != nullptr)
+        for (int i = tid; i < PT * T * NC; i += 256) {
+          const int r = i % PT, ct = i / PT, tp = ct % T, c = ct / T;
+          if (r < nr && c < nc)
+            e.dgrad[((long long)(c0 + c) * T + tp) * e.CoutW + r0 + r] =
+                f2bf(tile[r][c * T + (T - 1 - tp)]);
+        }
+    } else {
+      // fwd: [(sub, co = c0 + c)][ci = r0 + r]
+      for (int i = tid; i < PT * T * NC; i += 256) {
+        const int r = i % PT, cs = i / PT, c = cs % NC, sub = cs / NC;
+        if (r < nr && c < nc)
+          e.fwd[((long long)sub * e.Cout + c0 + c) * e.Cin + r0 + r] = f2bf(tile[r][c * T + sub]);
+      }
+      // dgrad: [ci = r0 + r][(sub, co = c0 + c)]
+      if (e.dgrad != nullptr)
+        for (int i = tid; i < PT * T * NC; i += 256) {
+          const int c = i % NC, rs = i / NC, sub = rs % T, r = rs / T;
+          if (r < nr && c < nc)
+            e.dgrad[((long long)(r0 + r) * T + sub) * e.Cout + c0 + c] = f2bf(tile[r][c * T + sub]);
+        }
     }
-    // -> dgrad [ci][(sub, co)] (co fastest)
-    if (e.dgrad != nullptr)
-      for (long long o = t0; o < total; o += stride) {
-        const int co = (int)(o % e.Cout);
-        const long long r = o / e.Cout;
-        const int sub = (int)(r % e.taps);
-        const int ci = (int)(r / e.taps);
-        e.dgrad[o] = f2bf(e.src[((long long)ci * e.Cout + co) * e.taps + sub]);
-      }
   }
 }
 
@@ -323,7 +337,8 @@ void adam_scalars_launch(float* s, double lr, double b1, double b2, hipStream_t 
 
 void weight_pack_launch(const PackEntry* entries_dev, int n_entries, long long max_elems,
                         hipStream_t st) {
-  const int gx = (int)std::max<long long>(1, std::min<long long>((max_elems + 255) / 256, 512));
+  // one workgroup per 32 x 32-channel tile of the largest entry (smaller entries loop less)
+  const int gx = (int)std::max<long long>(1, std::min<long long>((max_elems + 9215) / 9216, 1024));
   hipLaunchKernelGGL(weight_pack_kernel, dim3(gx, n_entries), dim3(256), 0, st, entries_dev);
 }
 

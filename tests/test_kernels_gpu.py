@@ -420,3 +420,56 @@ def test_deferred_bn_consumers_match_materialised(ops):
     for u, v in zip(h_pre, h_ref):
         assert rel_err(u, v) < 2e-3
     assert torch.equal(ops.head_logits(yh, wh, bh, bnh), ops.head_logits(ah, wh, bh))
+
+
+def test_out_params_respect_bounds(ops):
+    """Kernels that write into caller-provided buffers (in training: views into the one flat
+    fp32 gradient buffer) are given views into sentinel-filled guard buffers; the guard
+    regions on both sides must come back untouched (bounds checking)."""
+    torch.manual_seed(12)
+    G, S = 4099, 12345.0
+
+    def guarded(*shape):
+        n = math.prod(shape)
+        buf = torch.full((n + 2 * G,), S, device=DEV)
+        v = buf[G:G + n]
+        v.zero_()
+        return buf, v.view(*shape)
+
+    def intact(buf, v):
+        n = v.numel()
+        return bool((buf[:G] == S).all()) and bool((buf[G + n:] == S).all())
+
+    N, H, W, Ci, Co = 2, 24, 40, 32, 64
+    x = torch.randn(N, H, W, Ci, device=DEV).bfloat16()
+    dy = torch.randn(N, H, W, Co, device=DEV).bfloat16()
+    b, v = guarded(Co, Ci, 3, 3)
+    ops.conv3_wgrad(dy, x, None, None, None, v)
+    assert intact(b, v) and bool(v.abs().sum() > 0)
+    y = torch.randn(N, H, W, Co, device=DEV).bfloat16()
+    bg, vg = guarded(Co)
+    bb, vb = guarded(Co)
+    ops.bn_backward(dy, None, y, _bn4(Co, 3), torch.rand(Co, device=DEV) + 0.5, None, vg, vb)
+    assert intact(bg, vg) and intact(bb, vb)
+    xt = torch.randn(N, 8, 8, 64, device=DEV).bfloat16()
+    dout = torch.randn(N, 16, 16, 64, device=DEV).bfloat16()
+    bw, vw = guarded(64, 64, 2, 2)
+    bdb, vdb = guarded(64)
+    ops.convt_wgrad(xt, dout, vw, vdb)
+    assert intact(bw, vw) and intact(bdb, vdb)
+    a = torch.relu(torch.randn(N, H, W, 32, device=DEV)).bfloat16()
+    wh = torch.randn(6, 32, device=DEV) * 0.3
+    bh = torch.zeros(6, device=DEV)
+    lab = torch.randint(0, 6, (N, H, W), device=DEV)
+    out3 = ops.head_ce_fwd(a, wh, bh, lab, -100)
+    bhw, vhw = guarded(6, 32)
+    bhb, vhb = guarded(6)
+    ops.head_ce_bwd(a, wh, bh, lab, out3, None, -100, vhw, vhb)
+    assert intact(bhw, vhw) and intact(bhb, vhb)
+    n = 10_003
+    bufs = [guarded(n) for _ in range(4)]
+    p, g, m, v2 = (t for _, t in bufs)
+    p.copy_(torch.randn(n, device=DEV))
+    g.copy_(torch.randn(n, device=DEV))
+    ops.adam_step(p, g, m, v2, 0.9, 0.999, 1e-8, 0.0, 1e-3, 1.0)
+    assert all(intact(bb_, t) for bb_, t in bufs)
