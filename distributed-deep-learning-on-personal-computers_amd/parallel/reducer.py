@@ -20,7 +20,7 @@ MI355X design:
   nothing (no_sync semantics);
 * ``finish()`` makes the compute stream wait for every bucket (no host sync) before the
   optimizer step;
-* reduction: correct mean (sum * 1/W, or RCCL ``AVG``), ``sum``, or ``reference`` (the
+* reduction: correct mean (pre-scaled by 1/W, then SUM), ``sum``, or ``reference`` (the
   reference's skewed weights; for W=2 that is a plain sum, SURVEY.md §2.6);
 * optional lossy codec (fp16/int8 absmax, ref.py:25) as an all-gather of packed payloads
   + scales, decoded and summed in rank order (``parallel.codec``; fused HIP kernels on GPU).
@@ -151,13 +151,11 @@ class GradBucketReducer:
         b.launched = True
         g = self._seg(b)
         if self.codec == "none":
-            if self.reduce == "mean" and self.backend == "nccl":
-                b.work = dist.all_reduce(g, op=dist.ReduceOp.AVG, group=self.group,
-                                         async_op=True)
-            else:
-                if self.weight != 1.0:
-                    g.mul_(self.weight)
-                b.work = dist.all_reduce(g, group=self.group, async_op=True)
+            # pre-scaled SUM on every backend (exact for power-of-two world sizes; no
+            # dependence on the collective library's AVG support)
+            if self.weight != 1.0:
+                g.mul_(self.weight)
+            b.work = dist.all_reduce(g, group=self.group, async_op=True)
             return
         # lossy codec: encode -> all_gather(payload, scales) -> decode+sum at finish()
         segs = self._codec_segments(b)

@@ -73,3 +73,51 @@ def test_dp_two_ranks_hip_engine_gloo(side, overlap):
         assert o["buckets"] > 1 and o["launched"] == (o["buckets"] if overlap else 0), o
         assert o["max_err"] <= 1e-6 * max(o["scale"], 1.0), o
         assert o["replicas_equal"], o
+
+
+def _rccl_one_rank(rank, world):
+    """The nccl (= RCCL) code path of the reducer on a 1-rank group: async bucket
+    all-reduces launched from the weight-gradient side stream, waits, optimizer step."""
+    import os
+    os.environ["LOCAL_RANK"] = "0"
+    import torch.distributed as dist
+    from ddlpc.config import ModelConfig, TrainConfig
+    from ddlpc.data import device_random_batch
+    from ddlpc.parallel import GradBucketReducer
+    from ddlpc.train.trainer import Trainer
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=2,
+                      num_samples=1, test_holdout=0, impl="hip", backend="nccl")
+    tr = Trainer(cfg, device="cuda")
+    assert dist.get_backend() == "nccl"
+    # world 1 builds no reducer in the trainer: attach one explicitly (same code path)
+    red = GradBucketReducer(tr.flat, bucket_mb=1.0, use_hooks=False)
+    red.world = 2                       # force the collective path on a 1-rank group
+    red.weight = 0.5
+    tr.reducer = red
+    tr.model._engine.enable_direct_grads(red.mark_ready)
+    x, y = device_random_batch(2, 64, 6, tr.device, seed=3)
+    red.prepare(sync=False)
+    loss, _ = tr.model.loss_and_correct(x, y)
+    loss.backward()
+    torch.cuda.synchronize()
+    g_local = tr.flat.grad_buf.clone()
+    tr.optimizer.zero_grad()
+    red.prepare(sync=True)
+    loss, _ = tr.model.loss_and_correct(x, y)
+    loss.backward()
+    launched = red.stats["launched_in_backward"]
+    red.finish()
+    torch.cuda.synchronize()
+    g = tr.flat.grad_buf.clone()
+    tr.close()
+    # one rank: SUM of (0.5 * g_local) == 0.5 * g_local exactly
+    return {"launched": launched, "buckets": len(red.buckets),
+            "exact": bool(torch.equal(g, g_local * 0.5))}
+
+
+def test_rccl_reducer_path_one_rank():
+    res = run(_rccl_one_rank, 1, (), timeout=150)
+    o = res[0]
+    assert o["launched"] == o["buckets"] > 1 and o["exact"], o
