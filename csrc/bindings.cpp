@@ -207,7 +207,11 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
     part = at::empty({(int64_t)a.ksplit * a.npix * a.Cout}, opts.dtype(at::kFloat));
     a.part = part.data_ptr<float>();
   }
-  const int fin_grid = (int)std::min<long long>(std::max<long long>(1, a.npix / 64), 512);
+  // finalize: ~one pixel group per thread (the split-K layers are the small, latency-bound
+  // ones: a short grid-stride chain per thread beats fewer, longer-running workgroups)
+  const int fin_px_per_block = std::max(1, 256 / (a.Cout / 8));
+  const int fin_grid = (int)std::min<long long>(
+      std::max<long long>(1, (a.npix + fin_px_per_block - 1) / fin_px_per_block), 2048);
   if (want_stats) {
     const int items = a.nTilesM * a.nTilesN * a.ksplit;
     const int q = a.nTilesN * a.ksplit;
@@ -469,8 +473,10 @@ std::vector<at::Tensor> convt_dgrad(const at::Tensor& dout, const at::Tensor& wd
                 bny->numel() == dx.numel() && bny->scalar_type() == at::kBFloat16,
                 "convt_dgrad: bny must be the deferred pre-BN input (shape of dx, bf16)");
     a.bny = bptr(*bny);
+    // rows: one per workgroup of the widest tiling (128 x 64); a 128-wide tiling writes
+    // fewer rows — the unused ones are zeroed below so the row count is tiling independent
     const long long grid = ((a.M + 127) / 128) * (long long)((a.N + 63) / 64);
-    bnpart = at::empty({(int64_t)grid, 2, (int64_t)cin}, dout.options().dtype(at::kFloat));
+    bnpart = at::zeros({(int64_t)grid, 2, (int64_t)cin}, dout.options().dtype(at::kFloat));
     a.bnpart = bnpart.data_ptr<float>();
   }
   gemm_launch(a, cur_stream());

@@ -47,9 +47,11 @@ DDLPC_DEVICE int up_pixel(int m, int sub, int dims, int D, int H, int W) {
 // The dgrad gather addresses are formed without division in the k loop: a step's chunk
 // sits inside one sub-position (Cout % 32 == 0), whose up-sampled pixel is the row's base
 // pixel plus a per-sub offset.
-template <int MODE, int KC>
+template <int MODE, int KC, int BN>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
-  constexpr int BM = 128, BN = 64;
+  constexpr int BM = 128;
+  constexpr int NT = BN / 32;            // 16-col MFMA tiles per wave (2 wave columns)
+  constexpr int NBP = BN / 64;           // B pieces per thread per chunk
   constexpr int A_BYTES = KC * BM * 64, B_BYTES = KC * BN * 64;
   // deferred-BN constants live in otherwise idle LDS: FWD (scale|shift, 2 x 512 floats)
   // behind the operand tiles, used in the k loop; DGRAD (scale|shift|mean|invstd) behind the
@@ -90,8 +92,12 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
     if (MODE == GEMM_CONVT_FWD) arow_off[i] = (long long)m * p.K;
     else arow_off[i] = (long long)up_pixel(m, 0, p.dims, p.D, p.H, p.W) * p.Cout;
   }
-  const int n_b = n0 + (tid >> 2);
-  const int brow_off = n_b < p.N ? n_b * p.K : -1;
+  int brow_off[NBP];
+#pragma unroll
+  for (int i = 0; i < NBP; ++i) {
+    const int n_b = n0 + (tid >> 2) + 64 * i;
+    brow_off[i] = n_b < p.N ? n_b * p.K : -1;
+  }
   const int W2 = 2 * p.W, HW4 = 4 * p.H * p.W;
   auto sub_off = [&](int sub) {          // up-pixel offset of sub-position sub (x Cout)
     const int o = (p.dims == 2 ? (sub >> 1) * W2 + (sub & 1)
@@ -99,7 +105,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
     return o * p.Cout;
   };
 
-  uint4 ra[KC][2], rb[KC];
+  uint4 ra[KC][2], rb[KC][NBP];
   int kcur = 0;                          // k base of the step held in ra (FWD prologue)
   auto load = [&](int it) {
     kcur = it * KC * BK;
@@ -120,9 +126,12 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
           v = *reinterpret_cast<const uint4*>(p.A + arow_off[i] + aoff);
         ra[j][i] = v;
       }
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (brow_off >= 0 && k8 < p.K) v = *reinterpret_cast<const uint4*>(p.B + (long long)brow_off + k8);
-      rb[j] = v;
+#pragma unroll
+      for (int i = 0; i < NBP; ++i) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (brow_off[i] >= 0 && k8 < p.K) v = *reinterpret_cast<const uint4*>(p.B + (long long)brow_off[i] + k8);
+        rb[j][i] = v;
+      }
     }
   };
   auto store = [&]() {
@@ -141,15 +150,17 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
         }
         *reinterpret_cast<uint4*>(sA + j * BM * 64 + lds_off((tid >> 2) + 64 * i, cq)) = v;
       }
-      *reinterpret_cast<uint4*>(sB + j * BN * 64 + lds_off(tid >> 2, cq)) = rb[j];
+#pragma unroll
+      for (int i = 0; i < NBP; ++i)
+        *reinterpret_cast<uint4*>(sB + j * BN * 64 + lds_off((tid >> 2) + 64 * i, cq)) = rb[j][i];
     }
   };
 
-  f32x4_t acc[4][2];
+  f32x4_t acc[4][NT];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int nit = (p.K + BK * KC - 1) / (BK * KC);
   load(0);
@@ -160,25 +171,25 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
     if (it + 1 < nit) load(it + 1);
 #pragma unroll
     for (int j = 0; j < KC; ++j) {
-      uint4 af[4], bfr[2];
+      uint4 af[4], bfr[NT];
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
         af[mt] = *reinterpret_cast<const uint4*>(sA + j * BM * 64 + lds_off(wm * 64 + mt * 16 + (lane & 15), g));
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-        bfr[nt] = *reinterpret_cast<const uint4*>(sB + j * BN * 64 + lds_off(wn * 32 + nt * 16 + (lane & 15), g));
+      for (int nt = 0; nt < NT; ++nt)
+        bfr[nt] = *reinterpret_cast<const uint4*>(sB + j * BN * 64 + lds_off(wn * (BN / 2) + nt * 16 + (lane & 15), g));
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma16x16x32(af[mt], bfr[nt], acc[mt][nt]);
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(af[mt], bfr[nt], acc[mt][nt]);
     }
   }
 
   __syncthreads();
   bf16_t* sO = reinterpret_cast<bf16_t*>(smem);
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const int col = wn * 32 + nt * 16 + (lane & 15);
+  for (int nt = 0; nt < NT; ++nt) {
+    const int col = wn * (BN / 2) + nt * 16 + (lane & 15);
     float b = 0.f;
     if (MODE == GEMM_CONVT_FWD && p.bias != nullptr && n0 + col < p.N) b = p.bias[(n0 + col) % p.Cout];
 #pragma unroll
@@ -378,19 +389,25 @@ void gemm_launch(GemmArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(gemm_tn_wgrad_kernel, dim3(grid), dim3(256), 0, st, a);
     return;
   }
-  const long long grid = ((a.M + 127) / 128) * (long long)((a.N + 63) / 64);
   // measured (B=64 U-Net shapes): the gathered data-gradient A operand gains from wide
-  // steps; the forward (contiguous A, K = Cin) runs best at one chunk per step
+  // steps; the forward (contiguous A, K = Cin) runs best at one chunk per step.  The forward
+  // uses 128-wide N tiles when N allows (each A tile is read from L2 half as often)
+  static const int fwd_bn = [] { const char* e = getenv("DDLPC_CONVT_BN"); return e ? atoi(e) : 128; }();
+  static const int dgrad_bn = [] { const char* e = getenv("DDLPC_CONVT_DGRAD_BN"); return e ? atoi(e) : 128; }();
+  const int bn = (a.N % 128 == 0 && (a.mode == GEMM_CONVT_FWD ? fwd_bn : dgrad_bn) == 128) ? 128 : 64;
+  const long long grid = ((a.M + 127) / 128) * (long long)((a.N + bn - 1) / bn);
   const int kc = a.mode == GEMM_CONVT_FWD ? 1 : a.K <= 64 ? 2 : 4;
-#define DDLPC_GEMM_NT(MODE)                                                                  \
-  switch (kc) {                                                                             \
-    case 1: hipLaunchKernelGGL((gemm_nt_kernel<MODE, 1>), dim3((unsigned)grid), dim3(256), 0, st, a); break; \
-    case 2: hipLaunchKernelGGL((gemm_nt_kernel<MODE, 2>), dim3((unsigned)grid), dim3(256), 0, st, a); break; \
-    default: hipLaunchKernelGGL((gemm_nt_kernel<MODE, 4>), dim3((unsigned)grid), dim3(256), 0, st, a); break; \
+  if (a.mode == GEMM_CONVT_FWD) {
+    if (bn == 128) hipLaunchKernelGGL((gemm_nt_kernel<GEMM_CONVT_FWD, 1, 128>), dim3((unsigned)grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((gemm_nt_kernel<GEMM_CONVT_FWD, 1, 64>), dim3((unsigned)grid), dim3(256), 0, st, a);
+  } else if (bn == 128) {
+    if (kc == 2) hipLaunchKernelGGL((gemm_nt_kernel<GEMM_CONVT_DGRAD, 2, 128>), dim3((unsigned)grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((gemm_nt_kernel<GEMM_CONVT_DGRAD, 4, 128>), dim3((unsigned)grid), dim3(256), 0, st, a);
+  } else if (kc == 2) {
+    hipLaunchKernelGGL((gemm_nt_kernel<GEMM_CONVT_DGRAD, 2, 64>), dim3((unsigned)grid), dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((gemm_nt_kernel<GEMM_CONVT_DGRAD, 4, 64>), dim3((unsigned)grid), dim3(256), 0, st, a);
   }
-  if (a.mode == GEMM_CONVT_FWD) { DDLPC_GEMM_NT(GEMM_CONVT_FWD) }
-  else { DDLPC_GEMM_NT(GEMM_CONVT_DGRAD) }
-#undef DDLPC_GEMM_NT
 }
 
 }  // namespace ddlpc

@@ -123,7 +123,7 @@ bool head_supported(int C, int K);
 void head_ce_fwd_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
                         float* partial, float* out3, const float* bn4, int nblocks, long long P,
                         int C, int K, int ignore_index, hipStream_t st);
-// bnpart (with bn4): per-workgroup [2][C] BatchNorm-backward partial sums of the stored dA
+// (bnpart: unused — see head_ce.hip)
 void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
                         const float* gscale, const float* stats3, int unused, bf16_t* dA,
                         float* dW_partial, int nblocks, long long P, int C, int K,
