@@ -262,9 +262,11 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16_t* __restri
 
 // strided [N][C][S] (fp32 or bf16; NCHW or channels-last memory) -> [N][S][Cp] bf16 with the
 // channels zero-padded to Cp (the first conv reads 8-channel, 16-byte pixels)
-__global__ void to_nhwc_pad_kernel(const void* __restrict__ x, int in_dtype, bf16_t* __restrict__ y,
-                                   int N, int C, int Cp, long long S, long long sN, long long sC,
-                                   long long sS) {
+// one thread per (pixel, 8-channel group): gathers up to 8 input channels (strided NCHW or
+// channel-last, fp32 or bf16), pads with zeros, one 16-B store
+__global__ void to_nhwc_generic_kernel(const void* __restrict__ x, int in_dtype, bf16_t* __restrict__ y,
+                                       int N, int C, int Cp, long long S, long long sN, long long sC,
+                                       long long sS) {
   const long long total = (long long)N * Cp * S;
   for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < total;
        o += (long long)gridDim.x * blockDim.x) {
@@ -278,6 +280,32 @@ __global__ void to_nhwc_pad_kernel(const void* __restrict__ x, int in_dtype, bf1
                         : reinterpret_cast<const bf16_t*>(x)[i];
     }
     y[o] = v;
+  }
+}
+
+template <typename IDX>
+__global__ void to_nhwc_pad_kernel(const void* __restrict__ x, int in_dtype, bf16_t* __restrict__ y,
+                                   int N, int C, int Cp, long long S, long long sN, long long sC,
+                                   long long sS) {
+  const int G = Cp / 8;
+  const IDX total = (IDX)N * (IDX)S * G;
+  for (IDX o = blockIdx.x * (IDX)blockDim.x + threadIdx.x; o < total;
+       o += (IDX)gridDim.x * blockDim.x) {
+    const int gi = (int)(o % G);
+    const IDX ps = o / G;
+    const IDX s = ps % (IDX)S, n = ps / (IDX)S;
+    float f[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = gi * 8 + j;
+      f[j] = 0.f;
+      if (c < C) {
+        const long long i = (long long)n * sN + (long long)c * sC + (long long)s * sS;
+        f[j] = in_dtype == 0 ? reinterpret_cast<const float*>(x)[i]
+                             : bf2f(reinterpret_cast<const bf16_t*>(x)[i]);
+      }
+    }
+    reinterpret_cast<uint4*>(y)[o] = pack8(f);
   }
 }
 
@@ -389,10 +417,21 @@ void bilinear_up2_bwd_launch(const bf16_t* dy, float* dx_f32, bf16_t* dx, int di
 
 void to_nhwc_pad_launch(const void* x, int in_dtype, bf16_t* y, int N, int C, int Cp, long long S,
                         long long sN, long long sC, long long sS, hipStream_t st) {
-  const long long total = (long long)N * Cp * S;
+  if (Cp % 8 != 0) {
+    const long long total = (long long)N * Cp * S;
+    const int grid = (int)std::min<long long>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(to_nhwc_generic_kernel, dim3(grid), dim3(256), 0, st, x, in_dtype, y, N, C, Cp,
+                       S, sN, sC, sS);
+    return;
+  }
+  const long long total = (long long)N * S * (Cp / 8);
   const int grid = (int)std::min<long long>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(to_nhwc_pad_kernel, dim3(grid), dim3(256), 0, st, x, in_dtype, y, N, C, Cp, S,
-                     sN, sC, sS);
+  if (total < (1LL << 31))
+    hipLaunchKernelGGL(to_nhwc_pad_kernel<int>, dim3(grid), dim3(256), 0, st, x, in_dtype, y, N, C, Cp,
+                       S, sN, sC, sS);
+  else
+    hipLaunchKernelGGL(to_nhwc_pad_kernel<long long>, dim3(grid), dim3(256), 0, st, x, in_dtype, y, N,
+                       C, Cp, S, sN, sC, sS);
 }
 
 void channel_sum_launch(const bf16_t* x, long long P, int C, float* partial, int nblocks,
