@@ -65,7 +65,18 @@ def main():
     ap.add_argument("--verbose", type=int, default=0, help="1: progress lines on stderr")
     ap.add_argument("--hip-graph", type=int, default=int(os.environ.get("DDLPC_HIP_GRAPH", "0")),
                     help="1: replay the single-GPU train step as one hipGraph")
+    ap.add_argument("--heartbeat", type=float, default=0.0,
+                    help="seconds between 'alive' lines on stderr (long first-step autotuning)")
     args = ap.parse_args()
+    if args.heartbeat > 0:
+        import threading
+
+        def _beat():
+            t0 = time.time()
+            while True:
+                time.sleep(args.heartbeat)
+                print(f"alive {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
+        threading.Thread(target=_beat, daemon=True).start()
 
     from ddlpc.config import ModelConfig, TrainConfig
     from ddlpc.data import device_random_batch
