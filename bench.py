@@ -38,7 +38,8 @@ def _baseline(args):
     try:
         with open(p) as f:
             b = json.load(f).get("inhouse_baseline", {})
-        v = {32: b.get("images_per_sec_per_gpu"), 64: b.get("batch_64_images_per_sec")}.get(args.batch)
+        v = {32: b.get("images_per_sec_per_gpu"), 64: b.get("batch_64_images_per_sec"),
+             128: b.get("batch_128_images_per_sec")}.get(args.batch)
         return float(v) if v else None
     except Exception:
         return None
@@ -49,8 +50,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64,
-                    help="per-GPU batch (images); 64 = the largest batch with a measured in-house baseline")
+    ap.add_argument("--batch", type=int, default=128,
+                    help="per-GPU batch (images); 32 / 64 / 128 have measured in-house baselines")
     ap.add_argument("--accum", type=int, default=1)
     ap.add_argument("--tile", type=int, default=256)
     ap.add_argument("--width-divisor", type=int, default=2)
