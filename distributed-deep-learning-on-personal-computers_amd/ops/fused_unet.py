@@ -241,9 +241,14 @@ class _ConvTFn(torch.autograd.Function):
         rows = getattr(dout, "_ddlpc_colsum_rows", None)
         eng = ctx.engine
         if eng.direct_grads:
-            with eng.wgrad_stream(x, dout, rows, bn):
+            if eng.side_convt:
+                with eng.wgrad_stream(x, dout, rows, bn):
+                    F.convt_wgrad(x, dout, conv.weight.grad, conv.bias.grad, rows, bn)
+                    eng.ready(conv.weight, conv.bias)
+            else:
                 F.convt_wgrad(x, dout, conv.weight.grad, conv.bias.grad, rows, bn)
-                eng.ready(conv.weight, conv.bias)
+                with eng.wgrad_stream():
+                    eng.ready(conv.weight, conv.bias)
             return dx, None, None, None, None, None
         dw, db = F.convt_wgrad(x, dout, None, None, rows, bn)
         return dx, dw.view_as(conv.weight), db, None, None, None
@@ -342,6 +347,8 @@ class UNetEngine:
         self._side_used = False
         # deferred BatchNorm activations (see ``features``): DDLPC_DEFER_BN=all|convt|none
         self.defer_mode = os.environ.get("DDLPC_DEFER_BN", "all")
+        # transposed-conv weight gradients on the side stream too (DDLPC_SIDE_CONVT=0: main)
+        self.side_convt = os.environ.get("DDLPC_SIDE_CONVT", "1") != "0"
         self.enc = [_Block(b.double_conv, first=(i == 0), engine=self)
                     for i, b in enumerate(model.down_blocks())]
         self.mid = _Block(model.double_conv, first=False, engine=self)
@@ -391,6 +398,8 @@ class UNetEngine:
             self._side_used = False
         # deferred BatchNorm activations (see ``features``): DDLPC_DEFER_BN=all|convt|none
         self.defer_mode = os.environ.get("DDLPC_DEFER_BN", "all")
+        # transposed-conv weight gradients on the side stream too (DDLPC_SIDE_CONVT=0: main)
+        self.side_convt = os.environ.get("DDLPC_SIDE_CONVT", "1") != "0"
 
     def ready(self, *params):
         """Gradients of ``params`` are complete once the queued work finishes.  Called on
