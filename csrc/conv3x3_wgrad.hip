@@ -480,14 +480,30 @@ void launch_wg(ConvWgradArgs& a, hipStream_t st) {
 
 }  // namespace
 
+// pixel-tile size of the 2-D kernel.  BCO 64: 128-pixel tiles (two 60 KB workgroups per CU)
+// except for the large concat layers (two input tensors, >= 64x64 images), which measured
+// 25% faster with 96-pixel tiles (three 46 KB workgroups per CU) and slower elsewhere
+// (conv_micro, batch 128).  DDLPC_WGRAD64_PT = 64 | 96 | 128 | 256 forces one size.
+int conv3_wgrad2_pt(int bco, int C2, int H, int W) {
+  static const int force = [] { const char* e = getenv("DDLPC_WGRAD64_PT"); return e ? atoi(e) : 0; }();
+  if (bco == 32) return 256;
+  if (force == 64 || force == 96 || force == 128 || force == 256) return force;
+  return (C2 > 0 && H * W >= 64 * 64) ? 96 : 128;
+}
 void conv3_wgrad2_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
   const int grid = a.coTiles * a.ciChunks * a.splits;
+  const int pt = a.TH * 16;
   if (bco == 32)
     hipLaunchKernelGGL((conv3_wgrad2_kernel<32, 256>), dim3(grid), dim3(256), (Wg2Cfg<32, 256>::SMEM), st, a);
+  else if (pt == 256)
+    hipLaunchKernelGGL((conv3_wgrad2_kernel<64, 256>), dim3(grid), dim3(256), (Wg2Cfg<64, 256>::SMEM), st, a);
+  else if (pt == 96)
+    hipLaunchKernelGGL((conv3_wgrad2_kernel<64, 96>), dim3(grid), dim3(256), (Wg2Cfg<64, 96>::SMEM), st, a);
+  else if (pt == 64)
+    hipLaunchKernelGGL((conv3_wgrad2_kernel<64, 64>), dim3(grid), dim3(256), (Wg2Cfg<64, 64>::SMEM), st, a);
   else
     hipLaunchKernelGGL((conv3_wgrad2_kernel<64, 128>), dim3(grid), dim3(256), (Wg2Cfg<64, 128>::SMEM), st, a);
 }
-int conv3_wgrad2_pt(int bco) { return bco == 32 ? 256 : 128; }
 
 void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
   if (a.dims == 2) {

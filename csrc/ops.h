@@ -64,7 +64,7 @@ struct ConvWgradArgs {
 void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st);
 // 2-D LDS-DMA variant (16-wide pixel tiles of conv3_wgrad2_pt(bco) pixels; planes = 1)
 void conv3_wgrad2_launch(ConvWgradArgs& a, int bco, hipStream_t st);
-int conv3_wgrad2_pt(int bco);
+int conv3_wgrad2_pt(int bco, int C2, int H, int W);
 
 int conv3_wgrad_halo_cap(int dims);
 

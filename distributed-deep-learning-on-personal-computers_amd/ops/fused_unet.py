@@ -379,7 +379,8 @@ class UNetEngine:
         """Context for weight-gradient work: the side stream first waits for everything
         queued so far on the compute stream; tensors allocated there and read on the side
         stream are marked so the caching allocator does not recycle them early."""
-        if self.side is None or not self.direct_grads:
+        if self.side is None or not self.direct_grads or torch.cuda.is_current_stream_capturing():
+            # (hipGraph replay runs the captured streams serially: no gain from forking)
             return contextlib.nullcontext()
         cur = torch.cuda.current_stream(self.side.device)
         self.side.wait_stream(cur)
