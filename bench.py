@@ -64,6 +64,8 @@ def main():
     ap.add_argument("--codec", default="none")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--verbose", type=int, default=0, help="1: progress lines on stderr")
+    ap.add_argument("--schedule", default="auto", choices=["auto", "overlap", "serial"],
+                    help="weight-gradient stream: auto = time both during warm-up, keep the faster")
     ap.add_argument("--hip-graph", type=int, default=int(os.environ.get("DDLPC_HIP_GRAPH", "0")),
                     help="1: replay the single-GPU train step as one hipGraph")
     ap.add_argument("--heartbeat", type=float, default=0.0,
@@ -121,12 +123,22 @@ def main():
         step(i)
         if args.verbose and rank == 0:
             print(f"warmup step {i} done", file=sys.stderr, flush=True)
+    # schedule calibration (untimed): overlapped weight-gradient stream vs serial
+    sched = {}
+    if args.schedule == "auto":
+        sched = tr.choose_schedule(pool[0:1] if args.accum == 1 else
+                                   [pool[j % len(pool)] for j in range(args.accum)])
+        if rank == 0 and sched:
+            print(f"schedule: {sched}", file=sys.stderr, flush=True)
+    elif args.schedule == "serial" and tr.impl == "hip":
+        tr.model._engine.set_side_stream(False)
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
     sync()
     dt = time.perf_counter() - t0
+    mstats = torch.cuda.memory_stats(device) if dev == "cuda" else {}
     t = torch.tensor([dt], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -164,7 +176,12 @@ def main():
                        "optimizer": "Adam(lr=1e-3)", "loss": "CrossEntropy",
                        "train_loss_mean": round(loss["loss"], 4),
                        "peak_mem_gb": (round(torch.cuda.max_memory_allocated(device) / 2**30, 2)
-                                       if dev == "cuda" else None)},
+                                       if dev == "cuda" else None),
+                       "schedule": ("overlap" if sched.get("side_stream") else "serial") if sched
+                                   else args.schedule,
+                       "alloc_retries": mstats.get("num_alloc_retries"),
+                       "device_mallocs": mstats.get("num_device_alloc"),
+                       "device_frees": mstats.get("num_device_free")},
         }
         print(json.dumps(rec), flush=True)
     tr.close()

@@ -272,7 +272,11 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   // split-K over pixel tiles: enough blocks to fill the chip, but every block keeps >= 8
   // tiles so the fp32 partial slab stays small next to the MFMA work
   const int base = a.coTiles * a.ciChunks * a.planes;
-  const int target = 2 * num_cus();
+  // workgroups per CU to aim for (DDLPC_WGRAD_WG_PER_CU): the weight gradient runs
+  // concurrently with the data-gradient chain, and its resident workgroups' LDS decides
+  // what else fits on a CU
+  static const int wg_per_cu = [] { const char* e = getenv("DDLPC_WGRAD_WG_PER_CU"); return e ? std::max(1, atoi(e)) : 2; }();
+  const int target = wg_per_cu * num_cus();
   int splits = std::max(1, (target + base - 1) / base);
   splits = std::min(splits, std::max(1, a.nTiles / 8));
   a.splits = splits;

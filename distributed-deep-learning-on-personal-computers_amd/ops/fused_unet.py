@@ -344,6 +344,7 @@ class UNetEngine:
         # chain is dispatched first and the weight gradients fill what is left
         prio = int(os.environ.get("DDLPC_SIDE_PRIORITY", "1"))
         self.side = torch.cuda.Stream(dev, priority=prio) if use_side else None
+        self._side_stream = self.side
         self._side_used = False
         # deferred BatchNorm activations (see ``features``): DDLPC_DEFER_BN=all|convt|none
         self.defer_mode = os.environ.get("DDLPC_DEFER_BN", "all")
@@ -374,6 +375,14 @@ class UNetEngine:
                 raise RuntimeError("direct grads need persistent contiguous .grad buffers")
         self.direct_grads = True
         self.grad_ready = grad_ready
+
+    def set_side_stream(self, enabled: bool):
+        """Switch the weight-gradient side stream on/off between steps (see
+        ``Trainer.choose_schedule``)."""
+        if enabled and self._side_stream is None:
+            self._side_stream = torch.cuda.Stream(next(self.model.parameters()).device)
+        self.join()
+        self.side = self._side_stream if enabled else None
 
     def wgrad_stream(self, *tensors):
         """Context for weight-gradient work: the side stream first waits for everything

@@ -237,6 +237,32 @@ class Trainer:
         if k and self.step_count % k == 0:
             assert_replicas_identical(self.model)
 
+    def choose_schedule(self, micro_batches, steps: int = 3) -> Dict[str, float]:
+        """Time ``steps`` optimizer steps with the weight-gradient side stream and without
+        it, and keep the faster schedule.  (On some hosts the second hardware queue is
+        intermittently time-sliced and cross-stream waits cost milliseconds, which makes
+        the overlapped schedule several times slower than the serial one.)  All ranks
+        agree on the choice (MAX of the per-rank times).  Performs 2*steps+2 real steps."""
+        eng = self.model._engine if self.impl == "hip" else None
+        if eng is None or eng._side_stream is None or self.device.type != "cuda":
+            return {}
+        times = {}
+        for mode in (True, False):
+            eng.set_side_stream(mode)
+            self.train_step(micro_batches)
+            torch.cuda.synchronize(self.device)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                self.train_step(micro_batches)
+            torch.cuda.synchronize(self.device)
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=self.device)
+            if self.world > 1:
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            times[mode] = float(t.item()) / steps
+        best = times[True] <= times[False]
+        eng.set_side_stream(best)
+        return {"side_stream": best, "side_ms": times[True] * 1e3, "serial_ms": times[False] * 1e3}
+
     def fit(self) -> Dict[str, float]:
         c = self.cfg
         self.logger.header(c.batch_per_gpu, self.world, c.accum_steps, c.model.width_divisor)

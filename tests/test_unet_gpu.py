@@ -156,3 +156,19 @@ def test_hip_checkpoint_resume_is_exact(tmp_path):
     for k, v in tr2.model.state_dict().items():      # BN running statistics too
         assert torch.equal(v, want_state[k]), k
     tr2.close()
+
+
+def test_choose_schedule_times_both_and_keeps_faster():
+    from ddlpc.config import ModelConfig, TrainConfig
+    from ddlpc.data import device_random_batch
+    from ddlpc.train.trainer import Trainer
+    cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=4,
+                      num_samples=1, test_holdout=0, impl="hip")
+    tr = Trainer(cfg, device="cuda")
+    r = tr.choose_schedule([device_random_batch(4, 64, 6, tr.device)], steps=2)
+    assert set(r) == {"side_stream", "side_ms", "serial_ms"} and r["side_ms"] > 0
+    eng = tr.model._engine
+    assert (eng.side is not None) == r["side_stream"]
+    assert (r["side_ms"] <= r["serial_ms"]) == r["side_stream"]
+    assert tr.optimizer.step_count == 6
+    tr.close()
