@@ -255,7 +255,7 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   if (a.pscale) TORCH_CHECK(a.C1 <= 512, "prologue supports C1 <= 512");
   const int bco = a.Cout <= 32 ? 32 : 64;
   static const int use_v2 = [] { const char* e = getenv("DDLPC_WGRAD_V2"); return e ? atoi(e) : 1; }();
-  const bool v2 = use_v2 && g.dims == 2 && g.W >= 16 && (a.C2 == 0 || a.C1 % 32 == 0);
+  const bool v2 = use_v2 && (use_v2 != 2 || g.dims == 2) && g.W >= 16 && (a.C2 == 0 || a.C1 % 32 == 0);
   // 128-pixel tiles (v2: 16 x conv3_wgrad2_pt/16)
   if (v2) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad2_pt(bco, a.C2, g.H, g.W) / 16; }
   else if (g.dims == 2) { a.TD = 1; a.TW = g.W >= 16 ? 16 : 8; a.TH = 128 / a.TW; }

@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad_kernel(ConvWgradArgs p) {
   (void)tiles_per_img;
 }
 
-// ============================================================================ 2-D, v2
+// ============================================================================ v2 (2-D; 3-D as 1-deep tiles per depth tap plane)
 // Same GEMM and partial-slab contract, restructured like the forward kernels:
 //   * both operands arrive by LDS-DMA into DOUBLE-BUFFERED LDS (no VGPR round trip, no
 //     integer division in the tile loop: per-lane source geometry is tile independent);
@@ -305,8 +305,13 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
   int b = xcd_remap(blockIdx.x, gridDim.x);
   const int cic = b % p.ciChunks; b /= p.ciChunks;
   const int cot = b % p.coTiles; b /= p.coTiles;
+  // 3-D: one depth tap plane kd per workgroup (planes = 3).  With 1-deep pixel tiles the
+  // plane's 9 taps are a 2-D weight gradient of dY slice d against X slice d + kd - 1, so
+  // the (n, d) slices are the "images" and the X image is shifted by kd - 1
+  const int plane = b % p.planes; b /= p.planes;
   const int split = b;
   const int co0 = cot * BCO, ci0 = cic * BK;
+  const int dshift = p.planes == 3 ? plane - 1 : 0;
 
   const bool has_pro = p.pscale != nullptr;
   if (has_pro)
@@ -347,7 +352,9 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
     int t = tile;
     const int tw_i = t % p.tilesW; t /= p.tilesW;
     const int th_i = t % p.tilesH; t /= p.tilesH;
-    const int n = t;
+    const int n = t;                                 // (n, d) slice
+    const int dx = n % p.D + dshift;
+    const bool dok = dx >= 0 && dx < p.D;
     const int h0 = th_i * TH, w0 = tw_i * 16;
     const auto ry = make_rsrc(p.dY + n * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
     const int ybase = (h0 * p.W + w0) * p.Cout;
@@ -357,12 +364,12 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
       const bool ok = y_rel[i] >= 0 && w0 + y_pw[i] < p.W && h0 + y_ph[i] < p.H;
       dma16(ry, sY(buf) + (i * 4 + wave) * 1024, ok ? (unsigned)(ybase + y_rel[i]) * 2u : kOOB);
     }
-    const auto rx = make_rsrc(xsrc + n * img_px * Cs, (unsigned)(img_px * Cs * 2));
+    const auto rx = make_rsrc(xsrc + (n + (dok ? dshift : 0)) * img_px * Cs, (unsigned)(img_px * Cs * 2));
 #pragma unroll
     for (int i = 0; i < Cfg::X_ITERS; ++i) {
       if ((i * 4 + wave) >= Cfg::X_INSTR) break;
       const int gw = w0 + x_dw[i], gh = h0 + x_dh[i];
-      x_pix[i] = (gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && xch_ok) ? gh * p.W + gw : -1;
+      x_pix[i] = (gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && xch_ok && dok) ? gh * p.W + gw : -1;
       dma16(rx, sX(buf) + (i * 4 + wave) * 1024, x_pix[i] >= 0 ? (unsigned)(x_pix[i] * Cs + cs0) * 2u : kOOB);
     }
   };
@@ -454,19 +461,19 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
   }
 
   // ---- partial slab: part[split][co][tap][ci]
-  float* out = p.partial + (long long)split * p.Cout * 9 * p.Cin;
+  float* out = p.partial + (long long)split * p.Cout * p.taps * p.Cin;
 #pragma unroll
   for (int pi = 0; pi < Cfg::NP; ++pi) {
     const int pair = wave + 4 * pi;
     if (pair >= npairs) continue;
-    const int tap = half_only ? pair : pair >> 1;
+    const int tap = plane * 9 + (half_only ? pair : pair >> 1);
     const int ci = ci0 + (half_only ? 0 : (pair & 1) * 16) + (lane & 15);
 #pragma unroll
     for (int j = 0; j < Cfg::NCO; ++j)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int co = co0 + j * 16 + 4 * g + i;
-        if (co < p.Cout && ci < p.Cin) out[((long long)co * 9 + tap) * p.Cin + ci] = acc[j][pi][i];
+        if (co < p.Cout && ci < p.Cin) out[((long long)co * p.taps + tap) * p.Cin + ci] = acc[j][pi][i];
       }
   }
 }
@@ -491,7 +498,7 @@ int conv3_wgrad2_pt(int bco, int C2, int H, int W) {
   return (C2 > 0 && H * W >= 64 * 64) ? 96 : 128;
 }
 void conv3_wgrad2_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
-  const int grid = a.coTiles * a.ciChunks * a.splits;
+  const int grid = a.coTiles * a.ciChunks * a.planes * a.splits;
   const int pt = a.TH * 16;
   if (bco == 32)
     hipLaunchKernelGGL((conv3_wgrad2_kernel<32, 256>), dim3(grid), dim3(256), (Wg2Cfg<32, 256>::SMEM), st, a);

@@ -62,7 +62,8 @@ struct ConvWgradArgs {
   int coTiles, ciChunks, planes, splits;
 };
 void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st);
-// 2-D LDS-DMA variant (16-wide pixel tiles of conv3_wgrad2_pt(bco) pixels; planes = 1)
+// LDS-DMA variant (1 x TH x 16 pixel tiles of conv3_wgrad2_pt(bco) pixels; 3-D: planes = 3,
+// one depth tap plane per workgroup)
 void conv3_wgrad2_launch(ConvWgradArgs& a, int bco, hipStream_t st);
 int conv3_wgrad2_pt(int bco, int C2, int H, int W);
 

@@ -365,6 +365,34 @@ def test_conv3d_fwd_wgrad(ops):
     assert rel_err(nchw(dx), gx) < 1e-2
 
 
+@pytest.mark.parametrize("N,D,H,W,C1,C2,Cout,pro", [
+    (2, 5, 12, 20, 32, 0, 64, True), (1, 4, 16, 16, 32, 32, 32, True),
+    (2, 3, 8, 16, 64, 64, 64, False), (1, 4, 8, 16, 3, 0, 32, False),
+    (1, 3, 8, 8, 32, 0, 64, False)])
+def test_conv3d_wgrad(ops, N, D, H, W, C1, C2, Cout, pro):
+    # 3-D weight gradient: LDS-DMA kernel (one depth tap plane per workgroup, W >= 16) and
+    # the legacy kernel (W < 16)
+    torch.manual_seed(13)
+    x1 = torch.randn(N, C1, D, H, W, device=DEV).bfloat16()
+    x2 = torch.randn(N, C2, D, H, W, device=DEV).bfloat16() if C2 else None
+    dy = torch.randn(N, Cout, D, H, W, device=DEV).bfloat16()
+    scale = shift = None
+    a1 = x1.float()
+    if pro:
+        scale = torch.rand(C1, device=DEV) + 0.5
+        shift = torch.randn(C1, device=DEV) * 0.5
+        bc = (None, slice(None), None, None, None)
+        a1 = torch.relu(x1.float() * scale[bc] + shift[bc]).bfloat16().float()
+    xin = torch.cat([a1, x2.float()], 1) if x2 is not None else a1
+    xin1 = ops.to_nhwc_bf16(x1, 8) if C1 % 8 else nhwc(x1)
+    dw = ops.conv3_wgrad(nhwc(dy), xin1, nhwc(x2) if x2 is not None else None, scale, shift)
+    dw = dw[:, :C1 + C2]
+    w = torch.zeros(Cout, C1 + C2, 3, 3, 3, device=DEV, requires_grad=True)
+    (g,) = torch.autograd.grad(F.conv3d(xin, w, padding=1), w, dy.float())
+    assert dw.shape == g.shape
+    assert rel_err(dw, g) < 5e-3
+
+
 def _bn4(C, seed):
     g = torch.Generator(device=DEV).manual_seed(seed)
     mean = torch.randn(C, device=DEV, generator=g) * 0.2
