@@ -203,15 +203,16 @@ __global__ void bn_bwd_kernel(const bf16_t* __restrict__ dA, const bf16_t* __res
   }
 }
 
-// 2-D backward, v2: fully coalesced and unrolled.  A thread keeps one 8-channel group
+// Backward, v2: fully coalesced and unrolled.  A thread keeps one 8-channel group
 // (constants in registers); consecutive lanes walk consecutive 16-B pieces of memory:
-//   no pool: unit = pixel, lanes (cg) cover the pixel's C channels;
-//   pool:    unit = 2x2 window, lanes (kw, cg) cover the window's top-row pixel pair
-//            contiguously and each lane also handles the pixel below it; the window arg-max
-//            is completed with the kw partner lane (lane ^ G) — first maximum wins in
-//            PyTorch's (kh, kw) scan order.
-// Requires G = C/8 a power of two (pool: G <= 32) and even H, W for pool.
-template <bool POOL, int MODE>
+//   no pool: unit = pixel, lanes (cg) cover the pixel's C channels (3-D: N*D slices);
+//   pool:    unit = 2x2 (3-D: 2x2x2) window, lanes (kw, cg) cover the window's top-row pixel
+//            pair contiguously and each lane also handles the pixels below it (kh) and, in
+//            3-D, in the next slice (kd); the window arg-max is completed with the kw
+//            partner lane (lane ^ G) — first maximum wins in PyTorch's (kd, kh, kw) scan
+//            order.
+// Requires G = C/8 a power of two (pool: G <= 32) and even D, H, W for pool.
+template <int DIMS, bool POOL, int MODE>
 __global__ __launch_bounds__(256) void bn_bwd2_kernel(
     const bf16_t* __restrict__ dA, const bf16_t* __restrict__ dP, const bf16_t* __restrict__ y,
     const float* __restrict__ scale, const float* __restrict__ shift,
@@ -225,8 +226,9 @@ __global__ __launch_bounds__(256) void bn_bwd2_kernel(
   const int cg = tid % G, c8 = cg * 8;
   const int kw = POOL ? (tid / G) & 1 : 0;
   const int upb = 256 / L;                        // units per block per step
-  const int Wo = W / 2;
-  const int units = POOL ? N * (H / 2) * Wo : N * H * W;
+  const int Wo = W / 2, Ho = H / 2;
+  // N counts (n, d) slices; a 3-D pooled unit row covers slices 2*nd and 2*nd + 1
+  const int units = POOL ? (DIMS == 3 ? N / 2 : N) * Ho * Wo : N * H * W;
   const int stride = gridDim.x * upb;
   const float gs = gscale != nullptr ? gscale[0] : 1.0f;
   float sc[8], sh[8], is[8], nm[8], k1[8], m1[8], m2[8], s1[8], s2[8];
@@ -237,7 +239,7 @@ __global__ __launch_bounds__(256) void bn_bwd2_kernel(
     if (MODE == 1) { k1[j] = coefs[c8 + j]; m1[j] = coefs[C + c8 + j]; m2[j] = coefs[2 * C + c8 + j]; }
     s1[j] = 0.f; s2[j] = 0.f;
   }
-  constexpr int NK = POOL ? 2 : 1;                // pixels per lane per unit (kh)
+  constexpr int NK = POOL ? (DIMS == 3 ? 4 : 2) : 1;  // pixels per lane per unit (k = 2*kd + kh)
   for (int u0 = blockIdx.x * upb + tid / L; u0 < units; u0 += UNROLL * stride) {
     uint4 vy[UNROLL][NK], vd[UNROLL][NK], vp[UNROLL];
     long long off[UNROLL][NK];
@@ -249,9 +251,16 @@ __global__ __launch_bounds__(256) void bn_bwd2_kernel(
       const int uu = ok[r] ? u : u0;
       if (POOL) {
         const int rr = uu / Wo, wo = uu - rr * Wo;
-        const long long pix0 = (long long)rr * 2 * W + 2 * wo + kw;
-        off[r][0] = pix0 * C + c8;
-        off[r][NK - 1] = (pix0 + W) * C + c8;
+        long long pix0;
+        if (DIMS == 3) {
+          const int nd = rr / Ho, ho = rr - nd * Ho;
+          pix0 = ((long long)(2 * nd) * H + 2 * ho) * W + 2 * wo + kw;
+        } else {
+          pix0 = (long long)rr * 2 * W + 2 * wo + kw;
+        }
+#pragma unroll
+        for (int k = 0; k < NK; ++k)
+          off[r][k] = (pix0 + (long long)(k >> 1) * H * W + (k & 1) * W) * C + c8;
         vp[r] = *reinterpret_cast<const uint4*>(dP + (long long)uu * C + c8);
       } else {
         off[r][0] = (long long)uu * C + c8;
@@ -270,10 +279,10 @@ __global__ __launch_bounds__(256) void bn_bwd2_kernel(
       for (int k = 0; k < NK; ++k) { unpack8(vy[r][k], fy[k]); unpack8(vd[r][k], fd[k]); }
       if (POOL) {
         unpack8(vp[r], fp);
-        // bf16-rounded activations of my two pixels, partner's via lane ^ G
-        float a[2][8];
+        // bf16-rounded activations of my NK pixels, partner's via lane ^ G
+        float a[NK][8];
 #pragma unroll
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < NK; ++k)
 #pragma unroll
           for (int j = 0; j < 8; j += 2) {
             const uint32_t w2 = pack2(fmaxf(fmaf(fy[k][j], sc[j], sh[j]), 0.f),
@@ -282,16 +291,17 @@ __global__ __launch_bounds__(256) void bn_bwd2_kernel(
           }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float p0 = __shfl_xor(a[0][j], G, 64), p1 = __shfl_xor(a[1][j], G, 64);
-          // window values in scan order w = 2*kh + kw
-          const float v0 = kw ? p0 : a[0][j], v1 = kw ? a[0][j] : p0;
-          const float v2 = kw ? p1 : a[1][j], v3 = kw ? a[1][j] : p1;
+          // window values in scan order w = 2*k + kw (k = 2*kd + kh)
           int best = 0;
-          float bv = v0;
-          if (v1 > bv) { bv = v1; best = 1; }
-          if (v2 > bv) { bv = v2; best = 2; }
-          if (v3 > bv) { best = 3; }
-          bestk[j] = best;                        // routed to (kh, kw) = (best >> 1, best & 1)
+          float bv = 0.f;
+#pragma unroll
+          for (int k = 0; k < NK; ++k) {
+            const float pk = __shfl_xor(a[k][j], G, 64);
+            const float v0 = kw ? pk : a[k][j], v1 = kw ? a[k][j] : pk;
+            if (k == 0 || v0 > bv) { bv = v0; best = 2 * k; }
+            if (v1 > bv) { bv = v1; best = 2 * k + 1; }
+          }
+          bestk[j] = best;                        // routed to (k, kw) = (best >> 1, best & 1)
         }
       }
       if (!ok[r]) continue;
@@ -344,11 +354,30 @@ int bn_bwd_reduce_blocks(long long items) {
 }
 
 namespace {
-bool bn_bwd2_ok(int dims, bool pool, int H, int W, int C) {
+bool bn_bwd2_ok(int dims, bool pool, int D, int H, int W, int C) {
+  static const int v2 = [] { const char* e = getenv("DDLPC_BN_BWD_V2"); return e ? atoi(e) : 1; }();
   const int G = C / 8;
-  if (dims != 2 || C % 8 != 0 || (G & (G - 1)) != 0 || G > 256) return false;
-  if (pool && (G > 32 || H % 2 != 0 || W % 2 != 0)) return false;
+  if (!v2 || (v2 == 2 && dims == 3)) return false;
+  if (C % 8 != 0 || (G & (G - 1)) != 0 || G > 256) return false;
+  if (pool && (G > 32 || H % 2 != 0 || W % 2 != 0 || (dims == 3 && D % 2 != 0))) return false;
   return true;
+}
+
+template <int MODE>
+void bn_bwd2_launch(int grid, int dims, bool pool, const bf16_t* dA, const bf16_t* dP,
+                    const bf16_t* y, const float* scale, const float* shift, const float* mean,
+                    const float* invstd, const float* coefs, const float* gscale, float* partial,
+                    bf16_t* dY, int N, int D, int H, int W, int C, hipStream_t st) {
+  const int ND = N * (dims == 3 ? D : 1);
+  if (dims == 3 && pool)
+    hipLaunchKernelGGL((bn_bwd2_kernel<3, true, MODE>), dim3(grid), dim3(256), 0, st, dA, dP, y,
+                       scale, shift, mean, invstd, coefs, gscale, partial, dY, ND, H, W, C);
+  else if (pool)
+    hipLaunchKernelGGL((bn_bwd2_kernel<2, true, MODE>), dim3(grid), dim3(256), 0, st, dA, dP, y,
+                       scale, shift, mean, invstd, coefs, gscale, partial, dY, ND, H, W, C);
+  else
+    hipLaunchKernelGGL((bn_bwd2_kernel<2, false, MODE>), dim3(grid), dim3(256), 0, st, dA, dP, y,
+                       scale, shift, mean, invstd, coefs, gscale, partial, dY, ND, H, W, C);
 }
 }  // namespace
 
@@ -403,11 +432,9 @@ void bn_bwd_reduce_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y,
   const bool pool = dP != nullptr;
   const float* coefs = nullptr;
   bf16_t* dY = nullptr;
-  if (bn_bwd2_ok(dims, pool, H, W, C)) {
-    if (pool) hipLaunchKernelGGL((bn_bwd2_kernel<true, 0>), dim3(nblocks), dim3(256), 0, st, dA, dP, y,
-                                 scale, shift, mean, invstd, coefs, gscale, partial, dY, N, H, W, C);
-    else hipLaunchKernelGGL((bn_bwd2_kernel<false, 0>), dim3(nblocks), dim3(256), 0, st, dA, dP, y,
-                            scale, shift, mean, invstd, coefs, gscale, partial, dY, N, H, W, C);
+  if (bn_bwd2_ok(dims, pool, D, H, W, C)) {
+    bn_bwd2_launch<0>(nblocks, dims, pool, dA, dP, y, scale, shift, mean, invstd, coefs, gscale,
+                      partial, dY, N, D, H, W, C, st);
     return;
   }
   BN_BWD_DISPATCH(0, nblocks);
@@ -423,13 +450,11 @@ void bn_bwd_apply_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y, co
   const long long items = (long long)N * (pool ? (dims == 3 ? D / 2 : 1) * (H / 2) * (W / 2)
                                                 : (long long)D * H * W);
   const int per = std::max(1, 256 / G);
-  if (bn_bwd2_ok(dims, pool, H, W, C)) {
+  if (bn_bwd2_ok(dims, pool, D, H, W, C)) {
     const int upb = 256 / (pool ? 2 * G : G);
     const int grid2 = (int)std::max<long long>(1, std::min<long long>((items + 2 * upb - 1) / (2 * upb), 8192));
-    if (pool) hipLaunchKernelGGL((bn_bwd2_kernel<true, 1>), dim3(grid2), dim3(256), 0, st, dA, dP, y,
-                                 scale, shift, mean, invstd, coefs, gscale, partial, dY, N, H, W, C);
-    else hipLaunchKernelGGL((bn_bwd2_kernel<false, 1>), dim3(grid2), dim3(256), 0, st, dA, dP, y,
-                            scale, shift, mean, invstd, coefs, gscale, partial, dY, N, H, W, C);
+    bn_bwd2_launch<1>(grid2, dims, pool, dA, dP, y, scale, shift, mean, invstd, coefs, gscale,
+                      partial, dY, N, D, H, W, C, st);
     return;
   }
   const int grid = std::min(grid_for(items, per), 16384);

@@ -221,6 +221,41 @@ def test_bn_forward_backward(ops, N, H, W, C, pool):
     del pooled
 
 
+@pytest.mark.parametrize("N,D,H,W,C,pool", [
+    (2, 4, 8, 16, 32, True), (1, 6, 12, 8, 64, True), (1, 4, 16, 16, 256, True),
+    (2, 3, 8, 8, 32, False), (1, 2, 4, 6, 128, False)])
+def test_bn3d_forward_backward(ops, N, D, H, W, C, pool):
+    torch.manual_seed(14)
+    y = (torch.randn(N, C, D, H, W, device=DEV) * 2 + 0.5).bfloat16()
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    yf = y.float()
+    partial = torch.stack([yf.sum((0, 2, 3, 4)), (yf * yf).sum((0, 2, 3, 4))])[None].contiguous()
+    s4 = ops.bn_finalize(partial, float(N * D * H * W), gamma, beta, rm, rv, 0.1, 1e-5, True, None)
+    bn = torch.nn.BatchNorm3d(C).to(DEV)
+    with torch.no_grad():
+        bn.weight.copy_(gamma)
+        bn.bias.copy_(beta)
+    yr = yf.clone().requires_grad_(True)
+    ar = torch.relu(bn(yr))
+    a, p = ops.bn_relu_apply(nhwc(y), s4, pool)
+    assert rel_err(nchw(a), ar) < 5e-3
+    if pool:
+        assert rel_err(nchw(p), F.max_pool3d(nchw(a).float(), 2)) < 1e-6
+    dA = torch.randn(N, C, D, H, W, device=DEV).bfloat16()
+    dP = torch.randn(N, C, D // 2, H // 2, W // 2, device=DEV).bfloat16()
+    dy, dg, db = ops.bn_backward(nhwc(dA), nhwc(dP) if pool else None, nhwc(y), s4, gamma, None)
+    loss = (ar * dA.float()).sum()
+    if pool:   # the kernel routes the pooled gradient by the bf16 activations' arg-max
+        idx = F.max_pool3d(ar.bfloat16().float(), 2, return_indices=True)[1]
+        loss = loss + (ar.flatten(2).gather(2, idx.flatten(2)) * dP.float().flatten(2)).sum()
+    gy, gg, gb = torch.autograd.grad(loss, [yr, bn.weight, bn.bias])
+    assert rel_err(nchw(dy), gy) < 2e-2
+    assert rel_err(dg, gg) < 1e-2
+    assert rel_err(db, gb) < 1e-2
+
+
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 8, 8, 256, 256), (2, 16, 16, 64, 64), (1, 32, 32, 128, 128)])
 def test_convt(ops, N, H, W, Cin, Cout):
     torch.manual_seed(5)
