@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="")
     ap.add_argument("--passes", default="fwd,dgrad,wgrad")
+    ap.add_argument("--dims", type=int, default=2)
+    ap.add_argument("--tile", type=int, default=256, help="top-level image size (layer sizes scale)")
     a = ap.parse_args()
     from ddlpc.ops import _ext
     from ddlpc.ops.fused_unet import _ConvPack
@@ -43,16 +45,18 @@ def main():
         if a.only and a.only not in name:
             continue
         N = a.batch
-        x1 = torch.randn(N, H, H, C1, device=dev).bfloat16()
-        x2 = torch.randn(N, H, H, C2, device=dev).bfloat16() if C2 else None
-        dy = torch.randn(N, H, H, Co, device=dev).bfloat16()
+        H = H * a.tile // 256
+        sp = (H,) * a.dims
+        x1 = torch.randn(N, *sp, C1, device=dev).bfloat16()
+        x2 = torch.randn(N, *sp, C2, device=dev).bfloat16() if C2 else None
+        dy = torch.randn(N, *sp, Co, device=dev).bfloat16()
         conv = torch.nn.Module()
-        conv.weight = torch.nn.Parameter(torch.randn(Co, C1 + C2, 3, 3, device=dev) * 0.05)
+        conv.weight = torch.nn.Parameter(torch.randn(Co, C1 + C2, *(3,) * a.dims, device=dev) * 0.05)
         pk = _ConvPack(conv, 0, True)
         F.weight_pack(torch.tensor([pk.entry()], dtype=torch.int64, device=dev), 1, pk.numel())
         sc = torch.rand(C1, device=dev) + 0.5 if pro else None
         sh = torch.randn(C1, device=dev) * 0.1 if pro else None
-        flops = 2.0 * N * H * H * Co * 9 * (C1 + C2)
+        flops = 2.0 * N * H ** a.dims * Co * 3 ** a.dims * (C1 + C2)
         fns = {
             "fwd": lambda: F.conv3_fwd(x1, x2, pk.fwd, None, sc, sh, Co, 0, True),
             "dgrad": lambda: F.conv3_fwd(dy, None, pk.dgrad, None, None, None, C1 + C2,
