@@ -84,6 +84,11 @@ class TrainConfig:
     broadcast_buffers: bool = False      # BN running stats from rank 0 (reference: off)
     check_consistency_every: int = 0     # debug: all-reduce a param checksum every K steps
     timeout_s: int = 1800
+    # fault injection: rank `fault_rank` exits (code 17) right after
+    # optimizer step `fault_step`, on the first launch attempt only
+    # (TORCHELASTIC_RESTART_COUNT == 0) — exercises torchrun --max-restarts + resume auto
+    fault_rank: int = -1
+    fault_step: int = 0
     # ---- io ----------------------------------------------------------------------
     ckpt_dir: Optional[str] = None
     ckpt_every: int = 0                  # optimizer steps; 0 = only at end of train()

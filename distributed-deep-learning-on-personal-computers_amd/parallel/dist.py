@@ -70,6 +70,15 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800,
                   timeout=datetime.timedelta(seconds=timeout_s))
         if info.backend == "nccl":
             kw["device_id"] = info.device
+        attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+        if attempt != "0" and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
+            # a torchrun restart (--max-restarts): the agent's store still holds the failed
+            # attempt's keys, and gloo's full-mesh connect reads the dead peers' addresses
+            # from them (connection refused).  Rendezvous under a per-attempt prefix.
+            base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]),
+                                 info.world_size, False,
+                                 timeout=datetime.timedelta(seconds=timeout_s))
+            kw["store"] = dist.PrefixStore(f"ddlpc/attempt_{attempt}", base)
         dist.init_process_group(**kw)
     elif dist.is_initialized():
         info.rank, info.world_size = dist.get_rank(), dist.get_world_size()

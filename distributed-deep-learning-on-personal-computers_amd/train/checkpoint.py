@@ -4,7 +4,8 @@ The reference has NO checkpointing: its only model serialisati
 pickled ``[UNet, Adam, CrossEntropyLoss]`` wire message of the initial broadcast
 (ref.py:561).  This module adds:
 
-* ``torch.save({"model", "optimizer", "epoch", "step", "micro_step", "config", "rng"})``;
+* ``torch.save({"model", "optimizer", "epoch", "step", "micro_step", "epoch_step", "config",
+  "rng"})`` (``epoch_step``: optimizer steps done in ``epoch``, so a resume continues mid-epoch);
 * ``model`` is the standard ``state_dict`` with the reference's exact 166 keys
   (``down_conv{1..5}.double_conv.double_conv.{0,1,3,4}.*``, ``double_conv.double_conv.*``,
   ``up_conv{5..1}.up_sample.*``, ``up_conv{k}.double_conv.double_conv.*``,
@@ -39,11 +40,12 @@ def set_rng_state(st: Dict[str, Any]):
 
 def save_checkpoint(path: str, model: torch.nn.Module, optimizer=None, epoch: int = 0,
                     step: int = 0, micro_step: int = 0, config: Optional[dict] = None,
-                    extra: Optional[dict] = None):
+                    extra: Optional[dict] = None, epoch_step: int = 0):
     os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
     sd = {k: v.detach().cpu() if torch.is_tensor(v) else v
           for k, v in model.state_dict().items()}
     blob = {"model": sd, "epoch": int(epoch), "step": int(step), "micro_step": int(micro_step),
+            "epoch_step": int(epoch_step),
             "config": config or {}, "rng": rng_state(), "format": "ddlpc-ckpt-v1"}
     if optimizer is not None:
         osd = optimizer.state_dict()

@@ -105,6 +105,7 @@ class Trainer:
         self._graph_warm = 0
         self._static = None
         self.epoch = 0
+        self.epoch_step = 0              # optimizer steps done in the current epoch
         self.train_set, self.test_set = self._build_data()
         self.sampler = ShardedSampler(len(self.train_set), self.rank, self.world,
                                       shard=cfg.shard_data, shuffle=cfg.shuffle, seed=cfg.seed)
@@ -274,14 +275,20 @@ class Trainer:
             self.meter.reset()
             t_ep = time.perf_counter()
             pending: List[Tuple[torch.Tensor, torch.Tensor]] = []
-            steps_this_epoch = 0
+            # resumed mid-epoch: skip the micro-batches the checkpointed steps consumed
+            skip = self.epoch_step * c.accum_steps
+            steps_this_epoch = self.epoch_step
             for idx in self.sampler.batches(c.batch_per_gpu):
+                if skip > 0:
+                    skip -= 1
+                    continue
                 pending.append(self._to_device(*self.train_set.get(idx)))
                 if len(pending) < c.accum_steps:
                     continue
                 self.train_step(pending)
                 pending = []
                 steps_this_epoch += 1
+                self.epoch_step = steps_this_epoch
                 if c.log_every and self.step_count % c.log_every == 0:
                     m = self.meter.reduce()       # synchronises: phase events are complete
                     now = time.perf_counter()
@@ -295,6 +302,10 @@ class Trainer:
                     self.logger.log(rec)
                 if c.ckpt_dir and c.ckpt_every and self.step_count % c.ckpt_every == 0:
                     self.save()
+                if (self.rank == c.fault_rank and self.step_count == c.fault_step
+                        and os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") == "0"):
+                    self.logger.close()
+                    os._exit(17)                  # injected fault: this rank dies
                 if c.max_steps and self.step_count >= c.max_steps:
                     break
             # leftover micro-batches: gradients stay accumulated into the next epoch's first
@@ -311,6 +322,7 @@ class Trainer:
                 x, y = self.train_set.get(list(range(min(c.png_count, len(self.train_set)))))
                 dump_pngs(self.model, *self._to_device(x, y), c.png_dir, c.png_count)
             self.epoch += 1
+            self.epoch_step = 0
             if c.max_steps and self.step_count >= c.max_steps:
                 break
         if c.ckpt_dir:
@@ -364,7 +376,7 @@ class Trainer:
         if self.rank == 0:
             save_checkpoint(path, self.model, self.optimizer, epoch=self.epoch,
                             step=self.step_count, micro_step=self.micro_count,
-                            config=self.cfg.to_dict())
+                            config=self.cfg.to_dict(), epoch_step=self.epoch_step)
         if dist.is_available() and dist.is_initialized():
             dist.barrier()
         return path
@@ -374,6 +386,7 @@ class Trainer:
         self.epoch = int(blob.get("epoch", 0))
         self.step_count = int(blob.get("step", 0))
         self.micro_count = int(blob.get("micro_step", 0))
+        self.epoch_step = int(blob.get("epoch_step", 0))
         if self.model._engine is not None:
             self.model._engine.pack_weights()
         return blob
