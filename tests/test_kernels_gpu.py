@@ -30,7 +30,8 @@ def nchw(x):
 
 
 def rel_err(a, b):
-    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+    a, b = a.detach().float(), b.detach().float()
+    return float((a - b).norm() / b.norm().clamp_min(1e-12))
 
 
 def pack_conv(ops, w, need_dgrad=True):
