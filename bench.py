@@ -7,45 +7,32 @@ exactly K timed optimizer steps bracketed by barrier + device synchronize on bot
 the per-rank time is MAX-reduced and rank 0 prints ONE JSON line.  ``value`` is the
 aggregate images/sec over all N GPUs (weak scaling: fixed per-GPU batch).
 
+``--gpus N`` with N > 1 outside torchrun spawns torchrun itself (child process, before
+anything touches the GPU); a torchrun ``WORLD_SIZE`` that disagrees with ``--gpus`` is an
+error (exit 2) — a mis-launched run never publishes a 1-GPU number as an N-GPU one.
+
 Model/config (BASELINE.json): the reference U-Net (ref.py:620-656) with its shipped width
 divisor 2 (8.72 M params), 5 levels, conv-transpose up-sampling, 6 classes, 256x256 RGB
 synthetic Vaihingen-shape tiles, random-init weights, bf16 compute with fp32 master
-weights, CrossEntropy + Adam (ref.py:703-704), full forward + backward + gradient
-all-reduce + optimizer step inside the timed region.
+weights, CrossEntropy + Adam (ref.py:703-704).  Inside the timed region every step
+renders its batch in HBM (the trainer's own device input pipeline, ``synth_tiles``
+kernel, distinct sample indices per rank and step), then runs the full forward +
+backward + gradient all-reduce + optimizer step.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
-BASELINE_IMG_S = None   # set from BASELINE.json "inhouse_baseline" if present
+ROOT = os.path.dirname(os.path.abspath(__file__))
 
 
-def _baseline(args):
-    """In-house MIOpen baseline (BASELINE.json) for the SAME config, else None."""
-    if args.dims != 2 or args.tile != 256 or args.depth != 5 or args.width_divisor != 2 \
-            or args.classes != 6 or args.accum != 1:
-        return None
-    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "BASELINE.json")
-    try:
-        with open(p) as f:
-            b = json.load(f).get("inhouse_baseline", {})
-        v = {32: b.get("images_per_sec_per_gpu"), 64: b.get("batch_64_images_per_sec"),
-             128: b.get("batch_128_images_per_sec")}.get(args.batch)
-        return float(v) if v else None
-    except Exception:
-        return None
-
-
-def main():
+def _parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -61,8 +48,11 @@ def main():
     ap.add_argument("--impl", default=os.environ.get("DDLPC_IMPL", "hip"),
                     choices=["hip", "torch"])
     ap.add_argument("--bucket-mb", type=float, default=8.0)
+    ap.add_argument("--bucket-sweep", default="",
+                    help="comma list of bucket sizes (MB) timed after the main run (N>1), "
+                         "e.g. 2,4,8,16,35; reported as config.bucket_sweep")
+    ap.add_argument("--wire-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--codec", default="none")
-    ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--verbose", type=int, default=0, help="1: progress lines on stderr")
     ap.add_argument("--schedule", default="auto", choices=["auto", "overlap", "serial"],
                     help="weight-gradient stream: auto = time both during warm-up, keep the faster")
@@ -70,7 +60,67 @@ def main():
                     help="1: replay the single-GPU train step as one hipGraph")
     ap.add_argument("--heartbeat", type=float, default=0.0,
                     help="seconds between 'alive' lines on stderr (long first-step autotuning)")
-    args = ap.parse_args()
+    return ap.parse_args()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _launch_guard(args) -> None:
+    """Enforce the one-rank-per-GPU contract BEFORE any GPU call."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None:
+        if args.gpus > 1:
+            # not under torchrun: become the launcher (a child process, never an exec)
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                   f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+                   f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+            print(f"bench: spawning {args.gpus} ranks via torchrun", file=sys.stderr, flush=True)
+            sys.exit(subprocess.call(cmd))
+        return
+    if int(ws) != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={ws}: refusing to report a "
+              f"{ws}-rank number as {args.gpus}-GPU", file=sys.stderr, flush=True)
+        sys.exit(2)
+
+
+def _baseline(args):
+    """In-house MIOpen baseline (BASELINE.json) for the SAME config, else None."""
+    try:
+        with open(os.path.join(ROOT, "BASELINE.json")) as f:
+            b = json.load(f).get("inhouse_baseline", {})
+    except Exception:
+        return None
+    if args.accum != 1 or args.classes != 6 or args.depth != 5:
+        return None
+    if args.dims == 3:
+        if args.tile == 128 and args.width_divisor == 2:
+            v = b.get("d3_128_images_per_sec", {}).get(str(args.batch))
+            return float(v) if v else None
+        return None
+    if args.tile != 256:
+        return None
+    if args.width_divisor == 1:
+        v = b.get("wd1_images_per_sec", {}).get(str(args.batch))
+        return float(v) if v else None
+    if args.width_divisor != 2:
+        return None
+    v = {32: b.get("images_per_sec_per_gpu"), 64: b.get("batch_64_images_per_sec"),
+         128: b.get("batch_128_images_per_sec")}.get(args.batch)
+    return float(v) if v else None
+
+
+def main():
+    args = _parse()
+    _launch_guard(args)
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
     if args.heartbeat > 0:
         import threading
 
@@ -88,28 +138,39 @@ def main():
     cfg = TrainConfig(model=ModelConfig(out_classes=args.classes, depth=args.depth,
                                         width_divisor=args.width_divisor, dims=args.dims),
                       tile=args.tile, batch_per_gpu=args.batch, accum_steps=args.accum,
-                      num_samples=1, test_holdout=0, impl=args.impl, bucket_mb=args.bucket_mb,
+                      num_samples=1 << 30, test_holdout=0, impl=args.impl,
+                      bucket_mb=args.bucket_mb, wire_dtype=args.wire_dtype,
                       grad_codec=args.codec, log_dir=None, hip_graph=bool(args.hip_graph))
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     tr = Trainer(cfg, device=dev)
     world, rank = tr.world, tr.rank
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    assert world == args.gpus, (world, args.gpus)
     device = tr.device
-    # a small pool of distinct device-resident batches (synthetic; no host I/O in the loop)
+    B = args.batch
+    on_device_data = tr.impl == "hip" and dev == "cuda"
     pool = []
-    for i in range(4):
-        x, y = device_random_batch(args.batch, args.tile, args.classes, device,
-                                   seed=1000 * rank + i, dims=args.dims,
-                                   dtype=torch.bfloat16 if dev == "cuda" else torch.float32,
-                                   channels_last=(dev == "cuda"))
-        if tr.impl == "torch":
-            x = x.float() if dev == "cpu" else x
-        pool.append((x, y))
+    if not on_device_data:
+        # stock-op baseline / CPU: a small pre-rendered pool (the baseline's published
+        # numbers were measured this way)
+        for i in range(4):
+            x, y = device_random_batch(B, args.tile, args.classes, device,
+                                       seed=1000 * rank + i, dims=args.dims,
+                                       dtype=torch.bfloat16 if dev == "cuda" else torch.float32,
+                                       channels_last=(dev == "cuda"))
+            if dev == "cpu":
+                x = x.float()
+            pool.append((x, y))
+
+    def batch(k):
+        if on_device_data:
+            # global micro-batch k, this rank's slice of distinct sample indices
+            start = (k * world + rank) * B
+            idx = torch.arange(start, start + B, device=device, dtype=torch.int64)
+            return tr.train_set.get(idx)
+        return pool[k % len(pool)]
 
     def step(i):
-        mbs = [pool[(i * args.accum + j) % len(pool)] for j in range(args.accum)]
-        tr.train_step(mbs)
+        tr.train_step([batch(i * args.accum + j) for j in range(args.accum)])
 
     def sync():
         if dev == "cuda":
@@ -119,6 +180,17 @@ def main():
         if dev == "cuda":
             torch.cuda.synchronize()
 
+    def timed(n, first):
+        sync()
+        t0 = time.perf_counter()
+        for i in range(n):
+            step(first + i)
+        sync()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     for i in range(args.warmup):
         step(i)
         if args.verbose and rank == 0:
@@ -126,37 +198,43 @@ def main():
     # schedule calibration (untimed): overlapped weight-gradient stream vs serial
     sched = {}
     if args.schedule == "auto":
-        sched = tr.choose_schedule(pool[0:1] if args.accum == 1 else
-                                   [pool[j % len(pool)] for j in range(args.accum)])
+        sched = tr.choose_schedule([batch(10_000 + j) for j in range(args.accum)])
         if rank == 0 and sched:
             print(f"schedule: {sched}", file=sys.stderr, flush=True)
     elif args.schedule == "serial" and tr.impl == "hip":
         tr.model._engine.set_side_stream(False)
-    sync()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
-    sync()
-    dt = time.perf_counter() - t0
+    if tr.phases is not None:
+        tr.phases.read(reset=True)                 # phase means over the timed steps only
+    first = args.warmup + 100
+    dt = timed(args.steps, first)
+    phases = tr.phases.read() if tr.phases is not None else {}
     mstats = torch.cuda.memory_stats(device) if dev == "cuda" else {}
-    t = torch.tensor([dt], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
     ms = dt / args.steps * 1e3
-    imgs = args.batch * args.accum * world * args.steps
+    imgs = B * args.accum * world * args.steps
     value = imgs / dt
+    sweep = {}
+    if args.bucket_sweep and world > 1:
+        for mb in [float(v) for v in args.bucket_sweep.split(",") if v]:
+            nb = tr.set_bucket_mb(mb)
+            first += args.steps + 2
+            step(first - 1)                        # one untimed step at the new size
+            sweep[str(mb)] = {"buckets": nb,
+                              "ms_per_step": round(timed(args.steps, first) / args.steps * 1e3, 3)}
+        tr.set_bucket_mb(args.bucket_mb)
     base = _baseline(args)
     loss = tr.meter.reduce()
     if args.dims == 2:
         metric = f"images/sec (whole node), U-Net {args.tile}x{args.tile} {args.classes}-class tiles"
-        data_desc = (f"synthetic (Vaihingen-shape {args.tile}x{args.tile} RGB tiles, "
-                     f"{args.classes} classes, random-init weights)")
+        data_desc = (f"synthetic (Vaihingen-shape {args.tile}x{args.tile} RGB tiles rendered in HBM "
+                     f"per step, {args.classes} classes, random-init weights)")
     else:
         metric = (f"volumes/sec (whole node), 3-D U-Net {args.tile}^3 {args.classes}-class volumes")
-        data_desc = (f"synthetic ({args.tile}^3 3-channel volumes, {args.classes} classes, "
-                     "random-init weights)")
+        data_desc = (f"synthetic ({args.tile}^3 3-channel volumes rendered in HBM per step, "
+                     f"{args.classes} classes, random-init weights)")
+    if not on_device_data:
+        data_desc = data_desc.replace("rendered in HBM per step", "pre-rendered pool of 4 batches")
     if rank == 0:
+        red = tr.reducer
         rec = {
             "metric": metric,
             "value": round(value, 2), "unit": "images/s" if args.dims == 2 else "volumes/s",
@@ -168,8 +246,8 @@ def main():
             "data": data_desc,
             "config": {"model": f"UNet depth{args.depth} width/{args.width_divisor} "
                                 f"conv_transpose ({sum(p.numel() for p in tr.model.parameters())} params)",
-                       "global_batch": args.batch * args.accum * world,
-                       "per_gpu_batch": args.batch, "accum_steps": args.accum,
+                       "global_batch": B * args.accum * world,
+                       "per_gpu_batch": B, "accum_steps": args.accum,
                        "seq_len": None, "tile": args.tile, "dims": args.dims,
                        "classes": args.classes,
                        "parallelism": f"dp{world}", "impl": tr.impl,
@@ -179,6 +257,15 @@ def main():
                                        if dev == "cuda" else None),
                        "schedule": ("overlap" if sched.get("side_stream") else "serial") if sched
                                    else args.schedule,
+                       "schedule_probe_ms": ({k: round(v, 3) for k, v in sched.items()
+                                              if k.endswith("_ms")} if sched else None),
+                       "bucket_mb": args.bucket_mb,
+                       "buckets": len(red.buckets) if red is not None else 0,
+                       "wire_dtype": args.wire_dtype, "grad_codec": args.codec,
+                       "phase_ms": {k: round(v, 3) for k, v in phases.items()},
+                       "comm_wait_ms": (round(phases["comm_wait_ms"], 3)
+                                        if "comm_wait_ms" in phases else None),
+                       "bucket_sweep": sweep or None,
                        "alloc_retries": mstats.get("num_alloc_retries"),
                        "device_mallocs": mstats.get("num_device_alloc"),
                        "device_frees": mstats.get("num_device_free")},

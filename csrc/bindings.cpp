@@ -744,6 +744,66 @@ at::Tensor to_nhwc_bf16(const at::Tensor& x, int64_t cpad) {
   return y;
 }
 
+// ------------------------------------------------------------------------ input pipeline
+std::vector<int64_t> batch_shape(int64_t B, int64_t tile, int64_t dims) {
+  std::vector<int64_t> s = {B};
+  for (int i = 0; i < dims; ++i) s.push_back(tile);
+  return s;
+}
+
+// synthetic Vaihingen-shape batch rendered in HBM -> {x [B, (T,) T, T, cpad] bf16, y int64}
+std::vector<at::Tensor> synth_tiles(const at::Tensor& idx, int64_t seed, int64_t classes,
+                                    int64_t in_ch, int64_t tile, int64_t dims, int64_t grid,
+                                    double k, const at::Tensor& palette, int64_t cpad) {
+  CHECK_DEV(idx); CHECK_CONTIG(idx); CHECK_DEV(palette); CHECK_F32(palette); CHECK_CONTIG(palette);
+  TORCH_CHECK(idx.scalar_type() == at::kLong, "idx must be int64");
+  TORCH_CHECK(dims == 2 || dims == 3, "dims must be 2 or 3");
+  TORCH_CHECK(in_ch >= 1 && in_ch <= 8 && cpad >= in_ch && cpad <= 8, "1 <= in_ch <= cpad <= 8");
+  TORCH_CHECK(classes >= 1 && palette.numel() == classes * in_ch, "palette must be [classes][in_ch]");
+  TORCH_CHECK(grid >= 1 && grid <= tile && tile >= 1, "1 <= grid <= tile");
+  TORCH_CHECK((int64_t)tile * tile * (dims == 3 ? tile : 1) * 8 < (int64_t)UINT32_MAX,
+              "tile too large for the 32-bit per-pixel hash counter");
+  c10::DeviceGuard guard(idx.device());
+  const int64_t B = idx.numel();
+  std::vector<int64_t> xs = batch_shape(B, tile, dims);
+  at::Tensor y = at::empty(xs, idx.options());
+  xs.push_back(cpad);
+  at::Tensor x = at::empty(xs, idx.options().dtype(at::kBFloat16));
+  if (B > 0)
+    synth_tiles_launch(idx.data_ptr<int64_t>(), (int)B, (uint32_t)(seed & 0xffffffff), (int)classes,
+                       (int)in_ch, (int)tile, (int)dims, (int)grid, (float)k,
+                       palette.data_ptr<float>(), (int)cpad, bptr_mut(x), y.data_ptr<int64_t>(),
+                       cur_stream());
+  return {x, y};
+}
+
+// HBM-resident uint8 dataset [N, (D,) H, W, Cin] + uint8 labels -> gathered bf16 / int64 batch
+std::vector<at::Tensor> tile_gather(const at::Tensor& src, const at::Tensor& lab,
+                                    const at::Tensor& idx, int64_t cpad) {
+  CHECK_DEV(src); CHECK_CONTIG(src); CHECK_DEV(lab); CHECK_CONTIG(lab); CHECK_DEV(idx);
+  CHECK_CONTIG(idx);
+  TORCH_CHECK(src.scalar_type() == at::kByte && lab.scalar_type() == at::kByte, "uint8 dataset");
+  TORCH_CHECK(idx.scalar_type() == at::kLong, "idx must be int64");
+  TORCH_CHECK(src.dim() == lab.dim() + 1 && src.size(0) == lab.size(0), "images [N,...,C] / labels [N,...]");
+  const int64_t in_ch = src.size(-1);
+  TORCH_CHECK(in_ch >= 1 && in_ch <= 8 && cpad >= in_ch && cpad <= 8, "1 <= in_ch <= cpad <= 8");
+  for (int64_t i = 1; i < lab.dim(); ++i) TORCH_CHECK(src.size(i) == lab.size(i), "spatial mismatch");
+  c10::DeviceGuard guard(src.device());
+  const int64_t B = idx.numel();
+  const long long S = lab.numel() / std::max<int64_t>(1, lab.size(0));
+  std::vector<int64_t> ys = {B};
+  for (int64_t i = 1; i < lab.dim(); ++i) ys.push_back(lab.size(i));
+  at::Tensor y = at::empty(ys, idx.options());
+  std::vector<int64_t> xs = ys;
+  xs.push_back(cpad);
+  at::Tensor x = at::empty(xs, src.options().dtype(at::kBFloat16));
+  if (B > 0)
+    tile_gather_launch(src.data_ptr<uint8_t>(), lab.data_ptr<uint8_t>(), idx.data_ptr<int64_t>(),
+                       (int)B, S, (int)in_ch, (int)cpad, bptr_mut(x), y.data_ptr<int64_t>(),
+                       cur_stream());
+  return {x, y};
+}
+
 }  // namespace
 
 }  // namespace ddlpc
@@ -776,6 +836,9 @@ TORCH_LIBRARY(ddlpc, m) {
   m.def("bilinear_up2(Tensor x) -> Tensor");
   m.def("bilinear_up2_bwd(Tensor dy) -> Tensor");
   m.def("to_nhwc_bf16(Tensor x, int cpad=1) -> Tensor");
+  m.def("synth_tiles(Tensor idx, int seed, int classes, int in_ch, int tile, int dims, int grid, "
+        "float k, Tensor palette, int cpad) -> Tensor[]");
+  m.def("tile_gather(Tensor src, Tensor lab, Tensor idx, int cpad) -> Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
@@ -799,4 +862,6 @@ TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
   m.impl("bilinear_up2", &ddlpc::bilinear_up2);
   m.impl("bilinear_up2_bwd", &ddlpc::bilinear_up2_bwd);
   m.impl("to_nhwc_bf16", &ddlpc::to_nhwc_bf16);
+  m.impl("synth_tiles", &ddlpc::synth_tiles);
+  m.impl("tile_gather", &ddlpc::tile_gather);
 }

@@ -4,7 +4,7 @@
 // per-iteration pixel accuracy argmax(outputs,1)==y (ref.py:775).
 //
 // The logits never touch HBM during training: the forward kernel computes per-pixel logits
-// from the bf16 activation (C <= 64 channels, K <= 16 classes, fp32 math), the
+// from the bf16 activation (C in {8,16,32,64} channels, any K <= 16 classes, fp32 math), the
 // log-sum-exp loss, the arg-max hit and the valid-pixel count, reduced per block.  The
 // backward kernel recomputes the logits (192 MACs/pixel: far cheaper than storing them),
 // forms dlogits = (softmax - onehot) * dL / count, writes dA = dlogits . Wh (bf16) and
@@ -18,6 +18,21 @@ namespace {
 
 constexpr int MAXC = 64, MAXK = 16;
 
+// Classes: the kernels are instantiated for KP in {2, 4, 8, 16} (and 6, the
+// Vaihingen class count, unpadded) logit slots and take
+// the real class count K <= KP at run time; padded slots carry bias -inf and zero weights
+// (sW/sb staged that way in LDS), so they add exp(-inf) = 0 to the softmax, never win the
+// arg-max and receive a zero gradient.
+
+// An LDS offset the compiler cannot prove loop-invariant: the K*C head weights stay in LDS
+// (uniform-address broadcast reads, 4 per ds_read_b128) instead of being hoisted out of the
+// pixel loop into K*C live VGPRs (measured: 150-256 VGPRs, occupancy 1-3, spills at C=64).
+DDLPC_DEVICE int opaque_zero() {
+  int z = 0;
+  asm volatile("" : "+s"(z));
+  return z;
+}
+
 // The head's input activation, 8 channels at c8.  With a deferred BatchNorm (sBN != null:
 // scale [C] | shift [C] in LDS) the tensor holds the block's PRE-BN conv output y and the
 // activation relu(y*scale + shift) is formed here, rounded to bf16 exactly as a
@@ -27,24 +42,36 @@ DDLPC_DEVICE void act8(const bf16_t* ap, int c8, const float* sBN, float (&f)[8]
   const uint4 v = *reinterpret_cast<const uint4*>(ap + c8);
   unpack8(v, f);
   if (DEFER) {
-    // volatile LDS-broadcast reads: the compiler would otherwise hoist all 2*C constants out
-    // of the pixel loop into live registers and halve the kernel's occupancy
-    const volatile float* vb = sBN;
+    // opaque LDS offset: the compiler would otherwise hoist all 2*C constants out of the
+    // pixel loop into live registers and halve the kernel's occupancy
+    const float* vb = sBN + opaque_zero();
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], vb[c8 + j], vb[C + c8 + j]), 0.f);
     unpack8(pack8(f), f);
   }
 }
 
+// stage Wh [K][C] / bh [K] into LDS as KP padded rows
+template <int C, int KP>
+DDLPC_DEVICE void load_head(const float* Wh, const float* bh, int K, float* sW, float* sb) {
+  for (int i = threadIdx.x; i < KP * C; i += blockDim.x) sW[i] = i < K * C ? Wh[i] : 0.f;
+  if (threadIdx.x < KP) sb[threadIdx.x] = (int)threadIdx.x < K ? bh[threadIdx.x] : -INFINITY;
+}
+
+// stage != nullptr: also store the (bf16) activation row to LDS for the weight-gradient pass
 template <int C, int K, bool DEFER>
 DDLPC_DEVICE void logits_of(const bf16_t* ap, const float* sW, const float* sb, const float* sBN,
-                            float (&z)[K]) {
+                            float (&z)[K], bf16_t* stage = nullptr) {
+  const int o = opaque_zero();
+  sW += o;
+  sb += o;
 #pragma unroll
   for (int k = 0; k < K; ++k) z[k] = sb[k];
-#pragma unroll
+#pragma unroll 1
   for (int c8 = 0; c8 < C; c8 += 8) {
     float f[8];
     act8<C, DEFER>(ap, c8, sBN, f);
+    if (stage != nullptr) *reinterpret_cast<uint4*>(stage + c8) = pack8(f);
 #pragma unroll
     for (int k = 0; k < K; ++k)
 #pragma unroll
@@ -66,11 +93,10 @@ template <int C, int K, bool DEFER>
 __global__ __launch_bounds__(256) void head_ce_fwd_kernel(
     const bf16_t* __restrict__ a, const float* __restrict__ Wh, const float* __restrict__ bh,
     const int64_t* __restrict__ labels, float* __restrict__ partial, long long P,
-    int ignore_index, const float* __restrict__ bn4) {
+    int ignore_index, const float* __restrict__ bn4, int Kreal) {
   __shared__ __attribute__((aligned(16))) float sBNm[4 * C];
   __shared__ float sW[K * C], sb[K];
-  for (int i = threadIdx.x; i < K * C; i += blockDim.x) sW[i] = Wh[i];
-  if (threadIdx.x < K) sb[threadIdx.x] = bh[threadIdx.x];
+  load_head<C, K>(Wh, bh, Kreal, sW, sb);
   const float* sBN = DEFER ? load_bn<C>(bn4, sBNm, false) : nullptr;
   __syncthreads();
   float loss = 0.f, correct = 0.f, count = 0.f;
@@ -140,20 +166,25 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
     const bf16_t* __restrict__ a, const float* __restrict__ Wh, const float* __restrict__ bh,
     const int64_t* __restrict__ labels, const float* __restrict__ gscale,
     const float* __restrict__ stats3, bf16_t* __restrict__ dA, float* __restrict__ dWp,
-    long long P, int ignore_index, const float* __restrict__ bn4) {
+    long long P, int ignore_index, const float* __restrict__ bn4, int Kreal) {
   __shared__ __attribute__((aligned(16))) float sBNm[4 * C];
   __shared__ float sW[K * C], sb[K];
   __shared__ __attribute__((aligned(16))) bf16_t sA[256 * C];
   __shared__ float sD[256 * K];
-  for (int i = threadIdx.x; i < K * C; i += blockDim.x) sW[i] = Wh[i];
-  if (threadIdx.x < K) sb[threadIdx.x] = bh[threadIdx.x];
+  load_head<C, K>(Wh, bh, Kreal, sW, sb);
   const float* sBN = DEFER ? load_bn<C>(bn4, sBNm, false) : nullptr;
   __syncthreads();
   const float cnt = stats3[2];
   const float gs = (gscale != nullptr ? gscale[0] : 1.0f) / (cnt > 0.f ? cnt : 1.f);
   const int t = threadIdx.x;
-  float accw = 0.f;                                  // thread t < K*C: dW[k][c]; < K*C+K: db
+  // per-block partial row [dW (Kreal*C) | db (Kreal)]: output o = t + 256*r of thread t
+  constexpr int NO = (K * C + K + 255) / 256;
+  const int nout = Kreal * C + Kreal;
+  float accw[NO];
+#pragma unroll
+  for (int r = 0; r < NO; ++r) accw[r] = 0.f;
   const long long nper = (long long)gridDim.x * blockDim.x;
+#pragma unroll 1
   for (long long base = blockIdx.x * (long long)blockDim.x; base < P; base += nper) {
     const long long px = base + t;
     float d[K];
@@ -161,7 +192,7 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
     for (int k = 0; k < K; ++k) d[k] = 0.f;
     if (px < P) {
       float z[K];
-      logits_of<C, K, DEFER>(a + px * C, sW, sb, sBN, z);
+      logits_of<C, K, DEFER>(a + px * C, sW, sb, sBN, z, sA + t * C);
       const int64_t y = labels[px];
       float m = z[0];
 #pragma unroll
@@ -174,80 +205,98 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
 #pragma unroll
         for (int k = 0; k < K; ++k) d[k] = (z[k] * inv - (k == y ? 1.f : 0.f)) * gs;
       }
-      // dA = d . Wh
-#pragma unroll
-      for (int c8 = 0; c8 < C; c8 += 8) {
-        float o[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float s = 0.f;
-#pragma unroll
-          for (int k = 0; k < K; ++k) s = fmaf(d[k], sW[k * C + c8 + j], s);
-          o[j] = s;
-        }
-        *reinterpret_cast<uint4*>(dA + px * C + c8) = pack8(o);
-      }
-#pragma unroll
-      for (int c8 = 0; c8 < C; c8 += 8) {
-        float f[8];
-        act8<C, DEFER>(a + px * C, c8, sBN, f);
-        *reinterpret_cast<uint4*>(sA + t * C + c8) = pack8(f);
-      }
     } else {
 #pragma unroll
       for (int c8 = 0; c8 < C; c8 += 8) *reinterpret_cast<uint4*>(sA + t * C + c8) = make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) sD[t * K + k] = d[k];
+    if (px < P) {
+      // dA = d . Wh, one class row at a time (k loop kept rolled: C accumulators live, the
+      // weights stream from LDS as broadcast reads instead of K*C hoisted registers)
+      float o[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) o[c] = 0.f;
+#pragma unroll 1
+      for (int k = 0; k < Kreal; ++k) {
+        const float dk = sD[t * K + k];
+        const float* wr = sW + k * C;
+#pragma unroll
+        for (int c = 0; c < C; ++c) o[c] = fmaf(dk, wr[c], o[c]);
+      }
+#pragma unroll
+      for (int c8 = 0; c8 < C; c8 += 8) {
+        float q[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) q[j] = o[c8 + j];
+        *reinterpret_cast<uint4*>(dA + px * C + c8) = pack8(q);
+      }
+    }
     __syncthreads();
-    if (t < K * C) {
-      const int k = t / C, c = t % C;
-      float s = 0.f;
-      for (int i = 0; i < 256; ++i) s = fmaf(bf2f(sA[i * C + c]), sD[i * K + k], s);
-      accw += s;
-    } else if (t < K * C + K) {
-      const int k = t - K * C;
-      float s = 0.f;
-      for (int i = 0; i < 256; ++i) s += sD[i * K + k];
-      accw += s;
+#pragma unroll
+    for (int r = 0; r < NO; ++r) {
+      const int o = t + 256 * r;
+      if (o < Kreal * C) {
+        const int k = o / C, c = o % C;
+        float s = 0.f;
+#pragma unroll 8
+        for (int i = 0; i < 256; ++i) s = fmaf(bf2f(sA[i * C + c]), sD[i * K + k], s);
+        accw[r] += s;
+      } else if (o < nout) {
+        const int k = o - Kreal * C;
+        float s = 0.f;
+#pragma unroll 8
+        for (int i = 0; i < 256; ++i) s += sD[i * K + k];
+        accw[r] += s;
+      }
     }
     __syncthreads();
   }
-  if (t < K * C + K) dWp[(long long)blockIdx.x * (K * C + K) + t] = accw;
+#pragma unroll
+  for (int r = 0; r < NO; ++r) {
+    const int o = t + 256 * r;
+    if (o < nout) dWp[(long long)blockIdx.x * nout + o] = accw[r];
+  }
 }
 
 template <int C, int K, bool DEFER>
-__global__ void head_logits_kernel(const bf16_t* __restrict__ a, const float* __restrict__ Wh,
+__global__ __launch_bounds__(256) void head_logits_kernel(const bf16_t* __restrict__ a, const float* __restrict__ Wh,
                                    const float* __restrict__ bh, float* __restrict__ out,
-                                   long long P, long long HW, const float* __restrict__ bn4) {
+                                   long long P, long long HW, const float* __restrict__ bn4,
+                                   int Kreal) {
   __shared__ __attribute__((aligned(16))) float sBNm[4 * C];
   __shared__ float sW[K * C], sb[K];
-  for (int i = threadIdx.x; i < K * C; i += blockDim.x) sW[i] = Wh[i];
-  if (threadIdx.x < K) sb[threadIdx.x] = bh[threadIdx.x];
+  load_head<C, K>(Wh, bh, Kreal, sW, sb);
   const float* sBN = DEFER ? load_bn<C>(bn4, sBNm, false) : nullptr;
   __syncthreads();
+#pragma unroll 1
   for (long long px = blockIdx.x * (long long)blockDim.x + threadIdx.x; px < P;
        px += (long long)gridDim.x * blockDim.x) {
     float z[K];
     logits_of<C, K, DEFER>(a + px * C, sW, sb, sBN, z);
     const long long n = px / HW, s = px % HW;
 #pragma unroll
-    for (int k = 0; k < K; ++k) out[(n * K + k) * HW + s] = z[k];
+    for (int k = 0; k < K; ++k)
+      if (k < Kreal) out[(n * Kreal + k) * HW + s] = z[k];
   }
 }
 
-#define HEAD_SWITCH(C_, K_, ...)                                                  \
-  [&] {                                                                           \
-    if (C_ == 32 && K_ == 6) { constexpr int CC = 32, KK = 6; __VA_ARGS__; }        \
-    else if (C_ == 64 && K_ == 6) { constexpr int CC = 64, KK = 6; __VA_ARGS__; }   \
-    else if (C_ == 16 && K_ == 6) { constexpr int CC = 16, KK = 6; __VA_ARGS__; }   \
-    else if (C_ == 32 && K_ == 2) { constexpr int CC = 32, KK = 2; __VA_ARGS__; }   \
-    else if (C_ == 64 && K_ == 2) { constexpr int CC = 64, KK = 2; __VA_ARGS__; }   \
-    else if (C_ == 16 && K_ == 2) { constexpr int CC = 16, KK = 2; __VA_ARGS__; }   \
-    else if (C_ == 8 && K_ == 2) { constexpr int CC = 8, KK = 2; __VA_ARGS__; }     \
-    else if (C_ == 8 && K_ == 6) { constexpr int CC = 8, KK = 6; __VA_ARGS__; }     \
-    else { return false; }                                                        \
-    return true;                                                                  \
+// C in {8, 16, 32, 64} (64 / width_divisor channels) x padded class slots KP >= K
+#define HEAD_SWITCH_K(C_, K_, ...)                                                  \
+  if (K_ <= 2) { constexpr int KK = 2; __VA_ARGS__; }                               \
+  else if (K_ <= 4) { constexpr int KK = 4; __VA_ARGS__; }                          \
+  else if (K_ == 6) { constexpr int KK = 6; __VA_ARGS__; }                          \
+  else if (K_ <= 8) { constexpr int KK = 8; __VA_ARGS__; }                          \
+  else { constexpr int KK = 16; __VA_ARGS__; }
+#define HEAD_SWITCH(C_, K_, ...)                                                    \
+  [&] {                                                                             \
+    if ((K_) < 1 || (K_) > MAXK) return false;                                      \
+    if (C_ == 8) { constexpr int CC = 8; HEAD_SWITCH_K(C_, K_, __VA_ARGS__) }         \
+    else if (C_ == 16) { constexpr int CC = 16; HEAD_SWITCH_K(C_, K_, __VA_ARGS__) }  \
+    else if (C_ == 32) { constexpr int CC = 32; HEAD_SWITCH_K(C_, K_, __VA_ARGS__) }  \
+    else if (C_ == 64) { constexpr int CC = 64; HEAD_SWITCH_K(C_, K_, __VA_ARGS__) }  \
+    else { return false; }                                                          \
+    return true;                                                                    \
   }()
 
 }  // namespace
@@ -261,10 +310,10 @@ void head_ce_fwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
                         int C, int K, int ignore_index, hipStream_t st) {
   if (bn4 != nullptr)
     HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_fwd_kernel<CC, KK, true>), dim3(nblocks), dim3(256), 0,
-                                         st, a, Wh, bh, labels, partial, P, ignore_index, bn4));
+                                         st, a, Wh, bh, labels, partial, P, ignore_index, bn4, K));
   else
     HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_fwd_kernel<CC, KK, false>), dim3(nblocks), dim3(256), 0,
-                                         st, a, Wh, bh, labels, partial, P, ignore_index, bn4));
+                                         st, a, Wh, bh, labels, partial, P, ignore_index, bn4, K));
   hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(256), 0, st, partial, nblocks, out3);
 }
 
@@ -276,11 +325,11 @@ void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
   if (bn4 != nullptr)
     HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK, true>), dim3(nblocks), dim3(256), 0,
                                          st, a, Wh, bh, labels, gscale, stats3, dA, dW_partial, P,
-                                         ignore_index, bn4));
+                                         ignore_index, bn4, K));
   else
     HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK, false>), dim3(nblocks), dim3(256), 0,
                                          st, a, Wh, bh, labels, gscale, stats3, dA, dW_partial, P,
-                                         ignore_index, bn4));
+                                         ignore_index, bn4, K));
 }
 
 void head_logits_launch(const bf16_t* a, const float* Wh, const float* bh, float* logits,
@@ -288,10 +337,10 @@ void head_logits_launch(const bf16_t* a, const float* Wh, const float* bh, float
   const int grid = (int)std::min<long long>((P + 255) / 256, 4096);
   if (bn4 != nullptr)
     HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_logits_kernel<CC, KK, true>), dim3(grid), dim3(256), 0, st,
-                                         a, Wh, bh, logits, P, HW, bn4));
+                                         a, Wh, bh, logits, P, HW, bn4, K));
   else
     HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_logits_kernel<CC, KK, false>), dim3(grid), dim3(256), 0, st,
-                                         a, Wh, bh, logits, P, HW, bn4));
+                                         a, Wh, bh, logits, P, HW, bn4, K));
 }
 
 }  // namespace ddlpc

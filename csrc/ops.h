@@ -192,4 +192,11 @@ void channel_sum_launch(const bf16_t* x, long long P, int C, float* partial, int
 void to_nhwc_pad_launch(const void* x, int in_dtype, bf16_t* y, int N, int C, int Cp, long long S,
                         long long sN, long long sC, long long sS, hipStream_t st);
 
+// ---------------------------------------------------------------- input pipeline (data.hip)
+void synth_tiles_launch(const int64_t* idx, int B, uint32_t seed, int classes, int in_ch, int tile,
+                        int dims, int grid, float k, const float* palette, int cpad, bf16_t* x,
+                        int64_t* y, hipStream_t st);
+void tile_gather_launch(const uint8_t* src, const uint8_t* lab, const int64_t* idx, int B,
+                        long long S, int in_ch, int cpad, bf16_t* x, int64_t* y, hipStream_t st);
+
 }  // namespace ddlpc

@@ -63,6 +63,8 @@ class TrainConfig:
     test_holdout: int = 30               # last N pairs are the test split (ref.py:672-673)
     shard_data: bool = True              # False = reference "replicated data" mode (§2.2)
     shuffle: bool = True
+    data_on_device: bool = True          # GPU: render / keep the dataset in HBM (K20)
+    data_hbm_gb: Optional[float] = None  # HBM budget for a real dataset (None: half the free)
     # ---- optimisation ----------------------------------------------------------
     batch_per_gpu: int = 1               # batch_size, ref.py:686
     accum_steps: int = 1                 # frequency_sending_gradients, ref.py:685
@@ -80,6 +82,7 @@ class TrainConfig:
     reduce: str = "mean"                 # mean | sum | reference (the W=2 "sum" parity mode)
     grad_codec: str = "none"             # none | fp16_absmax | int8_absmax (ref.py:25)
     codec_scale: str = "bucket"          # global (reference parity) | bucket | tensor
+    wire_dtype: str = "fp32"             # fp32 all-reduce | bf16 transport, fp32 accumulate
     overlap_comm: bool = True
     broadcast_buffers: bool = False      # BN running stats from rank 0 (reference: off)
     check_consistency_every: int = 0     # debug: all-reduce a param checksum every K steps
@@ -111,6 +114,7 @@ class TrainConfig:
         for name, val, allowed in (("grad_codec", self.grad_codec, GRAD_CODECS),
                                    ("codec_scale", self.codec_scale, CODEC_SCALES),
                                    ("reduce", self.reduce, REDUCE_OPS),
+                                   ("wire_dtype", self.wire_dtype, ("fp32", "bf16")),
                                    ("data", self.data, DATA_KINDS),
                                    ("impl", self.impl, ("auto", "hip", "torch")),
                                    ("dtype", self.dtype, ("bf16", "fp32"))):

@@ -8,16 +8,26 @@ Reference behaviour (ref.py:660-674, ref.py:737-741):
   split (never evaluated in the reference; ``validate()`` uses it here).
 * Images are ``float32 / 255`` and transposed to NCHW; labels become ``int64``.
 
-The reference hard-codes 127 tiles of 512x512 and re-reads the directory every epoch
-(ref.py:732); here the directory is read once and the tile size comes from the data.
+The reference hard-codes 127 tiles of 512x512, re-reads the directory every epoch
+(ref.py:732) and copies every micro-batch from the host (ref.py:754-755).  Here:
 
-The synthetic generator (the benchmark data source; there is no network for the real
-ISPRS Vaihingen set) produces learnable tiles of the same shape: piecewise-constant
-6-class label maps from a coarse random grid, rendered with a per-class colour plus
-noise, seeded per sample index so every rank and every run sees the same sample ``i``.
+* the directory is read once; ``TileDataset`` keeps the raw uint8 NHWC tiles and, on a GPU,
+  ``to_device()`` uploads them ONCE to HBM (288 GB: the reference's 127 tiles of 512² are
+  100 MB), after which a batch is one gather kernel (``tile_gather``: /255, channel-last
+  bf16 padded to 8 channels, int64 labels — SURVEY.md K20).  Datasets too large for the
+  HBM budget stay in pinned host memory and are prefetched one batch ahead on a copy
+  stream;
+* the synthetic generator (the benchmark data source; there is no network for the real
+  ISPRS Vaihingen set) renders learnable tiles of the same shape — piecewise-constant
+  class maps from a coarse random lattice, a per-class colour plus noise — from a
+  counter-based hash of ``(seed, sample index, pixel)``.  On the HIP path a batch is ONE
+  kernel writing the first conv's input layout straight into HBM (``csrc/data.hip``);
+  ``render_synthetic`` is the bit-identical PyTorch twin (CPU tests, ``impl="torch"``).
+  Sample ``i`` never depends on which rank, batch slot or resume point renders it.
 """
 from __future__ import annotations
 
+import math
 import os
 from typing import List, Optional, Tuple
 
@@ -26,7 +36,9 @@ import torch
 
 # ISPRS Vaihingen palette order (impervious, building, low veg, tree, car, clutter).
 _PALETTE = np.array([[255, 255, 255], [0, 0, 255], [0, 255, 255],
-                     [0, 255, 0], [255, 255, 0], [255, 0, 0]], dtype=np.float32) / 255.0
+                     [0, 255, 0], [255, 255, 0], [255, 0, 0]], dtype=np.float32) / np.float32(255.0)
+
+_M32 = 0xFFFFFFFF
 
 
 def _read_image(path: str) -> np.ndarray:
@@ -70,68 +82,248 @@ def to_tensors(x: np.ndarray, y: np.ndarray) -> Tuple[torch.Tensor, torch.Tensor
     return xt, torch.from_numpy(y.astype("int64"))
 
 
-class TileDataset:
-    """In-memory (image, label) tiles; images NCHW float32, labels int64."""
+# ---------------------------------------------------------------------- engine input layout
+def engine_input(x_nhwc: torch.Tensor, in_channels: int) -> torch.Tensor:
+    """Wrap a channel-last bf16 batch whose channels are zero-padded (to 8) as the NCHW-shaped
+    view the model API takes.  The HIP engine recognises the attached padded tensor and uses
+    it as the first conv's input with no conversion pass; any other consumer sees an ordinary
+    [N, C, (D,) H, W] tensor."""
+    nd = x_nhwc.dim()
+    v = x_nhwc[..., :in_channels].permute(0, nd - 1, *range(1, nd - 1))
+    v._ddlpc_nhwc = x_nhwc
+    return v
 
-    def __init__(self, x: torch.Tensor, y: torch.Tensor):
-        assert x.shape[0] == y.shape[0]
-        self.x, self.y = x, y
 
-    def __len__(self):
-        return self.x.shape[0]
+# ---------------------------------------------------------------------- synthetic tiles
+def _mix32(x: torch.Tensor) -> torch.Tensor:
+    """lowbias32 integer hash on int64 tensors holding uint32 values (== csrc/data.hip)."""
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
 
-    def get(self, idx) -> Tuple[torch.Tensor, torch.Tensor]:
-        idx = torch.as_tensor(idx, dtype=torch.long)
-        return self.x[idx], self.y[idx]
 
-    @classmethod
-    def from_dir(cls, path: str, test_holdout: int = 30):
-        xtr, ytr, xte, yte = load_files(path, test_holdout)
-        return cls(*to_tensors(xtr, ytr)), cls(*to_tensors(xte, yte)) if len(xte) else None
+def _mix32_int(v: int) -> int:
+    v &= _M32
+    v ^= v >> 16
+    v = (v * 0x7FEB352D) & _M32
+    v ^= v >> 15
+    v = (v * 0x846CA68B) & _M32
+    return v ^ (v >> 16)
+
+
+def synthetic_palette(classes: int, in_channels: int) -> torch.Tensor:
+    """Per-class colours: the Vaihingen palette for <= 6 RGB classes, else hashed colours."""
+    if classes <= len(_PALETTE) and in_channels == 3:
+        return torch.from_numpy(_PALETTE[:classes].copy())
+    pal = np.empty((classes, in_channels), dtype=np.float32)
+    for k in range(classes):
+        for c in range(in_channels):
+            h = _mix32_int(0x5BD1E995 ^ _mix32_int(k * 16 + c))
+            pal[k, c] = np.float32(h >> 8) * np.float32(1.0 / 16777216.0)
+    return torch.from_numpy(pal)
+
+
+def noise_k(noise: float) -> float:
+    """fp32 scale of the Irwin-Hall noise (std ``noise``), rounded once, shared host/device."""
+    return float(np.float32(noise * math.sqrt(3.0)))
+
+
+def render_synthetic(idx, seed: int, classes: int, in_channels: int, tile: int, dims: int,
+                     grid: int = 8, noise: float = 0.15, device=None,
+                     palette: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """PyTorch twin of ``synth_tiles_kernel``: the same bits, NCHW float32 + int64 labels."""
+    device = torch.device(device) if device is not None else torch.device("cpu")
+    idx = torch.as_tensor(idx, dtype=torch.int64).reshape(-1).to(device)
+    B = idx.numel()
+    pal = (palette if palette is not None else synthetic_palette(classes, in_channels)).to(device)
+    ar = torch.arange(tile, device=device, dtype=torch.int64)
+    cg = (ar * grid) // tile                                    # nearest lattice cell
+    if dims == 2:
+        cell = cg[:, None] * grid + cg[None, :]
+    else:
+        cell = (cg[:, None, None] * grid + cg[None, :, None]) * grid + cg[None, None, :]
+    S = tile ** dims
+    skey = _mix32_int(seed ^ 0x9E3779B9)
+    key = _mix32(torch.full_like(idx, skey) ^ (idx & _M32))     # [B]
+    ckey = _mix32((cell.reshape(-1) + 0x632BE5AB) & _M32)       # [S]
+    lab = _mix32(key[:, None] ^ ckey[None, :]) % classes         # [B, S]
+    p = torch.arange(S, device=device, dtype=torch.int64)
+    xs = []
+    inv = torch.tensor(1.0 / 16777216.0, dtype=torch.float32, device=device)
+    k = torch.tensor(noise_k(noise), dtype=torch.float32, device=device)
+    for c in range(in_channels):
+        base = key[:, None] ^ _mix32((p * 8 + c + 0x1B873593) & _M32)[None, :]
+        s = None
+        for j in range(4):
+            u = (_mix32((base + j * 0x9E3779B9) & _M32) >> 8).to(torch.float32) * inv
+            s = u if s is None else s + u
+        n = (s - 2.0) * k
+        xs.append((pal[lab, c] + n).clamp_(0.0, 1.0))
+    x = torch.stack(xs, 1).reshape((B, in_channels) + (tile,) * dims)
+    return x, lab.reshape((B,) + (tile,) * dims)
 
 
 class SyntheticTiles:
-    """Deterministic synthetic Vaihingen-shape tiles (RGB, ``classes`` labels).
+    """Deterministic synthetic Vaihingen-shape tiles (``classes`` labels, ``in_channels``).
 
     ``get(indices)`` renders the requested samples; sample ``i`` depends only on
-    ``(seed, i)``.  Works for 2-D tiles (``dims=2``: [N,3,T,T]) and 3-D volumes
-    (``dims=3``: [N,C,T,T,T]).  ``device`` lets the GPU render batches directly in HBM.
+    ``(seed, i)``.  2-D tiles (``dims=2``: [N,C,T,T]) or 3-D volumes (``dims=3``).
+    ``device``/``layout`` select where and how a batch is produced:
+
+    * CPU (default): float32 NCHW via ``render_synthetic``;
+    * a GPU with ``layout="engine"``: one ``synth_tiles`` HIP kernel writes the HIP engine's
+      input (channel-last bf16, 8 channels) into HBM — see ``engine_input``;
+    * a GPU with ``layout="nchw"``: the PyTorch twin on the device (stock-op baseline).
     """
 
     def __init__(self, length: int, tile: int, classes: int = 6, in_channels: int = 3,
                  seed: int = 0, dims: int = 2, grid: int = 8, noise: float = 0.15,
-                 device: Optional[torch.device] = None):
+                 device: Optional[torch.device] = None, layout: str = "nchw"):
+        if layout not in ("nchw", "engine"):
+            raise ValueError(f"layout={layout!r}")
         self.length, self.tile, self.classes = length, tile, classes
         self.in_channels, self.seed, self.dims = in_channels, seed, dims
         self.grid, self.noise = max(1, min(grid, tile)), noise
         self.device = torch.device(device) if device is not None else torch.device("cpu")
-        pal = _PALETTE
-        if classes > len(pal) or in_channels != 3:
-            g = np.random.default_rng(1234)
-            pal = g.random((classes, in_channels), dtype=np.float32)
-        self.palette = torch.tensor(pal[:classes, :in_channels], dtype=torch.float32)
+        self.layout = layout if self.device.type == "cuda" else "nchw"
+        self.palette = synthetic_palette(classes, in_channels).to(self.device)
 
     def __len__(self):
         return self.length
 
-    def _sample(self, i: int):
-        g = torch.Generator().manual_seed(self.seed * 1_000_003 + int(i))
-        sp = (self.grid,) * self.dims
-        coarse = torch.randint(0, self.classes, (1, 1) + sp, generator=g).float()
-        full = torch.nn.functional.interpolate(coarse, size=(self.tile,) * self.dims,
-                                               mode="nearest")[0, 0].long()
-        img = self.palette[full]                                   # [..., C]
-        img = img + self.noise * torch.randn(img.shape, generator=g)
-        img = img.clamp_(0.0, 1.0)
-        perm = (self.dims,) + tuple(range(self.dims))
-        return img.permute(*perm).contiguous(), full
+    def get(self, idx) -> Tuple[torch.Tensor, torch.Tensor]:
+        if self.layout == "engine":
+            from ..ops import _ext
+            it = torch.as_tensor(idx, dtype=torch.int64).reshape(-1)
+            it = it.to(self.device, non_blocking=True)
+            xp, y = _ext.ops().synth_tiles(it, self.seed, self.classes, self.in_channels,
+                                           self.tile, self.dims, self.grid,
+                                           noise_k(self.noise), self.palette, 8)
+            return engine_input(xp, self.in_channels), y
+        return render_synthetic(idx, self.seed, self.classes, self.in_channels, self.tile,
+                                self.dims, self.grid, self.noise, self.device, self.palette)
+
+
+# ---------------------------------------------------------------------- real tiles
+class TileDataset:
+    """In-memory (image, label) tiles: uint8 NHWC images, uint8 label maps.
+
+    ``get`` returns the reference's tensors (float32 NCHW in [0,1], int64 labels) on the
+    host.  ``to_device`` moves the raw uint8 tiles to HBM once (or, above ``budget_bytes``,
+    to pinned host memory with a one-batch-ahead copy stream) and returns a dataset whose
+    ``get`` produces device batches.
+    """
+
+    def __init__(self, x: np.ndarray, y: np.ndarray):
+        x = np.asarray(x)
+        y = np.asarray(y)
+        assert x.shape[0] == y.shape[0] and x.ndim == y.ndim + 1
+        if x.dtype != np.uint8:
+            raise TypeError("TileDataset holds uint8 images (as read from disk)")
+        self.x = torch.from_numpy(np.ascontiguousarray(x))
+        self.y = torch.from_numpy(np.ascontiguousarray(y.astype(np.uint8)))
+
+    def __len__(self):
+        return self.x.shape[0]
+
+    @property
+    def in_channels(self) -> int:
+        return int(self.x.shape[-1])
 
     def get(self, idx) -> Tuple[torch.Tensor, torch.Tensor]:
-        idx = [int(i) for i in torch.as_tensor(idx).reshape(-1).tolist()]
-        xs, ys = zip(*(self._sample(i) for i in idx))
-        x = torch.stack(xs).to(self.device, non_blocking=True)
-        y = torch.stack(ys).to(self.device, non_blocking=True)
-        return x, y
+        idx = torch.as_tensor(idx, dtype=torch.long).reshape(-1)
+        x = self.x[idx].float().div_(255.0)
+        nd = x.dim()
+        return x.permute(0, nd - 1, *range(1, nd - 1)).contiguous(), self.y[idx].long()
+
+    def to_device(self, device, layout: str = "engine",
+                  budget_bytes: Optional[int] = None) -> "DeviceTileDataset":
+        return DeviceTileDataset(self, device, layout, budget_bytes)
+
+    @classmethod
+    def from_dir(cls, path: str, test_holdout: int = 30):
+        xtr, ytr, xte, yte = load_files(path, test_holdout)
+        return cls(xtr, ytr), (cls(xte, yte) if len(xte) else None)
+
+
+class DeviceTileDataset:
+    """``TileDataset`` served from the GPU.
+
+    * resident (raw bytes <= budget, default half the free HBM): the uint8 tiles live in
+      HBM; ``get`` = one ``tile_gather`` kernel (``layout="engine"``) or a device gather +
+      convert (``layout="nchw"``).  No host copy per step.
+    * streamed: pinned host tiles; ``get`` copies the batch's uint8 bytes on a side copy
+      stream (the NEXT batch can be prefetched with ``prefetch(idx)``) and converts on the
+      device.
+    """
+
+    def __init__(self, base: TileDataset, device, layout: str = "engine",
+                 budget_bytes: Optional[int] = None):
+        self.base = base
+        self.device = torch.device(device)
+        self.layout = layout
+        self.in_channels = base.in_channels
+        nbytes = base.x.numel() + base.y.numel()
+        if budget_bytes is None:
+            free, _ = torch.cuda.mem_get_info(self.device)
+            budget_bytes = free // 2
+        self.resident = nbytes <= budget_bytes
+        if self.resident:
+            self.x = base.x.to(self.device)
+            self.y = base.y.to(self.device)
+        else:
+            self.x = base.x.pin_memory()
+            self.y = base.y.pin_memory()
+            self.copy_stream = torch.cuda.Stream(self.device)
+            self._pending = None
+
+    def __len__(self):
+        return len(self.base)
+
+    def prefetch(self, idx):
+        """Start the host->device copy of a future batch (streamed mode only)."""
+        if self.resident:
+            return
+        key = tuple(int(i) for i in torch.as_tensor(idx).reshape(-1).tolist())
+        ii = torch.tensor(key, dtype=torch.long)
+        xs = self.x[ii].pin_memory()
+        ys = self.y[ii].pin_memory()
+        with torch.cuda.stream(self.copy_stream):
+            xd = xs.to(self.device, non_blocking=True)
+            yd = ys.to(self.device, non_blocking=True)
+        self._pending = (key, xd, yd)
+
+    def _fetch_raw(self, idx):
+        key = tuple(int(i) for i in torch.as_tensor(idx).reshape(-1).tolist())
+        if self._pending is None or self._pending[0] != key:
+            self.prefetch(list(key))
+        _, xd, yd = self._pending
+        self._pending = None
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_stream(self.copy_stream)
+        xd.record_stream(cur)
+        yd.record_stream(cur)
+        return xd, yd
+
+    def get(self, idx) -> Tuple[torch.Tensor, torch.Tensor]:
+        if self.resident:
+            src, lab = self.x, self.y
+            it = torch.as_tensor(idx, dtype=torch.int64).reshape(-1).to(self.device,
+                                                                         non_blocking=True)
+        else:
+            src, lab = self._fetch_raw(idx)
+            it = torch.arange(src.shape[0], device=self.device, dtype=torch.int64)
+        if self.layout == "engine":
+            from ..ops import _ext
+            xp, y = _ext.ops().tile_gather(src, lab, it, 8)
+            return engine_input(xp, self.in_channels), y
+        x = src.index_select(0, it).float().div_(255.0)
+        nd = x.dim()
+        mf = torch.channels_last if nd == 4 else torch.channels_last_3d
+        x = x.permute(0, nd - 1, *range(1, nd - 1)).contiguous(memory_format=mf)
+        return x, lab.index_select(0, it).long()
 
 
 def device_random_batch(batch: int, tile: int, classes: int, device, in_channels: int = 3,

@@ -7,7 +7,7 @@ pickle (ref.py:561); here each rank builds its own from the same config.
 
 Implementation: parameters, gradients and both moments live in flat fp32 buffers
 (``parallel.flat.FlatParams``).  On GPU one HIP launch (``adam_step`` in
-``csrc/adam.hip``) updates the whole model — 8.7 M elements, 4 streams read + 3 written,
+``csrc/misc.hip``) updates the whole model — 8.7 M elements, 4 streams read + 3 written,
 HBM-bound — and, when a weight-pack table is attached, ALSO writes the bf16 copies of the
 conv weights in the layouts the conv kernels consume (KRSC for forward, flipped CRSK for
 dgrad), so no separate cast/transpose pass runs before the next forward.  On CPU the

@@ -1,6 +1,6 @@
 """Gradient codec entry points (K16-K18 of SURVEY.md §2.5).
 
-GPU tensors go through the fused HIP kernels of ``csrc/codec.hip``:
+GPU tensors go through the fused HIP kernels of ``csrc/misc.hip``:
 ``codec_absmax`` (one multi-segment absmax pass, K16), ``codec_encode`` (quantise to
 fp16/int8 levels, K17) and ``codec_decode_sum`` (dequantise W payloads, weight and sum in
 rank order into the fp32 gradient, K18).  CPU tensors use the torch oracle in

@@ -320,11 +320,33 @@ class _Block:
                                    pool, defer)
 
 
+def check_supported(model: nn.Module):
+    """Fail loudly on geometries the kernels do not tile (instead of a mid-step TORCH_CHECK):
+    every conv width a multiple of 8 (16-byte channel-last pixels), the up-sampled half of
+    each concat and every transposed conv a multiple of 32 channels, a head over 8/16/32/64
+    channels and at most 16 classes."""
+    w = list(model.enc_widths)
+    k = model.conv_last.weight.shape[0]
+    problems = []
+    if any(c % 8 for c in w):
+        problems.append(f"widths {w} must be multiples of 8")
+    if any(c % 32 for c in w[1:]):
+        problems.append(f"decoder concat / transposed-conv widths {w[1:]} must be multiples of 32")
+    if w[0] not in (8, 16, 32, 64):
+        problems.append(f"head input width {w[0]} not in (8, 16, 32, 64)")
+    if not 1 <= k <= 16:
+        problems.append(f"out_classes {k} not in [1, 16]")
+    if problems:
+        raise ValueError("HIP engine: unsupported U-Net geometry: " + "; ".join(problems) +
+                         " (use impl='torch' for this configuration)")
+
+
 class UNetEngine:
     """Runs a ``models.UNet`` through the HIP kernels (attach with ``UNet.to_hip()``)."""
 
     def __init__(self, model: nn.Module, strict: bool = True):
         _ext.load(strict=strict)
+        check_supported(model)
         self.model = model
         dev = next(model.parameters()).device
         if dev.type != "cuda":
@@ -406,10 +428,6 @@ class UNetEngine:
         if self.side is not None and self._side_used:
             torch.cuda.current_stream(self.side.device).wait_stream(self.side)
             self._side_used = False
-        # deferred BatchNorm activations (see ``features``): DDLPC_DEFER_BN=all|convt|none
-        self.defer_mode = os.environ.get("DDLPC_DEFER_BN", "all")
-        # transposed-conv weight gradients on the side stream too (DDLPC_SIDE_CONVT=0: main)
-        self.side_convt = os.environ.get("DDLPC_SIDE_CONVT", "1") != "0"
 
     def ready(self, *params):
         """Gradients of ``params`` are complete once the queued work finishes.  Called on
@@ -442,12 +460,19 @@ class UNetEngine:
     def to_nhwc(self, x: torch.Tensor) -> torch.Tensor:
         """NCHW-shaped input -> channel-last bf16 with channels padded to 8 (16-byte pixels
         for the first conv's LDS-DMA).  bf16 channels_last input with C % 8 == 0 is used
-        zero-copy."""
+        zero-copy, and so is a batch from the device input pipeline (``data.engine_input``:
+        the generator / gather kernels already wrote this layout)."""
+        padded = getattr(x, "_ddlpc_nhwc", None)
+        if padded is not None and padded.shape[0] == x.shape[0]:
+            return padded
         nd = x.dim()
         perm = (0,) + tuple(range(2, nd)) + (1,)
         xt = x.permute(*perm)
         if xt.is_contiguous() and xt.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
             return xt
+        cl = torch.channels_last if nd == 4 else torch.channels_last_3d
+        if not (x.is_contiguous() or x.is_contiguous(memory_format=cl)):
+            x = x.contiguous(memory_format=cl)
         return _ops().to_nhwc_bf16(x, 8)
 
     # ------------------------------------------------------------------ graph

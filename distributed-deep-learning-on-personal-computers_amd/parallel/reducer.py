@@ -23,7 +23,12 @@ MI355X design:
 * reduction: correct mean (pre-scaled by 1/W, then SUM), ``sum``, or ``reference`` (the
   reference's skewed weights; for W=2 that is a plain sum, SURVEY.md §2.6);
 * optional lossy codec (fp16/int8 absmax, ref.py:25) as an all-gather of packed payloads
-  + scales, decoded and summed in rank order (``parallel.codec``; fused HIP kernels on GPU).
+  + scales, decoded and summed in rank order (``parallel.codec``; fused HIP kernels on GPU);
+* optional bf16 wire format (``wire_dtype="bf16"``, lossless codec off): half the bytes of
+  the fp32 all-reduce with fp32 accumulation — an all-to-all of bf16 chunks (the
+  reduce-scatter's transport), a rank-ordered fp32 sum of the owned chunk, and an
+  all-gather of the bf16 result; every rank receives identical bits.  For slow links (the
+  reference's "PCs over Ethernet" setting) this halves the exchange time.
 """
 from __future__ import annotations
 
@@ -39,7 +44,7 @@ from .flat import FlatParams
 
 class _Bucket:
     __slots__ = ("idx", "start", "end", "params", "pending", "work", "payload", "scales",
-                 "gathered", "launched")
+                 "gathered", "launched", "wire")
 
     def __init__(self, idx, start, end, params):
         self.idx, self.start, self.end, self.params = idx, start, end, params
@@ -47,13 +52,17 @@ class _Bucket:
         self.work = None
         self.payload = self.scales = self.gathered = None
         self.launched = False
+        self.wire = None                 # bf16 wire buffers (send, recv, owned chunk, out)
 
 
 class GradBucketReducer:
     def __init__(self, flat: FlatParams, group=None, bucket_mb: float = 8.0,
                  reduce: str = "mean", grad_codec: str = "none", codec_scale: str = "bucket",
-                 overlap: bool = True, use_hooks: bool = True):
+                 overlap: bool = True, use_hooks: bool = True, wire_dtype: str = "fp32"):
+        if wire_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"wire_dtype={wire_dtype!r}")
         self.flat = flat
+        self.wire_dtype = wire_dtype
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -155,6 +164,9 @@ class GradBucketReducer:
             # dependence on the collective library's AVG support)
             if self.weight != 1.0:
                 g.mul_(self.weight)
+            if self.wire_dtype == "bf16":
+                self._launch_bf16(b, g)
+                return
             b.work = dist.all_reduce(g, group=self.group, async_op=True)
             return
         # lossy codec: encode -> all_gather(payload, scales) -> decode+sum at finish()
@@ -167,6 +179,23 @@ class GradBucketReducer:
         w2 = dist.all_gather(b.gathered[1], b.scales, group=self.group, async_op=True)
         b.work = (w1, w2)
 
+    def _launch_bf16(self, b: _Bucket, g: torch.Tensor):
+        """bf16 transport, fp32 accumulation: all-to-all of bf16 chunks -> each rank sums the
+        chunk it owns in fp32, in rank order -> all-gather of the bf16 sums."""
+        n, W = g.numel(), self.world
+        chunk = -(-n // W)
+        if b.wire is None:
+            send = torch.zeros(chunk * W, dtype=torch.bfloat16, device=g.device)
+            b.wire = (send, torch.empty_like(send),
+                      torch.empty(chunk, dtype=torch.bfloat16, device=g.device),
+                      torch.empty_like(send))
+        send, recv, own, out = b.wire
+        send[:n].copy_(g)
+        dist.all_to_all_single(recv, send, group=self.group, async_op=True).wait()
+        own.copy_(recv.view(W, chunk).float().sum(0))
+        b.work = ("bf16", dist.all_gather_into_tensor(out, own, group=self.group,
+                                                      async_op=True))
+
     def _codec_segments(self, b: _Bucket) -> List[Tuple[int, int]]:
         if self.codec_scale == "tensor":
             return [(s - b.start, e - b.start) for s, e in (self.flat.span(p) for p in b.params)]
@@ -175,8 +204,6 @@ class GradBucketReducer:
     def finish(self):
         """Complete all reductions (launch stragglers); compute stream waits, host does not."""
         if self.world == 1:
-            if self.reduce == "sum" or self.weight == 1.0:
-                return
             return
         if self.codec != "none" and self.codec_scale == "global":
             self._finish_global_codec()
@@ -187,7 +214,11 @@ class GradBucketReducer:
         for b in self.buckets:
             if b.work is None:
                 continue
-            if isinstance(b.work, tuple):
+            if isinstance(b.work, tuple) and b.work[0] == "bf16":
+                b.work[1].wait()
+                g = self._seg(b)
+                g.copy_(b.wire[3][:g.numel()])
+            elif isinstance(b.work, tuple):
                 for w in b.work:
                     w.wait()
                 self._decode_bucket(b)

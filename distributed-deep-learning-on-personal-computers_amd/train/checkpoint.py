@@ -19,6 +19,7 @@ Files are written atomically (tmp + rename) by rank 0 only.
 from __future__ import annotations
 
 import os
+import re
 from typing import Any, Dict, Optional
 
 import torch
@@ -84,8 +85,9 @@ def load_checkpoint(path: str, model: Optional[torch.nn.Module] = None, optimize
 def latest_checkpoint(ckpt_dir: str) -> Optional[str]:
     if not ckpt_dir or not os.path.isdir(ckpt_dir):
         return None
-    cands = [f for f in os.listdir(ckpt_dir) if f.startswith("ckpt_") and f.endswith(".pt")]
+    # only the step-numbered files Trainer.save() writes (ckpt_final.pt etc. are ignored)
+    cands = [(int(m.group(1)), f) for f in os.listdir(ckpt_dir)
+             for m in [re.fullmatch(r"ckpt_(\d+)\.pt", f)] if m]
     if not cands:
         return None
-    cands.sort(key=lambda f: int(f[5:-3]))
-    return os.path.join(ckpt_dir, cands[-1])
+    return os.path.join(ckpt_dir, max(cands)[1])

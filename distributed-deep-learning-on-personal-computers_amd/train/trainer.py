@@ -21,7 +21,6 @@ every rank applies identical gradients — with the MI355X machinery underneath:
 from __future__ import annotations
 
 import contextlib
-import math
 import os
 import time
 from typing import Dict, List, Optional, Tuple
@@ -35,8 +34,8 @@ from ..models.unet import UNet
 from ..ops import _ext
 from ..ops.adam import FlatAdam
 from ..parallel import (GradBucketReducer, assert_replicas_identical, broadcast_buffers,
-                        broadcast_module, flatten_module, init_distributed)
-from ..utils.metrics import DeviceMeter, RunLogger, StepTimer, dump_pngs, iou_per_class
+                        broadcast_module, broadcast_tensors, flatten_module, init_distributed)
+from ..utils.metrics import DeviceMeter, RunLogger, dump_pngs
 from ..utils.tracing import PhaseTimer, StepProfiler, enable_ranges, trace_range
 from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
 
@@ -76,11 +75,7 @@ class Trainer:
             self.optimizer.weight_pack = model._engine.pack_weights
         self.reducer = None
         if self.world > 1:
-            self.reducer = GradBucketReducer(self.flat, bucket_mb=cfg.bucket_mb,
-                                             reduce=cfg.reduce, grad_codec=cfg.grad_codec,
-                                             codec_scale=cfg.codec_scale,
-                                             overlap=cfg.overlap_comm,
-                                             use_hooks=(self.impl != "hip"))
+            self.reducer = self._make_reducer(cfg.bucket_mb)
         if self.impl == "hip":
             # kernels write gradients straight into the flat grad buffer and trigger the
             # reducer's buckets themselves (no autograd accumulate pass)
@@ -111,26 +106,78 @@ class Trainer:
                                       shard=cfg.shard_data, shuffle=cfg.shuffle, seed=cfg.seed)
         if cfg.resume:
             path = latest_checkpoint(cfg.ckpt_dir) if cfg.resume == "auto" else cfg.resume
-            if path:
+            if path and os.path.exists(path):
                 self.load(path)
+            # only rank 0 writes checkpoints: on machines without a shared filesystem the
+            # other ranks find none, so rank 0's restored state is authoritative
+            self._broadcast_state()
+
+    def _make_reducer(self, bucket_mb: float) -> GradBucketReducer:
+        c = self.cfg
+        return GradBucketReducer(self.flat, bucket_mb=bucket_mb, reduce=c.reduce,
+                                 grad_codec=c.grad_codec, codec_scale=c.codec_scale,
+                                 overlap=c.overlap_comm, use_hooks=(self.impl != "hip"),
+                                 wire_dtype=c.wire_dtype)
+
+    def set_bucket_mb(self, bucket_mb: float) -> int:
+        """Re-bucket the gradient reducer between steps (bucket-size sweeps, SURVEY.md §5.8);
+        returns the number of buckets."""
+        if self.reducer is None:
+            return 0
+        self.reducer.remove_hooks()
+        self.cfg.bucket_mb = bucket_mb
+        self.reducer = self._make_reducer(bucket_mb)
+        if self.impl == "hip":
+            self.model._engine.enable_direct_grads(self.reducer.mark_ready)
+        return len(self.reducer.buckets)
+
+    def _broadcast_state(self):
+        """Rank 0's parameters, buffers, Adam moments and step counters -> every rank."""
+        if self.world == 1:
+            return
+        broadcast_module(self.model, src=0)
+        broadcast_tensors([self.optimizer.exp_avg, self.optimizer.exp_avg_sq], src=0)
+        cnt = torch.tensor([self.epoch, self.step_count, self.micro_count, self.epoch_step,
+                            self.optimizer.step_count], dtype=torch.int64, device=self.device)
+        dist.broadcast(cnt, src=0)
+        (self.epoch, self.step_count, self.micro_count, self.epoch_step,
+         opt_steps) = (int(v) for v in cnt.tolist())
+        self.optimizer.step_count = opt_steps
+        if self.optimizer._dev_scal is not None:
+            self.optimizer._dev_scal[0] = float(opt_steps)
+        if self.model._engine is not None:
+            self.model._engine.pack_weights()
 
     # ------------------------------------------------------------------ data
     def _build_data(self):
+        """Datasets that produce device batches directly on a GPU: the
+        synthetic generator renders in HBM, a real dataset is uploaded once as uint8."""
         c = self.cfg
+        cuda = self.device.type == "cuda"
+        layout = "engine" if self.impl == "hip" else "nchw"
         if c.data == "vaihingen_dir":
             if not c.data_dir:
                 raise ValueError("data=vaihingen_dir needs data_dir")
-            return TileDataset.from_dir(c.data_dir, c.test_holdout)
+            tr, te = TileDataset.from_dir(c.data_dir, c.test_holdout)
+            if cuda and c.data_on_device:
+                budget = None if c.data_hbm_gb is None else int(c.data_hbm_gb * 2**30)
+                tr = tr.to_device(self.device, layout, budget)
+                te = te.to_device(self.device, layout, budget) if te is not None else None
+            return tr, te
         n_total = c.num_samples + c.test_holdout
+        dev = self.device if (cuda and c.data_on_device) else None
         full = SyntheticTiles(n_total, c.tile, c.model.out_classes, c.model.in_channels,
-                              seed=c.seed, dims=c.model.dims)
+                              seed=c.seed, dims=c.model.dims, device=dev, layout=layout)
         return _Subset(full, 0, c.num_samples), _Subset(full, c.num_samples, n_total)
 
     def _to_device(self, x, y):
+        if x.device == self.device and getattr(x, "_ddlpc_nhwc", None) is not None:
+            return x, y.to(self.device, non_blocking=True)     # engine layout, already in HBM
         x = x.to(self.device, non_blocking=True)
         y = y.to(self.device, non_blocking=True)
-        if self.device.type == "cuda" and self.cfg.model.dims == 2:
-            x = x.to(memory_format=torch.channels_last)
+        if self.device.type == "cuda":
+            x = x.contiguous(memory_format=torch.channels_last if x.dim() == 4
+                             else torch.channels_last_3d)
             if self.impl == "hip":
                 x = x.to(torch.bfloat16)
         return x, y
@@ -270,19 +317,20 @@ class Trainer:
         last = {}
         t_start = time.perf_counter()
         log_t, log_step = t_start, self.step_count
+        prefetch = getattr(self.train_set, "prefetch", None)     # host-streamed datasets
         while self.epoch < c.epochs:
             self.sampler.set_epoch(self.epoch)
             self.meter.reset()
             t_ep = time.perf_counter()
             pending: List[Tuple[torch.Tensor, torch.Tensor]] = []
             # resumed mid-epoch: skip the micro-batches the checkpointed steps consumed
-            skip = self.epoch_step * c.accum_steps
+            batches = list(self.sampler.batches(c.batch_per_gpu))[self.epoch_step * c.accum_steps:]
             steps_this_epoch = self.epoch_step
-            for idx in self.sampler.batches(c.batch_per_gpu):
-                if skip > 0:
-                    skip -= 1
-                    continue
+            stopped = False
+            for bi, idx in enumerate(batches):
                 pending.append(self._to_device(*self.train_set.get(idx)))
+                if prefetch is not None and bi + 1 < len(batches):
+                    prefetch(batches[bi + 1])     # next batch's H2D copy overlaps this step
                 if len(pending) < c.accum_steps:
                     continue
                 self.train_step(pending)
@@ -305,9 +353,23 @@ class Trainer:
                 if (self.rank == c.fault_rank and self.step_count == c.fault_step
                         and os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") == "0"):
                     self.logger.close()
+                    mark_dir = c.ckpt_dir or c.log_dir
+                    if mark_dir:                  # evidence for tests / post-mortems
+                        os.makedirs(mark_dir, exist_ok=True)
+                        with open(os.path.join(mark_dir, f"fault_rank{self.rank}_step"
+                                               f"{self.step_count}.marker"), "w") as f:
+                            f.write("injected\n")
                     os._exit(17)                  # injected fault: this rank dies
                 if c.max_steps and self.step_count >= c.max_steps:
+                    stopped = bi + 1 < len(batches)
                     break
+            if stopped:
+                # max_steps inside an epoch: the epoch is NOT finished — keep (epoch,
+                # epoch_step) so a resume with a larger max_steps continues right here
+                last = self.meter.reduce()
+                last.update(epoch=self.epoch, epoch_s=time.perf_counter() - t_ep,
+                            steps=self.step_count, partial_epoch=True)
+                break
             # leftover micro-batches: gradients stay accumulated into the next epoch's first
             # step, as in the reference (ref.py:748: 127 % 50 = 27 carry over).
             for x, y in pending:

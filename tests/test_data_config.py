@@ -33,6 +33,8 @@ def test_load_files_reference_convention(tmp_path):
     assert torch.allclose(x, ref)
     tr, te = TileDataset.from_dir(str(d))
     assert len(tr) == 5 and len(te) == 30
+    xg, yg = tr.get([1, 4])                     # host get(): the reference's tensors
+    assert torch.equal(xg, x[[1, 4]]) and torch.equal(yg, y[[1, 4]])
 
 
 def test_synthetic_deterministic_and_learnable_shape():

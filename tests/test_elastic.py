@@ -37,7 +37,9 @@ def test_rank_failure_restart_resumes_to_identical_weights(tmp_path):
     r = _torchrun(["--ckpt-dir", el_dir, "--resume", "auto", "--fault-rank", "1",
                    "--fault-step", "2"], restarts=1)
     assert r.returncode == 0, r.stderr[-3000:]
-    assert "exitcode" in r.stderr or "17" in r.stderr     # the injected failure happened
+    # the injected failure happened (marker written by the dying rank), and torchrun restarted
+    assert os.path.exists(os.path.join(el_dir, "fault_rank1_step2.marker")), os.listdir(el_dir)
+    assert "exitcode: 17" in r.stderr or "exitcode  : 17" in r.stderr, r.stderr[-2000:]
     a = torch.load(os.path.join(ref_dir, "ckpt_4.pt"), weights_only=True)
     b = torch.load(os.path.join(el_dir, "ckpt_4.pt"), weights_only=True)
     assert a["step"] == b["step"] == 4 and a["epoch"] == b["epoch"]

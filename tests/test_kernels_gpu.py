@@ -279,9 +279,12 @@ def test_convt(ops, N, H, W, Cin, Cout):
     assert rel_err(db, gb) < 1e-3
 
 
-def test_head_ce(ops):
+@pytest.mark.parametrize("C,K", [(32, 6), (64, 6), (16, 3), (8, 2), (64, 11), (32, 16), (8, 1),
+                                 (64, 2)])
+def test_head_ce(ops, C, K):
+    """Any K <= 16 classes for C in {8, 16, 32, 64} (padded class slots, runtime K)."""
     torch.manual_seed(6)
-    N, H, W, C, K = 2, 32, 32, 32, 6
+    N, H, W = 2, 32, 32
     a = torch.relu(torch.randn(N, C, H, W, device=DEV)).bfloat16()
     wh = torch.randn(K, C, device=DEV) * 0.3
     bh = torch.randn(K, device=DEV) * 0.1
@@ -379,6 +382,43 @@ def test_bilinear(ops):
     (gx,) = torch.autograd.grad(ref, xr, dy.float())
     dx = ops.bilinear_up2_bwd(nhwc(dy))
     assert rel_err(nchw(dx), gx) < 1e-2
+
+
+def test_trilinear_3d(ops):
+    """3-D up-sampling (UpBlock bilinear mode with dims=3 -> trilinear, align_corners)."""
+    torch.manual_seed(19)
+    x = torch.randn(1, 16, 4, 6, 8, device=DEV).bfloat16()
+    y = ops.bilinear_up2(nhwc(x))
+    xr = x.float().requires_grad_(True)
+    ref = F.interpolate(xr, scale_factor=2, mode="trilinear", align_corners=True)
+    assert rel_err(nchw(y), ref) < 1e-2
+    dy = torch.randn_like(ref).bfloat16()
+    (gx,) = torch.autograd.grad(ref, xr, dy.float())
+    dx = ops.bilinear_up2_bwd(nhwc(dy))
+    assert rel_err(nchw(dx), gx) < 1e-2
+
+
+@pytest.mark.parametrize("N,D,H,W,Cin,Cout", [(1, 4, 4, 8, 64, 64), (2, 4, 8, 8, 128, 64)])
+def test_convt3d(ops, N, D, H, W, Cin, Cout):
+    """ConvTranspose3d(k2, s2) forward / data / weight gradients vs fp32 torch."""
+    torch.manual_seed(20)
+    x = torch.randn(N, Cin, D, H, W, device=DEV).bfloat16()
+    w = torch.randn(Cin, Cout, 2, 2, 2, device=DEV) / math.sqrt(Cin)
+    b = torch.randn(Cout, device=DEV) * 0.1
+    pk = pack_conv(ops, w)
+    out = ops.convt_fwd(nhwc(x), pk.fwd, b, Cout)
+    xr = x.float().requires_grad_(True)
+    wr = w.bfloat16().float().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    ref = F.conv_transpose3d(xr, wr, br, stride=2)
+    assert rel_err(nchw(out), ref) < 1e-2
+    dout = torch.randn_like(ref).bfloat16()
+    gx, gw, gb = torch.autograd.grad(ref, [xr, wr, br], dout.float())
+    dx = ops.convt_dgrad(nhwc(dout), pk.dgrad, Cin)[0]
+    assert rel_err(nchw(dx), gx) < 1e-2
+    dw, db = ops.convt_wgrad(nhwc(x), nhwc(dout))
+    assert rel_err(dw.view_as(gw), gw) < 5e-3
+    assert rel_err(db, gb) < 1e-3
 
 
 def test_conv3d_fwd_wgrad(ops):

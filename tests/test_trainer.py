@@ -113,3 +113,75 @@ def test_bench_torchrun_two_ranks_gloo():
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
     assert rec["config"]["global_batch"] == 4 and rec["value"] > 0
+
+
+def test_resume_with_max_steps_inside_an_epoch(tmp_path):
+    """max_steps stopping mid-epoch must not advance the epoch: a resume with a larger
+    max_steps continues inside the same epoch and reaches the same weights as one run."""
+    full = _cfg(tmp_path / "a", epochs=2, max_steps=None, shuffle=True, ckpt_dir=None,
+                log_dir=None)
+    _, t_full = train(full, device="cpu", return_trainer=True)
+    # 16 samples / (2 x 2) = 4 steps per epoch; stop after 3 (inside epoch 0), then resume
+    part = _cfg(tmp_path / "b", epochs=2, max_steps=3, shuffle=True, log_dir=None)
+    _, t1 = train(part, device="cpu", return_trainer=True)
+    assert (t1.epoch, t1.epoch_step, t1.step_count) == (0, 3, 3)
+    res = _cfg(tmp_path / "b", epochs=2, max_steps=None, shuffle=True, resume="auto",
+               log_dir=None)
+    _, t2 = train(res, device="cpu", return_trainer=True)
+    assert t2.step_count == t_full.step_count == 8
+    assert torch.allclose(t2.flat.param_buf, t_full.flat.param_buf, atol=1e-6)
+
+
+def test_latest_checkpoint_ignores_non_step_names(tmp_path):
+    from ddlpc.train.checkpoint import latest_checkpoint
+    for n in ("ckpt_3.pt", "ckpt_12.pt", "ckpt_final.pt", "ckpt_7.pt.tmp", "other.pt"):
+        (tmp_path / n).write_bytes(b"x")
+    assert latest_checkpoint(str(tmp_path)).endswith("ckpt_12.pt")
+
+
+def test_synthetic_sample_independent_of_batch_and_rank():
+    """Sample i renders identically whatever batch / rank / order asks for it (counter-based
+    hash), and the generator is learnable-shaped: piecewise-constant labels, bounded pixels."""
+    from ddlpc.data import SyntheticTiles
+    from ddlpc.data.datasets import render_synthetic, synthetic_palette
+    ds = SyntheticTiles(100, 32, classes=6, seed=5)
+    xa, ya = ds.get([3, 17, 42])
+    xb, yb = ds.get([42, 3])
+    assert torch.equal(xa[2], xb[0]) and torch.equal(ya[0], yb[1])
+    assert float(xa.min()) >= 0.0 and float(xa.max()) <= 1.0
+    assert ya[0, :4, :4].unique().numel() == 1          # one lattice cell (32/8 = 4 px)
+    x3, y3 = render_synthetic([1], 0, 10, 4, 8, 3, grid=2)
+    assert x3.shape == (1, 4, 8, 8, 8) and int(y3.max()) < 10
+    assert synthetic_palette(10, 4).shape == (10, 4)
+
+
+def _resume_rank(rank, world, ckdir):
+    import os as _os
+    from ddlpc.config import ModelConfig, TrainConfig
+    from ddlpc.train.trainer import Trainer
+    cfg = TrainConfig(model=ModelConfig(out_classes=2, depth=4, width_divisor=8), tile=32,
+                      num_samples=8, test_holdout=0, batch_per_gpu=2, epochs=1,
+                      ckpt_dir=_os.path.join(ckdir, f"rank{rank}"), resume="auto")
+    tr = Trainer(cfg, device="cpu")
+    out = {"step": tr.step_count, "epoch_step": tr.epoch_step,
+           "opt_step": tr.optimizer.step_count,
+           "p": float(tr.flat.param_buf.double().sum()),
+           "m": float(tr.optimizer.exp_avg.double().abs().sum())}
+    tr.close()
+    return out
+
+
+def test_resume_rank0_state_broadcast_without_shared_fs(tmp_path):
+    """Only rank 0 has the checkpoint file (no shared filesystem): every rank must adopt
+    rank 0's restored weights, Adam moments and counters."""
+    from dist_utils import run
+    cfg = _cfg(tmp_path, epochs=1, max_steps=3, ckpt_dir=str(tmp_path / "rank0"),
+               model=ModelConfig(out_classes=2, depth=4, width_divisor=8), tile=32,
+               num_samples=8, test_holdout=0, batch_per_gpu=2, accum_steps=1, log_dir=None)
+    _, tr = train(cfg, device="cpu", return_trainer=True)
+    want_p = float(tr.flat.param_buf.double().sum())
+    res = run(_resume_rank, 2, (str(tmp_path),), timeout=200)
+    for r in (0, 1):
+        o = res[r]
+        assert (o["step"], o["epoch_step"], o["opt_step"]) == (3, 3, 3), o
+        assert abs(o["p"] - want_p) < 1e-9 and o["m"] > 0, o

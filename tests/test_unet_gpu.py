@@ -13,19 +13,24 @@ def _cos(a, b):
     return float((a @ b) / (a.norm() * b.norm()).clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("depth,wd,tile,mode,dims", [
-    (5, 2, 128, "conv_transpose", 2), (4, 4, 64, "bilinear", 2), (3, 4, 32, "conv_transpose", 3)])
-def test_unet_engine_matches_torch(depth, wd, tile, mode, dims):
+@pytest.mark.parametrize("depth,wd,tile,mode,dims,classes", [
+    (5, 2, 128, "conv_transpose", 2, 6), (4, 4, 64, "bilinear", 2, 6),
+    (3, 4, 32, "conv_transpose", 3, 6),
+    (5, 1, 64, "conv_transpose", 2, 6),      # standard U-Net widths (NN_in_model = 1, ref.py:687)
+    (4, 2, 64, "conv_transpose", 2, 3),      # out_classes 3 (the CPU DP tests' config)
+    (4, 4, 64, "bilinear", 2, 11)])          # 16-channel head, 11 classes (padded to 16)
+def test_unet_engine_matches_torch(depth, wd, tile, mode, dims, classes):
     """HIP bf16 gradients must be as close to the fp32 oracle as stock PyTorch bf16 autocast."""
     from ddlpc.models import UNet
     torch.manual_seed(0)
-    ref = UNet(out_classes=6, width_divisor=wd, depth=depth, up_sample_mode=mode, dims=dims).cuda()
+    ref = UNet(out_classes=classes, width_divisor=wd, depth=depth, up_sample_mode=mode,
+               dims=dims).cuda()
     amp = copy.deepcopy(ref)
     hip = copy.deepcopy(ref).to_hip()
     N = 4
     shape = (N, 3) + (tile,) * dims
     x = torch.rand(shape, device="cuda").bfloat16().float()
-    y = torch.randint(0, 6, (N,) + (tile,) * dims, device="cuda")
+    y = torch.randint(0, classes, (N,) + (tile,) * dims, device="cuda")
     loss_r = F.cross_entropy(ref(x), y)
     loss_r.backward()
     with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -172,3 +177,35 @@ def test_choose_schedule_times_both_and_keeps_faster():
     assert (r["side_ms"] <= r["serial_ms"]) == r["side_stream"]
     assert tr.optimizer.step_count == 6
     tr.close()
+
+
+def test_hip_grad_accumulation_matches_fp32_oracle():
+    """accum_steps > 1 on the HIP path: the kernels ADD the second micro-batch's weight
+    gradients into the flat buffer (direct grads, incl. the padded first-layer path); the
+    accumulated gradient must match the fp32 oracle's sum over both micro-batches."""
+    from ddlpc.config import ModelConfig, TrainConfig
+    from ddlpc.data import device_random_batch
+    from ddlpc.models import UNet
+    from ddlpc.train.trainer import Trainer
+    cfg = TrainConfig(model=ModelConfig(out_classes=6, depth=4), tile=64, batch_per_gpu=4,
+                      num_samples=1, test_holdout=0, impl="hip", accum_steps=2)
+    tr = Trainer(cfg, device="cuda")
+    ref = UNet(out_classes=6, depth=4).cuda()
+    ref.load_state_dict(tr.model.state_dict())
+    mb = [device_random_batch(4, 64, 6, tr.device, seed=s) for s in (1, 2)]
+    tr.optimizer.zero_grad()
+    for x, y in mb:
+        loss, _ = tr.model.loss_and_correct(x, y)
+        loss.backward()
+    torch.cuda.synchronize()
+    for x, y in mb:
+        F.cross_entropy(ref(x.float().contiguous()), y).backward()
+    bad = []
+    for (n, pr), (_, ph) in zip(ref.named_parameters(), tr.model.named_parameters()):
+        if n.endswith((".0.bias", ".3.bias")) and "double_conv.double_conv" in n:
+            continue
+        c = _cos(pr.grad, ph.grad)
+        if c < 0.98:
+            bad.append((n, c))
+    tr.close()
+    assert not bad, bad
