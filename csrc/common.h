@@ -116,4 +116,12 @@ DDLPC_DEVICE int xcd_remap(int bid, int nblocks) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / kX;
 }
 
+// An offset the compiler cannot prove loop-invariant (an SGPR through an empty asm): LDS
+// tables indexed with it are re-read where used instead of being hoisted into live VGPRs.
+DDLPC_DEVICE int opaque_zero() {
+  int z = 0;
+  asm volatile("" : "+s"(z));
+  return z;
+}
+
 inline int ceil_div(long a, long b) { return static_cast<int>((a + b - 1) / b); }

@@ -15,8 +15,8 @@
 //       label   = coarse[(h*grid)/tile][(w*grid)/tile]           (nearest up-sampling)
 //       u_j     = (mix(key ^ mix(p*8 + ch + 0x1B873593) + j*0x9E3779B9) >> 8) * 2^-24
 //       x       = clamp(palette[label][ch] + (((u0+u1)+u2)+u3 - 2) * k, 0, 1)   -> bf16
-//     (Irwin-Hall noise: k = noise*sqrt(3) gives std `noise`; every float op is an
-//     explicitly rounded add/mul so the host twin matches bit for bit.)
+//     (Irwin-Hall noise: k = noise*sqrt(3) gives std `noise`; every float op rounds on its
+//     own — no FMA contraction — so the host twin matches bit for bit.)
 //   * tile_gather_kernel: a real dataset uploaded ONCE to HBM as uint8 NHWC (+ uint8 label
 //     maps): gather the batch's sample indices, /255 (IEEE division, as the reference's
 //     numpy op), pad, bf16; labels widen to int64.
@@ -37,6 +37,14 @@ DDLPC_DEVICE uint32_t mix32(uint32_t x) {
 }
 
 DDLPC_DEVICE float u24(uint32_t h) { return (float)(h >> 8) * (1.0f / 16777216.0f); }
+
+// a separately rounded fp32 multiply: HIP's __fmul_rn is a plain operator that the default
+// -ffp-contract=fast still fuses into the following add (the PyTorch twin rounds twice)
+DDLPC_DEVICE float mul_rn(float a, float b) {
+  float r;
+  asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 
 // one thread per pixel; spatial = tile^dims pixels per sample, row-major (d, h, w)
 __global__ __launch_bounds__(256) void synth_tiles_kernel(
@@ -69,7 +77,7 @@ __global__ __launch_bounds__(256) void synth_tiles_kernel(
         s = __fadd_rn(s, u24(mix32(base + 0x9E3779B9u)));
         s = __fadd_rn(s, u24(mix32(base + 2u * 0x9E3779B9u)));
         s = __fadd_rn(s, u24(mix32(base + 3u * 0x9E3779B9u)));
-        const float n = __fmul_rn(__fadd_rn(s, -2.0f), k);
+        const float n = mul_rn(__fadd_rn(s, -2.0f), k);
         v = fminf(fmaxf(__fadd_rn(palette[lab * in_ch + c], n), 0.f), 1.f);
       }
       f[c] = v;

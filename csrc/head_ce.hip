@@ -24,14 +24,9 @@ constexpr int MAXC = 64, MAXK = 16;
 // (sW/sb staged that way in LDS), so they add exp(-inf) = 0 to the softmax, never win the
 // arg-max and receive a zero gradient.
 
-// An LDS offset the compiler cannot prove loop-invariant: the K*C head weights stay in LDS
-// (uniform-address broadcast reads, 4 per ds_read_b128) instead of being hoisted out of the
-// pixel loop into K*C live VGPRs (measured: 150-256 VGPRs, occupancy 1-3, spills at C=64).
-DDLPC_DEVICE int opaque_zero() {
-  int z = 0;
-  asm volatile("" : "+s"(z));
-  return z;
-}
+// (opaque_zero, common.h: the K*C head weights stay in LDS — uniform-address broadcast
+// reads — instead of being hoisted out of the pixel loop into K*C live VGPRs; measured
+// 150-256 VGPRs, occupancy 1-3 and spills at C=64 without it)
 
 // The head's input activation, 8 channels at c8.  With a deferred BatchNorm (sBN != null:
 // scale [C] | shift [C] in LDS) the tensor holds the block's PRE-BN conv output y and the

@@ -16,8 +16,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("classes,tile,dims,grid", [(6, 64, 2, 8), (3, 50, 2, 8), (10, 16, 3, 4),
-                                                    (2, 33, 2, 5)])
+@pytest.mark.parametrize("classes,tile,dims,grid", [(6, 64, 2, 8), (3, 50, 2, 8), (10, 32, 2, 8),
+                                                    (6, 16, 3, 4), (10, 16, 3, 4), (2, 33, 2, 5)])
 def test_synth_tiles_kernel_matches_torch_twin(classes, tile, dims, grid):
     from ddlpc.data import SyntheticTiles
     from ddlpc.data.datasets import render_synthetic
@@ -31,7 +31,12 @@ def test_synth_tiles_kernel_matches_torch_twin(classes, tile, dims, grid):
     xr, yr = render_synthetic(idx, 11, classes, 3, tile, dims, grid=grid)
     assert torch.equal(y.cpu(), yr)
     want = xr.permute(0, *range(2, xr.dim()), 1).to(torch.bfloat16)
-    assert torch.equal(xp[..., :3].cpu(), want)
+    got = xp[..., :3].cpu()
+    bad = (got != want).nonzero()
+    assert bad.numel() == 0, (bad.shape[0], bad[:6].tolist(),
+                              [(float(got[tuple(i)]), float(want[tuple(i)]),
+                                float(xr.permute(0, *range(2, xr.dim()), 1)[tuple(i)]))
+                               for i in bad[:6].tolist()])
     # the NCHW view the model API sees
     assert x.shape == (len(idx), 3) + (tile,) * dims
 
@@ -51,8 +56,8 @@ def test_tile_gather_matches_host_dataset():
         assert torch.equal(y.cpu(), yh)
         assert torch.equal(x._ddlpc_nhwc[..., :3].cpu(), xh.permute(0, 2, 3, 1).bfloat16())
         dn = ds.to_device("cuda", "nchw", budget)
-        x2, y2 = dn.get(idx)
-        assert torch.equal(x2.cpu(), xh) and torch.equal(y2.cpu(), yh)
+        x2, y2 = dn.get(idx)                      # (torch's GPU /255 is a reciprocal multiply)
+        assert torch.allclose(x2.cpu(), xh, rtol=1e-6, atol=0) and torch.equal(y2.cpu(), yh)
 
 
 def _cfg(tmp_path, **kw):
@@ -104,6 +109,8 @@ def test_fit_vaihingen_dir_hbm_and_streamed(tmp_path):
         v = tr.validate()
         out.append((tr.flat.param_buf.clone(), m["loss"], v["val_loss"]))
         tr.close()
-    # the two data paths feed bit-identical batches -> bit-identical training
+    # the two data paths feed bit-identical batches -> bit-identical training (the held-out
+    # loss goes through torch's GPU cross_entropy sum, whose reduction order may vary)
     assert torch.equal(out[0][0], out[1][0])
-    assert out[0][1:] == out[1][1:]
+    assert out[0][1] == out[1][1]
+    assert abs(out[0][2] - out[1][2]) <= 1e-6 * abs(out[0][2])
