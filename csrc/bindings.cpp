@@ -583,16 +583,18 @@ std::vector<at::Tensor> head_ce_bwd(const at::Tensor& a, const at::Tensor& Wh, c
   c10::DeviceGuard guard(a.device());
   const int C = (int)a.size(-1), K = (int)Wh.size(0);
   const float* pbn = bn4_ptr(bn4, C);
+  TORCH_CHECK(head_supported(C, K), "head kernel: unsupported (C, K)");
   const long long P = a.numel() / C;
-  const int nb = (int)std::max<long long>(1, std::min<long long>((P + 255) / 256, 1024));
+  const int nb = head_ce_bwd_blocks(C, K, pbn != nullptr, P, num_cus());
   auto fopts = a.options().dtype(at::kFloat);
   at::Tensor dA = at::empty_like(a);
   at::Tensor part = at::empty({nb, K * C + K}, fopts);
-  at::Tensor bnpart = at::empty({0}, fopts);         // (no fused BN-backward partials)
+  // deferred BatchNorm input: the kernel also emits that BN's backward partial rows
+  at::Tensor bnpart = pbn != nullptr ? at::empty({nb, 2, C}, fopts) : at::empty({0}, fopts);
   head_ce_bwd_launch(bptr(a), Wh.data_ptr<float>(), bh.data_ptr<float>(), labels.data_ptr<int64_t>(),
                      fptr_opt(gscale), out3.data_ptr<float>(), 0, bptr_mut(dA),
-                     part.data_ptr<float>(), nb, P, C, K, (int)ignore_index, pbn, nullptr,
-                     cur_stream());
+                     part.data_ptr<float>(), nb, P, C, K, (int)ignore_index, pbn,
+                     pbn != nullptr ? bnpart.data_ptr<float>() : nullptr, cur_stream());
   const bool into = dw_out.has_value() && dw_out->defined();
   at::Tensor sums = reduce_rows(part, nb, K * C + K);   // rows are [dW (K*C) | db (K)]
   if (into) {

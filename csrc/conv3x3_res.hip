@@ -424,14 +424,18 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
 
 struct ResVariant { int wm, wn, mt, nt, halo; bool tap8; int tw, th, nbuf; };
 // BN 32 = 4x2 16x16 MFMA tiles per wave column, BN 64 = two wave columns; NBUF = halo ring
-constexpr ResVariant kRes[7] = {
+constexpr ResVariant kRes[8] = {
     {4, 1, 4, 2, 324, false, 16, 16, 2},   // 0: BM 256 BN 32, 4 waves, 2-deep (2 WG / CU)
     {8, 1, 4, 2, 612, false, 32, 16, 3},   // 1: BM 512 BN 32, 8 waves, 3-deep
     {4, 2, 4, 2, 324, false, 16, 16, 3},   // 2: BM 256 BN 64, 8 waves, 3-deep
     {4, 1, 4, 2, 324, true, 16, 16, 2},    // 3: image layer (TAP8), 4 waves, 2-deep
     {8, 1, 4, 2, 612, true, 32, 16, 3},    // 4: image layer (TAP8), 8 waves, 3-deep
     {8, 1, 4, 2, 612, false, 32, 16, 2},   // 5: BM 512 BN 32, 8 waves, 2-deep (large Cin)
-    {4, 2, 4, 2, 324, false, 16, 16, 2}};  // 6: BM 256 BN 64, 8 waves, 2-deep (large Cin)
+    {4, 2, 4, 2, 324, false, 16, 16, 2},   // 6: BM 256 BN 64, 8 waves, 2-deep (large Cin)
+    // 7: BM 256 BN 96, 8 waves x (2 x 6 tiles), 3-deep — the 96-channel data gradient of the
+    //    first decoder conv (dY: 32 ch -> d[up | skip]: 64 + 32 ch).  One workgroup covers all
+    //    96 output channels, so the dY halo is read once instead of once per 32-channel tile.
+    {8, 1, 2, 6, 324, false, 16, 16, 3}};
 
 int res_smem(const ResVariant& v, int Cin, int C1, bool pro) {
   const int bn = v.wn * v.nt * 16;
@@ -460,7 +464,7 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
   if (a.dims != 2 || a.W < 16 || a.H < 16) return -1;
   const bool pro = a.pscale != nullptr;
   const bool tap8 = a.Cin <= 8 && a.C2 == 0 && a.CinW == 8 && !pro;
-  const int bn = (a.Cout <= 32 || a.Cout % 64 != 0) ? 32 : 64;
+  const int bn = a.Cout == 96 ? 96 : (a.Cout <= 32 || a.Cout % 64 != 0) ? 32 : 64;
   // preference: 3-deep halo rings (latency hiding) first; DDLPC_RES_DEPTH=2 prefers the
   // 2-deep, two-workgroups-per-CU variants (A/B experiments)
   static const int depth = [] { const char* e = getenv("DDLPC_RES_DEPTH"); return e ? atoi(e) : 3; }();
@@ -469,6 +473,8 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
   if (tap8) {
     if (bn != 32) return -1;
     if (depth == 2) { cand[nc++] = 3; } else { cand[nc++] = 4; cand[nc++] = 3; }
+  } else if (bn == 96) {
+    cand[nc++] = 7;
   } else if (bn == 32) {
     if (depth == 2) { cand[nc++] = 0; cand[nc++] = 5; }
     else { cand[nc++] = 1; cand[nc++] = 5; cand[nc++] = 0; }
@@ -509,6 +515,7 @@ void conv3_res_launch(ConvFwdArgs& a, int variant, int grid, int smem, hipStream
     case 3: launch_res<4, 1, 4, 2, 324, true, 2>(a, grid, smem, st); break;
     case 4: launch_res<8, 1, 4, 2, 612, true, 3>(a, grid, smem, st); break;
     case 5: launch_res<8, 1, 4, 2, 612, false, 2>(a, grid, smem, st); break;
+    case 7: launch_res<8, 1, 2, 6, 324, false, 3>(a, grid, smem, st); break;
     default: launch_res<4, 2, 4, 2, 324, false, 2>(a, grid, smem, st); break;
   }
 }

@@ -153,105 +153,150 @@ __global__ void ce_finalize_kernel(const float* __restrict__ partial, int nb, fl
   }
 }
 
-// bn4 != null: deferred BatchNorm of the last decoder block (see act8).  (Its backward
-// partial sums are NOT reduced here: 2*C per-thread accumulators cost the kernel its
-// occupancy — measured slower than the separate reduction pass.)
+// Backward, channel-split: G = C/8 consecutive lanes share one pixel, each owning 8 channels
+// (one 16-B activation load).  Per pixel: partial logits over the lane's channels, summed over
+// the G lanes by shuffles; softmax-CE gradient d (fp32, identical on the G lanes); the lane's
+// 8 channels of dA = d . Wh (bf16 store); and per-lane accumulators for
+//   dWh[k][c8..c8+7] += a * d[k],   dbh[k] += d[k]  (lane c8 == 0),
+//   and, with a deferred BatchNorm (bn4 != null), the BN-backward partial sums of the
+//   stored dA:  sum dyh, sum dyh * xhat  with dyh = dA * [y*scale + shift > 0]
+// — so the last decoder block's BN backward skips its reduction pass.  Accumulators are
+// reduced once per (persistent) workgroup: shuffles over the lanes with equal c8, then a
+// fixed-order sum over the waves (deterministic), one partial row per workgroup.
 template <int C, int K, bool DEFER>
 __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
     const bf16_t* __restrict__ a, const float* __restrict__ Wh, const float* __restrict__ bh,
     const int64_t* __restrict__ labels, const float* __restrict__ gscale,
     const float* __restrict__ stats3, bf16_t* __restrict__ dA, float* __restrict__ dWp,
-    long long P, int ignore_index, const float* __restrict__ bn4, int Kreal) {
-  __shared__ __attribute__((aligned(16))) float sBNm[4 * C];
-  __shared__ float sW[K * C], sb[K];
-  __shared__ __attribute__((aligned(16))) bf16_t sA[256 * C];
-  __shared__ float sD[256 * K];
-  load_head<C, K>(Wh, bh, Kreal, sW, sb);
-  const float* sBN = DEFER ? load_bn<C>(bn4, sBNm, false) : nullptr;
+    long long P, int ignore_index, const float* __restrict__ bn4, float* __restrict__ bnpart,
+    int Kreal) {
+  constexpr int G = C / 8;                          // lanes per pixel
+  constexpr int PPB = 256 / G;                      // pixels per workgroup step
+  constexpr int NACC = 8 * K + K + (DEFER ? 16 : 0);
+  __shared__ float sred[4][G][NACC];
+  __shared__ __attribute__((aligned(16))) float sW[K * C];      // Wh, padded classes zero
+  __shared__ __attribute__((aligned(16))) float sXh[2 * C];     // invstd | -mean*invstd
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cg = lane % G, c8 = cg * 8;
+  for (int i = tid; i < K * C; i += 256) sW[i] = i < Kreal * C ? Wh[i] : 0.f;
+  if (DEFER)
+    for (int i = tid; i < C; i += 256) { sXh[i] = bn4[C + i]; sXh[C + i] = -bn4[i] * bn4[C + i]; }
+  // registers: bias (padded classes -inf) and the deferred BN's scale / shift (the ReLU
+  // mask); the K x 8 weights and the xhat constants are re-read from LDS per pixel
+  float bk[K], sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < K; ++k) bk[k] = k < Kreal ? bh[k] : -INFINITY;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = DEFER ? bn4[2 * C + c8 + j] : 0.f;
+    sh[j] = DEFER ? bn4[3 * C + c8 + j] : 0.f;
+  }
   __syncthreads();
   const float cnt = stats3[2];
   const float gs = (gscale != nullptr ? gscale[0] : 1.0f) / (cnt > 0.f ? cnt : 1.f);
-  const int t = threadIdx.x;
-  // per-block partial row [dW (Kreal*C) | db (Kreal)]: output o = t + 256*r of thread t
-  constexpr int NO = (K * C + K + 255) / 256;
-  const int nout = Kreal * C + Kreal;
-  float accw[NO];
+  float acc[NACC];
 #pragma unroll
-  for (int r = 0; r < NO; ++r) accw[r] = 0.f;
-  const long long nper = (long long)gridDim.x * blockDim.x;
+  for (int i = 0; i < NACC; ++i) acc[i] = 0.f;
+  const long long stride = (long long)gridDim.x * PPB;
+  // software pipeline: the next pixel's activation + label loads are in flight while this
+  // pixel computes (low occupancy: few waves per CU to cover the HBM latency otherwise)
+  long long px = (long long)blockIdx.x * PPB + tid / G;
+  uint4 a_nx = make_uint4(0, 0, 0, 0);
+  int64_t l_nx = 0;
+  if (px < P) { a_nx = *reinterpret_cast<const uint4*>(a + px * C + c8); l_nx = labels[px]; }
 #pragma unroll 1
-  for (long long base = blockIdx.x * (long long)blockDim.x; base < P; base += nper) {
-    const long long px = base + t;
+  for (; px < P; px += stride) {
+    float y8[8], f[8];
+    unpack8(a_nx, y8);
+    const int64_t lab = l_nx;
+    if (px + stride < P) {
+      a_nx = *reinterpret_cast<const uint4*>(a + (px + stride) * C + c8);
+      l_nx = labels[px + stride];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = DEFER ? fmaxf(fmaf(y8[j], sc[j], sh[j]), 0.f) : y8[j];
+    if (DEFER) unpack8(pack8(f), f);                // the activation rounded as materialised
+    const float* w = sW + opaque_zero() + c8;        // w[k * C + j]: this lane's 8 channels
+    float z[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t = fmaf(f[j], w[k * C + j], t);
+      z[k] = t;
+    }
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1)
+#pragma unroll
+      for (int k = 0; k < K; ++k) z[k] += __shfl_xor(z[k], o, 64);
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < K; ++k) { z[k] += bk[k]; m = fmaxf(m, z[k]); }
+    float se = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) { z[k] = __expf(z[k] - m); se += z[k]; }
+    const float inv = 1.f / se;
     float d[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) d[k] = 0.f;
-    if (px < P) {
-      float z[K];
-      logits_of<C, K, DEFER>(a + px * C, sW, sb, sBN, z, sA + t * C);
-      const int64_t y = labels[px];
-      float m = z[0];
+    for (int k = 0; k < K; ++k) d[k] = lab != ignore_index ? (z[k] * inv - (k == lab ? 1.f : 0.f)) * gs : 0.f;
+    float o8[8];
 #pragma unroll
-      for (int k = 1; k < K; ++k) m = fmaxf(m, z[k]);
-      float se = 0.f;
+    for (int j = 0; j < 8; ++j) {
+      float t = 0.f;
 #pragma unroll
-      for (int k = 0; k < K; ++k) { z[k] = __expf(z[k] - m); se += z[k]; }
-      const float inv = 1.f / se;
-      if (y != ignore_index) {
+      for (int k = 0; k < K; ++k) t = fmaf(d[k], w[k * C + j], t);
+      o8[j] = t;
+    }
+    const uint4 pk = pack8(o8);
+    *reinterpret_cast<uint4*>(dA + px * C + c8) = pk;
 #pragma unroll
-        for (int k = 0; k < K; ++k) d[k] = (z[k] * inv - (k == y ? 1.f : 0.f)) * gs;
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[k * 8 + j] = fmaf(f[j], d[k], acc[k * 8 + j]);
+    if (cg == 0) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc[8 * K + k] += d[k];
+    }
+    if (DEFER) {
+      float r[8];
+      unpack8(pk, r);                                // BN backward sees the stored dA
+      const float* xh = sXh + opaque_zero() + c8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float dyh = fmaf(y8[j], sc[j], sh[j]) > 0.f ? r[j] : 0.f;
+        acc[9 * K + j] += dyh;
+        acc[9 * K + 8 + j] = fmaf(dyh, fmaf(y8[j], xh[j], xh[C + j]), acc[9 * K + 8 + j]);
       }
+    }
+  }
+  // ---- workgroup reduction: lanes with equal c8 (xor over the pixel-slot bits), then waves
+#pragma unroll
+  for (int o = G; o < 64; o <<= 1)
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) acc[i] += __shfl_xor(acc[i], o, 64);
+  if (lane < G)
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) sred[wave][lane][i] = acc[i];
+  __syncthreads();
+  const int nout = Kreal * C + Kreal;
+  for (int o = tid; o < nout; o += 256) {            // [dW (k, c) | db (k)]
+    float t = 0.f;
+    if (o < Kreal * C) {
+      const int k = o / C, c = o % C;
+      for (int wv = 0; wv < 4; ++wv) t += sred[wv][c / 8][k * 8 + c % 8];
     } else {
-#pragma unroll
-      for (int c8 = 0; c8 < C; c8 += 8) *reinterpret_cast<uint4*>(sA + t * C + c8) = make_uint4(0, 0, 0, 0);
+      const int k = o - Kreal * C;
+      for (int wv = 0; wv < 4; ++wv) t += sred[wv][0][8 * K + k];
     }
-#pragma unroll
-    for (int k = 0; k < K; ++k) sD[t * K + k] = d[k];
-    if (px < P) {
-      // dA = d . Wh, one class row at a time (k loop kept rolled: C accumulators live, the
-      // weights stream from LDS as broadcast reads instead of K*C hoisted registers)
-      float o[C];
-#pragma unroll
-      for (int c = 0; c < C; ++c) o[c] = 0.f;
-#pragma unroll 1
-      for (int k = 0; k < Kreal; ++k) {
-        const float dk = sD[t * K + k];
-        const float* wr = sW + k * C;
-#pragma unroll
-        for (int c = 0; c < C; ++c) o[c] = fmaf(dk, wr[c], o[c]);
-      }
-#pragma unroll
-      for (int c8 = 0; c8 < C; c8 += 8) {
-        float q[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) q[j] = o[c8 + j];
-        *reinterpret_cast<uint4*>(dA + px * C + c8) = pack8(q);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < NO; ++r) {
-      const int o = t + 256 * r;
-      if (o < Kreal * C) {
-        const int k = o / C, c = o % C;
-        float s = 0.f;
-#pragma unroll 8
-        for (int i = 0; i < 256; ++i) s = fmaf(bf2f(sA[i * C + c]), sD[i * K + k], s);
-        accw[r] += s;
-      } else if (o < nout) {
-        const int k = o - Kreal * C;
-        float s = 0.f;
-#pragma unroll 8
-        for (int i = 0; i < 256; ++i) s += sD[i * K + k];
-        accw[r] += s;
-      }
-    }
-    __syncthreads();
+    dWp[(long long)blockIdx.x * nout + o] = t;
   }
-#pragma unroll
-  for (int r = 0; r < NO; ++r) {
-    const int o = t + 256 * r;
-    if (o < nout) dWp[(long long)blockIdx.x * nout + o] = accw[r];
-  }
+  if (DEFER)
+    for (int o = tid; o < 2 * C; o += 256) {        // [sum dyh (c) | sum dyh*xhat (c)]
+      const int half = o / C, c = o % C;
+      float t = 0.f;
+      for (int wv = 0; wv < 4; ++wv) t += sred[wv][c / 8][9 * K + 8 * half + c % 8];
+      bnpart[(long long)blockIdx.x * 2 * C + o] = t;
+    }
 }
 
 template <int C, int K, bool DEFER>
@@ -312,19 +357,37 @@ void head_ce_fwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
   hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(256), 0, st, partial, nblocks, out3);
 }
 
+// persistent grid of the channel-split backward: every workgroup resident at once (the
+// occupancy of the instantiation, from the HIP occupancy API), capped by the pixel count
+// (the SAME grid with and without the deferred BatchNorm — the smaller occupancy of the two
+// — so both paths reduce dWh in the same order: bit-identical weight gradients)
+int head_ce_bwd_blocks(int C, int K, bool /*defer*/, long long P, int num_cus) {
+  int per_cu = 8;
+  auto occ = [&](const void* fn) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 256, 0) == hipSuccess && n > 0)
+      per_cu = std::min(per_cu, n);
+    else
+      per_cu = std::min(per_cu, 1);
+  };
+  HEAD_SWITCH(C, K, occ(reinterpret_cast<const void*>(&head_ce_bwd_kernel<CC, KK, true>)));
+  HEAD_SWITCH(C, K, occ(reinterpret_cast<const void*>(&head_ce_bwd_kernel<CC, KK, false>)));
+  const long long ppb = 256 / (C / 8);
+  return (int)std::max<long long>(1, std::min<long long>((P + ppb - 1) / ppb, (long long)per_cu * num_cus));
+}
+
 void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
                         const float* gscale, const float* stats3, int /*unused*/, bf16_t* dA,
                         float* dW_partial, int nblocks, long long P, int C, int K,
-                        int ignore_index, const float* bn4, float* /*bnpart: unused*/,
-                        hipStream_t st) {
+                        int ignore_index, const float* bn4, float* bnpart, hipStream_t st) {
   if (bn4 != nullptr)
     HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK, true>), dim3(nblocks), dim3(256), 0,
                                          st, a, Wh, bh, labels, gscale, stats3, dA, dW_partial, P,
-                                         ignore_index, bn4, K));
+                                         ignore_index, bn4, bnpart, K));
   else
     HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK, false>), dim3(nblocks), dim3(256), 0,
                                          st, a, Wh, bh, labels, gscale, stats3, dA, dW_partial, P,
-                                         ignore_index, bn4, K));
+                                         ignore_index, bn4, bnpart, K));
 }
 
 void head_logits_launch(const bf16_t* a, const float* Wh, const float* bh, float* logits,
