@@ -58,6 +58,9 @@ def _parse():
                     help="weight-gradient stream: auto = time both during warm-up, keep the faster")
     ap.add_argument("--hip-graph", type=int, default=int(os.environ.get("DDLPC_HIP_GRAPH", "0")),
                     help="1: replay the single-GPU train step as one hipGraph")
+    ap.add_argument("--fixed-batch", type=int, default=0,
+                    help="diagnostic: 1 = reuse one rendered batch every step (no per-step "
+                         "input pipeline; reported in 'data')")
     ap.add_argument("--heartbeat", type=float, default=0.0,
                     help="seconds between 'alive' lines on stderr (long first-step autotuning)")
     return ap.parse_args()
@@ -169,8 +172,11 @@ def main():
             return tr.train_set.get(idx)
         return pool[k % len(pool)]
 
+    fixed = [batch(j) for j in range(args.accum)] if args.fixed_batch else None
+
     def step(i):
-        tr.train_step([batch(i * args.accum + j) for j in range(args.accum)])
+        tr.train_step(fixed if fixed is not None else
+                      [batch(i * args.accum + j) for j in range(args.accum)])
 
     def sync():
         if dev == "cuda":
@@ -233,6 +239,8 @@ def main():
                      f"{args.classes} classes, random-init weights)")
     if not on_device_data:
         data_desc = data_desc.replace("rendered in HBM per step", "pre-rendered pool of 4 batches")
+    elif args.fixed_batch:
+        data_desc = data_desc.replace("rendered in HBM per step", "ONE batch rendered once (diagnostic)")
     if rank == 0:
         red = tr.reducer
         rec = {
@@ -257,8 +265,9 @@ def main():
                                        if dev == "cuda" else None),
                        "schedule": ("overlap" if sched.get("side_stream") else "serial") if sched
                                    else args.schedule,
-                       "schedule_probe_ms": ({k: round(v, 3) for k, v in sched.items()
-                                              if k.endswith("_ms")} if sched else None),
+                       "schedule_probe_ms": ({k: (round(v, 3) if isinstance(v, float) else v)
+                                              for k, v in sched.items() if k.endswith("_ms")}
+                                             if sched else None),
                        "bucket_mb": args.bucket_mb,
                        "buckets": len(red.buckets) if red is not None else 0,
                        "wire_dtype": args.wire_dtype, "grad_codec": args.codec,

@@ -444,7 +444,7 @@ at::Tensor convt_fwd(const at::Tensor& x, const at::Tensor& wt, const c10::optio
   TORCH_CHECK((int64_t)a.M * (g.dims == 2 ? 4 : 8) < (int64_t)INT32_MAX, "convT: too many pixels for 32-bit pixel indices");
   at::Tensor out = at::empty(shape_with_c(g, (int)cout, 2), x.options());
   a.C = out.data_ptr();
-  gemm_launch(a, cur_stream());
+  if (!convt_res_launch(a, num_cus(), cur_stream())) gemm_launch(a, cur_stream());
   return out;
 }
 
@@ -477,13 +477,18 @@ std::vector<at::Tensor> convt_dgrad(const at::Tensor& dout, const at::Tensor& wd
                 bny->numel() == dx.numel() && bny->scalar_type() == at::kBFloat16,
                 "convt_dgrad: bny must be the deferred pre-BN input (shape of dx, bf16)");
     a.bny = bptr(*bny);
-    // rows: one per workgroup of the widest tiling (128 x 64); a 128-wide tiling writes
-    // fewer rows — the unused ones are zeroed below so the row count is tiling independent
-    const long long grid = ((a.M + 127) / 128) * (long long)((a.N + 63) / 64);
-    bnpart = at::zeros({(int64_t)grid, 2, (int64_t)cin}, dout.options().dtype(at::kFloat));
+  }
+  const int res_rows = convt_res_rows(a, num_cus());
+  if (a.bn4 != nullptr) {
+    // resident-weight kernel: one fully written row per persistent workgroup; GEMM fallback:
+    // one per workgroup of the widest tiling (128 x 64) — a 128-wide tiling writes fewer
+    // rows, the unused ones stay zero
+    const long long grid = res_rows > 0 ? res_rows : ((a.M + 127) / 128) * (long long)((a.N + 63) / 64);
+    bnpart = res_rows > 0 ? at::empty({(int64_t)grid, 2, (int64_t)cin}, dout.options().dtype(at::kFloat))
+                          : at::zeros({(int64_t)grid, 2, (int64_t)cin}, dout.options().dtype(at::kFloat));
     a.bnpart = bnpart.data_ptr<float>();
   }
-  gemm_launch(a, cur_stream());
+  if (res_rows == 0 || !convt_res_launch(a, num_cus(), cur_stream())) gemm_launch(a, cur_stream());
   return {dx, bnpart};
 }
 

@@ -101,6 +101,10 @@ enum GemmMode {
   GEMM_CONVT_WGRAD = 2, // TN: dW[ci][(sub, co)] = sum_px x[px][ci] * dOut[up(px, sub)][co]
 };
 void gemm_launch(GemmArgs& a, hipStream_t st);
+// resident-weight transposed-conv forward / data gradient (convt_res.hip): rows = BN-backward
+// partial rows the DGRAD launch writes (0: shape not covered -> gemm_launch)
+int convt_res_rows(const GemmArgs& a, int num_cus);
+bool convt_res_launch(GemmArgs& a, int num_cus, hipStream_t st);
 
 
 // ---------------------------------------------------------------- BatchNorm / ReLU / pool

@@ -285,31 +285,37 @@ class Trainer:
         if k and self.step_count % k == 0:
             assert_replicas_identical(self.model)
 
-    def choose_schedule(self, micro_batches, steps: int = 3) -> Dict[str, float]:
+    def choose_schedule(self, micro_batches, steps: int = 3, rounds: int = 2) -> Dict[str, float]:
         """Time ``steps`` optimizer steps with the weight-gradient side stream and without
-        it, and keep the faster schedule.  (On some hosts the second hardware queue is
-        intermittently time-sliced and cross-stream waits cost milliseconds, which makes
-        the overlapped schedule several times slower than the serial one.)  All ranks
-        agree on the choice (MAX of the per-rank times).  Performs 2*steps+2 real steps."""
+        it, alternating the two ``rounds`` times and keeping each mode's best round, and
+        switch to the faster schedule.  (The first timed slot after warm-up is sometimes
+        several times slower than steady state — measured at 1024^2 batch 64: 292 ms in the
+        first slot vs 166 ms in a dedicated run — so a single side-then-serial pass could
+        pick the wrong mode.)  All ranks agree on the choice (MAX of the per-rank times).
+        Performs rounds * 2 * (steps + 1) real steps."""
         eng = self.model._engine if self.impl == "hip" else None
         if eng is None or eng._side_stream is None or self.device.type != "cuda":
             return {}
-        times = {}
-        for mode in (True, False):
-            eng.set_side_stream(mode)
-            self.train_step(micro_batches)
-            torch.cuda.synchronize(self.device)
-            t0 = time.perf_counter()
-            for _ in range(steps):
+        times: Dict[bool, List[float]] = {True: [], False: []}
+        for _ in range(rounds):
+            for mode in (True, False):
+                eng.set_side_stream(mode)
                 self.train_step(micro_batches)
-            torch.cuda.synchronize(self.device)
-            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=self.device)
-            if self.world > 1:
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            times[mode] = float(t.item()) / steps
-        best = times[True] <= times[False]
+                torch.cuda.synchronize(self.device)
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    self.train_step(micro_batches)
+                torch.cuda.synchronize(self.device)
+                t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=self.device)
+                if self.world > 1:
+                    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                times[mode].append(float(t.item()) / steps)
+        best = min(times[True]) <= min(times[False])
         eng.set_side_stream(best)
-        return {"side_stream": best, "side_ms": times[True] * 1e3, "serial_ms": times[False] * 1e3}
+        return {"side_stream": best, "side_ms": min(times[True]) * 1e3,
+                "serial_ms": min(times[False]) * 1e3,
+                "side_rounds_ms": [round(v * 1e3, 3) for v in times[True]],
+                "serial_rounds_ms": [round(v * 1e3, 3) for v in times[False]]}
 
     def fit(self) -> Dict[str, float]:
         c = self.cfg

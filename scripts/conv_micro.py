@@ -95,8 +95,12 @@ def main():
         F.weight_pack(torch.tensor([pk.entry()], dtype=torch.int64, device=dev), 1, pk.numel())
         b = torch.zeros(C, device=dev)
         flops = 2.0 * N * H * H * C * 4 * C
+        bn4 = torch.stack([torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5,
+                           torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1]).contiguous()
         fns = {"tfwd": lambda: F.convt_fwd(x, pk.fwd, b, C),
+               "tfwdbn": lambda: F.convt_fwd(x, pk.fwd, b, C, bn4),
                "tdgrad": lambda: F.convt_dgrad(dout, pk.dgrad, C)[0],
+               "tdgradbn": lambda: F.convt_dgrad(dout, pk.dgrad, C, x, bn4)[0],
                "twgrad": lambda: F.convt_wgrad(x, dout)}
         for ps in tpasses:
             fn = fns[ps]

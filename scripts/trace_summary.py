@@ -1,10 +1,23 @@
 #!/usr/bin/env python
-"""Summarise a rocprofv3 kernel_trace.csv: per-dispatch durations of the LAST training step."""
+"""Summarise a rocprofv3 kernel trace (kernel_trace.csv or results .db): per-dispatch durations of the LAST training step."""
 import csv
 import sys
 from collections import defaultdict
 
-rows = list(csv.DictReader(open(sys.argv[1])))
+def load(path):
+    """kernel_trace.csv, or a rocprofv3 results .db (default output format)"""
+    if path.endswith(".db"):
+        import sqlite3
+        c = sqlite3.connect(path)
+        q = ("select name, start, end, grid_x, lds_size, vgpr_count, accum_vgpr_count, stream_id "
+             "from kernels order by start")
+        keys = ["Kernel_Name", "Start_Timestamp", "End_Timestamp", "Grid_Size_X", "LDS_Block_Size",
+                "VGPR_Count", "Accum_VGPR_Count", "Stream_Id"]
+        return [dict(zip(keys, r)) for r in c.execute(q)]
+    return list(csv.DictReader(open(path)))
+
+
+rows = load(sys.argv[1])
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 7
 # find adam dispatches as step boundaries
 idx = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
