@@ -276,6 +276,8 @@ def main():
                                         if "comm_wait_ms" in phases else None),
                        "bucket_sweep": sweep or None,
                        "alloc_retries": mstats.get("num_alloc_retries"),
+                       "side_lag_waits": (getattr(tr.model._engine, "lag_waits", None)
+                                          if tr.impl == "hip" else None),
                        "device_mallocs": mstats.get("num_device_alloc"),
                        "device_frees": mstats.get("num_device_free")},
         }

@@ -341,6 +341,26 @@ def check_supported(model: nn.Module):
                          " (use impl='torch' for this configuration)")
 
 
+class _SideSegment:
+    """``with`` body runs on the engine's side stream; on exit an event marks the segment's
+    end for the lag bound (``UNetEngine.wgrad_stream``)."""
+
+    def __init__(self, eng, cur, nbytes):
+        self.eng, self.cur, self.nbytes = eng, cur, nbytes
+        self.ctx = torch.cuda.stream(eng.side)
+
+    def __enter__(self):
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        ev = torch.cuda.Event()
+        ev.record(self.eng.side)
+        r = self.ctx.__exit__(*exc)
+        self.eng._retire(self.cur, ev, self.nbytes)
+        return r
+
+
 class UNetEngine:
     """Runs a ``models.UNet`` through the HIP kernels (attach with ``UNet.to_hip()``)."""
 
@@ -368,6 +388,15 @@ class UNetEngine:
         self.side = torch.cuda.Stream(dev, priority=prio) if use_side else None
         self._side_stream = self.side
         self._side_used = False
+        # memory the side stream's lag may hold back (see ``wgrad_stream``): default 6% of
+        # HBM (17 GB on MI355X; measured at 1024^2 x 128: 43 GB still ran out of HBM, 16 GB
+        # did not; 256^2 x 128 never reaches it), DDLPC_SIDE_LAG_GB overrides
+        lag_gb = os.environ.get("DDLPC_SIDE_LAG_GB")
+        self.side_lag_bytes = (int(float(lag_gb) * 2**30) if lag_gb else
+                               int(0.06 * torch.cuda.get_device_properties(dev).total_memory))
+        self._lag: List[Tuple[torch.cuda.Event, int]] = []
+        self._lag_bytes = 0
+        self.lag_waits = 0
         # deferred BatchNorm activations (see ``features``): DDLPC_DEFER_BN=all|convt|none
         self.defer_mode = os.environ.get("DDLPC_DEFER_BN", "all")
         # transposed-conv weight gradients on the side stream too (DDLPC_SIDE_CONVT=0: main)
@@ -409,7 +438,15 @@ class UNetEngine:
     def wgrad_stream(self, *tensors):
         """Context for weight-gradient work: the side stream first waits for everything
         queued so far on the compute stream; tensors allocated there and read on the side
-        stream are marked so the caching allocator does not recycle them early."""
+        stream are marked so the caching allocator does not recycle them early.
+
+        Lag bound: a freed tensor that was marked is only reusable once the side stream has
+        run everything queued at the time of the free, so the memory held back grows with
+        the side stream's lag.  At 1024^2 x batch 128 (169 GB resident) an unbounded lag
+        ran the allocator out of HBM (free-and-retry, 3-6x slower steps: the "two-stream"
+        slowdown at large batch).  When the marked
+        bytes of the not-yet-retired side segments exceed ``side_lag_bytes`` the compute
+        stream waits for the oldest ones (GPU-side event wait; the host never blocks)."""
         if self.side is None or not self.direct_grads or torch.cuda.is_current_stream_capturing():
             # (hipGraph replay runs the captured streams serially: no gain from forking)
             return contextlib.nullcontext()
@@ -417,17 +454,29 @@ class UNetEngine:
         self.side.wait_stream(cur)
         # (inside a hipGraph capture the allocator defers reuse of such blocks to the end
         # of the capture, so the replayed graph cannot race on them either)
+        nbytes = 0
         for t in tensors:
             if isinstance(t, torch.Tensor) and t.numel() and t.is_cuda:
                 t.record_stream(self.side)
+                nbytes += t.numel() * t.element_size()
         self._side_used = True
-        return torch.cuda.stream(self.side)
+        return _SideSegment(self, cur, nbytes)
 
     def join(self):
         """Compute stream waits for all queued weight-gradient work."""
         if self.side is not None and self._side_used:
             torch.cuda.current_stream(self.side.device).wait_stream(self.side)
             self._side_used = False
+        self._lag, self._lag_bytes = [], 0
+
+    def _retire(self, cur, ev, nbytes):
+        self._lag.append((ev, nbytes))
+        self._lag_bytes += nbytes
+        while self._lag_bytes > self.side_lag_bytes and len(self._lag) > 1:
+            ev0, nb0 = self._lag.pop(0)
+            cur.wait_event(ev0)
+            self._lag_bytes -= nb0
+            self.lag_waits += 1
 
     def ready(self, *params):
         """Gradients of ``params`` are complete once the queued work finishes.  Called on

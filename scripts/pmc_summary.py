@@ -5,6 +5,7 @@ import sys
 from collections import OrderedDict, defaultdict
 
 rows = list(csv.DictReader(open(sys.argv[1])))
+RAW = "--raw" in sys.argv
 agg = OrderedDict()
 for r in rows:
     k = (int(r["Dispatch_Id"]), r["Kernel_Name"].replace("void ", "").replace("ddlpc::(anonymous namespace)::", "").split("(")[0][:44])
@@ -14,6 +15,12 @@ for (d, name), c in agg.items():
         continue
     wc = c.get("SQ_WAVE_CYCLES", 0) or 1
     parts = [f"{d:5d} {name:44s}"]
+    if RAW:
+        print(" ".join(parts + [f"{k}={v:.4g}" for k, v in sorted(c.items())]))
+        continue
+    if "GRBM_GUI_ACTIVE" in c and "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+        # MFMA busy per SIMD-cycle (256 CUs x 4 SIMDs)
+        parts.append(f"mfma_util={c['SQ_VALU_MFMA_BUSY_CYCLES'] / (c['GRBM_GUI_ACTIVE'] * 1024):.3f}")
     for key in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
                 "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS"):
         if key in c:
