@@ -176,6 +176,10 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   if (cfg == 2 && a.nTilesM * a.nTilesN < 2 * num_cus()) { cfg = 3; plan(cfg); }
   TORCH_CHECK((g.dims == 3 ? a.TD + 2 : 1) * (a.TH + 2) * (a.TW + 2) <= conv3_fwd_cfg_halo(g.dims, cfg),
               "halo exceeds LDS capacity");
+  // the streaming kernel's epilogue: per-image buffer descriptors (32-bit offsets) and one
+  // output per 16-channel tile
+  TORCH_CHECK((long long)g.D * g.H * g.W * a.Cout * 4 < (1LL << 31), "conv3: image too large for 32-bit offsets");
+  TORCH_CHECK(a.Co1 == a.Cout || a.Co1 % 16 == 0, "split output needs Co1 % 16 == 0");
   at::Tensor y1 = at::empty(shape_with_c(g, a.Co1), opts);
   at::Tensor y2;
   if (a.Co1 < a.Cout) y2 = at::empty(shape_with_c(g, a.Cout - a.Co1), opts);

@@ -42,7 +42,7 @@ namespace {
 
 using namespace convlds;
 
-template <int DIMS, int WM, int WN, int MT, int NT, int HALO>
+template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB>
 struct Cfg {
   static constexpr int NW = WM * WN;                            // waves per workgroup (4 or 8)
   static constexpr int NTH = NW * 64;
@@ -53,7 +53,7 @@ struct Cfg {
   static constexpr int B_ITERS = (3 * BN * 4 / 64 + NW - 1) / NW;  // DMA instrs / wave / stage
   static constexpr int B_BYTES = B_ITERS * NW * 1024;           // one weight buffer
   static constexpr int SS_BYTES = 2 * 512 * 4;                  // prologue scale/shift
-  static constexpr int SMEM = SS_BYTES + 2 * A_BYTES + 2 * B_BYTES;
+  static constexpr int SMEM = SS_BYTES + 2 * A_BYTES + NBB * B_BYTES;   // NBB weight buffers
 };
 
 // Persistent workgroups walk (m tile, n tile) items; the stage stream runs across item
@@ -65,9 +65,10 @@ struct Cfg {
 // operand the pixel tile, so each lane's accumulator holds 4 CONSECUTIVE channels of one
 // pixel -> 8-byte bf16x4 stores; BN statistics are reduced with 4 lane shuffles and
 // written as one partial row per (m tile, wave row).
-template <int DIMS, int WM, int WN, int MT, int NT, int HALO>
+template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_kernel(ConvFwdArgs p) {
-  using C = Cfg<DIMS, WM, WN, MT, NT, HALO>;
+  using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
+  static_assert(NBB == 2 || NBB == 3, "2 or 3 weight-stage buffers");
   constexpr int BM = C::BM, BN = C::BN;
   constexpr int NG = DIMS == 2 ? 3 : 9;           // (kd, r) kernel rows per chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -187,7 +188,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   };
   // prologue BN+ReLU applied in LDS on the landed halo (padding stays zero); a_pix holds
   // this chunk's item (the next item's pixels are only loaded after this transform)
-  auto transform_A = [&](int k, int chunk, int buf) {
+  // (the halo buffer goes in as a restrict-qualified parameter so its LDS writes carry alias
+  // scopes: the compiler would otherwise drain the in-flight weight DMA before them)
+  auto transform_body = [&](int k, int chunk, char* __restrict__ Abuf) __attribute__((always_inline)) {
     const int cbase = (chunk0_of(k) + chunk) * BK;
     if (cbase >= p.C1) return;                      // X2 channels: no prologue
 #pragma unroll
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       const int e = (i * C::NW + wave) * 64 + lane;    // same element this lane DMA'd
       const int c8 = cbase + a_sub8[i];
       if (c8 < p.C1 && a_pix[i] >= 0) {
-        uint4* q = reinterpret_cast<uint4*>(sA(buf) + e * 16);
+        uint4* q = reinterpret_cast<uint4*>(Abuf + e * 16);
         float f[8];
         unpack8(*q, f);
 #pragma unroll
@@ -203,6 +206,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         *q = pack8(f);
       }
     }
+  };
+  auto transform_A = [&](int k, int chunk, int buf) __attribute__((always_inline)) {
+    transform_body(k, chunk, sA(buf));
   };
 
   // ---- per-lane fragment geometry (item independent)
@@ -244,8 +250,17 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   // ---- epilogue of item k straight from the accumulators:
   // lane holds channels co..co+3 (co = co0 + wn*NT*16 + nt*16 + 4*(lane>>4)) of pixel
   // (wm*MT*16 + mt*16 + (lane&15)) of the tile
-  auto epilogue = [&](int k) {
+  // Stores are buffer stores with an out-of-range offset for masked lanes: every wave issues
+  // exactly EPI_STORES per epilogue (no exec branches), so counted vmcnt waits stay exact.
+  constexpr int EPI_STORES = MT * NT;
+  auto epilogue = [&](int k) __attribute__((always_inline)) {
     const Item it = item_of(k);
+    const int Co2 = p.Cout - p.Co1;
+    const auto r1 = KS > 1 ? make_rsrc(p.part + ((long long)it.ks * p.npix + (long long)it.n_img * img_px) * p.Cout,
+                                       (unsigned)(img_px * p.Cout * 4))
+                           : make_rsrc(p.Y1 + it.n_img * img_px * p.Co1, (unsigned)(img_px * p.Co1 * 2));
+    const auto r2 = make_rsrc(p.Y2 != nullptr ? p.Y2 + it.n_img * img_px * Co2 : p.Y1,
+                              p.Y2 != nullptr ? (unsigned)(img_px * Co2 * 2) : 0u);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
@@ -253,14 +268,17 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       const int pd = DIMS == 3 ? pix / (p.TW * p.TH) : 0;
       const int gw = it.w0 + pw, gh = it.h0 + ph, gd = it.d0 + pd;
       const bool valid = gw < p.W && gh < p.H && gd < p.D;
-      const long long gpix = ((long long)(it.n_img * p.D + gd) * p.H + gh) * p.W + gw;
+      const int lpix = (gd * p.H + gh) * p.W + gw;        // pixel within the image (32-bit)
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int co = it.co0 + wn * (NT * 16) + nt * 16 + 4 * g;
+        const bool ok = valid && co < p.Cout;
         if (KS > 1) {            // split-K partial: fp32 [ks][pixel][Cout], finalized later
-          if (valid && co < p.Cout)
-            *reinterpret_cast<float4*>(p.part + ((long long)it.ks * p.npix + gpix) * p.Cout + co) =
-                make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]);
+          unsigned off = ok ? (unsigned)(lpix * p.Cout + co) * 4u : kOOB;
+          asm volatile("" : "+v"(off));
+          __builtin_amdgcn_raw_buffer_store_b128(
+              u32x4_t{__float_as_uint(acc[mt][nt][0]), __float_as_uint(acc[mt][nt][1]),
+                      __float_as_uint(acc[mt][nt][2]), __float_as_uint(acc[mt][nt][3])}, r1, off, 0, 0);
           acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
           continue;
         }
@@ -268,15 +286,18 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bias_r[nt][i];
         const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        if (valid && co < p.Cout) {
-          if (co < p.Co1) store_bf16x4(p.Y1 + gpix * p.Co1 + co, pk.x, pk.y);
-          else store_bf16x4(p.Y2 + gpix * (p.Cout - p.Co1) + (co - p.Co1), pk.x, pk.y);
+        // the 16-channel tile lies in one output (Co1 % 16 == 0): wave-uniform descriptor
+        const bool in1 = it.co0 + wn * (NT * 16) + nt * 16 < p.Co1 || p.Y2 == nullptr;
+        unsigned off = ok ? (unsigned)(in1 ? lpix * p.Co1 + co : lpix * Co2 + co - p.Co1) * 2u : kOOB;
+        asm volatile("" : "+v"(off));
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk.x, pk.y}, in1 ? r1 : r2, off, 0, 0);
+        if (ok) {
           // statistics of the stored (bf16-rounded) values
-          const float r0 = lo_bf(pk.x), r1 = hi_bf(pk.x), r2 = lo_bf(pk.y), r3 = hi_bf(pk.y);
+          const float r0 = lo_bf(pk.x), q1 = hi_bf(pk.x), q2 = lo_bf(pk.y), q3 = hi_bf(pk.y);
           s1[nt][0] += r0; s2[nt][0] += r0 * r0;
-          s1[nt][1] += r1; s2[nt][1] += r1 * r1;
-          s1[nt][2] += r2; s2[nt][2] += r2 * r2;
-          s1[nt][3] += r3; s2[nt][3] += r3 * r3;
+          s1[nt][1] += q1; s2[nt][1] += q1 * q1;
+          s1[nt][2] += q2; s2[nt][2] += q2 * q2;
+          s1[nt][3] += q3; s2[nt][3] += q3 * q3;
         }
         acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       }
@@ -286,7 +307,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   // ---- compute one stage: the 3 taps of kernel row (kd, r).  The operand pointers are
   // restrict-qualified so the LDS reads carry alias scopes and the compiler does not make
   // them wait (vmcnt) for the NEXT stage's in-flight LDS-DMA; vmcnt is managed by hand.
-  auto compute = [&](const char* __restrict__ A, const char* __restrict__ B, int kd, int r) {
+  auto compute = [&](const char* __restrict__ A, const char* __restrict__ B, int kd, int r) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       const int tapoff = (kd * HH2 + r) * HW2 + t;
@@ -303,19 +324,45 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     }
   };
 
+  // stage s computes kernel row grp of chunk `chunk` of item k.  NBB = 2: the weights of
+  // stage s+1 are issued at stage s; NBB = 3: those of stage s+2 (two stages of latency
+  // cover for the weight stream).  The next chunk's halo is issued at the chunk's first
+  // stage.  Per stage a wave issues [epilogue stores] [B] [A]; with NBB = 3 the wait for
+  // B(s) is the count of ops issued after it (snapshots of a per-wave issue counter).
+  auto stage_of = [&](int t, int& k1, int& chunk1, int& grp1) {
+    k1 = t / spi;
+    const int r1 = t % spi;
+    chunk1 = r1 / NG;
+    grp1 = r1 % NG;
+  };
+  int ops = 0, snap0 = 0, snap1 = 0;           // NBB = 3: ops issued so far; after B(s), B(s+1)
   if (S > 0) {
     issue_A(0, 0, 0);
     issue_B(0, 0, 0, 0);
+    ops = C::A_ITERS + C::B_ITERS;
+    snap0 = ops;
+    if (NBB == 3 && S > 1) {
+      int k1, c1, g1;
+      stage_of(1, k1, c1, g1);
+      issue_B(k1, c1, g1, 1);
+      ops += C::B_ITERS;
+      snap1 = ops;
+    }
   }
   for (int s = 0; s < S; ++s) {
     const int k = s / spi, rem = s % spi;
     const int chunk = rem / NG, grp = rem % NG;
     const int cseq = k * nchunks + chunk;           // global chunk sequence -> A buffer
     const bool more_chunks = cseq + 1 < my_items * nchunks;
-    // stage s needs B(s) (issued during s-1) and, at grp 0, A(cseq).  At grp 1 the next
-    // chunk's halo (issued after B(s) during s-1) may stay in flight.
-    if (NG > 1 && grp == 1 && more_chunks) dma_wait<C::A_ITERS>();
-    else dma_wait<0>();
+    if (NBB == 2) {
+      // stage s needs B(s) (issued during s-1) and, at grp 0, A(cseq).  At grp 1 the next
+      // chunk's halo (issued after B(s) during s-1) may stay in flight.
+      if (NG > 1 && grp == 1 && more_chunks) dma_wait<C::A_ITERS>();
+      else dma_wait<0>();
+    } else {
+      // A(cseq) was issued before B(s) (at the previous chunk's first stage or the prologue)
+      vm_wait_dyn(ops - snap0);
+    }
     lds_sync();
     if (grp == 0 && has_pro) {
       transform_A(k, chunk, cseq & 1);
@@ -323,16 +370,23 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     }
     // the previous item's epilogue runs here, BEFORE this stage's DMA is issued, so its
     // stores drain under this stage's compute (vmcnt retires in order)
-    if (rem == 0 && s > 0) epilogue(k - 1);
-    if (s + 1 < S) {
-      const int r1 = (s + 1) % spi;
-      issue_B((s + 1) / spi, r1 / NG, r1 % NG, (s + 1) & 1);
+    if (rem == 0 && s > 0) { epilogue(k - 1); ops += EPI_STORES; }
+    const int sn = s + NBB - 1;                     // stage whose weights are issued now
+    int snapn = 0;
+    if (sn < S) {
+      int k1, c1, g1;
+      stage_of(sn, k1, c1, g1);
+      issue_B(k1, c1, g1, sn % NBB);
+      ops += C::B_ITERS;
+      snapn = ops;
     }
     if (grp == 0 && more_chunks) {
       const int k1 = (cseq + 1) / nchunks;
       issue_A(k1, (cseq + 1) % nchunks, (cseq + 1) & 1);
+      ops += C::A_ITERS;
     }
-    compute(sA(cseq & 1), sB(s & 1), DIMS == 3 ? grp / 3 : 0, DIMS == 3 ? grp % 3 : grp);
+    if (NBB == 3) { snap0 = snap1; snap1 = snapn; }
+    compute(sA(cseq & 1), sB(s % NBB), DIMS == 3 ? grp / 3 : 0, DIMS == 3 ? grp % 3 : grp);
   }
   if (S > 0) epilogue(my_items - 1);
 
@@ -421,9 +475,9 @@ __global__ void conv_splitk_finalize_kernel(const float* __restrict__ part, int 
     }
 }
 
-template <int DIMS, int WM, int WN, int MT, int NT, int HALO>
+template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB = 2>
 void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
-  using C = Cfg<DIMS, WM, WN, MT, NT, HALO>;
+  using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
   const int items = a.nTilesM * a.nTilesN * a.ksplit;
   int grid = items;
   if (a.persist_blocks > 0 && grid > a.persist_blocks) {
@@ -431,8 +485,16 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
     grid = a.persist_blocks / q * q;
   }
   a.stat_rows = grid;
-  hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO>), dim3(grid), dim3(C::NTH),
+  hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB>), dim3(grid), dim3(C::NTH),
                      C::SMEM, st, a);
+}
+
+// weight-stage buffers of the 8-wave configuration: 2 (default) or 3 (DDLPC_CONV_NBB=3).
+// Measured at batch 128 (conv_micro, same box): the 3-deep ring is 2.8% slower over all
+// layers' forward + data gradient — the weight stream is not what limits this kernel.
+int conv_nbb() {
+  static const int v = [] { const char* e = getenv("DDLPC_CONV_NBB"); return e ? atoi(e) : 2; }();
+  return v == 3 ? 3 : 2;
 }
 
 int cfg_wm(int cfg) { return cfg <= 1 || cfg == 4 ? 4 : cfg == 2 ? 2 : 1; }
@@ -466,7 +528,10 @@ void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st) {
       case 0: launch_cfg<2, 4, 1, 4, 2, 384>(a, st); break;
       case 1: launch_cfg<2, 4, 1, 4, 4, 384>(a, st); break;
       case 2: launch_cfg<2, 2, 2, 4, 4, 192>(a, st); break;
-      case 4: launch_cfg<2, 4, 2, 4, 4, 384>(a, st); break;
+      case 4:   // one 124 KB workgroup per CU: room for a third weight-stage buffer
+        if (conv_nbb() == 3) launch_cfg<2, 4, 2, 4, 4, 384, 3>(a, st);
+        else launch_cfg<2, 4, 2, 4, 4, 384, 2>(a, st);
+        break;
       default: launch_cfg<2, 1, 4, 4, 2, 128>(a, st); break;
     }
   } else {

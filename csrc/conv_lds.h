@@ -33,6 +33,17 @@ DDLPC_DEVICE void dma_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (an immediate per case; n <= 47 here)
+DDLPC_DEVICE void vm_wait_dyn(int n) {
+#define VW4(b) case b: dma_wait<b>(); break; case b + 1: dma_wait<b + 1>(); break; \
+               case b + 2: dma_wait<b + 2>(); break; case b + 3: dma_wait<b + 3>(); break;
+  switch (n) {
+    VW4(0) VW4(4) VW4(8) VW4(12) VW4(16) VW4(20) VW4(24) VW4(28) VW4(32) VW4(36) VW4(40) VW4(44)
+    default: dma_wait<0>();
+  }
+#undef VW4
+}
+
 DDLPC_DEVICE __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }

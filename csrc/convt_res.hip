@@ -41,16 +41,6 @@ constexpr int T_ABYTES = TBM * ROWB;        // one ring slot (8 KB)
 
 template <int N>
 DDLPC_DEVICE void vmw() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (an immediate per case; n <= 47 here)
-DDLPC_DEVICE void vm_wait_dyn(int n) {
-#define VW4(b) case b: vmw<b>(); break; case b + 1: vmw<b + 1>(); break; \
-               case b + 2: vmw<b + 2>(); break; case b + 3: vmw<b + 3>(); break;
-  switch (n) {
-    VW4(0) VW4(4) VW4(8) VW4(12) VW4(16) VW4(20) VW4(24) VW4(28) VW4(32) VW4(36) VW4(40) VW4(44)
-    default: vmw<0>();
-  }
-#undef VW4
-}
 
 // up(m, 0): the up-sampled pixel of sub-position 0 of low-res pixel m (image-group relative)
 DDLPC_DEVICE int up0_of(int m, int dims, int H, int W) {

@@ -62,7 +62,9 @@ class Trainer:
         self.impl = resolve_impl(cfg.impl, self.device)
         self.model = model
         if self.device.type == "cuda" and self.impl == "torch":
-            model.to(memory_format=torch.channels_last)    # MIOpen NHWC path (baseline)
+            # MIOpen NHWC / NDHWC path (baseline)
+            model.to(memory_format=torch.channels_last if cfg.model.dims == 2
+                     else torch.channels_last_3d)
         self.flat = flatten_module(model)
         broadcast_module(model, src=0)               # ... and rank 0 is authoritative
         if self.impl == "hip":
