@@ -168,12 +168,21 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
     a.nTilesN = (a.Cout + conv3_fwd_cfg_bn(c) - 1) / conv3_fwd_cfg_bn(c);
   };
   plan(cfg);
-  if (cfg == 2 && g.dims == 2) {                // 256-pixel tiles on 8 waves if they fill the chip
+  static const int use_cfg4 = [] { const char* e = getenv("DDLPC_CONV_CFG4"); return e ? atoi(e) : 1; }();
+  if (cfg == 2 && g.dims == 2 && use_cfg4) {    // 256-pixel tiles on 8 waves if they fill the chip
     plan(4);
     if (a.nTilesM * a.nTilesN >= num_cus()) cfg = 4;
     else plan(cfg);
   }
   if (cfg == 2 && a.nTilesM * a.nTilesN < 2 * num_cus()) { cfg = 3; plan(cfg); }
+  // small images: a tile larger than the image computes padding (the 8x8 bottleneck layer
+  // under a 256-pixel tile is 75% padding: 48.6 -> 32.5 us with 64-pixel tiles, batch 128)
+  auto waste = [&](int c) {
+    plan(c);
+    return (double)a.nTilesM * conv3_fwd_cfg_bm(c) / ((double)g.N * g.D * g.H * g.W);
+  };
+  while ((cfg == 4 || cfg == 2) && waste(cfg) > 1.3) cfg = cfg == 4 ? 2 : 3;
+  plan(cfg);
   TORCH_CHECK((g.dims == 3 ? a.TD + 2 : 1) * (a.TH + 2) * (a.TW + 2) <= conv3_fwd_cfg_halo(g.dims, cfg),
               "halo exceeds LDS capacity");
   // the streaming kernel's epilogue: per-image buffer descriptors (32-bit offsets) and one

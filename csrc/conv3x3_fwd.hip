@@ -65,10 +65,11 @@ struct Cfg {
 // operand the pixel tile, so each lane's accumulator holds 4 CONSECUTIVE channels of one
 // pixel -> 8-byte bf16x4 stores; BN statistics are reduced with 4 lane shuffles and
 // written as one partial row per (m tile, wave row).
-template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB>
+template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, bool FDB>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_kernel(ConvFwdArgs p) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
-  static_assert(NBB == 2 || NBB == 3, "2 or 3 weight-stage buffers");
+  static_assert(NBB == 2 || NBB == 3 || (NBB == 4 && DIMS == 2), "2 / 3 weight-stage buffers, or 4 (super-stages)");
+  constexpr bool FRAG_DB = FDB;
   constexpr int BM = C::BM, BN = C::BN;
   constexpr int NG = DIMS == 2 ? 3 : 9;           // (kd, r) kernel rows per chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -308,19 +309,56 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   // restrict-qualified so the LDS reads carry alias scopes and the compiler does not make
   // them wait (vmcnt) for the NEXT stage's in-flight LDS-DMA; vmcnt is managed by hand.
   auto compute = [&](const char* __restrict__ A, const char* __restrict__ B, int kd, int r) __attribute__((always_inline)) {
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
+    // register double buffer: the fragments of tap t+1 are read while the MFMAs of tap t
+    // run (the sched barrier keeps the compiler from sinking the reads next to their use,
+    // which exposed the LDS latency between every 4 MFMAs: ~31% MFMA busy)
+    auto load_frags = [&](int t, uint4 (&xf)[MT], uint4 (&wf)[NT]) __attribute__((always_inline)) {
       const int tapoff = (kd * HH2 + r) * HW2 + t;
-      uint4 xf[MT], wf[NT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) xf[mt] = lds128(A + lds_off(hp0[mt] + tapoff, g));
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
         wf[nt] = lds128(B + lds_off(t * BN + wn * (NT * 16) + nt * 16 + (lane & 15), g));
+    };
+    uint4 xf[2][MT], wf[2][NT];
+    load_frags(0, xf[0], wf[0]);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      if (t + 1 < 3) load_frags(t + 1, xf[(t + 1) & 1], wf[(t + 1) & 1]);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[nt], xf[mt], acc[mt][nt]);
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[t & 1][nt], xf[t & 1][mt], acc[mt][nt]);
+      if (FRAG_DB) __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // super-stage body: taps of row r0 (halo A0, weights B0) then row r1 (A1, B1), fragments
+  // of tap t+1 read while tap t's MFMAs run, across the row boundary too
+  auto compute2 = [&](const char* __restrict__ A0, const char* __restrict__ B0, int r0,
+                      const char* __restrict__ A1, const char* __restrict__ B1, int r1)
+      __attribute__((always_inline)) {
+    auto load_frags = [&](int tt, uint4 (&xf)[MT], uint4 (&wf)[NT]) __attribute__((always_inline)) {
+      const int t = tt % 3;
+      const char* A = tt < 3 ? A0 : A1;
+      const char* B = tt < 3 ? B0 : B1;
+      const int tapoff = (tt < 3 ? r0 : r1) * HW2 + t;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) xf[mt] = lds128(A + lds_off(hp0[mt] + tapoff, g));
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        wf[nt] = lds128(B + lds_off(t * BN + wn * (NT * 16) + nt * 16 + (lane & 15), g));
+    };
+    uint4 xf[2][MT], wf[2][NT];
+    load_frags(0, xf[0], wf[0]);
+#pragma unroll
+    for (int tt = 0; tt < 6; ++tt) {
+      if (tt + 1 < 6) load_frags(tt + 1, xf[(tt + 1) & 1], wf[(tt + 1) & 1]);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[tt & 1][nt], xf[tt & 1][mt], acc[mt][nt]);
+      if (FRAG_DB) __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -335,58 +373,111 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     chunk1 = r1 / NG;
     grp1 = r1 % NG;
   };
-  int ops = 0, snap0 = 0, snap1 = 0;           // NBB = 3: ops issued so far; after B(s), B(s+1)
-  if (S > 0) {
-    issue_A(0, 0, 0);
-    issue_B(0, 0, 0, 0);
-    ops = C::A_ITERS + C::B_ITERS;
-    snap0 = ops;
-    if (NBB == 3 && S > 1) {
-      int k1, c1, g1;
-      stage_of(1, k1, c1, g1);
-      issue_B(k1, c1, g1, 1);
-      ops += C::B_ITERS;
-      snap1 = ops;
+  if constexpr (NBB <= 3) {
+    int ops = 0, snap0 = 0, snap1 = 0;           // NBB = 3: ops issued so far; after B(s), B(s+1)
+    if (S > 0) {
+      issue_A(0, 0, 0);
+      issue_B(0, 0, 0, 0);
+      ops = C::A_ITERS + C::B_ITERS;
+      snap0 = ops;
+      if (NBB == 3 && S > 1) {
+        int k1, c1, g1;
+        stage_of(1, k1, c1, g1);
+        issue_B(k1, c1, g1, 1);
+        ops += C::B_ITERS;
+        snap1 = ops;
+      }
     }
-  }
-  for (int s = 0; s < S; ++s) {
-    const int k = s / spi, rem = s % spi;
-    const int chunk = rem / NG, grp = rem % NG;
-    const int cseq = k * nchunks + chunk;           // global chunk sequence -> A buffer
-    const bool more_chunks = cseq + 1 < my_items * nchunks;
-    if (NBB == 2) {
-      // stage s needs B(s) (issued during s-1) and, at grp 0, A(cseq).  At grp 1 the next
-      // chunk's halo (issued after B(s) during s-1) may stay in flight.
-      if (NG > 1 && grp == 1 && more_chunks) dma_wait<C::A_ITERS>();
-      else dma_wait<0>();
-    } else {
-      // A(cseq) was issued before B(s) (at the previous chunk's first stage or the prologue)
-      vm_wait_dyn(ops - snap0);
-    }
-    lds_sync();
-    if (grp == 0 && has_pro) {
-      transform_A(k, chunk, cseq & 1);
+    for (int s = 0; s < S; ++s) {
+      const int k = s / spi, rem = s % spi;
+      const int chunk = rem / NG, grp = rem % NG;
+      const int cseq = k * nchunks + chunk;           // global chunk sequence -> A buffer
+      const bool more_chunks = cseq + 1 < my_items * nchunks;
+      if (NBB == 2) {
+        // stage s needs B(s) (issued during s-1) and, at grp 0, A(cseq).  At grp 1 the next
+        // chunk's halo (issued after B(s) during s-1) may stay in flight.
+        if (NG > 1 && grp == 1 && more_chunks) dma_wait<C::A_ITERS>();
+        else dma_wait<0>();
+      } else {
+        // A(cseq) was issued before B(s) (at the previous chunk's first stage or the prologue)
+        vm_wait_dyn(ops - snap0);
+      }
+      // prologue BN + ReLU on the pieces this lane DMA'd (own vmcnt covers them): before the
+      // stage barrier, which then also publishes the transformed halo (one barrier, not two)
+      if (grp == 0 && has_pro) transform_A(k, chunk, cseq & 1);
       lds_sync();
+      // the previous item's epilogue runs here, BEFORE this stage's DMA is issued, so its
+      // stores drain under this stage's compute (vmcnt retires in order)
+      if (rem == 0 && s > 0) { epilogue(k - 1); ops += EPI_STORES; }
+      const int sn = s + NBB - 1;                     // stage whose weights are issued now
+      int snapn = 0;
+      if (sn < S && !((p.diag & 1) && sn >= NBB)) {
+        int k1, c1, g1;
+        stage_of(sn, k1, c1, g1);
+        issue_B(k1, c1, g1, sn % NBB);
+        ops += C::B_ITERS;
+        snapn = ops;
+      }
+      if (grp == 0 && more_chunks && !((p.diag & 2) && cseq + 1 >= 2)) {
+        const int k1 = (cseq + 1) / nchunks;
+        issue_A(k1, (cseq + 1) % nchunks, (cseq + 1) & 1);
+        ops += C::A_ITERS;
+      }
+      if (NBB == 3) { snap0 = snap1; snap1 = snapn; }
+      compute(sA(cseq & 1), sB(s % NBB), DIMS == 3 ? grp / 3 : 0, DIMS == 3 ? grp % 3 : grp);
     }
-    // the previous item's epilogue runs here, BEFORE this stage's DMA is issued, so its
-    // stores drain under this stage's compute (vmcnt retires in order)
-    if (rem == 0 && s > 0) { epilogue(k - 1); ops += EPI_STORES; }
-    const int sn = s + NBB - 1;                     // stage whose weights are issued now
-    int snapn = 0;
-    if (sn < S) {
-      int k1, c1, g1;
-      stage_of(sn, k1, c1, g1);
-      issue_B(k1, c1, g1, sn % NBB);
-      ops += C::B_ITERS;
-      snapn = ops;
+  } else {
+    // NBB = 4, SUPER-STAGES (2-D): a barrier per TWO kernel rows (6 taps, 96 MFMAs per
+    // wave) instead of one — the per-stage barrier and the exposed first-tap LDS latency
+    // were most of the gap to the MFMA rate (operand DMA skipped: only 15-20% faster).
+    // Pairs p = (chunk sequence c, row r) in order; super-stage j computes pairs 2j, 2j+1
+    // (an item has 3 * nchunks pairs, nchunks even: items never straddle a super-stage).
+    // Weights of super-stage j+1 (two rows, B slots 2*((j+1)&1) + h) are issued at j; the
+    // halo of chunk c at super-stage floor((3c-4)/2)+1 (after chunk c-2's last use), one
+    // super-stage before its first use floor(3c/2), where it is transformed (prologue)
+    // before the barrier.  Everything issued at j-1 is awaited at j (dma_wait<0>).
+    const int P = my_items * nchunks * NG;
+    const int J = (P + 1) / 2;
+    const int total_chunks = my_items * nchunks;
+    auto issue_Bj = [&](int j) __attribute__((always_inline)) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int pp = 2 * j + h;
+        if (pp < P) {
+          const int cs = pp / NG;
+          issue_B(cs / nchunks, cs % nchunks, pp % NG, 2 * (j & 1) + h);
+        }
+      }
+    };
+    auto issue_Ac = [&](int c) __attribute__((always_inline)) {
+      if (c < total_chunks) issue_A(c / nchunks, c % nchunks, c & 1);
+    };
+    if (J > 0) {
+      issue_Ac(0);
+      issue_Ac(1);
+      issue_Bj(0);
     }
-    if (grp == 0 && more_chunks) {
-      const int k1 = (cseq + 1) / nchunks;
-      issue_A(k1, (cseq + 1) % nchunks, (cseq + 1) & 1);
-      ops += C::A_ITERS;
+    for (int j = 0; j < J; ++j) {
+      dma_wait<0>();
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int pp = 2 * j + h;
+        if (pp < P && pp % NG == 0 && has_pro) {
+          const int cs = pp / NG;
+          transform_A(cs / nchunks, cs % nchunks, cs & 1);
+        }
+      }
+      lds_sync();
+      const int k0 = (2 * j) / spi;
+      if ((2 * j) % spi == 0 && j > 0) epilogue(k0 - 1);
+      if (j + 1 < J) issue_Bj(j + 1);
+      if (j % 3 == 2) issue_Ac(2 * ((j + 1) / 3));
+      else if (j % 3 == 0 && j > 0) issue_Ac(2 * (j / 3) + 1);
+      // P is even (nchunks even): both pairs exist; one 6-tap fragment pipeline across them
+      const int c0 = (2 * j) / NG, c1 = (2 * j + 1) / NG;
+      compute2(sA(c0 & 1), sB(2 * (j & 1)), (2 * j) % NG, sA(c1 & 1), sB(2 * (j & 1) + 1),
+               (2 * j + 1) % NG);
     }
-    if (NBB == 3) { snap0 = snap1; snap1 = snapn; }
-    compute(sA(cseq & 1), sB(s % NBB), DIMS == 3 ? grp / 3 : 0, DIMS == 3 ? grp % 3 : grp);
   }
   if (S > 0) epilogue(my_items - 1);
 
@@ -475,6 +566,13 @@ __global__ void conv_splitk_finalize_kernel(const float* __restrict__ part, int 
     }
 }
 
+// fragment double buffering (sched barrier per tap): on by default except the 3-D 4x4-tile
+// configs (VGPR spill); DDLPC_CONV_FDB=0 turns it off for A/B
+bool conv_fdb() {
+  static const int v = [] { const char* e = getenv("DDLPC_CONV_FDB"); return e ? atoi(e) : 1; }();
+  return v != 0;
+}
+
 template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB = 2>
 void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
@@ -485,8 +583,21 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
     grid = a.persist_blocks / q * q;
   }
   a.stat_rows = grid;
-  hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB>), dim3(grid), dim3(C::NTH),
-                     C::SMEM, st, a);
+  static const int diag = [] { const char* e = getenv("DDLPC_DIAG_CONV"); return e ? atoi(e) : 0; }();
+  a.diag = diag;
+  constexpr bool FDB_OK = !(DIMS == 3 && MT * NT >= 16);
+  if (FDB_OK && conv_fdb())
+    hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK>), dim3(grid),
+                       dim3(C::NTH), C::SMEM, st, a);
+  else
+    hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, false>), dim3(grid),
+                       dim3(C::NTH), C::SMEM, st, a);
+}
+
+// super-stages (two kernel rows per barrier) in the 8-wave configuration (DDLPC_CONV_SUPER=0: off)
+int conv_super() {
+  static const int v = [] { const char* e = getenv("DDLPC_CONV_SUPER"); return e ? atoi(e) : 1; }();
+  return v;
 }
 
 // weight-stage buffers of the 8-wave configuration: 2 (default) or 3 (DDLPC_CONV_NBB=3).
@@ -528,10 +639,13 @@ void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st) {
       case 0: launch_cfg<2, 4, 1, 4, 2, 384>(a, st); break;
       case 1: launch_cfg<2, 4, 1, 4, 4, 384>(a, st); break;
       case 2: launch_cfg<2, 2, 2, 4, 4, 192>(a, st); break;
-      case 4:   // one 124 KB workgroup per CU: room for a third weight-stage buffer
-        if (conv_nbb() == 3) launch_cfg<2, 4, 2, 4, 4, 384, 3>(a, st);
+      case 4: {  // one workgroup per CU: room for 3 weight-stage buffers or 2 super-stages
+        const int nch = (a.Cin + 31) / 32 / a.ksplit;
+        if (conv_super() && nch % 2 == 0) launch_cfg<2, 4, 2, 4, 4, 384, 4>(a, st);
+        else if (conv_nbb() == 3) launch_cfg<2, 4, 2, 4, 4, 384, 3>(a, st);
         else launch_cfg<2, 4, 2, 4, 4, 384, 2>(a, st);
         break;
+      }
       default: launch_cfg<2, 1, 4, 4, 2, 128>(a, st); break;
     }
   } else {

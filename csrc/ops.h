@@ -35,6 +35,7 @@ struct ConvFwdArgs {
   int ksplit;                     // >1: split the channel chunks, fp32 partials to `part`
   float* part;                    // [ksplit][npix][Cout] fp32 (ksplit > 1)
   long long npix;                 // N * D * H * W
+  int diag;                       // diagnostics only (DDLPC_DIAG_CONV): bit 0 skip weight DMA after stage 1, bit 1 skip halo DMA after chunk 1
 };
 void conv3_splitk_finalize_launch(ConvFwdArgs& a, int grid, hipStream_t st);
 void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st);
