@@ -269,8 +269,14 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   const int bco = a.Cout <= 32 ? 32 : 64;
   static const int use_v2 = [] { const char* e = getenv("DDLPC_WGRAD_V2"); return e ? atoi(e) : 1; }();
   const bool v2 = use_v2 && (use_v2 != 2 || g.dims == 2) && g.W >= 16 && (a.C2 == 0 || a.C1 % 32 == 0);
-  // 128-pixel tiles (v2: 16 x conv3_wgrad2_pt/16)
-  if (v2) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad2_pt(bco, a.C2, g.H, g.W) / 16; }
+  // v3 (32x32x16 MFMA, conflict-free transposed reads): whole 32-channel input chunks
+  static const int use_v3 = [] { const char* e = getenv("DDLPC_WGRAD_V3"); return e ? atoi(e) : 1; }();
+  const bool v3 = v2 && use_v3 && a.C1 % 32 == 0 && a.C2 % 32 == 0;
+  // 128-pixel tiles (v2: 16 x conv3_wgrad2_pt/16; v3: 256 for 32 output channels, else 128)
+  // (DDLPC_WGRAD3_PT64 = 96 | 128: pixel tile of the 64-channel v3 kernel; default 128)
+  static const int v3_pt64 = [] { const char* e = getenv("DDLPC_WGRAD3_PT64"); return e ? atoi(e) : 128; }();
+  if (v3) { a.TD = 1; a.TW = 16; a.TH = bco == 32 ? 16 : (v3_pt64 == 96 && a.C2 > 0 ? 6 : 8); }
+  else if (v2) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad2_pt(bco, a.C2, g.H, g.W) / 16; }
   else if (g.dims == 2) { a.TD = 1; a.TW = g.W >= 16 ? 16 : 8; a.TH = 128 / a.TW; }
   else { a.TW = g.W >= 16 ? 16 : 8; a.TH = 4; a.TD = 128 / (a.TW * a.TH); }
   TORCH_CHECK(v2 || (a.TD + (g.dims == 3 ? 2 : 0)) * (a.TH + 2) * (a.TW + 2) <= conv3_wgrad_halo_cap(g.dims),
@@ -295,7 +301,8 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   a.splits = splits;
   auto part = at::empty({(int64_t)splits * a.Cout * a.taps * a.Cin}, dy.options().dtype(at::kFloat));
   a.partial = part.data_ptr<float>();
-  if (v2) conv3_wgrad2_launch(a, bco, cur_stream());
+  if (v3) conv3_wgrad3_launch(a, bco, cur_stream());
+  else if (v2) conv3_wgrad2_launch(a, bco, cur_stream());
   else conv3_wgrad_launch(a, bco, cur_stream());
   std::vector<int64_t> wshape = {a.Cout, a.Cin, 3, 3};
   if (g.dims == 3) wshape.push_back(3);

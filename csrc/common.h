@@ -81,6 +81,14 @@ DDLPC_DEVICE f32x4_t mfma16x16x32(const uint4& a, const uint4& b, f32x4_t c) {
                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
 }
 
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+// v_mfma_f32_32x32x16_bf16: A 32(m) x 16(k), B 16(k) x 32(n); lane l holds A[l & 31][8 (l >> 5) ..
+// + 7] and B[8 (l >> 5) .. + 7][l & 31]; D element i of lane l is D[8 (i / 4) + 4 (l >> 5) + i % 4][l & 31]
+DDLPC_DEVICE f32x16_t mfma32x32x16(const uint4& a, const uint4& b, f32x16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                 __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+
 DDLPC_DEVICE float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

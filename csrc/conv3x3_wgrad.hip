@@ -478,6 +478,208 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
   }
 }
 
+// ============================================================================ v3: 32x32x16 MFMA
+// Same GEMM, tiles, DMA pipeline and partial-slab contract as v2, but the MFMA is
+// v_mfma_f32_32x32x16_bf16 with M = 32 output channels and N = one tap x the 32-channel ci
+// chunk.  That operand shape makes every transposed read conflict-free on the natural
+// layouts: a 32-lane half-wave reads 4 consecutive pixel rows x 32 channels = 256
+// contiguous bytes of the X halo (64-B rows, any tap shift) — v2's 16x16x32 B reads took 8
+// pixels x 16 channels, 2-way bank conflicts on nearly every LDS instruction — and of dY
+// (64-B rows for 32 channels; 128-B rows get a 64-B-half XOR on row bit 1).
+// Waves split the pixel k-steps (BCO 32: 4-way; BCO 64: 2 co halves x 2-way), each wave
+// holds all 9 taps (9 x 16 fp32 accumulators), and the k-split partials are summed in LDS
+// in a fixed order at the end (deterministic).
+template <int BCO>
+DDLPC_DEVICE int wg3_yswz(int row) {             // XOR on the 16-B piece index
+  return BCO == 64 ? (((row >> 1) & 1) << 2) : 0;
+}
+
+template <int BCO, int PT>
+__global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
+  using namespace convlds;
+  using Cfg = Wg2Cfg<BCO, PT>;                     // DMA geometry / LDS budget as v2
+  constexpr int TH = Cfg::TH, HW2 = 18;
+  constexpr int NJ = BCO / 32;                     // 32-channel co tiles
+  constexpr int KW = 4 / NJ;                       // waves sharing a co tile (k-split)
+  constexpr int KS16 = PT / 16;                    // 16-pixel k-steps per tile
+  static_assert(KS16 % KW == 0, "k-steps must split evenly over the waves");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* s_scale = reinterpret_cast<float*>(smem);
+  float* s_shift = s_scale + 512;
+  char* base = smem + Cfg::SS_BYTES;
+  auto sY = [&](int b) { return base + b * (Cfg::Y_BYTES + Cfg::X_BYTES); };
+  auto sX = [&](int b) { return base + b * (Cfg::Y_BYTES + Cfg::X_BYTES) + Cfg::Y_BYTES; };
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wj = wave % NJ, wk = wave / NJ;        // co tile, k-step phase
+  int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int cic = b % p.ciChunks; b /= p.ciChunks;
+  const int cot = b % p.coTiles; b /= p.coTiles;
+  const int plane = b % p.planes; b /= p.planes;
+  const int split = b;
+  const int co0 = cot * BCO, ci0 = cic * BK;
+  const int dshift = p.planes == 3 ? plane - 1 : 0;
+
+  const bool has_pro = p.pscale != nullptr;
+  if (has_pro)
+    for (int c = tid; c < p.C1; c += 256) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
+  const int t_begin = (int)((long long)p.nTiles * split / p.splits);
+  const int t_end = (int)((long long)p.nTiles * (split + 1) / p.splits);
+  const long long img_px = (long long)p.H * p.W;
+
+  // ---- tile-independent per-lane DMA geometry (v2's, with the v3 dY swizzle)
+  int y_pw[Cfg::Y_ITERS], y_ph[Cfg::Y_ITERS], y_rel[Cfg::Y_ITERS];
+#pragma unroll
+  for (int i = 0; i < Cfg::Y_ITERS; ++i) {
+    const int e = (i * 4 + wave) * 64 + lane;
+    const int row = e / (BCO / 8), pc = e % (BCO / 8);
+    const int sp = pc ^ wg3_yswz<BCO>(row);
+    y_pw[i] = row % 16;
+    y_ph[i] = row / 16;
+    const int co = co0 + sp * 8;
+    y_rel[i] = co < p.Cout ? (y_ph[i] * p.W + y_pw[i]) * p.Cout + co : -1;
+  }
+  int x_dw[Cfg::X_ITERS], x_dh[Cfg::X_ITERS], x_pix[Cfg::X_ITERS];
+#pragma unroll
+  for (int i = 0; i < Cfg::X_ITERS; ++i) {
+    const int e = (i * 4 + wave) * 64 + lane;
+    const int px = e >> 2;
+    x_dw[i] = px < Cfg::HALO ? px % HW2 - 1 : -(1 << 20);
+    x_dh[i] = px / HW2 - 1;
+    x_pix[i] = -1;
+  }
+  const int c8l = ci0 + (lane & 3) * 8;
+  const bool second = ci0 >= p.C1;
+  const int Cs = second ? p.C2 : p.C1;
+  const int cs0 = second ? c8l - p.C1 : c8l;
+  const bf16_t* xsrc = second ? p.X2 : p.X1;
+  const bool xch_ok = cs0 < Cs;
+
+  auto issue = [&](int tile, int buf) __attribute__((always_inline)) {
+    int t = tile;
+    const int tw_i = t % p.tilesW; t /= p.tilesW;
+    const int th_i = t % p.tilesH; t /= p.tilesH;
+    const int n = t;
+    const int dx = n % p.D + dshift;
+    const bool dok = dx >= 0 && dx < p.D;
+    const int h0 = th_i * TH, w0 = tw_i * 16;
+    const auto ry = make_rsrc(p.dY + n * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
+    const int ybase = (h0 * p.W + w0) * p.Cout;
+#pragma unroll
+    for (int i = 0; i < Cfg::Y_ITERS; ++i) {
+      if ((i * 4 + wave) >= Cfg::Y_INSTR) break;
+      const bool ok = y_rel[i] >= 0 && w0 + y_pw[i] < p.W && h0 + y_ph[i] < p.H;
+      dma16(ry, sY(buf) + (i * 4 + wave) * 1024, ok ? (unsigned)(ybase + y_rel[i]) * 2u : kOOB);
+    }
+    const auto rx = make_rsrc(xsrc + (n + (dok ? dshift : 0)) * img_px * Cs, (unsigned)(img_px * Cs * 2));
+#pragma unroll
+    for (int i = 0; i < Cfg::X_ITERS; ++i) {
+      if ((i * 4 + wave) >= Cfg::X_INSTR) break;
+      const int gw = w0 + x_dw[i], gh = h0 + x_dh[i];
+      x_pix[i] = (gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && xch_ok && dok) ? gh * p.W + gw : -1;
+      dma16(rx, sX(buf) + (i * 4 + wave) * 1024, x_pix[i] >= 0 ? (unsigned)(x_pix[i] * Cs + cs0) * 2u : kOOB);
+    }
+  };
+  auto transform = [&](char* __restrict__ X) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < Cfg::X_ITERS; ++i) {
+      const int e = (i * 4 + wave) * 64 + lane;
+      if ((i * 4 + wave) < Cfg::X_INSTR && x_pix[i] >= 0) {
+        uint4* q = reinterpret_cast<uint4*>(X + e * 16);
+        float f[8];
+        unpack8(*q, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = min(c8l + j, p.C1 - 1);
+          f[j] = fmaxf(fmaf(f[j], s_scale[c], s_shift[c]), 0.0f);
+        }
+        *q = pack8(f);
+      }
+    }
+  };
+
+  // ---- per-lane transposed-read geometry.  16-lane group g4 = lane >> 4: columns
+  // (g4 & 1) * 16 + 4 * pq, pixel rows (g4 >> 1) * 8 + 4 * h + q within the 16-pixel k-step
+  const int g4 = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
+  int ya[2], xb[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = (g4 >> 1) * 8 + 4 * h + q;     // + 16 * ks (row bits 0..3 unchanged)
+    const int byte = wj * 64 + (g4 & 1) * 32 + 8 * pq;
+    const int pc = (byte >> 4) ^ wg3_yswz<BCO>(row);
+    ya[h] = row * Cfg::Y_ROWB + (pc << 4) + (byte & 15);
+    xb[h] = row * 64 + (g4 & 1) * 32 + 8 * pq;      // halo pixel row (+ 18 * ks + tap offset)
+  }
+  f32x16_t acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+
+  auto compute = [&](const char* __restrict__ Y, const char* __restrict__ X) __attribute__((always_inline)) {
+#pragma unroll
+    for (int kk = 0; kk < KS16 / KW; ++kk) {
+      const int ks = kk * KW + wk;
+      const uint2 alo = lds_read_tr16(Y + ks * 16 * Cfg::Y_ROWB + ya[0]);
+      const uint2 ahi = lds_read_tr16(Y + ks * 16 * Cfg::Y_ROWB + ya[1]);
+      const uint4 af = make_uint4(alo.x, alo.y, ahi.x, ahi.y);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int toff = (ks * HW2 + (tap / 3) * HW2 + tap % 3) * 64;
+        const uint2 lo = lds_read_tr16(X + toff + xb[0]);
+        const uint2 hi = lds_read_tr16(X + toff + xb[1]);
+        acc[tap] = mfma32x32x16(af, make_uint4(lo.x, lo.y, hi.x, hi.y), acc[tap]);
+      }
+    }
+  };
+
+  if (t_begin < t_end) issue(t_begin, 0);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int buf = (tile - t_begin) & 1;
+    dma_wait<0>();
+    if (has_pro && !second) transform(sX(buf));
+    lds_sync();
+    if (tile + 1 < t_end) issue(tile + 1, buf ^ 1);
+    compute(sY(buf), sX(buf));
+  }
+
+  // ---- k-split reduction over the KW waves of each co tile (fixed order, in LDS, one tap
+  // group at a time), then the partial slab part[split][co][tap][ci]
+  dma_wait<0>();
+  lds_sync();
+  float* red = reinterpret_cast<float*>(base);     // [KW-1][NJ][3 taps][16][64] floats
+  float* out = p.partial + (long long)split * p.Cout * p.taps * p.Cin;
+#pragma unroll
+  for (int tg = 0; tg < 3; ++tg) {
+    if (wk > 0) {
+#pragma unroll
+      for (int t3 = 0; t3 < 3; ++t3)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          red[((((wk - 1) * NJ + wj) * 3 + t3) * 16 + i) * 64 + lane] = acc[tg * 3 + t3][i];
+    }
+    lds_sync();
+    if (wk == 0) {
+#pragma unroll
+      for (int t3 = 0; t3 < 3; ++t3) {
+        const int tap = plane * 9 + tg * 3 + t3;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float v = acc[tg * 3 + t3][i];
+#pragma unroll
+          for (int w2 = 1; w2 < KW; ++w2) v += red[((((w2 - 1) * NJ + wj) * 3 + t3) * 16 + i) * 64 + lane];
+          // D layout of 32x32: column n = lane & 31 (ci), row m = 8 (i / 4) + 4 (lane >> 5) + i % 4
+          const int co = co0 + wj * 32 + 8 * (i >> 2) + 4 * (lane >> 5) + (i & 3);
+          const int ci = ci0 + (lane & 31);
+          if (co < p.Cout && ci < p.Cin) out[((long long)co * p.taps + tap) * p.Cin + ci] = v;
+        }
+      }
+    }
+    lds_sync();
+  }
+}
+
 template <int DIMS, int BCO>
 void launch_wg(ConvWgradArgs& a, hipStream_t st) {
   using Cfg = WgCfg<DIMS, BCO>;
@@ -510,6 +712,19 @@ void conv3_wgrad2_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
     hipLaunchKernelGGL((conv3_wgrad2_kernel<64, 64>), dim3(grid), dim3(256), (Wg2Cfg<64, 64>::SMEM), st, a);
   else
     hipLaunchKernelGGL((conv3_wgrad2_kernel<64, 128>), dim3(grid), dim3(256), (Wg2Cfg<64, 128>::SMEM), st, a);
+}
+
+void conv3_wgrad3_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
+  const int grid = a.coTiles * a.ciChunks * a.planes * a.splits;
+  const int pt = a.TH * 16;
+  if (bco == 32)
+    hipLaunchKernelGGL((conv3_wgrad3_kernel<32, 256>), dim3(grid), dim3(256), (Wg2Cfg<32, 256>::SMEM), st, a);
+  else if (pt == 256)
+    hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 256>), dim3(grid), dim3(256), (Wg2Cfg<64, 256>::SMEM), st, a);
+  else if (pt == 96)
+    hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 96>), dim3(grid), dim3(256), (Wg2Cfg<64, 96>::SMEM), st, a);
+  else
+    hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 128>), dim3(grid), dim3(256), (Wg2Cfg<64, 128>::SMEM), st, a);
 }
 
 void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st) {

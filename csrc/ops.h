@@ -67,6 +67,8 @@ void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st);
 // one depth tap plane per workgroup)
 void conv3_wgrad2_launch(ConvWgradArgs& a, int bco, hipStream_t st);
 int conv3_wgrad2_pt(int bco, int C2, int H, int W);
+// 32x32x16-MFMA variant (conflict-free transposed reads; Cin % 32 == 0, pixel tiles of 128 / 256)
+void conv3_wgrad3_launch(ConvWgradArgs& a, int bco, hipStream_t st);
 
 int conv3_wgrad_halo_cap(int dims);
 
