@@ -134,6 +134,8 @@ def main():
                 print(f"alive {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
         threading.Thread(target=_beat, daemon=True).start()
 
+    if args.impl == "hip" and not torch.cuda.is_available():
+        args.impl = "torch"            # CPU rehearsal (gloo): stock ops, same contract
     from ddlpc.config import ModelConfig, TrainConfig
     from ddlpc.data import device_random_batch
     from ddlpc.train.trainer import Trainer

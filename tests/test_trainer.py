@@ -105,7 +105,8 @@ def test_bench_torchrun_two_ranks_gloo():
                           "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
                           "--master-port", str(port), os.path.join(root, "bench.py"),
                           "--gpus", "2", "--impl", "torch", "--steps", "2", "--warmup", "1",
-                          "--batch", "2", "--tile", "64", "--width-divisor", "16"],
+                          "--batch", "2", "--tile", "64", "--width-divisor", "16",
+                          "--wire-dtype", "bf16", "--bucket-mb", "0.5", "--bucket-sweep", "0.25,1"],
                          capture_output=True, text=True, timeout=600, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.strip().splitlines() if l.startswith("{")]
@@ -113,6 +114,11 @@ def test_bench_torchrun_two_ranks_gloo():
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
     assert rec["config"]["global_batch"] == 4 and rec["value"] > 0
+    # multi-GPU reporting fields: bucket count, wire dtype, the bucket sweep
+    c = rec["config"]
+    assert c["wire_dtype"] == "bf16" and c["buckets"] >= 2 and "comm_wait_ms" in c
+    assert set(c["bucket_sweep"]) == {"0.25", "1.0"}
+    assert c["bucket_sweep"]["0.25"]["buckets"] > c["bucket_sweep"]["1.0"]["buckets"]
 
 
 def test_resume_with_max_steps_inside_an_epoch(tmp_path):
