@@ -58,6 +58,9 @@ def _parse():
                     help="weight-gradient stream: auto = time both during warm-up, keep the faster")
     ap.add_argument("--hip-graph", type=int, default=int(os.environ.get("DDLPC_HIP_GRAPH", "0")),
                     help="1: replay the single-GPU train step as one hipGraph")
+    ap.add_argument("--recompute", type=int, default=0,
+                    help="activation recompute in backward: 1 = first conv of each block, "
+                         "2 = both convs (less activation memory, more compute)")
     ap.add_argument("--fixed-batch", type=int, default=0,
                     help="diagnostic: 1 = reuse one rendered batch every step (no per-step "
                          "input pipeline; reported in 'data')")
@@ -145,7 +148,8 @@ def main():
                       tile=args.tile, batch_per_gpu=args.batch, accum_steps=args.accum,
                       num_samples=1 << 30, test_holdout=0, impl=args.impl,
                       bucket_mb=args.bucket_mb, wire_dtype=args.wire_dtype,
-                      grad_codec=args.codec, log_dir=None, hip_graph=bool(args.hip_graph))
+                      grad_codec=args.codec, log_dir=None, hip_graph=bool(args.hip_graph),
+                      recompute=int(args.recompute))
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     tr = Trainer(cfg, device=dev)
     world, rank = tr.world, tr.rank
@@ -263,6 +267,7 @@ def main():
                        "parallelism": f"dp{world}", "impl": tr.impl,
                        "optimizer": "Adam(lr=1e-3)", "loss": "CrossEntropy",
                        "train_loss_mean": round(loss["loss"], 4),
+                       "recompute": int(args.recompute),
                        "peak_mem_gb": (round(torch.cuda.max_memory_allocated(device) / 2**30, 2)
                                        if dev == "cuda" else None),
                        "schedule": ("overlap" if sched.get("side_stream") else "serial") if sched

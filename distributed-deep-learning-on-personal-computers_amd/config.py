@@ -108,6 +108,10 @@ class TrainConfig:
     # ---- execution -----------------------------------------------------------------
     impl: str = "auto"                   # auto | hip | torch   (hip = hand-written kernels)
     hip_graph: bool = False              # capture the train step in a hipGraph
+    recompute: int = 0                   # HIP engine activation recompute in backward (SURVEY 5.7,
+                                         # batches beyond HBM): 1 = each block's first conv output,
+                                         # 2 = both conv outputs of blocks that hand out a
+                                         # materialised activation (+1 / +2 conv forwards)
 
     def validate(self):
         self.model.validate()

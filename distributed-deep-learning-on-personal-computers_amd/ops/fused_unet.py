@@ -127,21 +127,34 @@ class _DoubleConvFn(torch.autograd.Function):
         ctx.blk = blk
         ctx.pool = pool
         ctx.defer = defer
+        # activation recompute: y1 is not kept; backward re-runs conv1 (same kernel, same
+        # bits) from the saved inputs.  b1 rides along for that (its own grad stays zero)
+        # recompute level 2 also drops y2 when the block hands out a materialised activation
+        # (a deferred block's y2 IS its output, held by the consumer anyway)
+        rc = int(blk.engine.recompute) if training else 0
+        ctx.recompute = rc
+        ctx.recompute_y2 = rc >= 2 and not defer
+        ctx.b1 = b1 if rc else None
+        ctx.b2 = b2 if ctx.recompute_y2 else None
+        empty = torch.empty(0, device=y1.device, dtype=y1.dtype)
+        y1_keep = empty if rc else y1
+        y2_keep = empty if ctx.recompute_y2 else y2
         if defer:
             # deferred activation: the block hands out its PRE-BN output y2 with the BN
             # statistics s2; the consumer (transposed conv / head kernels) applies BN + ReLU
             # on load and returns dL/da2 with BN-backward partial sums attached
             ctx.has_x2 = x2 is not None
             ctx.x1_requires_grad = ctx.needs_input_grad[0]
-            ctx.save_for_backward(x1, x2 if x2 is not None else torch.empty(0), y1, y2, s1, s2,
-                                  g1, g2)
+            ctx.save_for_backward(x1, x2 if x2 is not None else torch.empty(0), y1_keep, y2, s1,
+                                  s2, g1, g2)                     # (y2: the output itself)
             ctx.set_materialize_grads(False)
             ctx.mark_non_differentiable(s2)
             return y2, None, s2
         a2, pooled = F.bn_relu_apply(y2, s2, pool)
         ctx.has_x2 = x2 is not None
         ctx.x1_requires_grad = ctx.needs_input_grad[0]
-        ctx.save_for_backward(x1, x2 if x2 is not None else torch.empty(0), y1, y2, s1, s2, g1, g2)
+        ctx.save_for_backward(x1, x2 if x2 is not None else torch.empty(0), y1_keep, y2_keep, s1,
+                              s2, g1, g2)
         ctx.set_materialize_grads(False)
         if pool:
             return a2, pooled, None
@@ -160,6 +173,10 @@ class _DoubleConvFn(torch.autograd.Function):
             dpool = dpool.contiguous()
         if da2 is None and dpool is None:
             return (None,) * 13
+        if ctx.recompute:
+            y1 = F.conv3_fwd(x1, x2, blk.pack1.fwd, ctx.b1, None, None, blk.pack1.cout, 0, False)[0]
+        if ctx.recompute_y2:
+            y2 = F.conv3_fwd(y1, None, blk.pack2.fwd, ctx.b2, s1[2], s1[3], blk.pack2.cout, 0, False)[0]
         # BN-backward partial sums already reduced by the consumer's kernel (deferred BN)
         part2 = getattr(da2, "_ddlpc_bn_partial", None) if ctx.defer else None
         bn1, bn2 = blk.bn1.bn, blk.bn2.bn
@@ -401,6 +418,7 @@ class UNetEngine:
         self.defer_mode = os.environ.get("DDLPC_DEFER_BN", "all")
         # transposed-conv weight gradients on the side stream too (DDLPC_SIDE_CONVT=0: main)
         self.side_convt = os.environ.get("DDLPC_SIDE_CONVT", "1") != "0"
+        self.recompute = 0               # Trainer sets cfg.recompute: 0 / 1 (y1) / 2 (y1, y2)
         self.enc = [_Block(b.double_conv, first=(i == 0), engine=self)
                     for i, b in enumerate(model.down_blocks())]
         self.mid = _Block(model.double_conv, first=False, engine=self)

@@ -70,6 +70,7 @@ class Trainer:
         if self.impl == "hip":
             _ext.ops()                               # fail loudly if kernels are missing
             model.to_hip()
+            model._engine.recompute = int(cfg.recompute)
         self.optimizer = FlatAdam(self.flat, lr=cfg.lr, betas=cfg.betas, eps=cfg.eps,
                                   weight_decay=cfg.weight_decay,
                                   use_hip=(self.impl == "hip"))

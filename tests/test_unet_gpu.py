@@ -226,3 +226,32 @@ def test_hip_grad_accumulation_matches_fp32_oracle():
             bad.append((n, ch, ca))
     tr.close()
     assert not bad, bad
+
+
+def test_recompute_matches_stored_activations():
+    """cfg.recompute: block conv outputs are recomputed in backward instead of
+    kept (1: first conv, 2: both where the block output is materialised).  Same kernels, same
+    inputs -> the same bits: two optimizer steps at every level from the same init end in
+    identical parameters, each level with less peak memory than the one below."""
+    from ddlpc.config import ModelConfig, TrainConfig
+    from ddlpc.data import device_random_batch
+    from ddlpc.train.trainer import Trainer
+    out = {}
+    for rc in (0, 1, 2):
+        cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=128, batch_per_gpu=8,
+                          num_samples=1, test_holdout=0, impl="hip", recompute=rc)
+        tr = Trainer(cfg, device="cuda")
+        batches = [device_random_batch(8, 128, 6, tr.device, seed=40 + j) for j in range(2)]
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats()
+        base = torch.cuda.memory_allocated()
+        for b in batches:
+            tr.train_step([b])
+        torch.cuda.synchronize()
+        # peak above what was resident before the steps (the other trainer's state and the
+        # batches count in both runs alike)
+        out[rc] = (tr.flat.param_buf.clone(), torch.cuda.max_memory_allocated() - base)
+        tr.close()
+        del tr, batches
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][0], out[2][0])
+    assert out[2][1] < out[1][1] < out[0][1], (out[0][1], out[1][1], out[2][1])
