@@ -99,7 +99,9 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
                                   const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                                   const c10::optional<at::Tensor>& pscale,
                                   const c10::optional<at::Tensor>& pshift, int64_t cout,
-                                  int64_t co1, bool want_stats) {
+                                  int64_t co1, bool want_stats,
+                                  const c10::optional<at::Tensor>& pscale2,
+                                  const c10::optional<at::Tensor>& pshift2) {
   CHECK_DEV(x1); CHECK_CONTIG(x1); CHECK_BF16(x1); CHECK_BF16(w); CHECK_CONTIG(w);
   c10::DeviceGuard guard(x1.device());
   const Geo g = geo_of(x1);
@@ -129,6 +131,11 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   a.X2 = dual ? bptr(*x2) : nullptr;
   a.pscale = fptr_opt(pscale);
   a.pshift = fptr_opt(pshift);
+  a.pscale2 = fptr_opt(pscale2);
+  a.pshift2 = fptr_opt(pshift2);
+  if (a.pscale2 != nullptr)
+    TORCH_CHECK(dual && a.pshift2 != nullptr && a.C1 + a.C2 <= 512 && pscale2->numel() == a.C2,
+                "X2 prologue: needs x2, both pscale2/pshift2 [C2], and C1 + C2 <= 512");
   a.Wt = bptr(w);
   a.bias = fptr_opt(bias);
   TORCH_CHECK(a.C2 == 0 || a.C1 % 32 == 0, "concat: first input needs C1 % 32 == 0");
@@ -245,7 +252,9 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
 at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
                        const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& pscale,
                        const c10::optional<at::Tensor>& pshift,
-                       const c10::optional<at::Tensor>& out) {
+                       const c10::optional<at::Tensor>& out,
+                       const c10::optional<at::Tensor>& pscale2,
+                       const c10::optional<at::Tensor>& pshift2) {
   CHECK_DEV(dy); CHECK_CONTIG(dy); CHECK_BF16(dy); CHECK_CONTIG(x1); CHECK_BF16(x1);
   c10::DeviceGuard guard(dy.device());
   const Geo g = geo_of(x1);
@@ -265,7 +274,10 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   a.X2 = dual ? bptr(*x2) : nullptr;
   a.pscale = fptr_opt(pscale);
   a.pshift = fptr_opt(pshift);
+  a.pscale2 = fptr_opt(pscale2);
+  a.pshift2 = fptr_opt(pshift2);
   if (a.pscale) TORCH_CHECK(a.C1 <= 512, "prologue supports C1 <= 512");
+  if (a.pscale2) TORCH_CHECK(dual && a.pshift2 && a.C1 + a.C2 <= 512, "X2 prologue: x2, pscale2/pshift2, C1 + C2 <= 512");
   const int bco = a.Cout <= 32 ? 32 : 64;
   static const int use_v2 = [] { const char* e = getenv("DDLPC_WGRAD_V2"); return e ? atoi(e) : 1; }();
   const bool v2 = use_v2 && (use_v2 != 2 || g.dims == 2) && g.W >= 16 && (a.C2 == 0 || a.C1 % 32 == 0);
@@ -303,6 +315,8 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   a.splits = splits;
   auto part = at::empty({(int64_t)splits * a.Cout * a.taps * a.Cin}, dy.options().dtype(at::kFloat));
   a.partial = part.data_ptr<float>();
+  TORCH_CHECK(a.pscale2 == nullptr || v2, "X2 prologue needs the v2/v3 weight-gradient kernels "
+              "(2-D or 3-D, W >= 16, C1 % 32 == 0)");
   if (v3) conv3_wgrad3_launch(a, bco, cur_stream());
   else if (v2) conv3_wgrad2_launch(a, bco, cur_stream());
   else conv3_wgrad_launch(a, bco, cur_stream());
@@ -350,13 +364,15 @@ at::Tensor bn_finalize(const at::Tensor& partial, double count, const at::Tensor
   return st;
 }
 
-std::vector<at::Tensor> bn_relu_apply(const at::Tensor& y, const at::Tensor& stats4, bool pool) {
+std::vector<at::Tensor> bn_relu_apply(const at::Tensor& y, const at::Tensor& stats4, bool pool,
+                                      bool full) {
   CHECK_DEV(y); CHECK_CONTIG(y); CHECK_BF16(y);
   c10::DeviceGuard guard(y.device());
   const Geo g = geo_of(y);
   TORCH_CHECK(g.C % 8 == 0, "C must be a multiple of 8");
   const float* s = stats4.data_ptr<float>();
-  at::Tensor a = at::empty_like(y);
+  TORCH_CHECK(full || pool, "bn_relu_apply: full=False only with pool (deferred skip)");
+  at::Tensor a = full ? at::empty_like(y) : at::empty({0}, y.options());
   at::Tensor p;
   if (pool) {
     TORCH_CHECK(g.H % 2 == 0 && g.W % 2 == 0 && (g.dims == 2 || g.D % 2 == 0), "pool needs even dims");
@@ -364,7 +380,7 @@ std::vector<at::Tensor> bn_relu_apply(const at::Tensor& y, const at::Tensor& sta
                                           : std::vector<int64_t>{g.N, g.D / 2, g.H / 2, g.W / 2, g.C};
     p = at::empty(ps, y.options());
   }
-  bn_relu_apply_launch(bptr(y), s + 2 * g.C, s + 3 * g.C, bptr_mut(a),
+  bn_relu_apply_launch(bptr(y), s + 2 * g.C, s + 3 * g.C, full ? bptr_mut(a) : nullptr,
                        pool ? bptr_mut(p) : nullptr, g.dims, g.N, g.D, g.H, g.W, g.C, cur_stream());
   return {a, p.defined() ? p : at::empty({0}, y.options())};
 }
@@ -839,11 +855,12 @@ std::vector<at::Tensor> tile_gather(const at::Tensor& src, const at::Tensor& lab
 
 TORCH_LIBRARY(ddlpc, m) {
   m.def("conv3_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, Tensor? pscale, Tensor? pshift, "
-        "int cout, int co1, bool stats) -> Tensor[]");
-  m.def("conv3_wgrad(Tensor dy, Tensor x1, Tensor? x2, Tensor? pscale, Tensor? pshift, Tensor(a!)? out=None) -> Tensor");
+        "int cout, int co1, bool stats, Tensor? pscale2=None, Tensor? pshift2=None) -> Tensor[]");
+  m.def("conv3_wgrad(Tensor dy, Tensor x1, Tensor? x2, Tensor? pscale, Tensor? pshift, Tensor(a!)? out=None, "
+        "Tensor? pscale2=None, Tensor? pshift2=None) -> Tensor");
   m.def("bn_finalize(Tensor partial, float count, Tensor gamma, Tensor beta, Tensor(a!) running_mean, "
         "Tensor(b!) running_var, float momentum, float eps, bool update_running, Tensor(c!)? nbt) -> Tensor");
-  m.def("bn_relu_apply(Tensor y, Tensor stats4, bool pool) -> Tensor[]");
+  m.def("bn_relu_apply(Tensor y, Tensor stats4, bool pool, bool full=True) -> Tensor[]");
   m.def("bn_backward(Tensor? dA, Tensor? dP, Tensor y, Tensor stats4, Tensor gamma, Tensor? gscale, "
         "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None, Tensor? partial=None) -> Tensor[]");
   m.def("convt_fwd(Tensor x, Tensor wt, Tensor? bias, int cout, Tensor? bn4=None) -> Tensor");

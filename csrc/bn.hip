@@ -71,7 +71,7 @@ __global__ void bn_relu_apply_kernel(const bf16_t* __restrict__ y, const float* 
             f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
           }
           const uint4 v = pack8(f);
-          *reinterpret_cast<uint4*>(out + pix * C + c8) = v;
+          if (out != nullptr) *reinterpret_cast<uint4*>(out + pix * C + c8) = v;
           float r[8];
           unpack8(v, r);                       // pool the bf16-rounded activations
 #pragma unroll

@@ -96,8 +96,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   const int S = my_items * spi;
 
   const bool has_pro = p.pscale != nullptr;
+  const bool has_pro2 = p.pscale2 != nullptr;         // deferred skip: X2 channels at C1 + c
   if (has_pro)
     for (int c = tid; c < p.C1; c += C::NTH) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
+  if (has_pro2)
+    for (int c = tid; c < p.C2; c += C::NTH) { s_scale[p.C1 + c] = p.pscale2[c]; s_shift[p.C1 + c] = p.pshift2[c]; }
 
   const auto rW = make_rsrc(p.Wt, (unsigned)((long long)p.Cout * p.taps * p.CinW * 2));
 
@@ -193,12 +196,14 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   // scopes: the compiler would otherwise drain the in-flight weight DMA before them)
   auto transform_body = [&](int k, int chunk, char* __restrict__ Abuf) __attribute__((always_inline)) {
     const int cbase = (chunk0_of(k) + chunk) * BK;
-    if (cbase >= p.C1) return;                      // X2 channels: no prologue
+    const bool x2ch = cbase >= p.C1;                // X2 channels: prologue only if deferred
+    if (x2ch ? !has_pro2 : !has_pro) return;
+    const int climit = x2ch ? p.Cin : p.C1;
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
       const int e = (i * C::NW + wave) * 64 + lane;    // same element this lane DMA'd
       const int c8 = cbase + a_sub8[i];
-      if (c8 < p.C1 && a_pix[i] >= 0) {
+      if (c8 < climit && a_pix[i] >= 0) {
         uint4* q = reinterpret_cast<uint4*>(Abuf + e * 16);
         float f[8];
         unpack8(*q, f);
@@ -404,7 +409,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       }
       // prologue BN + ReLU on the pieces this lane DMA'd (own vmcnt covers them): before the
       // stage barrier, which then also publishes the transformed halo (one barrier, not two)
-      if (grp == 0 && has_pro) transform_A(k, chunk, cseq & 1);
+      if (grp == 0 && (has_pro || has_pro2)) transform_A(k, chunk, cseq & 1);
       lds_sync();
       // the previous item's epilogue runs here, BEFORE this stage's DMA is issued, so its
       // stores drain under this stage's compute (vmcnt retires in order)
@@ -462,7 +467,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int pp = 2 * j + h;
-        if (pp < P && pp % NG == 0 && has_pro) {
+        if (pp < P && pp % NG == 0 && (has_pro || has_pro2)) {
           const int cs = pp / NG;
           transform_A(cs / nchunks, cs % nchunks, cs & 1);
         }

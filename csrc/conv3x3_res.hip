@@ -60,9 +60,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   constexpr int NW = C::NW, BN = C::BN;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bool has_pro = p.pscale != nullptr;
-  const int ss_bytes = res_ss_bytes(p.C1, has_pro);
+  const bool has_pro2 = p.pscale2 != nullptr;          // deferred skip: X2 channels at C1 + c
+  const int NSS = has_pro2 ? p.Cin : p.C1;             // channels with prologue constants
+  const int ss_bytes = res_ss_bytes(NSS, has_pro || has_pro2);
   float* s_scale = reinterpret_cast<float*>(smem);
-  float* s_shift = s_scale + p.C1;
+  float* s_shift = s_scale + NSS;
   char* sW = smem + ss_bytes;
   char* sA0 = sW + res_w_bytes(p.Cin, BN, TAP8);
   auto sA = [&](int b) { return sA0 + b * C::A_BYTES; };
@@ -84,6 +86,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
 
   if (has_pro)
     for (int c = tid; c < p.C1; c += C::NTH) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
+  if (has_pro2)
+    for (int c = tid; c < p.C2; c += C::NTH) { s_scale[p.C1 + c] = p.pscale2[c]; s_shift[p.C1 + c] = p.pshift2[c]; }
 
   // bias of this block's channel tile, loaded once (a global load inside the epilogue would
   // make the compiler wait vmcnt(0) — on this tile's stores — before every use); loaded
@@ -194,12 +198,12 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   // prologue on the pieces THIS lane DMA'd (a_valid still describes the chunk's item):
   // packed fp32 FMA, bf16 rounding, ReLU as a packed signed-16-bit max on the bf16 bits
   auto transform_body = [&](char* __restrict__ Ab, const float* __restrict__ scl,
-                            const float* __restrict__ shf_, int cbase, uint32_t vm) {
+                            const float* __restrict__ shf_, int cbase, uint32_t vm, int climit) {
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
       const int e = (i * NW + wave) * 64 + lane;
       const int c8 = cbase + a_sub8[i];
-      if (((vm >> i) & 1u) && c8 < p.C1) {
+      if (((vm >> i) & 1u) && c8 < climit) {
         uint4* q = reinterpret_cast<uint4*>(Ab + e * 16);
         const uint4 v = *q;
         const float4* scp = reinterpret_cast<const float4*>(scl + c8);
@@ -227,8 +231,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   // in-flight halo DMAs of later ring slots before these reads)
   auto transform_A = [&](int chunk, int buf) {
     const int cbase = chunk * BK;
-    if (cbase >= p.C1) return;
-    transform_body(sA(buf), s_scale, s_shift, cbase, get_vmask(buf));
+    const bool x2ch = cbase >= p.C1;                   // X2 chunk: prologue only if deferred
+    if (x2ch ? !has_pro2 : !has_pro) return;
+    transform_body(sA(buf), s_scale, s_shift, cbase, get_vmask(buf), x2ch ? p.Cin : p.C1);
   };
 
   // ---- per-lane fragment geometry
@@ -342,7 +347,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
       }
     }
     const int buf = s % NBUF;
-    if (!TAP8 && has_pro) transform_A(c, buf);
+    if (!TAP8 && (has_pro || has_pro2)) transform_A(c, buf);
     lds_sync();
     epi_prev = (c == 0 && s > 0);
     if (epi_prev) epilogue(k - 1);
@@ -437,7 +442,7 @@ constexpr ResVariant kRes[8] = {
     //    96 output channels, so the dY halo is read once instead of once per 32-channel tile.
     {8, 1, 2, 6, 324, false, 16, 16, 3}};
 
-int res_smem(const ResVariant& v, int Cin, int C1, bool pro) {
+int res_smem(const ResVariant& v, int Cin, int C1, bool pro) {   // C1: channels with constants
   const int bn = v.wn * v.nt * 16;
   const int nw = v.wm * v.wn;
   const int instr = ((v.tap8 ? v.halo : v.halo * 4) + 63) / 64;
@@ -483,7 +488,7 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
   }
   for (int i = 0; i < nc; ++i) {
     const ResVariant& v = kRes[cand[i]];
-    const int sm = res_smem(v, a.Cin, a.C1, pro);
+    const int sm = res_smem(v, a.Cin, a.pscale2 != nullptr ? a.Cin : a.C1, pro || a.pscale2 != nullptr);
     const int nw = v.wm * v.wn;
     // 4-wave blocks need 2 per CU (2 waves / SIMD); 8-wave blocks use ~200 VGPRs: 1 per CU
     const int bpc = nw == 4 ? (sm <= 80 * 1024 ? 2 : 0) : (sm <= 160 * 1024 ? 1 : 0);

@@ -314,8 +314,11 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
   const int dshift = p.planes == 3 ? plane - 1 : 0;
 
   const bool has_pro = p.pscale != nullptr;
+  const bool has_pro2 = p.pscale2 != nullptr;           // deferred skip: X2 channels at C1 + c
   if (has_pro)
     for (int c = tid; c < p.C1; c += 256) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
+  if (has_pro2)
+    for (int c = tid; c < p.C2; c += 256) { s_scale[p.C1 + c] = p.pscale2[c]; s_shift[p.C1 + c] = p.pshift2[c]; }
   const int t_begin = (int)((long long)p.nTiles * split / p.splits);
   const int t_end = (int)((long long)p.nTiles * (split + 1) / p.splits);
   const long long img_px = (long long)p.H * p.W;
@@ -383,7 +386,7 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
         unpack8(*q, f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int c = min(c8l + j, p.C1 - 1);
+          const int c = min(c8l + j, (second ? p.Cin : p.C1) - 1);
           f[j] = fmaxf(fmaf(f[j], s_scale[c], s_shift[c]), 0.0f);
         }
         *q = pack8(f);
@@ -454,7 +457,7 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
   for (int tile = t_begin; tile < t_end; ++tile) {
     const int buf = (tile - t_begin) & 1;
     dma_wait<0>();
-    if (has_pro && !second) transform(buf);
+    if (second ? has_pro2 : has_pro) transform(buf);
     lds_sync();
     if (tile + 1 < t_end) issue(tile + 1, buf ^ 1);
     compute(sY(buf), sX(buf));
@@ -522,8 +525,11 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
   const int dshift = p.planes == 3 ? plane - 1 : 0;
 
   const bool has_pro = p.pscale != nullptr;
+  const bool has_pro2 = p.pscale2 != nullptr;           // deferred skip: X2 channels at C1 + c
   if (has_pro)
     for (int c = tid; c < p.C1; c += 256) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
+  if (has_pro2)
+    for (int c = tid; c < p.C2; c += 256) { s_scale[p.C1 + c] = p.pscale2[c]; s_shift[p.C1 + c] = p.pshift2[c]; }
   const int t_begin = (int)((long long)p.nTiles * split / p.splits);
   const int t_end = (int)((long long)p.nTiles * (split + 1) / p.splits);
   const long long img_px = (long long)p.H * p.W;
@@ -591,7 +597,7 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
         unpack8(*q, f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int c = min(c8l + j, p.C1 - 1);
+          const int c = min(c8l + j, (second ? p.Cin : p.C1) - 1);
           f[j] = fmaxf(fmaf(f[j], s_scale[c], s_shift[c]), 0.0f);
         }
         *q = pack8(f);
@@ -638,7 +644,7 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
   for (int tile = t_begin; tile < t_end; ++tile) {
     const int buf = (tile - t_begin) & 1;
     dma_wait<0>();
-    if (has_pro && !second) transform(sX(buf));
+    if (second ? has_pro2 : has_pro) transform(sX(buf));
     lds_sync();
     if (tile + 1 < t_end) issue(tile + 1, buf ^ 1);
     compute(sY(buf), sX(buf));

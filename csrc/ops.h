@@ -21,6 +21,8 @@ struct ConvFwdArgs {
   const bf16_t* X2;
   const float* pscale;            // optional BN-apply + ReLU prologue on X1 (per channel)
   const float* pshift;
+  const float* pscale2;           // optional prologue on X2 (a deferred skip tensor; C1 + C2 <= 512)
+  const float* pshift2;
   const bf16_t* Wt;               // [Cout][taps][CinW]
   const float* bias;              // optional
   bf16_t* Y1;
@@ -57,6 +59,8 @@ struct ConvWgradArgs {
   const bf16_t* X2;
   const float* pscale;
   const float* pshift;
+  const float* pscale2;           // prologue on X2 (deferred skip), C1 + C2 <= 512
+  const float* pshift2;
   float* partial;                 // [splits][Cout][taps][Cin]
   int TD, TH, TW;
   int tilesD, tilesH, tilesW, nTiles;
@@ -111,6 +115,7 @@ bool convt_res_launch(GemmArgs& a, int num_cus, hipStream_t st);
 
 
 // ---------------------------------------------------------------- BatchNorm / ReLU / pool
+// out may be null with pool (deferred skip: only the pooled tensor is materialised)
 void bn_relu_apply_launch(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
                           bf16_t* pooled, int dims, int N, int D, int H, int W, int C,
                           hipStream_t st);

@@ -114,12 +114,20 @@ class _BNState:
 
 class _DoubleConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x1, x2, w1, b1, g1, be1, w2, b2, g2, be2, blk, pool: bool, defer: bool):
+    def forward(ctx, x1, x2, w1, b1, g1, be1, w2, b2, g2, be2, blk, pool: bool, defer: bool,
+                x2_bn: Optional[torch.Tensor] = None, defer_skip: bool = False):
+        # x2_bn: statistics of a deferred skip (x2 = the encoder block's PRE-BN y2): its BN +
+        # ReLU is applied on load by the conv / weight-gradient kernels' X2 prologue
+        # defer_skip (encoder blocks): hand out the pre-BN y2 as the skip and materialise only
+        # the pooled activation
         F = _ops()
         p1, p2 = blk.pack1, blk.pack2
         training = blk.bn1.bn.training
         c1 = p1.cout
-        y1, _, st1 = F.conv3_fwd(x1, x2, p1.fwd, b1, None, None, c1, 0, training)
+        sc2 = x2_bn[2] if x2_bn is not None else None
+        sh2 = x2_bn[3] if x2_bn is not None else None
+        ctx.x2_bn = x2_bn
+        y1, _, st1 = F.conv3_fwd(x1, x2, p1.fwd, b1, None, None, c1, 0, training, sc2, sh2)
         count = float(y1.numel() // c1)
         s1 = blk.bn1.finalize(st1, count) if training else blk.bn1.eval_stats()
         y2, _, st2 = F.conv3_fwd(y1, None, p2.fwd, b2, s1[2], s1[3], p2.cout, 0, training)
@@ -150,6 +158,17 @@ class _DoubleConvFn(torch.autograd.Function):
             ctx.set_materialize_grads(False)
             ctx.mark_non_differentiable(s2)
             return y2, None, s2
+        if defer_skip:
+            # the skip leaves as y2 (its BN + ReLU is applied by the decoder's concat conv);
+            # only the pooled activation is written.  s2 rides along (non-differentiable)
+            _, pooled = F.bn_relu_apply(y2, s2, True, False)
+            ctx.has_x2 = x2 is not None
+            ctx.x1_requires_grad = ctx.needs_input_grad[0]
+            ctx.save_for_backward(x1, x2 if x2 is not None else torch.empty(0), y1_keep, y2, s1,
+                                  s2, g1, g2)
+            ctx.set_materialize_grads(False)
+            ctx.mark_non_differentiable(s2)
+            return y2, pooled, s2
         a2, pooled = F.bn_relu_apply(y2, s2, pool)
         ctx.has_x2 = x2 is not None
         ctx.x1_requires_grad = ctx.needs_input_grad[0]
@@ -172,9 +191,13 @@ class _DoubleConvFn(torch.autograd.Function):
         if dpool is not None:
             dpool = dpool.contiguous()
         if da2 is None and dpool is None:
-            return (None,) * 13
+            return (None,) * 15
+        x2_bn = ctx.x2_bn
+        sc2 = x2_bn[2] if x2_bn is not None else None
+        sh2 = x2_bn[3] if x2_bn is not None else None
         if ctx.recompute:
-            y1 = F.conv3_fwd(x1, x2, blk.pack1.fwd, ctx.b1, None, None, blk.pack1.cout, 0, False)[0]
+            y1 = F.conv3_fwd(x1, x2, blk.pack1.fwd, ctx.b1, None, None, blk.pack1.cout, 0, False,
+                             sc2, sh2)[0]
         if ctx.recompute_y2:
             y2 = F.conv3_fwd(y1, None, blk.pack2.fwd, ctx.b2, s1[2], s1[3], blk.pack2.cout, 0, False)[0]
         # BN-backward partial sums already reduced by the consumer's kernel (deferred BN)
@@ -199,16 +222,16 @@ class _DoubleConvFn(torch.autograd.Function):
         padded_in = x2 is None and x1.shape[-1] != w1.shape[1]   # first layer: 3 -> 8 ch
         if direct:
             dy1, _, _ = F.bn_backward(da1, None, y1, s1, g1, None, bn1.weight.grad, bn1.bias.grad)
-            with eng.wgrad_stream(dy1, x1, x2):
+            with eng.wgrad_stream(dy1, x1, x2, x2_bn):
                 if padded_in:
                     w1.grad.add_(F.conv3_wgrad(dy1, x1, None, None, None)[:, :w1.shape[1]])
                 else:
-                    F.conv3_wgrad(dy1, x1, x2, None, None, w1.grad)
+                    F.conv3_wgrad(dy1, x1, x2, None, None, w1.grad, sc2, sh2)
                 eng.ready(bn1.weight, bn1.bias, w1, blk.conv1.bias)
             dg1 = dbe1 = dw1 = None
         else:
             dy1, dg1, dbe1 = F.bn_backward(da1, None, y1, s1, g1, None)
-            dw1 = F.conv3_wgrad(dy1, x1, x2, None, None)
+            dw1 = F.conv3_wgrad(dy1, x1, x2, None, None, None, sc2, sh2)
             dw1 = (dw1[:, :w1.shape[1]] if padded_in else dw1).reshape(w1.shape)
         dx1 = dx2 = None
         if ctx.needs_input_grad[0] or (x2 is not None and ctx.needs_input_grad[1]):
@@ -228,7 +251,7 @@ class _DoubleConvFn(torch.autograd.Function):
         # conv biases feeding a training-mode BN have an exactly-zero gradient
         zb1 = torch.zeros_like(g1) if (not direct and ctx.needs_input_grad[3]) else None
         zb2 = torch.zeros_like(g2) if (not direct and ctx.needs_input_grad[7]) else None
-        return (dx1, dx2, dw1, zb1, dg1, dbe1, dw2, zb2, dg2, dbe2, None, None, None)
+        return (dx1, dx2, dw1, zb1, dg1, dbe1, dw2, zb2, dg2, dbe2, None, None, None, None, None)
 
 
 class _ConvTFn(torch.autograd.Function):
@@ -329,12 +352,13 @@ class _Block:
         self.pack1 = _ConvPack(self.conv1, 0, need_dgrad=not first)
         self.pack2 = _ConvPack(self.conv2, 0, need_dgrad=True)
 
-    def __call__(self, x1, x2, pool: bool, defer: bool = False):
-        """-> (activation, pooled | None, None) or, deferred, (pre-BN y2, None, stats s2)."""
+    def __call__(self, x1, x2, pool: bool, defer: bool = False, x2_bn=None, defer_skip=False):
+        """-> (activation, pooled | None, None) or, deferred, (pre-BN y2, None, stats s2), or
+        with defer_skip (pre-BN y2 as the skip, pooled, stats s2)."""
         return _DoubleConvFn.apply(x1, x2, self.conv1.weight, self.conv1.bias,
                                    self.bn1.bn.weight, self.bn1.bn.bias, self.conv2.weight,
                                    self.conv2.bias, self.bn2.bn.weight, self.bn2.bn.bias, self,
-                                   pool, defer)
+                                   pool, defer, x2_bn, defer_skip)
 
 
 def check_supported(model: nn.Module):
@@ -419,6 +443,9 @@ class UNetEngine:
         # transposed-conv weight gradients on the side stream too (DDLPC_SIDE_CONVT=0: main)
         self.side_convt = os.environ.get("DDLPC_SIDE_CONVT", "1") != "0"
         self.recompute = 0               # Trainer sets cfg.recompute: 0 / 1 (y1) / 2 (y1, y2)
+        # encoder skips handed out pre-BN (see ``defer_skip_levels``): saves ~1 GB at
+        # 256^2 x 128 but measured ~1.2% slower end to end (docs/PERF.md), so opt-in
+        self.defer_skip = os.environ.get("DDLPC_DEFER_SKIP", "0") != "0"
         self.enc = [_Block(b.double_conv, first=(i == 0), engine=self)
                     for i, b in enumerate(model.down_blocks())]
         self.mid = _Block(model.double_conv, first=False, engine=self)
@@ -554,22 +581,40 @@ class UNetEngine:
         self._ensure_packed()
         h = self.to_nhwc(x)
         skips = []
-        for blk in self.enc:
-            skip, h, _ = blk(h, None, True)
-            skips.append(skip)
+        dskip = self.defer_skip_levels(x)
+        for lvl, blk in enumerate(self.enc):
+            skip, h, s_skip = blk(h, None, True, defer_skip=dskip[lvl])
+            skips.append((skip, s_skip))
         n = len(self.dec)
         mode = self.defer_mode                       # "all" | "convt" | "none"
         feeds_convt = [pack is not None and mode != "none" for _, pack, _ in self.dec]
         defer_last = defer_last and mode == "all"
         h, _, s = self.mid(h, None, False, defer=n > 0 and feeds_convt[0])
-        for i, ((ub, pack, blk), skip) in enumerate(zip(self.dec, reversed(skips))):
+        for i, ((ub, pack, blk), (skip, s_skip)) in enumerate(zip(self.dec, reversed(skips))):
             if pack is not None:
                 up = _ConvTFn.apply(h, ub.up_sample.weight, ub.up_sample.bias, pack, self, s)
             else:
                 up = _BilinearFn.apply(h)
             defer = feeds_convt[i + 1] if i + 1 < n else defer_last
-            h, _, s = blk(up, skip, False, defer=defer)
+            h, _, s = blk(up, skip, False, defer=defer, x2_bn=s_skip)
         return h, s
+
+    def defer_skip_levels(self, x: torch.Tensor) -> List[bool]:
+        """Encoder levels whose skip tensor stays pre-BN (BN + ReLU applied on load by the
+        decoder's concat conv, forward and weight gradient): 2-D, the skip image at least 16
+        wide (the weight-gradient kernels with the X2 prologue) and the concat at most 512
+        channels (prologue constants in LDS).  Opt-in with DDLPC_DEFER_SKIP=1 (or engine.defer_skip)."""
+        if not self.defer_skip or x.dim() != 4:
+            return [False] * len(self.enc)
+        out = []
+        w = x.shape[-1]
+        for lvl, blk in enumerate(self.enc):
+            ub, _pack, dblk = self.dec[len(self.dec) - 1 - lvl]
+            c_up = dblk.conv1.weight.shape[1] - blk.conv2.weight.shape[0]
+            c_skip = blk.conv2.weight.shape[0]
+            ok = (w >> lvl) >= 16 and c_up % 32 == 0 and c_up + c_skip <= 512
+            out.append(bool(ok))
+        return out
 
     def _head_params(self):
         w = self.head.weight

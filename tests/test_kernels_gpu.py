@@ -586,3 +586,29 @@ def test_out_params_respect_bounds(ops):
     g.copy_(torch.randn(n, device=DEV))
     ops.adam_step(p, g, m, v2, 0.9, 0.999, 1e-8, 0.0, 1e-3, 1.0)
     assert all(intact(bb_, t) for bb_, t in bufs)
+
+
+@pytest.mark.parametrize("H,C1,C2,Cout", [(32, 64, 32, 32), (16, 128, 64, 64), (64, 32, 32, 32)])
+def test_deferred_skip_prologue_matches_materialised(ops, H, C1, C2, Cout):
+    """Deferred skip (encoder a2 never materialised): the concat conv's X2 prologue applies
+    BN + ReLU on load in the forward kernels (resident / streaming) and the weight-gradient
+    kernels bit-identically to the materialised activation; bn_relu_apply(full=False) writes
+    the same pooled tensor."""
+    torch.manual_seed(21)
+    N, W = 2, H
+    up = torch.randn(N, H, W, C1, device=DEV).bfloat16()
+    y = torch.randn(N, H, W, C2, device=DEV).bfloat16()
+    bn4 = _bn4(C2, 3)
+    a, p_full = ops.bn_relu_apply(y, bn4, True)
+    _, p_def = ops.bn_relu_apply(y, bn4, True, False)
+    assert torch.equal(p_full, p_def)
+    w = torch.randn(Cout, C1 + C2, 3, 3, device=DEV) / math.sqrt(9 * (C1 + C2))
+    pk = pack_conv(ops, w)
+    b = torch.randn(Cout, device=DEV) * 0.1
+    y_mat, _, st_mat = ops.conv3_fwd(up, a, pk.fwd, b, None, None, Cout, 0, True)
+    y_def, _, st_def = ops.conv3_fwd(up, y, pk.fwd, b, None, None, Cout, 0, True, bn4[2], bn4[3])
+    assert torch.equal(y_mat, y_def) and torch.equal(st_mat, st_def)
+    dy = torch.randn(N, H, W, Cout, device=DEV).bfloat16()
+    dw_mat = ops.conv3_wgrad(dy, up, a, None, None)
+    dw_def = ops.conv3_wgrad(dy, up, y, None, None, None, bn4[2], bn4[3])
+    assert torch.equal(dw_mat, dw_def)
