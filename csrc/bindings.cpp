@@ -99,12 +99,15 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
                                   const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                                   const c10::optional<at::Tensor>& pscale,
                                   const c10::optional<at::Tensor>& pshift, int64_t cout,
-                                  int64_t co1, bool want_stats,
+                                  int64_t co1, bool want_stats_in,
                                   const c10::optional<at::Tensor>& pscale2,
-                                  const c10::optional<at::Tensor>& pshift2) {
+                                  const c10::optional<at::Tensor>& pshift2,
+                                  const c10::optional<at::Tensor>& bnb_y,
+                                  const c10::optional<at::Tensor>& bnb_s4) {
   CHECK_DEV(x1); CHECK_CONTIG(x1); CHECK_BF16(x1); CHECK_BF16(w); CHECK_CONTIG(w);
   c10::DeviceGuard guard(x1.device());
   const Geo g = geo_of(x1);
+  bool want_stats = want_stats_in;
   ConvFwdArgs a{};
   a.dims = g.dims; a.N = g.N; a.D = g.D; a.H = g.H; a.W = g.W;
   a.C1 = g.C;
@@ -138,6 +141,21 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
                 "X2 prologue: needs x2, both pscale2/pshift2 [C2], and C1 + C2 <= 512");
   a.Wt = bptr(w);
   a.bias = fptr_opt(bias);
+  if (bnb_y.has_value() && bnb_y->defined()) {
+    // BN-backward epilogue: the stats rows become that BN's (sum dyh, sum dyh*xhat) partials
+    CHECK_CONTIG(*bnb_y); CHECK_BF16(*bnb_y);
+    TORCH_CHECK(bnb_s4.has_value() && bnb_s4->defined() && bnb_s4->numel() == 4 * cout,
+                "bnb: stats4 [4][Cout] required");
+    CHECK_F32(*bnb_s4); CHECK_CONTIG(*bnb_s4);
+    const Geo gy = geo_of(*bnb_y);
+    TORCH_CHECK(g.dims == 2 && gy.N == g.N && gy.H == g.H && gy.W == g.W && gy.C == cout,
+                "bnb: 2-D, y must have the output's shape");
+    TORCH_CHECK(a.Co1 == a.Cout && a.pscale == nullptr && a.pscale2 == nullptr && a.bias == nullptr,
+                "bnb: single output, no prologue, no bias");
+    a.bnb_y = bptr(*bnb_y);
+    a.bnb_s4 = bnb_s4->data_ptr<float>();
+    want_stats = true;
+  }
   TORCH_CHECK(a.C2 == 0 || a.C1 % 32 == 0, "concat: first input needs C1 % 32 == 0");
   TORCH_CHECK((a.C1 % 8 == 0) && (a.C2 % 8 == 0), "input channels must be multiples of 8 "
               "(the engine pads the 3-channel image to 8)");
@@ -855,7 +873,8 @@ std::vector<at::Tensor> tile_gather(const at::Tensor& src, const at::Tensor& lab
 
 TORCH_LIBRARY(ddlpc, m) {
   m.def("conv3_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, Tensor? pscale, Tensor? pshift, "
-        "int cout, int co1, bool stats, Tensor? pscale2=None, Tensor? pshift2=None) -> Tensor[]");
+        "int cout, int co1, bool stats, Tensor? pscale2=None, Tensor? pshift2=None, Tensor? bnb_y=None, "
+        "Tensor? bnb_s4=None) -> Tensor[]");
   m.def("conv3_wgrad(Tensor dy, Tensor x1, Tensor? x2, Tensor? pscale, Tensor? pshift, Tensor(a!)? out=None, "
         "Tensor? pscale2=None, Tensor? pshift2=None) -> Tensor");
   m.def("bn_finalize(Tensor partial, float count, Tensor gamma, Tensor beta, Tensor(a!) running_mean, "

@@ -65,10 +65,12 @@ struct Cfg {
 // operand the pixel tile, so each lane's accumulator holds 4 CONSECUTIVE channels of one
 // pixel -> 8-byte bf16x4 stores; BN statistics are reduced with 4 lane shuffles and
 // written as one partial row per (m tile, wave row).
-template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, bool FDB>
+template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, bool FDB, bool BNB>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_kernel(ConvFwdArgs p) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
   static_assert(NBB == 2 || NBB == 3 || (NBB == 4 && DIMS == 2), "2 / 3 weight-stage buffers, or 4 (super-stages)");
+  // BN-backward epilogue: 2-D, and not with the counted waits of the 3-deep weight ring
+  static_assert(!BNB || (DIMS == 2 && NBB != 3), "BNB: 2-D, NBB 2 or 4");
   constexpr bool FRAG_DB = FDB;
   constexpr int BM = C::BM, BN = C::BN;
   constexpr int NG = DIMS == 2 ? 3 : 9;           // (kd, r) kernel rows per chunk
@@ -141,6 +143,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   // B: row (tap-in-group, channel) -> byte offset without the (chunk, group) term
   // every item of a block has the same n tile (launcher: grid % (KS * nTilesN) == 0)
   const int co0_blk = (int)blockIdx.x / KS % p.nTilesN * BN;
+  // BNB (a data gradient: no prologue, so the prologue constants' LDS holds the BN-backward
+  // table [4][BN]; published by the first stage barrier)
+  if constexpr (BNB) bnb_fill(s_scale, BN, co0_blk, p.Cout, p.bnb_s4, tid, C::NTH);
   int b_off[C::B_ITERS], b_sub8[C::B_ITERS];
 #pragma unroll
   for (int i = 0; i < C::B_ITERS; ++i) {
@@ -259,6 +264,25 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   // Stores are buffer stores with an out-of-range offset for masked lanes: every wave issues
   // exactly EPI_STORES per epilogue (no exec branches), so counted vmcnt waits stay exact.
   constexpr int EPI_STORES = MT * NT;
+  // BNB: y at an item's output pixels, loaded into VGPRs at the item's last stage (after that
+  // stage's DMA) and consumed by its epilogue after the next stage's full wait
+  uint2 ybuf[MT][NT];
+  auto issue_Y = [&](int kk) __attribute__((always_inline)) {
+    const Item it = item_of(kk);
+    const auto ry = make_rsrc(p.bnb_y + it.n_img * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
+      const int gw = it.w0 + pix % p.TW, gh = it.h0 + (pix / p.TW) % p.TH;
+      const bool valid = gw < p.W && gh < p.H;
+      const int lpix = gh * p.W + gw;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int co = it.co0 + wn * (NT * 16) + nt * 16 + 4 * g;
+        ybuf[mt][nt] = buf_load8(ry, valid && co < p.Cout ? (unsigned)(lpix * p.Cout + co) * 2u : kOOB);
+      }
+    }
+  };
   auto epilogue = [&](int k) __attribute__((always_inline)) {
     const Item it = item_of(k);
     const int Co2 = p.Cout - p.Co1;
@@ -267,17 +291,21 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
                            : make_rsrc(p.Y1 + it.n_img * img_px * p.Co1, (unsigned)(img_px * p.Co1 * 2));
     const auto r2 = make_rsrc(p.Y2 != nullptr ? p.Y2 + it.n_img * img_px * Co2 : p.Y1,
                               p.Y2 != nullptr ? (unsigned)(img_px * Co2 * 2) : 0u);
+    // channel tiles outer: the BNB constants of one tile are read once (the scheduler
+    // barrier below keeps the next tile's reads from being hoisted: VGPR pressure)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
-      const int pw = pix % p.TW, ph = (pix / p.TW) % p.TH;
-      const int pd = DIMS == 3 ? pix / (p.TW * p.TH) : 0;
-      const int gw = it.w0 + pw, gh = it.h0 + ph, gd = it.d0 + pd;
-      const bool valid = gw < p.W && gh < p.H && gd < p.D;
-      const int lpix = (gd * p.H + gh) * p.W + gw;        // pixel within the image (32-bit)
+    for (int nt = 0; nt < NT; ++nt) {
+      const int co = it.co0 + wn * (NT * 16) + nt * 16 + 4 * g;
+      BnbC kb;
+      if constexpr (BNB) kb = bnb_load(s_scale, BN, wn * (NT * 16) + nt * 16 + 4 * g);
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const int co = it.co0 + wn * (NT * 16) + nt * 16 + 4 * g;
+      for (int mt = 0; mt < MT; ++mt) {
+        const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
+        const int pw = pix % p.TW, ph = (pix / p.TW) % p.TH;
+        const int pd = DIMS == 3 ? pix / (p.TW * p.TH) : 0;
+        const int gw = it.w0 + pw, gh = it.h0 + ph, gd = it.d0 + pd;
+        const bool valid = gw < p.W && gh < p.H && gd < p.D;
+        const int lpix = (gd * p.H + gh) * p.W + gw;        // pixel within the image (32-bit)
         const bool ok = valid && co < p.Cout;
         if (KS > 1) {            // split-K partial: fp32 [ks][pixel][Cout], finalized later
           unsigned off = ok ? (unsigned)(lpix * p.Cout + co) * 4u : kOOB;
@@ -297,7 +325,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         unsigned off = ok ? (unsigned)(in1 ? lpix * p.Co1 + co : lpix * Co2 + co - p.Co1) * 2u : kOOB;
         asm volatile("" : "+v"(off));
         __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk.x, pk.y}, in1 ? r1 : r2, off, 0, 0);
-        if (ok) {
+        if constexpr (BNB) {
+          bnb_accum(pk, ybuf[mt][nt], ok, kb, s1[nt], s2[nt]);
+        } else if (ok) {
           // statistics of the stored (bf16-rounded) values
           const float r0 = lo_bf(pk.x), q1 = hi_bf(pk.x), q2 = lo_bf(pk.y), q3 = hi_bf(pk.y);
           s1[nt][0] += r0; s2[nt][0] += r0 * r0;
@@ -307,6 +337,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         }
         acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       }
+      if constexpr (BNB) __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -428,6 +459,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         issue_A(k1, (cseq + 1) % nchunks, (cseq + 1) & 1);
         ops += C::A_ITERS;
       }
+      // BNB: the item's last stage loads y for its epilogue (next stage: grp 0, full wait)
+      if (BNB && KS == 1 && rem == spi - 1) issue_Y(k);
       if (NBB == 3) { snap0 = snap1; snap1 = snapn; }
       compute(sA(cseq & 1), sB(s % NBB), DIMS == 3 ? grp / 3 : 0, DIMS == 3 ? grp % 3 : grp);
     }
@@ -478,13 +511,18 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       if (j + 1 < J) issue_Bj(j + 1);
       if (j % 3 == 2) issue_Ac(2 * ((j + 1) / 3));
       else if (j % 3 == 0 && j > 0) issue_Ac(2 * (j / 3) + 1);
+      // BNB: an item's last super-stage loads y for its epilogue (awaited by the next one)
+      if (BNB && KS == 1 && (2 * j + 2) % spi == 0) issue_Y((2 * j + 2) / spi - 1);
       // P is even (nchunks even): both pairs exist; one 6-tap fragment pipeline across them
       const int c0 = (2 * j) / NG, c1 = (2 * j + 1) / NG;
       compute2(sA(c0 & 1), sB(2 * (j & 1)), (2 * j) % NG, sA(c1 & 1), sB(2 * (j & 1) + 1),
                (2 * j + 1) % NG);
     }
   }
-  if (S > 0) epilogue(my_items - 1);
+  if (S > 0) {
+    if (BNB) dma_wait<0>();
+    epilogue(my_items - 1);
+  }
 
   // ---- one BN-statistics partial row per workgroup: shuffle over the 16 pixel lanes,
   // per-wave-row LDS slots summed in a fixed order (bit-reproducible), one row write
@@ -524,7 +562,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 __global__ void conv_splitk_finalize_kernel(const float* __restrict__ part, int KS, long long npix,
                                             int Cout, int Co1, const float* __restrict__ bias,
                                             bf16_t* __restrict__ Y1, bf16_t* __restrict__ Y2,
-                                            float* __restrict__ stats) {
+                                            float* __restrict__ stats, const bf16_t* __restrict__ bnb_y,
+                                            const float* __restrict__ bnb_s4) {
   const int G = Cout / 8;
   const int per = (blockDim.x / G) * G;
   const int tid = threadIdx.x;
@@ -533,6 +572,14 @@ __global__ void conv_splitk_finalize_kernel(const float* __restrict__ part, int 
   float s1[8], s2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  // BN-backward partials (ConvFwdArgs::bnb_y): constants of this thread's 8 channels
+  float bsc[8], bsh[8], bis[8], bnm[8];
+  if (bnb_y != nullptr && tid < per)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bsc[j] = bnb_s4[2 * Cout + c8 + j]; bsh[j] = bnb_s4[3 * Cout + c8 + j];
+      bis[j] = bnb_s4[Cout + c8 + j]; bnm[j] = -bnb_s4[c8 + j] * bis[j];
+    }
   if (tid < per) {
     for (long long px = blockIdx.x * (long long)(per / G) + tid / G; px < npix;
          px += (long long)gridDim.x * (per / G)) {
@@ -551,8 +598,20 @@ __global__ void conv_splitk_finalize_kernel(const float* __restrict__ part, int 
       if (stats != nullptr) {
         float r[8];
         unpack8(pk, r);
+        if (bnb_y != nullptr) {
+          float yy[8];
+          unpack8(*reinterpret_cast<const uint4*>(bnb_y + px * Cout + c8), yy);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { s1[j] += r[j]; s2[j] += r[j] * r[j]; }
+          for (int j = 0; j < 8; ++j) {
+            const float a = fmaf(yy[j], bsc[j], bsh[j]);
+            const float dyh = a > 0.f ? r[j] : 0.f;
+            s1[j] += dyh;
+            s2[j] = fmaf(dyh, fmaf(yy[j], bis[j], bnm[j]), s2[j]);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { s1[j] += r[j]; s2[j] += r[j] * r[j]; }
+        }
       }
     }
   }
@@ -591,11 +650,18 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   static const int diag = [] { const char* e = getenv("DDLPC_DIAG_CONV"); return e ? atoi(e) : 0; }();
   a.diag = diag;
   constexpr bool FDB_OK = !(DIMS == 3 && MT * NT >= 16);
+  if constexpr (DIMS == 2 && NBB != 3) {
+    if (a.bnb_y != nullptr) {
+      hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK, true>), dim3(grid),
+                         dim3(C::NTH), C::SMEM, st, a);
+      return;
+    }
+  }
   if (FDB_OK && conv_fdb())
-    hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK>), dim3(grid),
+    hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK, false>), dim3(grid),
                        dim3(C::NTH), C::SMEM, st, a);
   else
-    hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, false>), dim3(grid),
+    hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, false, false>), dim3(grid),
                        dim3(C::NTH), C::SMEM, st, a);
 }
 
@@ -635,7 +701,7 @@ int conv3_fwd_cfg_halo(int dims, int cfg) {
 
 void conv3_splitk_finalize_launch(ConvFwdArgs& a, int grid, hipStream_t st) {
   hipLaunchKernelGGL(conv_splitk_finalize_kernel, dim3(grid), dim3(256), 0, st, a.part, a.ksplit,
-                     a.npix, a.Cout, a.Co1, a.bias, a.Y1, a.Y2, a.stats);
+                     a.npix, a.Cout, a.Co1, a.bias, a.Y1, a.Y2, a.stats, a.bnb_y, a.bnb_s4);
 }
 
 void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st) {
@@ -647,7 +713,7 @@ void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st) {
       case 4: {  // one workgroup per CU: room for 3 weight-stage buffers or 2 super-stages
         const int nch = (a.Cin + 31) / 32 / a.ksplit;
         if (conv_super() && nch % 2 == 0) launch_cfg<2, 4, 2, 4, 4, 384, 4>(a, st);
-        else if (conv_nbb() == 3) launch_cfg<2, 4, 2, 4, 4, 384, 3>(a, st);
+        else if (conv_nbb() == 3 && a.bnb_y == nullptr) launch_cfg<2, 4, 2, 4, 4, 384, 3>(a, st);
         else launch_cfg<2, 4, 2, 4, 4, 384, 2>(a, st);
         break;
       }

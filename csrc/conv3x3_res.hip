@@ -53,16 +53,18 @@ DDLPC_HOST_DEVICE int res_w_bytes(int Cin, int BN, bool tap8) {
   return tap8 ? 3 * BN * ROWB : ((Cin + BK - 1) / BK) * 9 * BN * ROWB;
 }
 
-template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF, bool SPLIT>
+template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF, bool SPLIT, bool BNB>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_kernel(ConvFwdArgs p) {
   using C = RCfg<WM, WN, MT, NT, HALO, TAP8, NBUF>;
   static_assert(NBUF == 2 || NBUF == 3, "halo ring depth");
+  static_assert(!BNB || (!SPLIT && !TAP8), "BN-backward epilogue: single output, no image layer");
   constexpr int NW = C::NW, BN = C::BN;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bool has_pro = p.pscale != nullptr;
   const bool has_pro2 = p.pscale2 != nullptr;          // deferred skip: X2 channels at C1 + c
   const int NSS = has_pro2 ? p.Cin : p.C1;             // channels with prologue constants
-  const int ss_bytes = res_ss_bytes(NSS, has_pro || has_pro2);
+  // BNB (a data gradient: no prologue): the LDS table of the BN-backward constants instead
+  const int ss_bytes = BNB ? 16 * BN : res_ss_bytes(NSS, has_pro || has_pro2);
   float* s_scale = reinterpret_cast<float*>(smem);
   float* s_shift = s_scale + NSS;
   char* sW = smem + ss_bytes;
@@ -88,6 +90,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     for (int c = tid; c < p.C1; c += C::NTH) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
   if (has_pro2)
     for (int c = tid; c < p.C2; c += C::NTH) { s_scale[p.C1 + c] = p.pscale2[c]; s_shift[p.C1 + c] = p.pshift2[c]; }
+  float* s_bnb = reinterpret_cast<float*>(smem);       // BNB: [4][BN] (published by the first barrier)
+  if constexpr (BNB) bnb_fill(s_bnb, BN, co0, p.Cout, p.bnb_s4, tid, C::NTH);
 
   // bias of this block's channel tile, loaded once (a global load inside the epilogue would
   // make the compiler wait vmcnt(0) — on this tile's stores — before every use); loaded
@@ -269,20 +273,44 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   // issues exactly EPI_STORES of them per epilogue (no exec branches), which keeps the
   // counted vmcnt waits exact.
   constexpr int EPI_STORES = MT * NT * (SPLIT ? 2 : 1);
-  auto epilogue = [&](int k) {
-    const Item it = item_of(k);
-    const int Co2 = p.Cout - p.Co1;
-    const auto r1 = make_rsrc(p.Y1 + (long long)it.n_img * img_px * p.Co1, (unsigned)(img_px * p.Co1 * 2));
-    const auto r2 = SPLIT ? make_rsrc(p.Y2 + (long long)it.n_img * img_px * Co2, (unsigned)(img_px * Co2 * 2)) : r1;
+  // BNB: y at this item's output pixels, loaded into VGPRs at the item's last stage (before
+  // that stage's halo DMA) and consumed by its epilogue one stage later
+  constexpr int YL = BNB ? MT * NT : 0;
+  uint2 ybuf[MT][NT];
+  auto issue_Y = [&](int kk) __attribute__((always_inline)) {
+    const Item it = item_of(kk);
+    const auto ry = make_rsrc(p.bnb_y + (long long)it.n_img * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
       const int gw = it.w0 + pix % p.TW, gh = it.h0 + pix / p.TW;
       const bool valid = gw < p.W && gh < p.H;
-      const int lp = gh * p.W + gw;                     // pixel within the image (32-bit)
+      const int lp = gh * p.W + gw;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * g;
+        ybuf[mt][nt] = buf_load8(ry, valid && co < p.Cout ? (unsigned)(lp * p.Cout + co) * 2u : kOOB);
+      }
+    }
+  };
+  auto epilogue = [&](int k) {
+    const Item it = item_of(k);
+    const int Co2 = p.Cout - p.Co1;
+    const auto r1 = make_rsrc(p.Y1 + (long long)it.n_img * img_px * p.Co1, (unsigned)(img_px * p.Co1 * 2));
+    const auto r2 = SPLIT ? make_rsrc(p.Y2 + (long long)it.n_img * img_px * Co2, (unsigned)(img_px * Co2 * 2)) : r1;
+    // channel tiles outer: the BNB constants of one tile are read once (and the scheduler
+    // barrier below keeps the next tile's reads from being hoisted: VGPR pressure)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * g;
+      BnbC kb;
+      if constexpr (BNB) kb = bnb_load(s_bnb, BN, wn * (NT * 16) + nt * 16 + 4 * g);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
+        const int gw = it.w0 + pix % p.TW, gh = it.h0 + pix / p.TW;
+        const bool valid = gw < p.W && gh < p.H;
+        const int lp = gh * p.W + gw;                     // pixel within the image (32-bit)
         float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bias_r[nt][i];
@@ -303,22 +331,28 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
           __builtin_amdgcn_raw_buffer_store_b64(d, r1, o1, 0, 0);
           __builtin_amdgcn_raw_buffer_store_b64(d, r2, o2, 0, 0);
         }
-        // statistics of the stored (bf16-rounded) values; masked lanes add zeros
-        const float r0 = ok ? lo_bf(pk.x) : 0.f, q1 = ok ? hi_bf(pk.x) : 0.f;
-        const float q2 = ok ? lo_bf(pk.y) : 0.f, q3 = ok ? hi_bf(pk.y) : 0.f;
-        s1[nt][0] += r0; s2[nt][0] += r0 * r0;
-        s1[nt][1] += q1; s2[nt][1] += q1 * q1;
-        s1[nt][2] += q2; s2[nt][2] += q2 * q2;
-        s1[nt][3] += q3; s2[nt][3] += q3 * q3;
+        if constexpr (BNB) {
+          bnb_accum(pk, ybuf[mt][nt], ok, kb, s1[nt], s2[nt]);
+        } else {
+          // statistics of the stored (bf16-rounded) values; masked lanes add zeros
+          const float r0 = ok ? lo_bf(pk.x) : 0.f, q1 = ok ? hi_bf(pk.x) : 0.f;
+          const float q2 = ok ? lo_bf(pk.y) : 0.f, q3 = ok ? hi_bf(pk.y) : 0.f;
+          s1[nt][0] += r0; s2[nt][0] += r0 * r0;
+          s1[nt][1] += q1; s2[nt][1] += q1 * q1;
+          s1[nt][2] += q2; s2[nt][2] += q2 * q2;
+          s1[nt][3] += q3; s2[nt][3] += q3 * q3;
+        }
         acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       }
+      if constexpr (BNB) __builtin_amdgcn_sched_barrier(0);
     }
   };
 
   // ---- pipeline: the halo of stage s+NBUF-1 is issued at stage s (ring of NBUF buffers).
-  // Per stage a wave issues: [epilogue stores of the previous item] then [A_ITERS DMAs],
-  // so at stage s the ops younger than DMA(s) are exactly those of stage s-1 (NBUF = 3)
-  // or none (NBUF = 2) plus the prologue's extra DMA at s = 0.
+  // Per stage a wave issues: [epilogue stores of the previous item] [BNB: y loads, at an
+  // item's last stage] then [A_ITERS DMAs], so at stage s the ops younger than DMA(s) are
+  // exactly those of stage s-1 (NBUF = 3) or none (NBUF = 2) plus the prologue's extra DMA
+  // at s = 0.
   auto next_of = [&](int k0, int c0, int& k1, int& c1) {
     k1 = k0; c1 = c0 + 1;
     if (c1 == nch) { c1 = 0; ++k1; }
@@ -338,7 +372,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     } else {
       // younger than DMA(s): s == 0 -> DMA(1); s >= 1 -> [stores(s-1)] + [DMA(s+1)]
       const bool dma_next = s + 1 < S;
-      if (s == 0) {
+      if (BNB && s > 0) {
+        // stage s-1 issued [stores if it ran an epilogue] [y loads if it was an item's last]
+        // [DMA(s+1)]
+        vm_wait_dyn((epi_prev ? EPI_STORES : 0) + (c == 0 ? YL : 0) + (dma_next ? C::A_ITERS : 0));
+      } else if (s == 0) {
         if (dma_next) vm_wait<C::A_ITERS>(); else vm_wait<0>();
       } else if (epi_prev) {
         if (dma_next) vm_wait<C::A_ITERS + EPI_STORES>(); else vm_wait<EPI_STORES>();
@@ -350,7 +388,12 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     if (!TAP8 && (has_pro || has_pro2)) transform_A(c, buf);
     lds_sync();
     epi_prev = (c == 0 && s > 0);
-    if (epi_prev) epilogue(k - 1);
+    if (epi_prev) {
+      // BNB, 3-deep ring: the y loads (issued before DMA(s+1)) must have landed
+      if (BNB && NBUF == 3) { if (s + 1 < S) vm_wait<C::A_ITERS>(); else vm_wait<0>(); }
+      epilogue(k - 1);
+    }
+    if (BNB && c == nch - 1) issue_Y(k);              // before this stage's DMA
     if (s + NBUF - 1 < S) {
       issue_A(kp, cp, (s + NBUF - 1) % NBUF);
       int k1, c1;
@@ -394,7 +437,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     compute(sA(buf), TAP8 ? sW : sW + c * 9 * BN * ROWB);
     k = k1; c = c1;
   }
-  if (S > 0) epilogue(k - 1);
+  if (S > 0) {
+    if (BNB) vm_wait<0>();
+    epilogue(k - 1);
+  }
 
   // ---- one BN-statistics partial row per workgroup (layout of conv3_fwd_kernel)
   if (p.stats != nullptr) {
@@ -442,22 +488,30 @@ constexpr ResVariant kRes[8] = {
     //    96 output channels, so the dY halo is read once instead of once per 32-channel tile.
     {8, 1, 2, 6, 324, false, 16, 16, 3}};
 
-int res_smem(const ResVariant& v, int Cin, int C1, bool pro) {   // C1: channels with constants
+int res_smem(const ResVariant& v, int Cin, int C1, bool pro, bool bnb) {   // C1: channels with constants
   const int bn = v.wn * v.nt * 16;
   const int nw = v.wm * v.wn;
   const int instr = ((v.tap8 ? v.halo : v.halo * 4) + 63) / 64;
   const int a_bytes = (instr + nw - 1) / nw * nw * 1024;
-  return res_ss_bytes(C1, pro) + res_w_bytes(Cin, bn, v.tap8) + v.nbuf * a_bytes;
+  return (bnb ? 16 * bn : res_ss_bytes(C1, pro)) + res_w_bytes(Cin, bn, v.tap8) + v.nbuf * a_bytes;
 }
 
 template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF>
 void launch_res(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
   if (a.Co1 < a.Cout)
-    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, true>), dim3(grid),
+    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, true, false>), dim3(grid),
                        dim3(WM * WN * 64), smem, st, a);
-  else
-    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, false>), dim3(grid),
+  else if constexpr (!TAP8 && WN * NT * 16 != 96) {
+    if (a.bnb_y != nullptr)
+      hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, false, true>), dim3(grid),
+                         dim3(WM * WN * 64), smem, st, a);
+    else
+      hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, false, false>), dim3(grid),
+                         dim3(WM * WN * 64), smem, st, a);
+  } else {
+    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, false, false>), dim3(grid),
                        dim3(WM * WN * 64), smem, st, a);
+  }
 }
 
 }  // namespace
@@ -476,9 +530,10 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
   int cand[3];
   int nc = 0;
   if (tap8) {
-    if (bn != 32) return -1;
+    if (bn != 32 || a.bnb_y != nullptr) return -1;
     if (depth == 2) { cand[nc++] = 3; } else { cand[nc++] = 4; cand[nc++] = 3; }
   } else if (bn == 96) {
+    if (a.bnb_y != nullptr) return -1;                 // no BN-backward epilogue at BN 96
     cand[nc++] = 7;
   } else if (bn == 32) {
     if (depth == 2) { cand[nc++] = 0; cand[nc++] = 5; }
@@ -488,7 +543,8 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
   }
   for (int i = 0; i < nc; ++i) {
     const ResVariant& v = kRes[cand[i]];
-    const int sm = res_smem(v, a.Cin, a.pscale2 != nullptr ? a.Cin : a.C1, pro || a.pscale2 != nullptr);
+    const int sm = res_smem(v, a.Cin, a.pscale2 != nullptr ? a.Cin : a.C1, pro || a.pscale2 != nullptr,
+                            a.bnb_y != nullptr);
     const int nw = v.wm * v.wn;
     // 4-wave blocks need 2 per CU (2 waves / SIMD); 8-wave blocks use ~200 VGPRs: 1 per CU
     const int bpc = nw == 4 ? (sm <= 80 * 1024 ? 2 : 0) : (sm <= 160 * 1024 ? 1 : 0);

@@ -55,5 +55,56 @@ DDLPC_DEVICE void dma16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, unsigned 
 
 DDLPC_DEVICE uint4 lds128(const char* p) { return *reinterpret_cast<const uint4*>(p); }
 
+// 8-byte buffer load into VGPRs, issued unconditionally (masked lanes pass kOOB and read
+// zeros): the per-wave load count stays fixed for the counted vmcnt waits
+DDLPC_DEVICE uint2 buf_load8(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  asm volatile("" : "+v"(off));
+  const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  return make_uint2(v.x, v.y);
+}
+
+// ---- BN-backward epilogue (ConvFwdArgs::bnb_y): LDS table [4][nb] of (scale, shift,
+// invstd, -mean*invstd) for the channels [co0, co0 + nb) of a workgroup's n tile
+DDLPC_DEVICE void bnb_fill(float* tab, int nb, int co0, int Cout, const float* s4, int tid, int nth) {
+  for (int i = tid; i < nb; i += nth) {
+    const int c = co0 + i;
+    const bool ok = c < Cout;
+    const float is = ok ? s4[Cout + c] : 0.f;
+    tab[i] = ok ? s4[2 * Cout + c] : 0.f;
+    tab[nb + i] = ok ? s4[3 * Cout + c] : 0.f;
+    tab[2 * nb + i] = is;
+    tab[3 * nb + i] = ok ? -s4[c] * is : 0.f;
+  }
+}
+// the constants of 4 consecutive channels (table column col)
+struct BnbC { float4 sc, sh, is, nm; };
+// (restrict: alias scopes, so the compiler does not drain in-flight LDS-DMA before the reads)
+DDLPC_DEVICE BnbC bnb_load(const float* __restrict__ tab, int nb, int col) {
+  tab += opaque_zero();              // re-read per use, not hoisted into live VGPRs
+  BnbC k;
+  k.sc = *reinterpret_cast<const float4*>(tab + col);
+  k.sh = *reinterpret_cast<const float4*>(tab + nb + col);
+  k.is = *reinterpret_cast<const float4*>(tab + 2 * nb + col);
+  k.nm = *reinterpret_cast<const float4*>(tab + 3 * nb + col);
+  return k;
+}
+// (sum dyh, sum dyh*xhat) of those 4 channels of one pixel: pk = the stored bf16 dA, yv = y;
+// the arithmetic of bn_bwd2_kernel's reduction pass
+DDLPC_DEVICE void bnb_accum(uint2 pk, uint2 yv, bool ok, const BnbC& k, float (&s1)[4], float (&s2)[4]) {
+  const float d[4] = {ok ? lo_bf(pk.x) : 0.f, ok ? hi_bf(pk.x) : 0.f, ok ? lo_bf(pk.y) : 0.f,
+                      ok ? hi_bf(pk.y) : 0.f};
+  const float y[4] = {lo_bf(yv.x), hi_bf(yv.x), lo_bf(yv.y), hi_bf(yv.y)};
+  const float scf[4] = {k.sc.x, k.sc.y, k.sc.z, k.sc.w}, shf[4] = {k.sh.x, k.sh.y, k.sh.z, k.sh.w};
+  const float isf[4] = {k.is.x, k.is.y, k.is.z, k.is.w}, nmf[4] = {k.nm.x, k.nm.y, k.nm.z, k.nm.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = fmaf(y[i], scf[i], shf[i]);
+    const float dyh = a > 0.f ? d[i] : 0.f;
+    const float xh = fmaf(y[i], isf[i], nmf[i]);
+    s1[i] += dyh;
+    s2[i] = fmaf(dyh, xh, s2[i]);
+  }
+}
+
 }  // namespace convlds
 }  // namespace ddlpc

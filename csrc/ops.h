@@ -38,6 +38,12 @@ struct ConvFwdArgs {
   float* part;                    // [ksplit][npix][Cout] fp32 (ksplit > 1)
   long long npix;                 // N * D * H * W
   int diag;                       // diagnostics only (DDLPC_DIAG_CONV): bit 0 skip weight DMA after stage 1, bit 1 skip halo DMA after chunk 1
+  // BN-backward epilogue (data gradient dA of a conv whose input went through BN + ReLU):
+  // `stats` rows then hold (sum dyh, sum dyh * xhat) with dyh = [y*scale + shift > 0] * dA,
+  // xhat = (y - mean) * invstd — the reduction pass of that BN's backward, fused.  2-D,
+  // single output, no prologue.
+  const bf16_t* bnb_y;            // y [N][H][W][Cout] (pre-BN activations of that layer)
+  const float* bnb_s4;            // [4][Cout]: mean, invstd, scale, shift
 };
 void conv3_splitk_finalize_launch(ConvFwdArgs& a, int grid, hipStream_t st);
 void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st);

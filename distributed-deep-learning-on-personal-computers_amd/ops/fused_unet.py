@@ -216,12 +216,19 @@ class _DoubleConvFn(torch.autograd.Function):
             dy2, dg2, dbe2 = F.bn_backward(da2, dpool, y2, s2, g2, None, None, None, part2)
             dw2 = F.conv3_wgrad(dy2, y1, None, s1[2], s1[3]).view_as(blk.conv2.weight)
         p1, p2 = blk.pack1, blk.pack2
-        da1, _, _ = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False)
+        part1 = None
+        if eng.bnb_epilogue and y1.dim() == 4:
+            # the epilogue also reduces BN1 backward's (sum dyh, sum dyh*xhat) against y1
+            da1, _, part1 = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False,
+                                        None, None, y1, s1)
+        else:
+            da1, _, _ = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False)
         # ---- first conv
         w1 = blk.conv1.weight
         padded_in = x2 is None and x1.shape[-1] != w1.shape[1]   # first layer: 3 -> 8 ch
         if direct:
-            dy1, _, _ = F.bn_backward(da1, None, y1, s1, g1, None, bn1.weight.grad, bn1.bias.grad)
+            dy1, _, _ = F.bn_backward(da1, None, y1, s1, g1, None, bn1.weight.grad, bn1.bias.grad,
+                                      part1)
             with eng.wgrad_stream(dy1, x1, x2, x2_bn):
                 if padded_in:
                     w1.grad.add_(F.conv3_wgrad(dy1, x1, None, None, None)[:, :w1.shape[1]])
@@ -230,7 +237,7 @@ class _DoubleConvFn(torch.autograd.Function):
                 eng.ready(bn1.weight, bn1.bias, w1, blk.conv1.bias)
             dg1 = dbe1 = dw1 = None
         else:
-            dy1, dg1, dbe1 = F.bn_backward(da1, None, y1, s1, g1, None)
+            dy1, dg1, dbe1 = F.bn_backward(da1, None, y1, s1, g1, None, None, None, part1)
             dw1 = F.conv3_wgrad(dy1, x1, x2, None, None, None, sc2, sh2)
             dw1 = (dw1[:, :w1.shape[1]] if padded_in else dw1).reshape(w1.shape)
         dx1 = dx2 = None
@@ -446,6 +453,9 @@ class UNetEngine:
         # encoder skips handed out pre-BN (see ``defer_skip_levels``): saves ~1 GB at
         # 256^2 x 128 but measured ~1.2% slower end to end (docs/PERF.md), so opt-in
         self.defer_skip = os.environ.get("DDLPC_DEFER_SKIP", "0") != "0"
+        # BN1 backward's reduction pass fused into the epilogue of the data gradient that
+        # produces its input gradient (2-D; DDLPC_BNB_EPI=0: separate reduction kernel)
+        self.bnb_epilogue = os.environ.get("DDLPC_BNB_EPI", "1") != "0"
         self.enc = [_Block(b.double_conv, first=(i == 0), engine=self)
                     for i, b in enumerate(model.down_blocks())]
         self.mid = _Block(model.double_conv, first=False, engine=self)

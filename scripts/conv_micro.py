@@ -40,7 +40,8 @@ def main():
     from ddlpc.ops.fused_unet import _ConvPack
     F = _ext.ops()
     dev = "cuda"
-    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+    fns_ref_us = {}
+    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "dgradbn": 0.0}
     for name, H, C1, C2, Co, pro in LAYERS:
         if a.only and a.only not in name:
             continue
@@ -62,11 +63,18 @@ def main():
             "dgrad": lambda: F.conv3_fwd(dy, None, pk.dgrad, None, None, None, C1 + C2,
                                          C1 if C2 else 0, False),
             "wgrad": lambda: F.conv3_wgrad(dy, x1, x2, sc, sh),
+            # data gradient with the BN-backward reduction against y fused into its epilogue
+            "dgradbn": lambda: F.conv3_fwd(dy, None, pk.dgrad, None, None, None, C1, 0, False,
+                                           None, None, x1, bn4),
         }
+        bn4 = torch.stack([torch.randn(C1, device=dev) * 0.1, torch.rand(C1, device=dev) + 0.5,
+                           torch.rand(C1, device=dev) + 0.5, torch.randn(C1, device=dev) * 0.1]).contiguous()
         for ps in a.passes.split(","):
             if ps.startswith("t"):
                 continue
-            if ps == "dgrad" and name == "enc1.a":
+            if ps.startswith("dgrad") and name == "enc1.a":
+                continue
+            if ps == "dgradbn" and (C2 or a.dims != 2):
                 continue
             fn = fns[ps]
             fn()
@@ -79,6 +87,10 @@ def main():
             e1.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / a.iters
             tot[ps] += us
+            if ps == "dgradbn":
+                tot["dgrad_b_layers"] = tot.get("dgrad_b_layers", 0.0) + fns_ref_us.get(name, 0.0)
+            if ps == "dgrad":
+                fns_ref_us[name] = us
             print(f"{name:8s} {ps:6s} {us:9.1f} us  {flops / us / 1e6:8.1f} TF/s", flush=True)
     # transposed-conv up-sampling (2x2 stride 2), channels preserved: (name, Hin, C)
     UPS = [("up5", 8, 256), ("up4", 16, 256), ("up3", 32, 256), ("up2", 64, 128), ("up1", 128, 64)]

@@ -133,6 +133,44 @@ def test_conv3_dgrad_resident(ops, C1, C2, Cout):
         assert rel_err(nchw(dx2), ref[:, C1:]) < 1e-2
 
 
+# BN-backward reduction fused into the data-gradient epilogue (ConvFwdArgs::bnb_y): shapes
+# covering the resident kernel (BN 32 / 64, ragged edges), the streaming kernel (cfg 0/1,
+# cfg 4 super-stages and its 2-deep path for an odd chunk count) and the split-K finalize
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [
+    (2, 256, 256, 32, 32), (2, 256, 256, 64, 64), (3, 200, 232, 32, 32),
+    (16, 64, 64, 128, 128), (16, 64, 64, 128, 96), (2, 16, 16, 32, 32), (2, 32, 32, 64, 64),
+    (1, 16, 16, 128, 128), (2, 8, 8, 256, 256)])
+def test_conv3_dgrad_bn_backward_epilogue(ops, N, H, W, Cin, Cout):
+    torch.manual_seed(11)
+    w = torch.randn(Cout, Cin, 3, 3, device=DEV) / math.sqrt(9 * Cin)
+    dy = torch.randn(N, Cout, H, W, device=DEV).bfloat16()
+    y = torch.randn(N, Cin, H, W, device=DEV).bfloat16()
+    mean = torch.randn(Cin, device=DEV) * 0.2
+    invstd = torch.rand(Cin, device=DEV) + 0.5
+    gamma = torch.rand(Cin, device=DEV) + 0.5
+    beta = torch.randn(Cin, device=DEV) * 0.3
+    scale = gamma * invstd
+    s4 = torch.stack([mean, invstd, scale, beta - mean * scale]).contiguous()
+    pk = pack_conv(ops, w)
+    da0, _, _ = ops.conv3_fwd(nhwc(dy), None, pk.dgrad, None, None, None, Cin, 0, False)
+    da, _, part = ops.conv3_fwd(nhwc(dy), None, pk.dgrad, None, None, None, Cin, 0, False,
+                                None, None, nhwc(y), s4)
+    assert torch.equal(da, da0)                       # the epilogue only adds the partials
+    p = part.double().sum(0)
+    yf, df = nchw(nhwc(y)).double(), nchw(da).double()
+    a = yf * scale.double()[None, :, None, None] + s4[3].double()[None, :, None, None]
+    dyh = torch.where(a > 0, df, torch.zeros_like(df))
+    xh = (yf - mean.double()[None, :, None, None]) * invstd.double()[None, :, None, None]
+    ref1, ref2 = dyh.sum((0, 2, 3)), (dyh * xh).sum((0, 2, 3))
+    assert torch.allclose(p[0], ref1, rtol=1e-4, atol=1e-2 * math.sqrt(N * H * W))
+    assert torch.allclose(p[1], ref2, rtol=1e-4, atol=1e-2 * math.sqrt(N * H * W))
+    # the BN backward from those partials == the one with its own reduction pass
+    dY0, dg0, db0 = ops.bn_backward(da, None, nhwc(y), s4, gamma, None)
+    dY1, dg1, db1 = ops.bn_backward(da, None, nhwc(y), s4, gamma, None, None, None, part)
+    assert rel_err(dY1, dY0) < 2e-3
+    assert rel_err(dg1, dg0) < 1e-4 and rel_err(db1, db0) < 1e-4
+
+
 @pytest.mark.parametrize("C1,C2,Cout", [(64, 32, 32), (0, 64, 32), (256, 256, 256)])
 def test_conv3_dgrad_split(ops, C1, C2, Cout):
     torch.manual_seed(2)
