@@ -65,12 +65,13 @@ struct Cfg {
 // operand the pixel tile, so each lane's accumulator holds 4 CONSECUTIVE channels of one
 // pixel -> 8-byte bf16x4 stores; BN statistics are reduced with 4 lane shuffles and
 // written as one partial row per (m tile, wave row).
-template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, bool FDB, bool BNB>
+template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, bool FDB, bool BNB, bool ILV>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_kernel(ConvFwdArgs p) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
   static_assert(NBB == 2 || NBB == 3 || (NBB == 4 && DIMS == 2), "2 / 3 weight-stage buffers, or 4 (super-stages)");
   // BN-backward epilogue: 2-D, and not with the counted waits of the 3-deep weight ring
   static_assert(!BNB || (DIMS == 2 && NBB != 3), "BNB: 2-D, NBB 2 or 4");
+  static_assert(!ILV || NBB == 4, "DMA issue interleaved with the MFMAs: super-stages only");
   constexpr bool FRAG_DB = FDB;
   constexpr int BM = C::BM, BN = C::BN;
   constexpr int NG = DIMS == 2 ? 3 : 9;           // (kd, r) kernel rows per chunk
@@ -263,7 +264,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   // (wm*MT*16 + mt*16 + (lane&15)) of the tile
   // Stores are buffer stores with an out-of-range offset for masked lanes: every wave issues
   // exactly EPI_STORES per epilogue (no exec branches), so counted vmcnt waits stay exact.
-  constexpr int EPI_STORES = MT * NT;
+  // stores per epilogue: single bf16 output -> 16-byte stores of channel-tile pairs (pair16);
+  // split output / split-K fp32 partials -> one store per tile
+  static_assert(NT % 2 == 0, "channel tiles come in pairs");
+  const bool pairs = KS == 1 && p.Y2 == nullptr;
+  const int EPI_STORES = pairs ? MT * NT / 2 : MT * NT;
   // BNB: y at an item's output pixels, loaded into VGPRs at the item's last stage (after that
   // stage's DMA) and consumed by its epilogue after the next stage's full wait
   uint2 ybuf[MT][NT];
@@ -291,8 +296,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
                            : make_rsrc(p.Y1 + it.n_img * img_px * p.Co1, (unsigned)(img_px * p.Co1 * 2));
     const auto r2 = make_rsrc(p.Y2 != nullptr ? p.Y2 + it.n_img * img_px * Co2 : p.Y1,
                               p.Y2 != nullptr ? (unsigned)(img_px * Co2 * 2) : 0u);
-    // channel tiles outer: the BNB constants of one tile are read once (the scheduler
+    // pass 1, channel tiles outer: the BNB constants of one tile are read once (the scheduler
     // barrier below keeps the next tile's reads from being hoisted: VGPR pressure)
+    uint2 pkv[MT][NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int co = it.co0 + wn * (NT * 16) + nt * 16 + 4 * g;
@@ -320,11 +326,14 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bias_r[nt][i];
         const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        // the 16-channel tile lies in one output (Co1 % 16 == 0): wave-uniform descriptor
-        const bool in1 = it.co0 + wn * (NT * 16) + nt * 16 < p.Co1 || p.Y2 == nullptr;
-        unsigned off = ok ? (unsigned)(in1 ? lpix * p.Co1 + co : lpix * Co2 + co - p.Co1) * 2u : kOOB;
-        asm volatile("" : "+v"(off));
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk.x, pk.y}, in1 ? r1 : r2, off, 0, 0);
+        pkv[mt][nt] = pk;
+        if (!pairs) {
+          // the 16-channel tile lies in one output (Co1 % 16 == 0): wave-uniform descriptor
+          const bool in1 = it.co0 + wn * (NT * 16) + nt * 16 < p.Co1 || p.Y2 == nullptr;
+          unsigned off = ok ? (unsigned)(in1 ? lpix * p.Co1 + co : lpix * Co2 + co - p.Co1) * 2u : kOOB;
+          asm volatile("" : "+v"(off));
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk.x, pk.y}, in1 ? r1 : r2, off, 0, 0);
+        }
         if constexpr (BNB) {
           bnb_accum(pk, ybuf[mt][nt], ok, kb, s1[nt], s2[nt]);
         } else if (ok) {
@@ -338,6 +347,25 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       }
       if constexpr (BNB) __builtin_amdgcn_sched_barrier(0);
+    }
+    if (!pairs) return;
+    // pass 2: 16-byte stores of channel-tile pairs
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
+      const int pw = pix % p.TW, ph = (pix / p.TW) % p.TH;
+      const int pd = DIMS == 3 ? pix / (p.TW * p.TH) : 0;
+      const int gw = it.w0 + pw, gh = it.h0 + ph, gd = it.d0 + pd;
+      const bool valid = gw < p.W && gh < p.H && gd < p.D;
+      const int lpix = (gd * p.H + gh) * p.W + gw;
+#pragma unroll
+      for (int np = 0; np < NT / 2; ++np) {
+        const uint4 q = pair16(pkv[mt][2 * np], pkv[mt][2 * np + 1]);
+        const int co = it.co0 + wn * (NT * 16) + np * 32 + pair16_ch(lane);
+        unsigned off = valid && co < p.Cout ? (unsigned)(lpix * p.Cout + co) * 2u : kOOB;
+        asm volatile("" : "+v"(off));
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, r1, off, 0, 0);
+      }
     }
   };
 
@@ -372,7 +400,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   // super-stage body: taps of row r0 (halo A0, weights B0) then row r1 (A1, B1), fragments
   // of tap t+1 read while tap t's MFMAs run, across the row boundary too
   auto compute2 = [&](const char* __restrict__ A0, const char* __restrict__ B0, int r0,
-                      const char* __restrict__ A1, const char* __restrict__ B1, int r1)
+                      const char* __restrict__ A1, const char* __restrict__ B1, int r1, auto&& hook)
       __attribute__((always_inline)) {
     auto load_frags = [&](int tt, uint4 (&xf)[MT], uint4 (&wf)[NT]) __attribute__((always_inline)) {
       const int t = tt % 3;
@@ -394,6 +422,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[tt & 1][nt], xf[tt & 1][mt], acc[mt][nt]);
+      hook(tt);                                   // ILV: this tap's share of the next DMAs
       if (FRAG_DB) __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -508,15 +537,70 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       lds_sync();
       const int k0 = (2 * j) / spi;
       if ((2 * j) % spi == 0 && j > 0) epilogue(k0 - 1);
-      if (j + 1 < J) issue_Bj(j + 1);
-      if (j % 3 == 2) issue_Ac(2 * ((j + 1) / 3));
-      else if (j % 3 == 0 && j > 0) issue_Ac(2 * (j / 3) + 1);
+      // chunk whose halo is issued at this super-stage (-1: none)
+      const int cA = j % 3 == 2 ? 2 * ((j + 1) / 3) : (j % 3 == 0 && j > 0) ? 2 * (j / 3) + 1 : -1;
+      if constexpr (!ILV) {
+        if (j + 1 < J) issue_Bj(j + 1);
+        if (cA >= 0) issue_Ac(cA);
+      }
       // BNB: an item's last super-stage loads y for its epilogue (awaited by the next one)
       if (BNB && KS == 1 && (2 * j + 2) % spi == 0) issue_Y((2 * j + 2) / spi - 1);
       // P is even (nchunks even): both pairs exist; one 6-tap fragment pipeline across them
       const int c0 = (2 * j) / NG, c1 = (2 * j + 1) / NG;
-      compute2(sA(c0 & 1), sB(2 * (j & 1)), (2 * j) % NG, sA(c1 & 1), sB(2 * (j & 1) + 1),
-               (2 * j + 1) % NG);
+      if constexpr (ILV) {
+        // ILV: the next super-stage's DMAs (2 x B_ITERS weight pieces, A_ITERS halo pieces)
+        // issued between the taps' MFMAs instead of in one burst before them: every wave of
+        // the workgroup left the barrier together, so a burst stalls both waves of a SIMD
+        // in their issue at once (an LDS-DMA instruction costs ~60-185 issue cycles)
+        bool hB[2];
+        int sB_off[2], chB[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int pp = 2 * (j + 1) + h;
+          hB[h] = j + 1 < J && pp < P;
+          const int cs = hB[h] ? pp / NG : 0;
+          chB[h] = chunk0_of(cs / nchunks) + cs % nchunks;
+          sB_off[h] = ((pp % NG) * 3 * p.CinW + chB[h] * BK) * 2;
+        }
+        const bool doA = cA >= 0 && cA < total_chunks;
+        int c0A = 0, CsA = p.C1;
+        __amdgpu_buffer_rsrc_t rA = rW;
+        if (doA) {
+          const int kA = cA / nchunks;
+          if (kA != a_item) set_item_pixels(kA);
+          const int cbase = (chunk0_of(kA) + cA % nchunks) * BK;
+          const bool second = cbase >= p.C1;
+          CsA = second ? p.C2 : p.C1;
+          c0A = second ? cbase - p.C1 : cbase;
+          rA = make_rsrc((second ? p.X2 : p.X1) + a_nimg * img_px * CsA, (unsigned)(img_px * CsA * 2));
+        }
+        auto hook = [&](int tt) __attribute__((always_inline)) {
+#pragma unroll
+          for (int q = 0; q < 2 * C::B_ITERS; ++q) {
+            if (q * 6 / (2 * C::B_ITERS) != tt) continue;
+            const int h = q / C::B_ITERS, i = q % C::B_ITERS;
+            if (hB[h]) {
+              const bool ok = b_off[i] >= 0 && chB[h] * BK + b_sub8[i] < p.CinW;
+              dma16(rW, sB(2 * ((j + 1) & 1) + h) + (i * C::NW + wave) * 1024,
+                    ok ? (unsigned)(b_off[i] + sB_off[h]) : kOOB);
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < C::A_ITERS; ++i) {
+            if (i * 6 / C::A_ITERS != tt) continue;
+            if (doA) {
+              const int c8 = c0A + a_sub8[i];
+              const unsigned off = (a_pix[i] >= 0 && c8 < CsA) ? (unsigned)(a_pix[i] * CsA + c8) * 2u : kOOB;
+              dma16(rA, sA(cA & 1) + (i * C::NW + wave) * 1024, off);
+            }
+          }
+        };
+        compute2(sA(c0 & 1), sB(2 * (j & 1)), (2 * j) % NG, sA(c1 & 1), sB(2 * (j & 1) + 1),
+                 (2 * j + 1) % NG, hook);
+      } else {
+        compute2(sA(c0 & 1), sB(2 * (j & 1)), (2 * j) % NG, sA(c1 & 1), sB(2 * (j & 1) + 1),
+                 (2 * j + 1) % NG, [](int) {});
+      }
     }
   }
   if (S > 0) {
@@ -637,6 +721,13 @@ bool conv_fdb() {
   return v != 0;
 }
 
+// super-stages: next-stage DMAs interleaved with the MFMAs (DDLPC_CONV_ILV=1).  Measured at
+// batch 128 (conv_micro, same box): 1-2% slower per layer than one burst, so off
+bool conv_ilv() {
+  static const int v = [] { const char* e = getenv("DDLPC_CONV_ILV"); return e ? atoi(e) : 0; }();
+  return v != 0;
+}
+
 template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB = 2>
 void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
@@ -650,18 +741,29 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   static const int diag = [] { const char* e = getenv("DDLPC_DIAG_CONV"); return e ? atoi(e) : 0; }();
   a.diag = diag;
   constexpr bool FDB_OK = !(DIMS == 3 && MT * NT >= 16);
+  if constexpr (NBB == 4) {
+    if (conv_ilv()) {
+      if (a.bnb_y != nullptr)
+        hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK, true, true>), dim3(grid),
+                           dim3(C::NTH), C::SMEM, st, a);
+      else
+        hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK, false, true>), dim3(grid),
+                           dim3(C::NTH), C::SMEM, st, a);
+      return;
+    }
+  }
   if constexpr (DIMS == 2 && NBB != 3) {
     if (a.bnb_y != nullptr) {
-      hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK, true>), dim3(grid),
+      hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK, true, false>), dim3(grid),
                          dim3(C::NTH), C::SMEM, st, a);
       return;
     }
   }
   if (FDB_OK && conv_fdb())
-    hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK, false>), dim3(grid),
+    hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK, false, false>), dim3(grid),
                        dim3(C::NTH), C::SMEM, st, a);
   else
-    hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, false, false>), dim3(grid),
+    hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, false, false, false>), dim3(grid),
                        dim3(C::NTH), C::SMEM, st, a);
 }
 

@@ -272,7 +272,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   // Stores are buffer stores with an out-of-range offset for masked lanes: every wave
   // issues exactly EPI_STORES of them per epilogue (no exec branches), which keeps the
   // counted vmcnt waits exact.
-  constexpr int EPI_STORES = MT * NT * (SPLIT ? 2 : 1);
+  // PAIRS: 16-byte stores of channel-tile pairs (pair16).  Measured per layer at batch 128
+  // (profiles/conv_micro_b128_pair16_r2.txt): 5-10% faster on the BN 64 and image-layer
+  // variants, 4-6% slower on the 32-channel 3x3 layers (BN 32) -> 8-byte stores there
+  constexpr bool PAIRS = !SPLIT && (TAP8 || BN >= 64) && NT % 2 == 0;
+  constexpr int EPI_STORES = SPLIT ? MT * NT * 2 : PAIRS ? MT * NT / 2 : MT * NT;
   // BNB: y at this item's output pixels, loaded into VGPRs at the item's last stage (before
   // that stage's halo DMA) and consumed by its epilogue one stage later
   constexpr int YL = BNB ? MT * NT : 0;
@@ -298,8 +302,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     const int Co2 = p.Cout - p.Co1;
     const auto r1 = make_rsrc(p.Y1 + (long long)it.n_img * img_px * p.Co1, (unsigned)(img_px * p.Co1 * 2));
     const auto r2 = SPLIT ? make_rsrc(p.Y2 + (long long)it.n_img * img_px * Co2, (unsigned)(img_px * Co2 * 2)) : r1;
-    // channel tiles outer: the BNB constants of one tile are read once (and the scheduler
-    // barrier below keeps the next tile's reads from being hoisted: VGPR pressure)
+    // pass 1, channel tiles outer: bias, bf16 rounding, statistics (the BNB constants of one
+    // tile are read once; the scheduler barrier keeps the next tile's reads from being
+    // hoisted: VGPR pressure)
+    uint2 pkv[MT][NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * g;
@@ -309,27 +315,28 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
       for (int mt = 0; mt < MT; ++mt) {
         const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
         const int gw = it.w0 + pix % p.TW, gh = it.h0 + pix / p.TW;
-        const bool valid = gw < p.W && gh < p.H;
-        const int lp = gh * p.W + gw;                     // pixel within the image (32-bit)
+        const bool ok = gw < p.W && gh < p.H && co < p.Cout;
         float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bias_r[nt][i];
         const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        const bool ok = valid && co < p.Cout;
-        const u32x2_t d = u32x2_t{pk.x, pk.y};
-        // the offsets go through an opaque asm so the compiler cannot turn the masked
-        // store into a branch around it (the store COUNT must not depend on the data)
-        if (!SPLIT) {
-          unsigned o1 = ok ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
-          asm volatile("" : "+v"(o1));
-          __builtin_amdgcn_raw_buffer_store_b64(d, r1, o1, 0, 0);
-        } else {
-          const bool in1 = co < p.Co1;
-          unsigned o1 = (ok && in1) ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
-          unsigned o2 = (ok && !in1) ? (unsigned)(lp * Co2 + co - p.Co1) * 2u : kOOB;
-          asm volatile("" : "+v"(o1), "+v"(o2));
-          __builtin_amdgcn_raw_buffer_store_b64(d, r1, o1, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b64(d, r2, o2, 0, 0);
+        pkv[mt][nt] = pk;
+        if constexpr (!PAIRS) {
+          // 8-byte stores right away (split output: one of the two offsets is out of range)
+          const int lp = gh * p.W + gw;
+          const u32x2_t d = u32x2_t{pk.x, pk.y};
+          if constexpr (!SPLIT) {
+            unsigned o1 = ok ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
+            asm volatile("" : "+v"(o1));
+            __builtin_amdgcn_raw_buffer_store_b64(d, r1, o1, 0, 0);
+          } else {
+            const bool in1 = co < p.Co1;
+            unsigned o1 = (ok && in1) ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
+            unsigned o2 = (ok && !in1) ? (unsigned)(lp * Co2 + co - p.Co1) * 2u : kOOB;
+            asm volatile("" : "+v"(o1), "+v"(o2));
+            __builtin_amdgcn_raw_buffer_store_b64(d, r1, o1, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(d, r2, o2, 0, 0);
+          }
         }
         if constexpr (BNB) {
           bnb_accum(pk, ybuf[mt][nt], ok, kb, s1[nt], s2[nt]);
@@ -345,6 +352,26 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
         acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       }
       if constexpr (BNB) __builtin_amdgcn_sched_barrier(0);
+    }
+    // pass 2 (PAIRS): 16-byte stores.  Buffer stores with an out-of-range offset for masked
+    // lanes; the offsets go through an opaque asm so the compiler cannot turn a masked store
+    // into a branch around it (the store COUNT must not depend on the data)
+    if constexpr (PAIRS) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
+        const int gw = it.w0 + pix % p.TW, gh = it.h0 + pix / p.TW;
+        const bool valid = gw < p.W && gh < p.H;
+        const int lp = gh * p.W + gw;                   // pixel within the image (32-bit)
+#pragma unroll
+        for (int np = 0; np < NT / 2; ++np) {
+          const uint4 q = pair16(pkv[mt][2 * np], pkv[mt][2 * np + 1]);
+          const int co = co0 + wn * (NT * 16) + np * 32 + pair16_ch(lane);
+          unsigned o1 = valid && co < p.Cout ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
+          asm volatile("" : "+v"(o1));
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, r1, o1, 0, 0);
+        }
+      }
     }
   };
 

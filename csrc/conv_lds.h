@@ -63,6 +63,19 @@ DDLPC_DEVICE uint2 buf_load8(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return make_uint2(v.x, v.y);
 }
 
+// 16-byte epilogue stores from the 16x16 MFMA D layout (A = weights, B = pixels): lane l
+// holds channels 4g..4g+3 (g = l >> 4) of pixel l & 15 for each 16-channel tile.  For two
+// adjacent tiles (lo, hi) one v_permlane16_swap per dword leaves every lane 8 consecutive
+// channels of its pixel — lanes 0-15: lo 0-7, 16-31: hi 0-7, 32-47: lo 8-15, 48-63: hi 8-15
+// (channel offset pair16_ch within the 32-channel pair): half the store instructions of the
+// 8-byte layout, whole 64-byte pixel rows per instruction
+DDLPC_DEVICE uint4 pair16(uint2 lo, uint2 hi) {
+  const auto x = __builtin_amdgcn_permlane16_swap(lo.x, hi.x, false, false);
+  const auto y = __builtin_amdgcn_permlane16_swap(lo.y, hi.y, false, false);
+  return make_uint4(x[0], y[0], x[1], y[1]);
+}
+DDLPC_DEVICE int pair16_ch(int lane) { return ((lane >> 4) & 1) * 16 + (lane >> 5) * 8; }
+
 // ---- BN-backward epilogue (ConvFwdArgs::bnb_y): LDS table [4][nb] of (scale, shift,
 // invstd, -mean*invstd) for the channels [co0, co0 + nb) of a workgroup's n tile
 DDLPC_DEVICE void bnb_fill(float* tab, int nb, int co0, int Cout, const float* s4, int tid, int nth) {

@@ -14,7 +14,8 @@ import threading
 import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib")
-LIB_PATH = os.path.join(_LIB_DIR, "libddlpc_hip.so")
+# DDLPC_LIB_PATH: load another build of the same library (A/B of kernel variants)
+LIB_PATH = os.environ.get("DDLPC_LIB_PATH") or os.path.join(_LIB_DIR, "libddlpc_hip.so")
 _lock = threading.Lock()
 _loaded = False
 _error = None
