@@ -24,5 +24,5 @@ elif [ "$CFG" = "torch_d3" ]; then     # stock PyTorch; MIOpen's exhaustive 3-D 
   # in 15 min (and logged missing CK instances), so FAST find mode (its heuristic choice)
   MIOPEN_FIND_MODE=FAST run d3_128_b8_torch 900 --impl torch --dims 3 --tile 128 --batch 8 --steps 5 --warmup 3
 elif [ "$CFG" = "torch_wd1" ]; then
-  run wd1_b64_torch 900 --impl torch --width-divisor 1 --batch 64 --steps 10 --warmup 3
+  MIOPEN_FIND_MODE=FAST run wd1_b64_torch 900 --impl torch --width-divisor 1 --batch 64 --steps 10 --warmup 3
 fi
