@@ -568,9 +568,26 @@ std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
   a.dims = g.dims; a.Nimg = g.N; a.D = g.D; a.H = g.H; a.W = g.W;
   a.Cin = g.C; a.Cout = go.C;
   a.bn4 = bn4_ptr(bn4, g.C);
-  const int base = ((a.M + 63) / 64) * ((a.N + 63) / 64);
-  int splits = std::max(1, (4 * num_cus() + base - 1) / base);
-  splits = std::min(splits, std::max(1, a.K / 256));
+  // v2 kernel (64 x 64 wave tiles, LDS-DMA stages): enough 128 x 128 workgroups for two per
+  // CU, every split >= 4 stages of 64 pixels; DDLPC_CONVT_WG2=0 keeps the v1 kernel
+  static const int use_wg2 = [] { const char* e = getenv("DDLPC_CONVT_WG2"); return e ? atoi(e) : 1; }();
+  int splits;
+  a.wg2 = use_wg2 && g.C % 8 == 0 && go.C % 8 == 0 && g.C <= 512;
+  if (a.wg2) {
+    const int tiles = convt_wgrad2_tiles(a);
+    splits = std::max(1, (2 * num_cus() + tiles - 1) / tiles);
+    splits = std::min(splits, std::max(1, a.K / 256));
+    // the kernel addresses a split's dOut rows through one buffer descriptor (32-bit
+    // offsets): bound the rows a split can span (up to 2 extra input rows / planes)
+    const long long per = ((long long)a.K + splits - 1) / splits + 64;
+    const long long span = g.dims == 2 ? 4 * per + 8LL * g.W : 8 * per + 16LL * g.H * g.W;
+    if (span * go.C * 2 >= (1LL << 31)) a.wg2 = 0;
+  }
+  if (!a.wg2) {
+    const int base = ((a.M + 63) / 64) * ((a.N + 63) / 64);
+    splits = std::max(1, (4 * num_cus() + base - 1) / base);
+    splits = std::min(splits, std::max(1, a.K / 256));
+  }
   a.splits = splits;
   auto fopts = x.options().dtype(at::kFloat);
   at::Tensor part = at::empty({(int64_t)splits * a.M * a.N}, fopts);
@@ -639,21 +656,23 @@ std::vector<at::Tensor> head_ce_bwd(const at::Tensor& a, const at::Tensor& Wh, c
                                     const c10::optional<at::Tensor>& gscale, int64_t ignore_index,
                                     const c10::optional<at::Tensor>& dw_out,
                                     const c10::optional<at::Tensor>& db_out,
-                                    const c10::optional<at::Tensor>& bn4) {
+                                    const c10::optional<at::Tensor>& bn4, bool store_da) {
   CHECK_DEV(a); CHECK_CONTIG(a);
   c10::DeviceGuard guard(a.device());
   const int C = (int)a.size(-1), K = (int)Wh.size(0);
   const float* pbn = bn4_ptr(bn4, C);
   TORCH_CHECK(head_supported(C, K), "head kernel: unsupported (C, K)");
+  TORCH_CHECK(store_da || pbn != nullptr, "head_ce_bwd: store_da=False needs the deferred BN (bn4)");
   const long long P = a.numel() / C;
   const int nb = head_ce_bwd_blocks(C, K, pbn != nullptr, P, num_cus());
   auto fopts = a.options().dtype(at::kFloat);
-  at::Tensor dA = at::empty_like(a);
+  // store_da=False: the stats pass of the two-pass backward (head_ce_bn_bwd writes dY)
+  at::Tensor dA = store_da ? at::empty_like(a) : at::empty({0}, a.options());
   at::Tensor part = at::empty({nb, K * C + K}, fopts);
   // deferred BatchNorm input: the kernel also emits that BN's backward partial rows
   at::Tensor bnpart = pbn != nullptr ? at::empty({nb, 2, C}, fopts) : at::empty({0}, fopts);
   head_ce_bwd_launch(bptr(a), Wh.data_ptr<float>(), bh.data_ptr<float>(), labels.data_ptr<int64_t>(),
-                     fptr_opt(gscale), out3.data_ptr<float>(), 0, bptr_mut(dA),
+                     fptr_opt(gscale), out3.data_ptr<float>(), 0, store_da ? bptr_mut(dA) : nullptr,
                      part.data_ptr<float>(), nb, P, C, K, (int)ignore_index, pbn,
                      pbn != nullptr ? bnpart.data_ptr<float>() : nullptr, cur_stream());
   const bool into = dw_out.has_value() && dw_out->defined();
@@ -673,6 +692,48 @@ std::vector<at::Tensor> head_ce_bwd(const at::Tensor& a, const at::Tensor& Wh, c
   at::Tensor dW = red.narrow(0, 0, K * C).view({K, C});
   at::Tensor db = red.narrow(0, K * C, K);
   return {dA, dW, db, bnpart};
+}
+
+// Second pass of the two-pass head backward: the last decoder block's BatchNorm backward
+// applied to the recomputed head gradient.  partial: the stats pass's [R][2][C] rows;
+// returns {dY, dgamma, dbeta} like bn_backward (accumulated into the outs when given)
+std::vector<at::Tensor> head_ce_bn_bwd(const at::Tensor& a, const at::Tensor& Wh, const at::Tensor& bh,
+                                       const at::Tensor& labels, const at::Tensor& out3,
+                                       const c10::optional<at::Tensor>& gscale, int64_t ignore_index,
+                                       const at::Tensor& bn4, const at::Tensor& partial,
+                                       const at::Tensor& gamma,
+                                       const c10::optional<at::Tensor>& dgamma_out,
+                                       const c10::optional<at::Tensor>& dbeta_out) {
+  CHECK_DEV(a); CHECK_CONTIG(a); CHECK_BF16(a);
+  c10::DeviceGuard guard(a.device());
+  const int C = (int)a.size(-1), K = (int)Wh.size(0);
+  const float* pbn = bn4_ptr(bn4, C);
+  TORCH_CHECK(head_supported(C, K), "head kernel: unsupported (C, K)");
+  CHECK_F32(partial); CHECK_CONTIG(partial); CHECK_F32(gamma);
+  TORCH_CHECK(partial.numel() % (2 * C) == 0 && partial.numel() > 0, "partial rows must be [R][2][C]");
+  const long long P = a.numel() / C;
+  const int nb = (int)(partial.numel() / (2 * C));
+  auto fopts = a.options().dtype(at::kFloat);
+  const bool into = dgamma_out.has_value() && dgamma_out->defined();
+  at::Tensor dgamma = into ? *dgamma_out : at::empty({C}, fopts);
+  at::Tensor dbeta = into ? *dbeta_out : at::empty({C}, fopts);
+  at::Tensor coefs = at::empty({3, C}, fopts);
+  const float* s = pbn;
+  if (nb <= 2048) {
+    bn_grad_finalize_rows_launch(partial.data_ptr<float>(), nb, C, (double)P, gamma.data_ptr<float>(),
+                                 s + C, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+                                 coefs.data_ptr<float>(), into, cur_stream());
+  } else {
+    at::Tensor sums = reduce_rows(partial, nb, 2 * C);
+    bn_grad_finalize_launch(sums.data_ptr<double>(), C, (double)P, gamma.data_ptr<float>(), s + C,
+                            dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+                            coefs.data_ptr<float>(), into, cur_stream());
+  }
+  at::Tensor dY = at::empty_like(a);
+  head_bn_apply_launch(bptr(a), Wh.data_ptr<float>(), bh.data_ptr<float>(), labels.data_ptr<int64_t>(),
+                       fptr_opt(gscale), out3.data_ptr<float>(), pbn, coefs.data_ptr<float>(),
+                       bptr_mut(dY), P, C, K, (int)ignore_index, cur_stream());
+  return {dY, dgamma, dbeta};
 }
 
 at::Tensor head_logits(const at::Tensor& a, const at::Tensor& Wh, const at::Tensor& bh,
@@ -888,7 +949,11 @@ TORCH_LIBRARY(ddlpc, m) {
         "Tensor? colsum_rows=None, Tensor? bn4=None) -> Tensor[]");
   m.def("head_ce_fwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, int ignore_index, Tensor? bn4=None) -> Tensor");
   m.def("head_ce_bwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, Tensor out3, Tensor? gscale, "
-        "int ignore_index, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, Tensor? bn4=None) -> Tensor[]");
+        "int ignore_index, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, Tensor? bn4=None, "
+        "bool store_da=True) -> Tensor[]");
+  m.def("head_ce_bn_bwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, Tensor out3, Tensor? gscale, "
+        "int ignore_index, Tensor bn4, Tensor partial, Tensor gamma, Tensor(a!)? dgamma_out=None, "
+        "Tensor(b!)? dbeta_out=None) -> Tensor[]");
   m.def("head_logits(Tensor a, Tensor Wh, Tensor bh, Tensor? bn4=None) -> Tensor");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float eps, "
         "float wd, float step_size, float inv_sqrt_bc2) -> ()");
@@ -917,6 +982,7 @@ TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
   m.impl("convt_wgrad", &ddlpc::convt_wgrad);
   m.impl("head_ce_fwd", &ddlpc::head_ce_fwd);
   m.impl("head_ce_bwd", &ddlpc::head_ce_bwd);
+  m.impl("head_ce_bn_bwd", &ddlpc::head_ce_bn_bwd);
   m.impl("head_logits", &ddlpc::head_logits);
   m.impl("adam_step", &ddlpc::adam_step);
   m.impl("adam_step_dev", &ddlpc::adam_step_dev);

@@ -14,7 +14,10 @@
 // NT tile: 128 x 64 per 256-thread workgroup, 4 waves of 64 x 32 (4 x 2 v_mfma 16x16x32),
 // 32-deep K chunks staged through swizzled LDS with register prefetch (same scheme as the
 // 3x3 conv).  TN tile: 64 x 64, 4 waves of 32 x 32, 64-pixel K chunks.
+#include <type_traits>
+
 #include "common.h"
+#include "conv_lds.h"
 #include "ops.h"
 
 namespace ddlpc {
@@ -381,9 +384,235 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_wgrad_kernel(GemmArgs p) {
     }
 }
 
+// ---------------------------------------------------------------- TN v2 (weight gradient)
+// Same product as gemm_tn_wgrad_kernel with MFMA-sized per-wave tiles: 4 waves of 64 x 64
+// (4 x 4 v_mfma 16x16x32 per 32-pixel k step: 16 transposed LDS reads per 16 MFMAs, a
+// quarter of the v1 kernel's LDS traffic per FLOP, which saturated the LDS array), a
+// BM x BN = 128 x 128 (or 64 x 256 for 64 input channels) workgroup tile, 64-pixel stages
+// that arrive by LDS-DMA (buffer_load ... lds, double-buffered, counted vmcnt waits) and
+// an XOR swizzle on 32-byte groups so every ds_read_b64_tr_b16 half-wave (8 pixel rows x
+// 32 B) touches all 64 banks once.  The gathered dOut rows (4 / 8 sub-positions per input
+// pixel) and x are addressed through per-workgroup buffer descriptors (32-bit offsets
+// relative to the split's first row: tensors beyond 4 GB are fine).  The deferred BN + ReLU
+// of x is applied in LDS by the lane that DMA'd each piece, before the stage barrier.
+template <int BM>
+struct Tn2Cfg {
+  static constexpr int BN = BM == 128 ? 128 : 256;
+  static constexpr int WN = BN / 64;                  // waves along n (BM / 64 along m)
+  // 64 input channels (the 256^2-level transposed conv: 1.3 GB of operands, 69 GFLOP per
+  // pass at batch 128 — memory bound): 32-pixel stages in a 3-deep ring, the DMA of stage
+  // s + 2 in flight while s computes.  Wider layers (compute heavier): 64-pixel stages,
+  // double-buffered.  (measured per shape, profiles/convt_wgrad_micro_*_s2.txt)
+  static constexpr int KT = BM == 64 ? 32 : 64;
+  static constexpr int NBUF = BM == 64 ? 3 : 2;
+  static constexpr int A_RB = BM * 2, B_RB = BN * 2;  // LDS row bytes
+  static constexpr int A_BYTES = KT * A_RB, B_BYTES = KT * B_RB;
+  static constexpr int NA = A_BYTES / 4096;           // DMA instructions per wave per stage
+  static constexpr int NB = B_BYTES / 4096;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int BN_FLOATS = BM == 128 ? 512 : 64;   // deferred-BN table (M <= 512 / 64)
+  static constexpr int SMEM = NBUF * STAGE + 2 * BN_FLOATS * 4;
+};
+// 32-byte group swizzle of LDS row `row` (rows of >= 256 B: 3 bits; 128-B rows: 2 bits) —
+// conflict-free for the half-wave row sets {r..r+3, r+8..r+11} of the transposed reads
+template <int RB>
+DDLPC_DEVICE int tn2_swz(int row) {
+  return RB >= 256 ? ((row & 3) | (((row >> 3) & 1) << 2)) : (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
+}
+
+template <int BM>
+__global__ __launch_bounds__(256, 2) void gemm_tn_wgrad2_kernel(GemmArgs p) {
+  using namespace convlds;
+  using Cf = Tn2Cfg<BM>;
+  constexpr int BN = Cf::BN, KT = Cf::KT, WN = Cf::WN;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NBUF = Cf::NBUF, NBF = Cf::BN_FLOATS;
+  float* s_bn = reinterpret_cast<float*>(smem + NBUF * Cf::STAGE);  // scale [NBF] | shift [NBF]
+  auto sA = [&](int b) { return smem + b * Cf::STAGE; };
+  auto sB = [&](int b) { return smem + b * Cf::STAGE + Cf::A_BYTES; };
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const bool has_bn = p.bn4 != nullptr;
+  if (has_bn)
+    for (int i = tid; i < p.M; i += 256) { s_bn[i] = p.bn4[2 * p.M + i]; s_bn[NBF + i] = p.bn4[3 * p.M + i]; }
+  const int nTilesN = (p.N + BN - 1) / BN, nTilesM = (p.M + BM - 1) / BM;
+  int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = b % nTilesN; b /= nTilesN;
+  const int mtile = b % nTilesM; b /= nTilesM;
+  const int split = b;
+  const int m0 = mtile * BM, n0 = ntile * BN;
+  const long long npx = (long long)p.K;
+  const long long per = ((npx + p.splits - 1) / p.splits + KT - 1) / KT * KT;
+  const long long k_begin = per * split;
+  const long long k_end = k_begin + per < npx ? k_begin + per : npx;
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  if (k_begin < k_end) {
+    const int S = p.dims == 2 ? 4 : 8;
+    // buffer descriptors relative to this split's first rows (32-bit offsets)
+    const long long a_lo = k_begin;
+    const auto ra = make_rsrc(p.A + a_lo * p.Cin, (unsigned)((k_end - a_lo) * p.Cin * 2));
+    const long long kb0 = k_begin - k_begin % p.W;           // row start: up_pixel is monotone
+    const long long b_lo = up_pixel((int)kb0, 0, p.dims, p.D, p.H, p.W);
+    const long long b_hi = (long long)up_pixel((int)(k_end - 1), S - 1, p.dims, p.D, p.H, p.W) + 1;
+    const auto rb = make_rsrc(p.B + b_lo * p.Cout, (unsigned)((b_hi - b_lo) * p.Cout * 2));
+    // per-lane DMA geometry (tile independent): LDS piece e = (i*4 + wave)*64 + lane
+    int a_row[Cf::NA], a_col[Cf::NA], b_row[Cf::NB], b_col[Cf::NB], b_sub[Cf::NB];
+#pragma unroll
+    for (int i = 0; i < Cf::NA; ++i) {
+      const int e = (i * 4 + wave) * 64 + lane;
+      const int ppr = Cf::A_RB / 16;
+      const int row = e / ppr, pc = e % ppr;
+      const int lp = (((pc >> 1) ^ tn2_swz<Cf::A_RB>(row)) << 1) | (pc & 1);
+      a_row[i] = row;
+      a_col[i] = m0 + lp * 8 < p.M ? m0 + lp * 8 : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < Cf::NB; ++i) {
+      const int e = (i * 4 + wave) * 64 + lane;
+      const int ppr = Cf::B_RB / 16;
+      const int row = e / ppr, pc = e % ppr;
+      const int lp = (((pc >> 1) ^ tn2_swz<Cf::B_RB>(row)) << 1) | (pc & 1);
+      const int n = n0 + lp * 8;
+      b_row[i] = row;
+      b_sub[i] = n < p.N ? n / p.Cout : -1;
+      b_col[i] = n < p.N ? n % p.Cout : 0;
+    }
+    auto issue = [&](long long k0, int buf) {
+#pragma unroll
+      for (int i = 0; i < Cf::NA; ++i) {
+        const long long px = k0 + a_row[i];
+        const bool ok = px < k_end && a_col[i] >= 0;
+        dma16(ra, sA(buf) + (i * 4 + wave) * 1024,
+              ok ? (unsigned)(((px - a_lo) * p.Cin + a_col[i]) * 2) : kOOB);
+      }
+#pragma unroll
+      for (int i = 0; i < Cf::NB; ++i) {
+        const long long px = k0 + b_row[i];
+        const bool ok = px < k_end && b_sub[i] >= 0;
+        const long long up = ok ? up_pixel((int)px, b_sub[i], p.dims, p.D, p.H, p.W) : b_lo;
+        dma16(rb, sB(buf) + (i * 4 + wave) * 1024,
+              ok ? (unsigned)(((up - b_lo) * p.Cout + b_col[i]) * 2) : kOOB);
+      }
+    };
+    auto transform = [&](long long k0, int buf) {      // deferred BN + ReLU of this lane's x pieces
+#pragma unroll
+      for (int i = 0; i < Cf::NA; ++i) {
+        if (k0 + a_row[i] < k_end && a_col[i] >= 0) {
+          uint4* q = reinterpret_cast<uint4*>(sA(buf) + ((i * 4 + wave) * 64 + lane) * 16);
+          float f[8];
+          unpack8(*q, f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], s_bn[a_col[i] + j], s_bn[NBF + a_col[i] + j]), 0.f);
+          *q = pack8(f);
+        }
+      }
+    };
+    // transposed-read geometry: lane (g, q, pp) reads row 8g + q (+4) of a 32-row k step,
+    // columns 4pp..4pp+3 of a 16-wide m / n fragment
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    auto frag_off = [&](int row, int col, auto rb_tag) {
+      constexpr int RB = decltype(rb_tag)::value;
+      const int grp = (col >> 4) ^ tn2_swz<RB>(row);
+      return row * RB + grp * 32 + (col & 15) * 2;
+    };
+    using RA = std::integral_constant<int, Cf::A_RB>;
+    using RBt = std::integral_constant<int, Cf::B_RB>;
+    const int nst = (int)((k_end - k_begin + KT - 1) / KT);
+    __syncthreads();                                     // s_bn visible
+    // prologue: stages 0 .. NBUF-2 in flight (empty stages past the end are not issued;
+    // the waits below count only what was issued)
+#pragma unroll
+    for (int j = 0; j < NBUF - 1; ++j)
+      if (j < nst) issue(k_begin + (long long)j * KT, j);
+    constexpr int PER = Cf::NA + Cf::NB;
+#pragma unroll 1
+    for (int st = 0; st < nst; ++st) {
+      const int buf = st % NBUF;
+      const long long k0 = k_begin + (long long)st * KT;
+      if constexpr (NBUF == 2) {
+        // double buffer: stage st + 1 goes out before waiting for st (its buffer was freed
+        // by the trailing barrier of the previous iteration)
+        if (st + 1 < nst) { issue(k0 + KT, buf ^ 1); dma_wait<PER>(); }
+        else dma_wait<0>();
+        if (has_bn) transform(k0, buf);
+        lds_sync();
+      } else {
+        // ring: stages issued after st = min(NBUF - 2, nst - 1 - st)
+        const int after = min(NBUF - 2, nst - 1 - st);
+        if (NBUF >= 4 && after >= 2) dma_wait<2 * PER>();
+        else if (after >= 1) dma_wait<PER>();
+        else dma_wait<0>();
+        if (has_bn) transform(k0, buf);
+        lds_sync();
+        // the buffer of stage st - 1 is free (every wave is past its compute): refill it
+        if (st + NBUF - 1 < nst) issue(k0 + (long long)(NBUF - 1) * KT, (st + NBUF - 1) % NBUF);
+      }
+      const char* A_ = sA(buf);
+      const char* B_ = sB(buf);
+#pragma unroll
+      for (int ks = 0; ks < KT / 32; ++ks) {
+      const int r0 = ks * 32 + 8 * g + q;
+      uint4 af[4], bfr[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int c = wm * 64 + mt * 16 + 4 * pp;
+        const uint2 lo = lds_read_tr16(A_ + frag_off(r0, c, RA{}));
+        const uint2 hi = lds_read_tr16(A_ + frag_off(r0 + 4, c, RA{}));
+        af[mt] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int c = wn * 64 + nt * 16 + 4 * pp;
+        const uint2 lo = lds_read_tr16(B_ + frag_off(r0, c, RBt{}));
+        const uint2 hi = lds_read_tr16(B_ + frag_off(r0 + 4, c, RBt{}));
+        bfr[nt] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16x16x32(af[mt], bfr[nt], acc[mt][nt]);
+      }
+      // 2-deep ring: the next iteration refills THIS buffer right after its barrier, so
+      // every wave must be done reading it first
+      if (NBUF == 2) lds_sync();
+    }
+  }
+  float* out = p.partial + (long long)split * p.M * p.N;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int n = n0 + wn * 64 + nt * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * 64 + mt * 16 + 4 * (lane >> 4) + i;
+        if (m < p.M && n < p.N) out[(long long)m * p.N + n] = acc[mt][nt][i];
+      }
+    }
+}
+
 }  // namespace
 
+int convt_wgrad2_tiles(const GemmArgs& a) {
+  const int bm = a.M <= 64 ? 64 : 128;
+  const int bn = bm == 64 ? 256 : 128;
+  return ((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+}
+
 void gemm_launch(GemmArgs& a, hipStream_t st) {
+  if (a.mode == GEMM_CONVT_WGRAD && a.wg2) {
+    const int grid = convt_wgrad2_tiles(a) * a.splits;
+    if (a.M <= 64)
+      hipLaunchKernelGGL(gemm_tn_wgrad2_kernel<64>, dim3(grid), dim3(256), Tn2Cfg<64>::SMEM, st, a);
+    else
+      hipLaunchKernelGGL(gemm_tn_wgrad2_kernel<128>, dim3(grid), dim3(256), Tn2Cfg<128>::SMEM, st, a);
+    return;
+  }
   if (a.mode == GEMM_CONVT_WGRAD) {
     const int grid = ((a.M + 63) / 64) * ((a.N + 63) / 64) * a.splits;
     hipLaunchKernelGGL(gemm_tn_wgrad_kernel, dim3(grid), dim3(256), 0, st, a);

@@ -9,6 +9,11 @@
 // backward kernel recomputes the logits (192 MACs/pixel: far cheaper than storing them),
 // forms dlogits = (softmax - onehot) * dL / count, writes dA = dlogits . Wh (bf16) and
 // reduces dWh = sum a (x) dlogits, dbh = sum dlogits through an LDS tile per 256 pixels.
+// With the last decoder block's BatchNorm deferred into the head (the training default) the
+// backward runs in two passes: a stats pass (dWh, dbh, that BN's backward partial sums; no
+// dA store) and head_bn_apply_kernel, which recomputes dA and writes the BN's dY directly —
+// y + labels are read twice, but dA never round-trips through HBM and the separate BN-apply
+// pass over (dA, y) disappears (256^2 x 128: 5.1 -> 3.2 tensor-sized HBM transfers).
 #include "common.h"
 #include "ops.h"
 
@@ -163,13 +168,63 @@ __global__ void ce_finalize_kernel(const float* __restrict__ partial, int nb, fl
 // — so the last decoder block's BN backward skips its reduction pass.  Accumulators are
 // reduced once per (persistent) workgroup: shuffles over the lanes with equal c8, then a
 // fixed-order sum over the waves (deterministic), one partial row per workgroup.
+// One pixel of the channel-split backward (shared by head_ce_bwd_kernel and
+// head_bn_apply_kernel so both form bit-identical values): from this lane's 8 raw input
+// channels av and the label, the activation f (the deferred BN + ReLU, bf16-rounded), the
+// softmax-CE gradient d[K] (identical on the G lanes of the pixel) and the lane's 8
+// channels of dA = d . Wh, rounded to bf16 (pk) exactly as stored.
 template <int C, int K, bool DEFER>
+DDLPC_DEVICE void head_pixel(const uint4 av, const int64_t lab, const float* __restrict__ w,
+                             const float (&bk)[K], const float (&sc)[8], const float (&sh)[8],
+                             float gs, int ignore_index, float (&y8)[8], float (&f)[8],
+                             float (&d)[K], uint4& pk) {
+  constexpr int G = C / 8;
+  unpack8(av, y8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = DEFER ? fmaxf(fmaf(y8[j], sc[j], sh[j]), 0.f) : y8[j];
+  if (DEFER) unpack8(pack8(f), f);                // the activation rounded as materialised
+  float z[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t = fmaf(f[j], w[k * C + j], t);
+    z[k] = t;
+  }
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1)
+#pragma unroll
+    for (int k = 0; k < K; ++k) z[k] += __shfl_xor(z[k], o, 64);
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < K; ++k) { z[k] += bk[k]; m = fmaxf(m, z[k]); }
+  float se = 0.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k) { z[k] = __expf(z[k] - m); se += z[k]; }
+  const float inv = 1.f / se;
+#pragma unroll
+  for (int k = 0; k < K; ++k) d[k] = lab != ignore_index ? (z[k] * inv - (k == lab ? 1.f : 0.f)) * gs : 0.f;
+  float o8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) t = fmaf(d[k], w[k * C + j], t);
+    o8[j] = t;
+  }
+  pk = pack8(o8);
+}
+
+// STORE = false (deferred BN only): the stats pass of the two-pass head backward — dWh,
+// dbh and the BN-backward partials, no dA (head_bn_apply_kernel recomputes it)
+template <int C, int K, bool DEFER, bool STORE = true>
 __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
     const bf16_t* __restrict__ a, const float* __restrict__ Wh, const float* __restrict__ bh,
     const int64_t* __restrict__ labels, const float* __restrict__ gscale,
     const float* __restrict__ stats3, bf16_t* __restrict__ dA, float* __restrict__ dWp,
     long long P, int ignore_index, const float* __restrict__ bn4, float* __restrict__ bnpart,
     int Kreal) {
+  static_assert(STORE || DEFER, "the stats-only pass exists for the deferred BatchNorm");
   constexpr int G = C / 8;                          // lanes per pixel
   constexpr int PPB = 256 / G;                      // pixels per workgroup step
   constexpr int NACC = 8 * K + K + (DEFER ? 16 : 0);
@@ -206,49 +261,17 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
   if (px < P) { a_nx = *reinterpret_cast<const uint4*>(a + px * C + c8); l_nx = labels[px]; }
 #pragma unroll 1
   for (; px < P; px += stride) {
-    float y8[8], f[8];
-    unpack8(a_nx, y8);
+    const uint4 a_cur = a_nx;
     const int64_t lab = l_nx;
     if (px + stride < P) {
       a_nx = *reinterpret_cast<const uint4*>(a + (px + stride) * C + c8);
       l_nx = labels[px + stride];
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = DEFER ? fmaxf(fmaf(y8[j], sc[j], sh[j]), 0.f) : y8[j];
-    if (DEFER) unpack8(pack8(f), f);                // the activation rounded as materialised
-    const float* w = sW + opaque_zero() + c8;        // w[k * C + j]: this lane's 8 channels
-    float z[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      float t = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) t = fmaf(f[j], w[k * C + j], t);
-      z[k] = t;
-    }
-#pragma unroll
-    for (int o = 1; o < G; o <<= 1)
-#pragma unroll
-      for (int k = 0; k < K; ++k) z[k] += __shfl_xor(z[k], o, 64);
-    float m = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < K; ++k) { z[k] += bk[k]; m = fmaxf(m, z[k]); }
-    float se = 0.f;
-#pragma unroll
-    for (int k = 0; k < K; ++k) { z[k] = __expf(z[k] - m); se += z[k]; }
-    const float inv = 1.f / se;
-    float d[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) d[k] = lab != ignore_index ? (z[k] * inv - (k == lab ? 1.f : 0.f)) * gs : 0.f;
-    float o8[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float t = 0.f;
-#pragma unroll
-      for (int k = 0; k < K; ++k) t = fmaf(d[k], w[k * C + j], t);
-      o8[j] = t;
-    }
-    const uint4 pk = pack8(o8);
-    *reinterpret_cast<uint4*>(dA + px * C + c8) = pk;
+    float y8[8], f[8], d[K];
+    uint4 pk;
+    head_pixel<C, K, DEFER>(a_cur, lab, sW + opaque_zero() + c8, bk, sc, sh, gs, ignore_index,
+                            y8, f, d, pk);
+    if (STORE) *reinterpret_cast<uint4*>(dA + px * C + c8) = pk;
 #pragma unroll
     for (int k = 0; k < K; ++k)
 #pragma unroll
@@ -297,6 +320,74 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
       for (int wv = 0; wv < 4; ++wv) t += sred[wv][c / 8][9 * K + 8 * half + c % 8];
       bnpart[(long long)blockIdx.x * 2 * C + o] = t;
     }
+}
+
+// Second pass of the two-pass head backward (deferred BatchNorm of the last decoder
+// block): recomputes dA exactly as head_ce_bwd_kernel stores it (head_pixel) and applies
+// that BatchNorm's backward to it in registers,
+//   dY = k * (dyh - m1 - xhat * m2),  dyh = dA * [y*scale + shift > 0]
+// (coefs = [k | m1 | m2] x C from the stats pass's partial rows; the arithmetic of
+// bn_bwd2_kernel's apply, same operand order) — dA never reaches HBM and the separate
+// BN-apply pass (read dA + y, write dY) is gone: y + labels in, dY out.
+// Two pixels per lane per iteration with all loads first (memory-level parallelism).
+template <int C, int K>
+__global__ __launch_bounds__(256) void head_bn_apply_kernel(
+    const bf16_t* __restrict__ a, const float* __restrict__ Wh, const float* __restrict__ bh,
+    const int64_t* __restrict__ labels, const float* __restrict__ gscale,
+    const float* __restrict__ stats3, const float* __restrict__ bn4,
+    const float* __restrict__ coefs, bf16_t* __restrict__ dY, long long P, int ignore_index,
+    int Kreal) {
+  constexpr int G = C / 8;
+  constexpr int PPB = 256 / G;
+  constexpr int U = 2;
+  __shared__ __attribute__((aligned(16))) float sW[K * C];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int cg = lane % G, c8 = cg * 8;
+  for (int i = tid; i < K * C; i += 256) sW[i] = i < Kreal * C ? Wh[i] : 0.f;
+  float bk[K], sc[8], sh[8], is[8], nm[8], k1[8], m1[8], m2[8];
+#pragma unroll
+  for (int k = 0; k < K; ++k) bk[k] = k < Kreal ? bh[k] : -INFINITY;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = bn4[2 * C + c8 + j]; sh[j] = bn4[3 * C + c8 + j];
+    is[j] = bn4[C + c8 + j]; nm[j] = -bn4[c8 + j] * is[j];
+    k1[j] = coefs[c8 + j]; m1[j] = coefs[C + c8 + j]; m2[j] = coefs[2 * C + c8 + j];
+  }
+  __syncthreads();
+  const float cnt = stats3[2];
+  const float gs = (gscale != nullptr ? gscale[0] : 1.0f) / (cnt > 0.f ? cnt : 1.f);
+  const long long stride = (long long)gridDim.x * PPB;
+#pragma unroll 1
+  for (long long px0 = (long long)blockIdx.x * PPB + tid / G; px0 < P; px0 += U * stride) {
+    uint4 av[U];
+    int64_t lab[U];
+#pragma unroll
+    for (int r = 0; r < U; ++r) {
+      const long long px = px0 + r * stride;
+      const long long pq = px < P ? px : px0;
+      av[r] = *reinterpret_cast<const uint4*>(a + pq * C + c8);
+      lab[r] = labels[pq];
+    }
+#pragma unroll
+    for (int r = 0; r < U; ++r) {
+      const long long px = px0 + r * stride;
+      if (px >= P) break;                            // uniform over the G lanes of a pixel
+      float y8[8], f[8], d[K];
+      uint4 pk;
+      head_pixel<C, K, true>(av[r], lab[r], sW + opaque_zero() + c8, bk, sc, sh, gs,
+                             ignore_index, y8, f, d, pk);
+      float rr[8], o[8];
+      unpack8(pk, rr);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float av2 = fmaf(y8[j], sc[j], sh[j]);
+        const float dyh = av2 > 0.f ? rr[j] : 0.f;
+        const float xh = fmaf(y8[j], is[j], nm[j]);
+        o[j] = k1[j] * (dyh - m1[j] - xh * m2[j]);
+      }
+      *reinterpret_cast<uint4*>(dY + px * C + c8) = pack8(o);
+    }
+  }
 }
 
 template <int C, int K, bool DEFER>
@@ -372,6 +463,9 @@ int head_ce_bwd_blocks(int C, int K, bool /*defer*/, long long P, int num_cus) {
   };
   HEAD_SWITCH(C, K, occ(reinterpret_cast<const void*>(&head_ce_bwd_kernel<CC, KK, true>)));
   HEAD_SWITCH(C, K, occ(reinterpret_cast<const void*>(&head_ce_bwd_kernel<CC, KK, false>)));
+  // DDLPC_HEAD_BWD_PER_CU: workgroups per CU in the grid (A/B knob; default: resident ones)
+  static const int pc = [] { const char* e = getenv("DDLPC_HEAD_BWD_PER_CU"); return e ? atoi(e) : 0; }();
+  if (pc > 0) per_cu = pc;
   const long long ppb = 256 / (C / 8);
   return (int)std::max<long long>(1, std::min<long long>((P + ppb - 1) / ppb, (long long)per_cu * num_cus));
 }
@@ -380,7 +474,11 @@ void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
                         const float* gscale, const float* stats3, int /*unused*/, bf16_t* dA,
                         float* dW_partial, int nblocks, long long P, int C, int K,
                         int ignore_index, const float* bn4, float* bnpart, hipStream_t st) {
-  if (bn4 != nullptr)
+  if (bn4 != nullptr && dA == nullptr)               // stats pass of the two-pass backward
+    HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK, true, false>), dim3(nblocks), dim3(256), 0,
+                                         st, a, Wh, bh, labels, gscale, stats3, dA, dW_partial, P,
+                                         ignore_index, bn4, bnpart, K));
+  else if (bn4 != nullptr)
     HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK, true>), dim3(nblocks), dim3(256), 0,
                                          st, a, Wh, bh, labels, gscale, stats3, dA, dW_partial, P,
                                          ignore_index, bn4, bnpart, K));
@@ -388,6 +486,22 @@ void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
     HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK, false>), dim3(nblocks), dim3(256), 0,
                                          st, a, Wh, bh, labels, gscale, stats3, dA, dW_partial, P,
                                          ignore_index, bn4, bnpart, K));
+}
+
+int head_bn_apply_blocks(long long P, int C) {
+  const long long ppb = 256 / (C / 8);
+  static const int cap = [] { const char* e = getenv("DDLPC_HEAD_APPLY_BLOCKS"); return e ? atoi(e) : 4096; }();
+  return (int)std::max<long long>(1, std::min<long long>((P + 2 * ppb - 1) / (2 * ppb), cap));
+}
+
+void head_bn_apply_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
+                          const float* gscale, const float* stats3, const float* bn4,
+                          const float* coefs, bf16_t* dY, long long P, int C, int K,
+                          int ignore_index, hipStream_t st) {
+  const int nb = head_bn_apply_blocks(P, C);
+  HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_bn_apply_kernel<CC, KK>), dim3(nb), dim3(256), 0, st,
+                                       a, Wh, bh, labels, gscale, stats3, bn4, coefs, dY, P,
+                                       ignore_index, K));
 }
 
 void head_logits_launch(const bf16_t* a, const float* Wh, const float* bh, float* logits,

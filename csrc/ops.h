@@ -107,6 +107,7 @@ struct GemmArgs {
   const float* bn4;
   const bf16_t* bny;
   float* bnpart;
+  int wg2;                        // WGRAD: 1 = gemm_tn_wgrad2_kernel (tile from convt_wgrad2_tiles)
 };
 enum GemmMode {
   GEMM_CONVT_FWD = 0,   // A = x[px][Cin], B = Wt[(sub, co)][Cin] -> scatter to 2x up, + bias
@@ -114,6 +115,7 @@ enum GemmMode {
   GEMM_CONVT_WGRAD = 2, // TN: dW[ci][(sub, co)] = sum_px x[px][ci] * dOut[up(px, sub)][co]
 };
 void gemm_launch(GemmArgs& a, hipStream_t st);
+int convt_wgrad2_tiles(const GemmArgs& a);
 // resident-weight transposed-conv forward / data gradient (convt_res.hip): rows = BN-backward
 // partial rows the DGRAD launch writes (0: shape not covered -> gemm_launch)
 int convt_res_rows(const GemmArgs& a, int num_cus);
@@ -149,6 +151,13 @@ void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
                         const float* gscale, const float* stats3, int unused, bf16_t* dA,
                         float* dW_partial, int nblocks, long long P, int C, int K,
                         int ignore_index, const float* bn4, float* bnpart, hipStream_t st);
+// two-pass backward with the deferred BatchNorm of the last decoder block: dA == nullptr in
+// head_ce_bwd_launch runs the stats pass (dWh, dbh, BN partials); this second pass
+// recomputes dA and writes that BatchNorm's dY (coefs = [k | m1 | m2] x C)
+void head_bn_apply_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
+                          const float* gscale, const float* stats3, const float* bn4,
+                          const float* coefs, bf16_t* dY, long long P, int C, int K,
+                          int ignore_index, hipStream_t st);
 void head_logits_launch(const bf16_t* a, const float* Wh, const float* bh, float* logits_nchw,
                         long long P, long long HW, int C, int K, const float* bn4, hipStream_t st);
 

@@ -24,7 +24,8 @@ Execution model (SURVEY.md §2.5 kernel inventory -> fusion plan):
   once (it is the skip tensor / next input);
 * ``ConvTranspose(2, 2)`` is a GEMM with a pixel-shuffle epilogue (``_ConvTFn``);
 * the 1x1 head, softmax cross-entropy, its gradient and the pixel-accuracy count are one
-  fused kernel pair (``_HeadCEFn``): logits never reach HBM in training.
+  fused kernel pair (``_HeadCEFn``): logits never reach HBM in training; its backward is
+  two passes (stats, then recompute + the last block's BN backward: dA never stored).
 
 Conv biases feeding a training-mode BatchNorm receive an exactly-zero gradient (the BN
 mean subtraction cancels them); stock PyTorch returns float noise of ~1e-9 there.
@@ -186,7 +187,9 @@ class _DoubleConvFn(torch.autograd.Function):
         blk = ctx.blk
         eng = blk.engine
         x2 = x2 if ctx.has_x2 else None
-        if da2 is not None:
+        # head gradient still to be formed (two-pass head backward, see _HeadCEFn)
+        head = getattr(da2, "_ddlpc_head", None) if (ctx.defer and da2 is not None) else None
+        if da2 is not None and head is None:
             da2 = da2.contiguous()
         if dpool is not None:
             dpool = dpool.contiguous()
@@ -206,14 +209,20 @@ class _DoubleConvFn(torch.autograd.Function):
         direct = eng.direct_grads
         # ---- second conv: BN2 + ReLU (+ unpool + skip sum) backward, then its gradients
         if direct:
-            dy2, _, _ = F.bn_backward(da2, dpool, y2, s2, g2, None, bn2.weight.grad, bn2.bias.grad,
-                                      part2)
+            if head is not None:
+                dy2, _, _ = F.head_ce_bn_bwd(*head, s2, part2, g2, bn2.weight.grad, bn2.bias.grad)
+            else:
+                dy2, _, _ = F.bn_backward(da2, dpool, y2, s2, g2, None, bn2.weight.grad,
+                                          bn2.bias.grad, part2)
             with eng.wgrad_stream(dy2, y1, s1):
                 F.conv3_wgrad(dy2, y1, None, s1[2], s1[3], blk.conv2.weight.grad)
                 eng.ready(bn2.weight, bn2.bias, blk.conv2.weight, blk.conv2.bias)
             dg2 = dbe2 = dw2 = None
         else:
-            dy2, dg2, dbe2 = F.bn_backward(da2, dpool, y2, s2, g2, None, None, None, part2)
+            if head is not None:
+                dy2, dg2, dbe2 = F.head_ce_bn_bwd(*head, s2, part2, g2, None, None)
+            else:
+                dy2, dg2, dbe2 = F.bn_backward(da2, dpool, y2, s2, g2, None, None, None, part2)
             dw2 = F.conv3_wgrad(dy2, y1, None, s1[2], s1[3]).view_as(blk.conv2.weight)
         p1, p2 = blk.pack1, blk.pack2
         part1 = None
@@ -331,16 +340,25 @@ class _HeadCEFn(torch.autograd.Function):
         bn = bn if ctx.has_bn else None
         gs = dloss.reshape(1).float().contiguous() if dloss is not None else None
         eng = ctx.engine
+        # two-pass backward with the deferred BatchNorm: this pass reduces dWh, dbh and the
+        # BN partials without storing dA; the block's backward then runs head_ce_bn_bwd,
+        # which recomputes dA and applies the BatchNorm backward in registers (no dA
+        # round trip through HBM, no separate BN-apply pass).  DDLPC_HEAD_APPLY=0: one pass
+        two_pass = bn is not None and eng.head_apply
         if eng.direct_grads:
             head = eng.head
             da, _, _, part = _ops().head_ce_bwd(a, wh, bh, labels, out3, gs, ctx.ignore_index,
-                                                head.weight.grad, head.bias.grad, bn)
+                                                head.weight.grad, head.bias.grad, bn, not two_pass)
             with eng.wgrad_stream():
                 eng.ready(head.weight, head.bias)
             dw = db = None
         else:
             da, dw, db, part = _ops().head_ce_bwd(a, wh, bh, labels, out3, gs, ctx.ignore_index,
-                                                  None, None, bn)
+                                                  None, None, bn, not two_pass)
+        if two_pass:
+            # stand-in gradient of the right shape (no storage); the consumer recognises it
+            da = torch.zeros((), dtype=a.dtype, device=a.device).expand(a.shape)
+            da._ddlpc_head = (a, wh, bh, labels, out3, gs, ctx.ignore_index)
         if bn is not None:
             da._ddlpc_bn_partial = part
         return da, dw, db, None, None, None, None
@@ -456,6 +474,9 @@ class UNetEngine:
         # BN1 backward's reduction pass fused into the epilogue of the data gradient that
         # produces its input gradient (2-D; DDLPC_BNB_EPI=0: separate reduction kernel)
         self.bnb_epilogue = os.environ.get("DDLPC_BNB_EPI", "1") != "0"
+        # two-pass head backward with the last block's BN backward fused into the second
+        # pass (see _HeadCEFn.backward; DDLPC_HEAD_APPLY=0: dA stored + separate BN apply)
+        self.head_apply = os.environ.get("DDLPC_HEAD_APPLY", "1") != "0"
         self.enc = [_Block(b.double_conv, first=(i == 0), engine=self)
                     for i, b in enumerate(model.down_blocks())]
         self.mid = _Block(model.double_conv, first=False, engine=self)

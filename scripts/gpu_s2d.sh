@@ -1,0 +1,24 @@
+#!/bin/bash
+# round 2 session 2, pass D: convT weight gradient v2 with a 3/4-stage DMA ring: numerics,
+# micro A/B vs v1, overlapped-schedule kernel trace (both streams)
+set -o pipefail
+cd "$(dirname "$0")/.."
+O=gpurun_out/${PASS:-s2d}
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -q --timeout 150 --timeout-method thread tests/test_kernels_gpu.py -k "convt or deferred or out_params" > $O/pytest_k.log 2>&1 || { tail -40 $O/pytest_k.log; exit 1; }
+tail -2 $O/pytest_k.log
+timeout -k 10 200 python -u scripts/conv_micro.py --batch 128 --passes twgrad > $O/micro_v2.txt 2>&1 || { tail -20 $O/micro_v2.txt; exit 1; }
+DDLPC_CONVT_WG2=0 timeout -k 10 200 python -u scripts/conv_micro.py --batch 128 --passes twgrad > $O/micro_v1.txt 2>&1 || { tail -20 $O/micro_v1.txt; exit 1; }
+cat $O/micro_v2.txt $O/micro_v1.txt
+run() { local name=$1 to=$2; shift 2; timeout -k 10 $to "$@" > $O/$name.json 2> $O/$name.err; local rc=$?; echo "== $name rc=$rc"; python scripts/summ_bench.py $O/$name.json; [ $rc -eq 0 ] || exit $rc; }
+run bench_w2 200 python -u bench.py
+run bench_w1 200 env DDLPC_CONVT_WG2=0 python -u bench.py
+run bench_w2b 200 python -u bench.py
+run bench_w1b 200 env DDLPC_CONVT_WG2=0 python -u bench.py
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o run -- \
+  python3 bench.py --steps 5 --warmup 3 --schedule serial > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 4; }
+f=$(find $O/prof -name '*kernel_trace.csv' | head -1)
+python scripts/trace_summary.py "$f" 7 > $O/prof_streams.txt 2>&1; python scripts/stream_summary.py "$f" >> $O/prof_streams.txt 2>&1
+cp "$f" $O/serial_trace.csv
+cat $O/prof_streams.txt | head -30

@@ -573,6 +573,38 @@ def test_deferred_bn_consumers_match_materialised(ops, Cin, Cout, H):
     assert torch.equal(ops.head_logits(yh, wh, bh, bnh), ops.head_logits(ah, wh, bh))
 
 
+@pytest.mark.parametrize("C,K,H", [(32, 6, 12), (16, 3, 9), (64, 2, 8), (8, 16, 5)])
+def test_head_two_pass_bn_backward(ops, C, K, H):
+    """Two-pass head backward (stats pass without the dA store, then head_ce_bn_bwd: dA
+    recomputed and the deferred BatchNorm's backward applied in registers) equals the
+    one-pass path — head_ce_bwd storing dA, then bn_backward on it with the same partials —
+    bit for bit: dWh, dbh, the BN partials, dgamma, dbeta and dY.  Odd H leaves a partial
+    pixel pair / workgroup step; ignore_index pixels included."""
+    torch.manual_seed(5)
+    N, W = 2, H + 3
+    yh = torch.randn(N, H, W, C, device=DEV).bfloat16()
+    bnh = _bn4(C, 3)
+    wh = torch.randn(K, C, device=DEV) * 0.3
+    bh = torch.randn(K, device=DEV) * 0.1
+    lab = torch.randint(0, K, (N, H, W), device=DEV)
+    lab[0, 0, :2] = -100
+    o = ops.head_ce_fwd(yh, wh, bh, lab, -100, bnh)
+    gs = torch.tensor([0.75], device=DEV)
+    gamma = torch.rand(C, device=DEV) + 0.5
+    da1, dw1, db1, part1 = ops.head_ce_bwd(yh, wh, bh, lab, o, gs, -100, None, None, bnh)
+    d0, dw2, db2, part2 = ops.head_ce_bwd(yh, wh, bh, lab, o, gs, -100, None, None, bnh, False)
+    assert d0.numel() == 0
+    assert torch.equal(dw1, dw2) and torch.equal(db1, db2) and torch.equal(part1, part2)
+    ref = ops.bn_backward(da1, None, yh, bnh, gamma, None, None, None, part1)
+    got = ops.head_ce_bn_bwd(yh, wh, bh, lab, o, gs, -100, bnh, part2, gamma)
+    for u, v in zip(got, ref):
+        assert torch.equal(u, v)
+    # accumulate into caller buffers (direct-grad mode)
+    dgo, dbo = torch.ones(C, device=DEV), torch.ones(C, device=DEV)
+    ops.head_ce_bn_bwd(yh, wh, bh, lab, o, gs, -100, bnh, part2, gamma, dgo, dbo)
+    assert torch.allclose(dgo, ref[1] + 1) and torch.allclose(dbo, ref[2] + 1)
+
+
 def test_out_params_respect_bounds(ops):
     """Kernels that write into caller-provided buffers (in training: views into the one flat
     fp32 gradient buffer) are given views into sentinel-filled guard buffers; the guard
