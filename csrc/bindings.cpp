@@ -298,7 +298,9 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   if (a.pscale2) TORCH_CHECK(dual && a.pshift2 && a.C1 + a.C2 <= 512, "X2 prologue: x2, pscale2/pshift2, C1 + C2 <= 512");
   const int bco = a.Cout <= 32 ? 32 : 64;
   static const int use_v2 = [] { const char* e = getenv("DDLPC_WGRAD_V2"); return e ? atoi(e) : 1; }();
-  const bool v2 = use_v2 && (use_v2 != 2 || g.dims == 2) && g.W >= 16 && (a.C2 == 0 || a.C1 % 32 == 0);
+  // (images narrower than the 16-pixel tile rows run with masked columns: DDLPC_WGRAD_MINW)
+  static const int min_w = [] { const char* e = getenv("DDLPC_WGRAD_MINW"); return e ? atoi(e) : 16; }();
+  const bool v2 = use_v2 && (use_v2 != 2 || g.dims == 2) && g.W >= min_w && (a.C2 == 0 || a.C1 % 32 == 0);
   // v3 (32x32x16 MFMA, conflict-free transposed reads): whole 32-channel input chunks
   static const int use_v3 = [] { const char* e = getenv("DDLPC_WGRAD_V3"); return e ? atoi(e) : 1; }();
   // (the large 64-channel concat layers stay on v2's 96-pixel tiles: 4-5% faster there)
