@@ -299,7 +299,8 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   const int bco = a.Cout <= 32 ? 32 : 64;
   static const int use_v2 = [] { const char* e = getenv("DDLPC_WGRAD_V2"); return e ? atoi(e) : 1; }();
   // (images narrower than the 16-pixel tile rows run with masked columns: DDLPC_WGRAD_MINW)
-  static const int min_w = [] { const char* e = getenv("DDLPC_WGRAD_MINW"); return e ? atoi(e) : 16; }();
+  // (8: the 8x8 bottleneck layers, 10% faster than the v1 kernel there)
+  static const int min_w = [] { const char* e = getenv("DDLPC_WGRAD_MINW"); return e ? atoi(e) : 8; }();
   const bool v2 = use_v2 && (use_v2 != 2 || g.dims == 2) && g.W >= min_w && (a.C2 == 0 || a.C1 % 32 == 0);
   // v3 (32x32x16 MFMA, conflict-free transposed reads): whole 32-channel input chunks
   static const int use_v3 = [] { const char* e = getenv("DDLPC_WGRAD_V3"); return e ? atoi(e) : 1; }();
@@ -550,6 +551,106 @@ std::vector<at::Tensor> convt_dgrad(const at::Tensor& dout, const at::Tensor& wd
   return {dx, bnpart};
 }
 
+// bias gradient of a transposed conv: per-channel sum of dOut.  When dOut came out of a
+// conv3 data-gradient epilogue, its per-workgroup channel sums are already there (rows
+// [R][2][Ctot], sum part first): reduce those instead of re-reading dOut.
+static at::Tensor convt_bias_grad(const at::Tensor& x, const at::Tensor& dout, const Geo& go,
+                                  const c10::optional<at::Tensor>& colsum_rows,
+                                  const c10::optional<at::Tensor>& db_out, bool into) {
+  auto fopts = x.options().dtype(at::kFloat);
+  at::Tensor db = into ? *db_out : at::empty({go.C}, fopts);
+  if (colsum_rows.has_value() && colsum_rows->defined() && colsum_rows->numel() > 0) {
+    const at::Tensor& cr = *colsum_rows;
+    TORCH_CHECK(cr.dim() == 3 && cr.size(1) == 2 && cr.size(2) >= go.C, "colsum rows [R][2][C]");
+    const int R = (int)cr.size(0);
+    at::Tensor ctmp = R > 64 ? at::empty({(int64_t)((R + 63) / 64) * go.C}, x.options().dtype(at::kDouble))
+                             : at::empty({0}, x.options().dtype(at::kDouble));
+    reduce_rows_scatter_launch(cr.data_ptr<float>(), R, go.C, ctmp.data_ptr<double>(),
+                               db.data_ptr<float>(), 2, 0, 0, 0, into, cur_stream(), 2 * cr.size(2));
+  } else {
+    const long long P = (long long)go.N * go.D * go.H * go.W;
+    const int nb = (int)std::max<long long>(1, std::min<long long>((P + 1023) / 1024, 1024));
+    at::Tensor cpart = at::empty({nb, go.C}, fopts);
+    channel_sum_launch(bptr(dout), P, go.C, cpart.data_ptr<float>(), nb, cur_stream());
+    at::Tensor ctmp = nb > 64 ? at::empty({(int64_t)((nb + 63) / 64) * go.C},
+                                          x.options().dtype(at::kDouble))
+                              : at::empty({0}, x.options().dtype(at::kDouble));
+    reduce_rows_scatter_launch(cpart.data_ptr<float>(), nb, go.C, ctmp.data_ptr<double>(),
+                               db.data_ptr<float>(), 2, 0, 0, 0, into, cur_stream());
+  }
+  return db;
+}
+
+// Fused data + weight gradient of a 2-D 64 -> 64-channel transposed conv (dOut read once):
+// returns {dx, bnpart (deferred BN of x: [R][2][64] rows, else empty), dW, db} (dW / db
+// accumulated into the outs when given, empty then).  Other shapes: the separate kernels.
+std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
+                                    const c10::optional<at::Tensor>& dw_out,
+                                    const c10::optional<at::Tensor>& db_out,
+                                    const c10::optional<at::Tensor>& colsum_rows,
+                                    const c10::optional<at::Tensor>& bn4);
+
+bool convt_bwd_fused_ok(const at::Tensor& x, const at::Tensor& dout) {
+  if (x.dim() != 4 || dout.dim() != 4 || x.size(3) != 64 || dout.size(3) != 64) return false;
+  if (dout.size(1) != 2 * x.size(1) || dout.size(2) != 2 * x.size(2)) return false;
+  static const int on = [] { const char* e = getenv("DDLPC_CONVT_FUSED"); return e ? atoi(e) : 1; }();
+  if (!on) return false;
+  const long long K = x.size(0) * x.size(1) * x.size(2);
+  if (K * 4 >= (long long)INT32_MAX) return false;
+  // one buffer descriptor per split over its dOut rows (32-bit offsets)
+  const long long splits = std::max<long long>(1, std::min<long long>(2LL * num_cus(), K / 128));
+  const long long per = (K + splits - 1) / splits + 64;
+  return (4 * per + 8LL * x.size(2)) * 64 * 2 < (1LL << 31);
+}
+
+std::vector<at::Tensor> convt_bwd_fused(const at::Tensor& x, const at::Tensor& dout, const at::Tensor& wd,
+                                        const c10::optional<at::Tensor>& dw_out,
+                                        const c10::optional<at::Tensor>& db_out,
+                                        const c10::optional<at::Tensor>& colsum_rows,
+                                        const c10::optional<at::Tensor>& bn4) {
+  CHECK_DEV(x); CHECK_CONTIG(x); CHECK_BF16(x); CHECK_CONTIG(dout); CHECK_BF16(dout);
+  CHECK_BF16(wd); CHECK_CONTIG(wd);
+  c10::DeviceGuard guard(x.device());
+  const bool into = dw_out.has_value() && dw_out->defined();
+  auto fopts = x.options().dtype(at::kFloat);
+  if (!convt_bwd_fused_ok(x, dout)) {
+    const bool has_bn = bn4.has_value() && bn4->defined();
+    auto r = convt_dgrad(dout, wd, x.size(3), has_bn ? c10::optional<at::Tensor>(x) : c10::nullopt, bn4);
+    auto w = convt_wgrad(x, dout, dw_out, db_out, colsum_rows, bn4);
+    return {r[0], r[1], w[0], w[1]};
+  }
+  TORCH_CHECK(wd.numel() == 64 * 256, "convt_bwd_fused: packed dgrad weights must be [64][256]");
+  const Geo g = geo_of(x);
+  const Geo go = geo_of(dout);
+  GemmArgs a{};
+  a.mode = GEMM_CONVT_WGRAD;
+  a.M = 64; a.N = 256;
+  a.K = g.N * g.H * g.W;
+  a.A = bptr(x);
+  a.B = bptr(dout);
+  a.Wd2 = bptr(wd);
+  a.dims = 2; a.Nimg = g.N; a.D = 1; a.H = g.H; a.W = g.W;
+  a.Cin = 64; a.Cout = 64;
+  a.bn4 = bn4_ptr(bn4, 64);
+  a.splits = (int)std::max<long long>(1, std::min<long long>(2LL * num_cus(), (long long)a.K / 128));
+  at::Tensor dx = at::empty_like(x);
+  a.C = dx.data_ptr();
+  at::Tensor part = at::empty({(int64_t)a.splits * 64 * 256}, fopts);
+  a.partial = part.data_ptr<float>();
+  at::Tensor bnpart = at::empty({a.bn4 != nullptr ? (int64_t)a.splits : 0, 2, 64}, fopts);
+  if (a.bn4 != nullptr) a.bnpart = bnpart.data_ptr<float>();
+  convt_bwd_fused_launch(a, cur_stream());
+  at::Tensor dW = into ? *dw_out : at::empty({64, 64, 2, 2}, fopts);
+  const long long NW = 64LL * 256;
+  at::Tensor tmp = a.splits > 64 ? at::empty({(int64_t)((a.splits + 63) / 64) * NW}, x.options().dtype(at::kDouble))
+                                 : at::empty({0}, x.options().dtype(at::kDouble));
+  reduce_rows_scatter_launch(part.data_ptr<float>(), a.splits, NW, tmp.data_ptr<double>(),
+                             dW.data_ptr<float>(), 1, 64, 4, 64, into, cur_stream());
+  at::Tensor db = convt_bias_grad(x, dout, go, colsum_rows, db_out, into);
+  if (into) return {dx, bnpart, at::empty({0}, fopts), at::empty({0}, fopts)};
+  return {dx, bnpart, dW, db};
+}
+
 std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
                                     const c10::optional<at::Tensor>& dw_out,
                                     const c10::optional<at::Tensor>& db_out,
@@ -605,29 +706,7 @@ std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
                                : at::empty({0}, x.options().dtype(at::kDouble));
   reduce_rows_scatter_launch(part.data_ptr<float>(), splits, NW, tmp.data_ptr<double>(),
                              dW.data_ptr<float>(), 1, g.C, S, go.C, into, cur_stream());
-  // bias gradient: per-channel sum of dOut.  When dOut came out of a conv3 data-gradient
-  // epilogue, its per-workgroup channel sums are already there (rows [R][2][Ctot], sum part
-  // first): reduce those instead of re-reading dOut.
-  at::Tensor db = into ? *db_out : at::empty({go.C}, fopts);
-  if (colsum_rows.has_value() && colsum_rows->defined() && colsum_rows->numel() > 0) {
-    const at::Tensor& cr = *colsum_rows;
-    TORCH_CHECK(cr.dim() == 3 && cr.size(1) == 2 && cr.size(2) >= go.C, "colsum rows [R][2][C]");
-    const int R = (int)cr.size(0);
-    at::Tensor ctmp = R > 64 ? at::empty({(int64_t)((R + 63) / 64) * go.C}, x.options().dtype(at::kDouble))
-                             : at::empty({0}, x.options().dtype(at::kDouble));
-    reduce_rows_scatter_launch(cr.data_ptr<float>(), R, go.C, ctmp.data_ptr<double>(),
-                               db.data_ptr<float>(), 2, 0, 0, 0, into, cur_stream(), 2 * cr.size(2));
-  } else {
-    const long long P = (long long)go.N * go.D * go.H * go.W;
-    const int nb = (int)std::max<long long>(1, std::min<long long>((P + 1023) / 1024, 1024));
-    at::Tensor cpart = at::empty({nb, go.C}, fopts);
-    channel_sum_launch(bptr(dout), P, go.C, cpart.data_ptr<float>(), nb, cur_stream());
-    at::Tensor ctmp = nb > 64 ? at::empty({(int64_t)((nb + 63) / 64) * go.C},
-                                          x.options().dtype(at::kDouble))
-                              : at::empty({0}, x.options().dtype(at::kDouble));
-    reduce_rows_scatter_launch(cpart.data_ptr<float>(), nb, go.C, ctmp.data_ptr<double>(),
-                               db.data_ptr<float>(), 2, 0, 0, 0, into, cur_stream());
-  }
+  at::Tensor db = convt_bias_grad(x, dout, go, colsum_rows, db_out, into);
   if (into) return {at::empty({0}, fopts), at::empty({0}, fopts)};
   return {dW, db};
 }
@@ -949,6 +1028,8 @@ TORCH_LIBRARY(ddlpc, m) {
   m.def("convt_dgrad(Tensor dout, Tensor wd, int cin, Tensor? bny=None, Tensor? bn4=None) -> Tensor[]");
   m.def("convt_wgrad(Tensor x, Tensor dout, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, "
         "Tensor? colsum_rows=None, Tensor? bn4=None) -> Tensor[]");
+  m.def("convt_bwd_fused(Tensor x, Tensor dout, Tensor wd, Tensor(a!)? dw_out=None, "
+        "Tensor(b!)? db_out=None, Tensor? colsum_rows=None, Tensor? bn4=None) -> Tensor[]");
   m.def("head_ce_fwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, int ignore_index, Tensor? bn4=None) -> Tensor");
   m.def("head_ce_bwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, Tensor out3, Tensor? gscale, "
         "int ignore_index, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, Tensor? bn4=None, "
@@ -982,6 +1063,7 @@ TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
   m.impl("convt_fwd", &ddlpc::convt_fwd);
   m.impl("convt_dgrad", &ddlpc::convt_dgrad);
   m.impl("convt_wgrad", &ddlpc::convt_wgrad);
+  m.impl("convt_bwd_fused", &ddlpc::convt_bwd_fused);
   m.impl("head_ce_fwd", &ddlpc::head_ce_fwd);
   m.impl("head_ce_bwd", &ddlpc::head_ce_bwd);
   m.impl("head_ce_bn_bwd", &ddlpc::head_ce_bn_bwd);

@@ -183,13 +183,20 @@ DDLPC_DEVICE void head_pixel(const uint4 av, const int64_t lab, const float* __r
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] = DEFER ? fmaxf(fmaf(y8[j], sc[j], sh[j]), 0.f) : y8[j];
   if (DEFER) unpack8(pack8(f), f);                // the activation rounded as materialised
+  // packed f32 math (v_pk_fma_f32: two channels per instruction) — this kernel pair is
+  // VALU-issue bound; the per-channel operation order of dA and dWh is unchanged
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  const f2_t* w2 = reinterpret_cast<const f2_t*>(w);
+  f2_t f2[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) f2[jj] = f2_t{f[2 * jj], f[2 * jj + 1]};
   float z[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    float t = 0.f;
+    f2_t t2 = f2_t{0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < 8; ++j) t = fmaf(f[j], w[k * C + j], t);
-    z[k] = t;
+    for (int jj = 0; jj < 4; ++jj) t2 = __builtin_elementwise_fma(f2[jj], w2[(k * C) / 2 + jj], t2);
+    z[k] = t2.x + t2.y;
   }
 #pragma unroll
   for (int o = 1; o < G; o <<= 1)
@@ -204,14 +211,15 @@ DDLPC_DEVICE void head_pixel(const uint4 av, const int64_t lab, const float* __r
   const float inv = 1.f / se;
 #pragma unroll
   for (int k = 0; k < K; ++k) d[k] = lab != ignore_index ? (z[k] * inv - (k == lab ? 1.f : 0.f)) * gs : 0.f;
-  float o8[8];
+  f2_t o2[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float t = 0.f;
+  for (int jj = 0; jj < 4; ++jj) o2[jj] = f2_t{0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < K; ++k) t = fmaf(d[k], w[k * C + j], t);
-    o8[j] = t;
-  }
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+      o2[jj] = __builtin_elementwise_fma(f2_t{d[k], d[k]}, w2[(k * C) / 2 + jj], o2[jj]);
+  const float o8[8] = {o2[0].x, o2[0].y, o2[1].x, o2[1].y, o2[2].x, o2[2].y, o2[3].x, o2[3].y};
   pk = pack8(o8);
 }
 
@@ -272,10 +280,18 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
     head_pixel<C, K, DEFER>(a_cur, lab, sW + opaque_zero() + c8, bk, sc, sh, gs, ignore_index,
                             y8, f, d, pk);
     if (STORE) *reinterpret_cast<uint4*>(dA + px * C + c8) = pk;
+    {
+      typedef float f2_t __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int k = 0; k < K; ++k)
+      for (int k = 0; k < K; ++k)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[k * 8 + j] = fmaf(f[j], d[k], acc[k * 8 + j]);
+        for (int jj = 0; jj < 4; ++jj) {
+          const f2_t r = __builtin_elementwise_fma(f2_t{f[2 * jj], f[2 * jj + 1]}, f2_t{d[k], d[k]},
+                                                   f2_t{acc[k * 8 + 2 * jj], acc[k * 8 + 2 * jj + 1]});
+          acc[k * 8 + 2 * jj] = r.x;
+          acc[k * 8 + 2 * jj + 1] = r.y;
+        }
+    }
     if (cg == 0) {
 #pragma unroll
       for (int k = 0; k < K; ++k) acc[8 * K + k] += d[k];

@@ -108,6 +108,7 @@ struct GemmArgs {
   const bf16_t* bny;
   float* bnpart;
   int wg2;                        // WGRAD: 1 = gemm_tn_wgrad2_kernel (tile from convt_wgrad2_tiles)
+  const bf16_t* Wd2;              // fused backward: packed data-gradient weights [Cin][S*Cout]
 };
 enum GemmMode {
   GEMM_CONVT_FWD = 0,   // A = x[px][Cin], B = Wt[(sub, co)][Cin] -> scatter to 2x up, + bias
@@ -116,6 +117,10 @@ enum GemmMode {
 };
 void gemm_launch(GemmArgs& a, hipStream_t st);
 int convt_wgrad2_tiles(const GemmArgs& a);
+// fused data + weight gradient of a 2-D 64 -> 64-channel transposed conv (convt_gemm.hip):
+// A = x [px][64], B = dOut, C = dx [px][64] (bf16), Wd2 = packed dgrad weights, partial =
+// [splits][64][256] weight-gradient slab, bn4/bnpart = deferred BN of x and its partial rows
+void convt_bwd_fused_launch(GemmArgs& a, hipStream_t st);
 // resident-weight transposed-conv forward / data gradient (convt_res.hip): rows = BN-backward
 // partial rows the DGRAD launch writes (0: shape not covered -> gemm_launch)
 int convt_res_rows(const GemmArgs& a, int num_cus);

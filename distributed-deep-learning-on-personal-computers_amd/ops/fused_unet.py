@@ -287,15 +287,31 @@ class _ConvTFn(torch.autograd.Function):
         x, bn = ctx.saved_tensors
         bn = bn if ctx.has_bn else None
         dout = dout.contiguous()
+        eng = ctx.engine
+        conv = ctx.pack.conv
+        rows = getattr(dout, "_ddlpc_colsum_rows", None)
+        if (eng.convt_fused and ctx.needs_input_grad[0] and x.dim() == 4 and x.shape[-1] == 64
+                and ctx.pack.cout == 64):
+            # 64 -> 64-channel 2-D transposed conv (the 256^2 level): one kernel reads dOut
+            # once for both gradients (convt_bwd_fused; other shapes fall back inside)
+            if eng.direct_grads:
+                dx, part, _, _ = F.convt_bwd_fused(x, dout, ctx.pack.dgrad, conv.weight.grad,
+                                                   conv.bias.grad, rows, bn)
+                with eng.wgrad_stream():
+                    eng.ready(conv.weight, conv.bias)
+                dw = db = None
+            else:
+                dx, part, dw, db = F.convt_bwd_fused(x, dout, ctx.pack.dgrad, None, None, rows, bn)
+                dw = dw.view_as(conv.weight)
+            if bn is not None:
+                dx._ddlpc_bn_partial = part
+            return dx, dw, db, None, None, None
         dx = None
         if ctx.needs_input_grad[0]:
             dx, part = F.convt_dgrad(dout, ctx.pack.dgrad, ctx.pack.cin, x if bn is not None else None,
                                      bn)
             if bn is not None:
                 dx._ddlpc_bn_partial = part
-        conv = ctx.pack.conv
-        rows = getattr(dout, "_ddlpc_colsum_rows", None)
-        eng = ctx.engine
         if eng.direct_grads:
             if eng.side_convt:
                 with eng.wgrad_stream(x, dout, rows, bn):
@@ -477,6 +493,9 @@ class UNetEngine:
         # two-pass head backward with the last block's BN backward fused into the second
         # pass (see _HeadCEFn.backward; DDLPC_HEAD_APPLY=0: dA stored + separate BN apply)
         self.head_apply = os.environ.get("DDLPC_HEAD_APPLY", "1") != "0"
+        # 64 -> 64-channel transposed conv: data + weight gradient in one kernel
+        # (DDLPC_CONVT_FUSED=0: separate kernels, weight gradient on the side stream)
+        self.convt_fused = os.environ.get("DDLPC_CONVT_FUSED", "1") != "0"
         self.enc = [_Block(b.double_conv, first=(i == 0), engine=self)
                     for i, b in enumerate(model.down_blocks())]
         self.mid = _Block(model.double_conv, first=False, engine=self)

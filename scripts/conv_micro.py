@@ -113,7 +113,10 @@ def main():
                "tfwdbn": lambda: F.convt_fwd(x, pk.fwd, b, C, bn4),
                "tdgrad": lambda: F.convt_dgrad(dout, pk.dgrad, C)[0],
                "tdgradbn": lambda: F.convt_dgrad(dout, pk.dgrad, C, x, bn4)[0],
-               "twgrad": lambda: F.convt_wgrad(x, dout)}
+               "twgrad": lambda: F.convt_wgrad(x, dout),
+               # full backward with the deferred BN: fused kernel vs the separate pair
+               "tbwdf": lambda: F.convt_bwd_fused(x, dout, pk.dgrad, None, None, None, bn4),
+               "tbwds": lambda: (F.convt_dgrad(dout, pk.dgrad, C, x, bn4), F.convt_wgrad(x, dout, None, None, None, bn4))}
         for ps in tpasses:
             fn = fns[ps]
             fn()

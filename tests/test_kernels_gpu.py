@@ -440,6 +440,47 @@ def test_trilinear_3d(ops):
     assert rel_err(nchw(dx), gx) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W,bn", [(2, 16, 16, False), (3, 12, 20, True), (1, 40, 24, True),
+                                      (4, 8, 8, True)])
+def test_convt_bwd_fused(ops, N, H, W, bn):
+    """Fused data + weight gradient of the 64 -> 64 transposed conv (dOut read once) against
+    the separate kernels (dx and the BN partials bit for bit: same MFMA k order is not
+    guaranteed, so dx to bf16 rounding; dW / db / partials to fp32 tolerance) and fp32 torch.
+    Odd pixel counts leave partial 32-pixel stages; the deferred BN of x is applied to the
+    weight-gradient operand in registers."""
+    torch.manual_seed(21)
+    C = 64
+    x = torch.randn(N, H, W, C, device=DEV).bfloat16()
+    w = torch.randn(C, C, 2, 2, device=DEV) / math.sqrt(C)
+    pk = pack_conv(ops, w)
+    dout = torch.randn(N, 2 * H, 2 * W, C, device=DEV).bfloat16()
+    bn4 = _bn4(C, 7) if bn else None
+    dx, part, dw, db = ops.convt_bwd_fused(x, dout, pk.dgrad, None, None, None, bn4)
+    rdx, rpart = ops.convt_dgrad(dout, pk.dgrad, C, x if bn else None, bn4)
+    rdw, rdb = ops.convt_wgrad(x, dout, None, None, None, bn4)
+    assert rel_err(dx, rdx) < 1e-2
+    assert rel_err(dw, rdw) < 1e-4 and rel_err(db, rdb) < 1e-5
+    # vs fp32 torch (deferred BN: the activation relu(x*scale+shift) rounded to bf16)
+    xa = ops.bn_relu_apply(x, bn4, False)[0] if bn else x
+    xr = xa.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.bfloat16().float().requires_grad_(True)
+    ref = F.conv_transpose2d(xr, wr, None, stride=2)
+    gx, gw = torch.autograd.grad(ref, [xr, wr], dout.float().permute(0, 3, 1, 2))
+    assert rel_err(dw, gw) < 5e-3
+    if not bn:
+        assert rel_err(dx.permute(0, 3, 1, 2), gx) < 1e-2
+        return
+    gamma = torch.rand(C, device=DEV) + 0.5
+    a = ops.bn_backward(dx, None, x, bn4, gamma, None, None, None, part)
+    b = ops.bn_backward(dx, None, x, bn4, gamma, None)
+    for u, v in zip(a, b):
+        assert rel_err(u, v) < 2e-3
+    # into caller buffers (direct grads): accumulated
+    dwo, dbo = torch.ones_like(dw), torch.ones_like(db)
+    ops.convt_bwd_fused(x, dout, pk.dgrad, dwo, dbo, None, bn4)
+    assert torch.allclose(dwo, dw + 1, atol=1e-5) and torch.allclose(dbo, db + 1, atol=1e-5)
+
+
 @pytest.mark.parametrize("N,D,H,W,Cin,Cout", [(1, 4, 4, 8, 64, 64), (2, 4, 8, 8, 128, 64)])
 def test_convt3d(ops, N, D, H, W, Cin, Cout):
     """ConvTranspose3d(k2, s2) forward / data / weight gradients vs fp32 torch."""
