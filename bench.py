@@ -275,6 +275,9 @@ def main():
                        "schedule_probe_ms": ({k: (round(v, 3) if isinstance(v, float) else v)
                                               for k, v in sched.items() if k.endswith("_ms")}
                                              if sched else None),
+                       "schedule_probe_alloc_retries": ({k: v for k, v in sched.items()
+                                                         if k.endswith("_alloc_retries")}
+                                                        if sched else None),
                        "bucket_mb": args.bucket_mb,
                        "buckets": len(red.buckets) if red is not None else 0,
                        "wire_dtype": args.wire_dtype, "grad_codec": args.codec,

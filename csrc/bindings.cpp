@@ -272,7 +272,10 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
                        const c10::optional<at::Tensor>& pshift,
                        const c10::optional<at::Tensor>& out,
                        const c10::optional<at::Tensor>& pscale2,
-                       const c10::optional<at::Tensor>& pshift2) {
+                       const c10::optional<at::Tensor>& pshift2,
+                       const c10::optional<at::Tensor>& dy_y,
+                       const c10::optional<at::Tensor>& dy_s4,
+                       const c10::optional<at::Tensor>& dy_coefs) {
   CHECK_DEV(dy); CHECK_CONTIG(dy); CHECK_BF16(dy); CHECK_CONTIG(x1); CHECK_BF16(x1);
   c10::DeviceGuard guard(dy.device());
   const Geo g = geo_of(x1);
@@ -310,6 +313,19 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   // 128-pixel tiles (v2: 16 x conv3_wgrad2_pt/16; v3: 256 for 32 output channels, else 128)
   // (DDLPC_WGRAD3_PT64 = 96 | 128: pixel tile of the 64-channel v3 kernel; default 128)
   static const int v3_pt64 = [] { const char* e = getenv("DDLPC_WGRAD3_PT64"); return e ? atoi(e) : 128; }();
+  if (dy_y.has_value() && dy_y->defined()) {
+    // dy holds dA; BN backward applied on load (v2 kernel only)
+    CHECK_CONTIG(*dy_y); CHECK_BF16(*dy_y);
+    TORCH_CHECK(v2 && !v3 && g.dims == 2 && dy_y->numel() == dy.numel(),
+                "conv3_wgrad: the dY prologue needs the v2 kernel (2-D, C1 % 32 != 0 or a 32-channel "
+                "first layer) and y of dY's shape");
+    TORCH_CHECK(dy_s4.has_value() && dy_s4->numel() == 4 * a.Cout && dy_coefs.has_value() &&
+                dy_coefs->numel() == 3 * a.Cout, "conv3_wgrad: dy_s4 [4][Cout] and dy_coefs [3][Cout]");
+    CHECK_F32(*dy_s4); CHECK_F32(*dy_coefs);
+    a.dyy = bptr(*dy_y);
+    a.dys4 = dy_s4->data_ptr<float>();
+    a.dycoef = dy_coefs->data_ptr<float>();
+  }
   if (v3) { a.TD = 1; a.TW = 16; a.TH = bco == 32 ? 16 : (v3_pt64 == 96 && a.C2 > 0 ? 6 : 8); }
   else if (v2) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad2_pt(bco, a.C2, g.H, g.W) / 16; }
   else if (g.dims == 2) { a.TD = 1; a.TW = g.W >= 16 ? 16 : 8; a.TH = 128 / a.TW; }
@@ -470,6 +486,39 @@ std::vector<at::Tensor> bn_backward(const c10::optional<at::Tensor>& dA,
   bn_bwd_apply_launch(pA, pP, bptr(y), s + 2 * C, s + 3 * C, s, s + C, coefs.data_ptr<float>(), gs,
                       bptr_mut(dY), g.dims, g.N, g.D, g.H, g.W, C, cur_stream());
   return {dY, dgamma, dbeta};
+}
+
+// BatchNorm backward WITHOUT the apply pass: from precomputed (sum dyh, sum dyh*xhat) rows,
+// dgamma / dbeta (accumulated into the outs when given) and the dY coefficients [k|m1|m2]
+// for a consumer that applies the backward on load (conv3_wgrad's dY prologue)
+std::vector<at::Tensor> bn_grad_coefs(const at::Tensor& partial, const at::Tensor& y,
+                                      const at::Tensor& stats4, const at::Tensor& gamma,
+                                      const c10::optional<at::Tensor>& dgamma_out,
+                                      const c10::optional<at::Tensor>& dbeta_out) {
+  CHECK_F32(partial); CHECK_CONTIG(partial); CHECK_F32(gamma);
+  c10::DeviceGuard guard(partial.device());
+  const Geo g = geo_of(y);
+  const int C = g.C;
+  TORCH_CHECK(partial.numel() % (2 * C) == 0 && partial.numel() > 0, "partial rows must be [R][2][C]");
+  const int nb = (int)(partial.numel() / (2 * C));
+  auto fopts = partial.options();
+  const bool into = dgamma_out.has_value() && dgamma_out->defined();
+  at::Tensor dgamma = into ? *dgamma_out : at::empty({C}, fopts);
+  at::Tensor dbeta = into ? *dbeta_out : at::empty({C}, fopts);
+  at::Tensor coefs = at::empty({3, C}, fopts);
+  const float* s = stats4.data_ptr<float>();
+  const double count = (double)g.N * g.D * g.H * g.W;
+  if (nb <= 2048) {
+    bn_grad_finalize_rows_launch(partial.data_ptr<float>(), nb, C, count, gamma.data_ptr<float>(),
+                                 s + C, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+                                 coefs.data_ptr<float>(), into, cur_stream());
+  } else {
+    at::Tensor sums = reduce_rows(partial, nb, 2 * C);
+    bn_grad_finalize_launch(sums.data_ptr<double>(), C, count, gamma.data_ptr<float>(), s + C,
+                            dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+                            coefs.data_ptr<float>(), into, cur_stream());
+  }
+  return {coefs, dgamma, dbeta};
 }
 
 static const float* bn4_ptr(const c10::optional<at::Tensor>& bn4, int C) {
@@ -1018,10 +1067,13 @@ TORCH_LIBRARY(ddlpc, m) {
         "int cout, int co1, bool stats, Tensor? pscale2=None, Tensor? pshift2=None, Tensor? bnb_y=None, "
         "Tensor? bnb_s4=None) -> Tensor[]");
   m.def("conv3_wgrad(Tensor dy, Tensor x1, Tensor? x2, Tensor? pscale, Tensor? pshift, Tensor(a!)? out=None, "
-        "Tensor? pscale2=None, Tensor? pshift2=None) -> Tensor");
+        "Tensor? pscale2=None, Tensor? pshift2=None, Tensor? dy_y=None, Tensor? dy_s4=None, "
+        "Tensor? dy_coefs=None) -> Tensor");
   m.def("bn_finalize(Tensor partial, float count, Tensor gamma, Tensor beta, Tensor(a!) running_mean, "
         "Tensor(b!) running_var, float momentum, float eps, bool update_running, Tensor(c!)? nbt) -> Tensor");
   m.def("bn_relu_apply(Tensor y, Tensor stats4, bool pool, bool full=True) -> Tensor[]");
+  m.def("bn_grad_coefs(Tensor partial, Tensor y, Tensor stats4, Tensor gamma, "
+        "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None) -> Tensor[]");
   m.def("bn_backward(Tensor? dA, Tensor? dP, Tensor y, Tensor stats4, Tensor gamma, Tensor? gscale, "
         "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None, Tensor? partial=None) -> Tensor[]");
   m.def("convt_fwd(Tensor x, Tensor wt, Tensor? bias, int cout, Tensor? bn4=None) -> Tensor");
@@ -1059,6 +1111,7 @@ TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
   m.impl("conv3_wgrad", &ddlpc::conv3_wgrad);
   m.impl("bn_finalize", &ddlpc::bn_finalize);
   m.impl("bn_relu_apply", &ddlpc::bn_relu_apply);
+  m.impl("bn_grad_coefs", &ddlpc::bn_grad_coefs);
   m.impl("bn_backward", &ddlpc::bn_backward);
   m.impl("convt_fwd", &ddlpc::convt_fwd);
   m.impl("convt_dgrad", &ddlpc::convt_dgrad);

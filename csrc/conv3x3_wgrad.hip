@@ -275,7 +275,7 @@ struct Wg2Cfg {
   static constexpr int X_INSTR = (X_PIECES + 63) / 64;
   static constexpr int X_ITERS = (X_INSTR + 3) / 4;
   static constexpr int X_BYTES = X_INSTR * 1024;
-  static constexpr int SS_BYTES = 2 * 512 * 4;
+  static constexpr int SS_BYTES = 2 * 512 * 4 + 7 * BCO * 4;   // X prologue | dY prologue tables
   static constexpr int SMEM = SS_BYTES + 2 * (Y_BYTES + X_BYTES);
   static constexpr int KSTEPS = PT / 32;
 };
@@ -319,12 +319,33 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
     for (int c = tid; c < p.C1; c += 256) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
   if (has_pro2)
     for (int c = tid; c < p.C2; c += 256) { s_scale[p.C1 + c] = p.pscale2[c]; s_shift[p.C1 + c] = p.pshift2[c]; }
+  // dY prologue (BN backward on load): table [7][BCO] = scale, shift, invstd, -mean*invstd,
+  // k, m1, m2 of this workgroup's output channels
+  const bool has_dyp = p.dyy != nullptr;
+  float* s_dy = s_scale + 1024;
+  if (has_dyp)
+    for (int i = tid; i < BCO; i += 256) {
+      const int c = co0 + i;
+      const bool ok = c < p.Cout;
+      const float is = ok ? p.dys4[p.Cout + c] : 0.f;
+      s_dy[i] = ok ? p.dys4[2 * p.Cout + c] : 0.f;
+      s_dy[BCO + i] = ok ? p.dys4[3 * p.Cout + c] : 0.f;
+      s_dy[2 * BCO + i] = is;
+      s_dy[3 * BCO + i] = ok ? -p.dys4[c] * is : 0.f;
+      s_dy[4 * BCO + i] = ok ? p.dycoef[c] : 0.f;
+      s_dy[5 * BCO + i] = ok ? p.dycoef[p.Cout + c] : 0.f;
+      s_dy[6 * BCO + i] = ok ? p.dycoef[2 * p.Cout + c] : 0.f;
+    }
   const int t_begin = (int)((long long)p.nTiles * split / p.splits);
   const int t_end = (int)((long long)p.nTiles * (split + 1) / p.splits);
   const long long img_px = (long long)p.H * p.W;
 
   // ---- tile-independent per-lane DMA geometry
   int y_pw[Cfg::Y_ITERS], y_ph[Cfg::Y_ITERS], y_rel[Cfg::Y_ITERS];
+  // dY prologue: the lane's pieces of y (loaded to registers with the dA DMA of the same
+  // tile) and whether each piece is a real (pixel, channel group)
+  uint4 yv[Cfg::Y_ITERS];
+  bool y_ok[Cfg::Y_ITERS];
 #pragma unroll
   for (int i = 0; i < Cfg::Y_ITERS; ++i) {
     const int e = (i * 4 + wave) * 64 + lane;
@@ -366,6 +387,12 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
       if ((i * 4 + wave) >= Cfg::Y_INSTR) break;
       const bool ok = y_rel[i] >= 0 && w0 + y_pw[i] < p.W && h0 + y_ph[i] < p.H;
       dma16(ry, sY(buf) + (i * 4 + wave) * 1024, ok ? (unsigned)(ybase + y_rel[i]) * 2u : kOOB);
+      if (has_dyp) {
+        const auto ryy = make_rsrc(p.dyy + n * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
+        const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(ryy, ok ? (unsigned)(ybase + y_rel[i]) * 2u : kOOB, 0, 0);
+        yv[i] = make_uint4(v.x, v.y, v.z, v.w);
+        y_ok[i] = ok;
+      }
     }
     const auto rx = make_rsrc(xsrc + (n + (dok ? dshift : 0)) * img_px * Cs, (unsigned)(img_px * Cs * 2));
 #pragma unroll
@@ -374,6 +401,30 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
       const int gw = w0 + x_dw[i], gh = h0 + x_dh[i];
       x_pix[i] = (gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && xch_ok && dok) ? gh * p.W + gw : -1;
       dma16(rx, sX(buf) + (i * 4 + wave) * 1024, x_pix[i] >= 0 ? (unsigned)(x_pix[i] * Cs + cs0) * 2u : kOOB);
+    }
+  };
+  // dY = k (dA [y*scale + shift > 0] - m1 - xhat m2) on the lane's own landed pieces
+  auto transform_dy = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < Cfg::Y_ITERS; ++i) {
+      if ((i * 4 + wave) < Cfg::Y_INSTR && y_ok[i]) {
+        const int e = (i * 4 + wave) * 64 + lane;
+        const int row = e / (BCO / 8), pc = e % (BCO / 8);
+        const int cl = (pc ^ wg2_yswz<BCO>(row)) * 8;   // channel offset within the co tile
+        uint4* qd = reinterpret_cast<uint4*>(sY(buf) + e * 16);
+        float fd[8], fy[8], o[8];
+        unpack8(*qd, fd);
+        unpack8(yv[i], fy);
+        const float* t = s_dy + opaque_zero() + cl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float a = fmaf(fy[j], t[j], t[BCO + j]);
+          const float dyh = a > 0.f ? fd[j] : 0.f;
+          const float xh = fmaf(fy[j], t[2 * BCO + j], t[3 * BCO + j]);
+          o[j] = t[4 * BCO + j] * (dyh - t[5 * BCO + j] - xh * t[6 * BCO + j]);
+        }
+        *qd = pack8(o);
+      }
     }
   };
   auto transform = [&](int buf) {
@@ -453,11 +504,13 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
     }
   };
 
+  if (has_dyp) __syncthreads();                       // s_dy visible
   if (t_begin < t_end) issue(t_begin, 0);
   for (int tile = t_begin; tile < t_end; ++tile) {
     const int buf = (tile - t_begin) & 1;
     dma_wait<0>();
     if (second ? has_pro2 : has_pro) transform(buf);
+    if (has_dyp) transform_dy(buf);
     lds_sync();
     if (tile + 1 < t_end) issue(tile + 1, buf ^ 1);
     compute(sY(buf), sX(buf));

@@ -71,6 +71,14 @@ struct ConvWgradArgs {
   int TD, TH, TW;
   int tilesD, tilesH, tilesW, nTiles;
   int coTiles, ciChunks, planes, splits;
+  // BN-backward prologue on the output-gradient operand (v2 kernel, 2-D): dY holds dA (the
+  // gradient w.r.t. the BN + ReLU output) and the kernel forms
+  //   dY = k * (dA [y*scale + shift > 0] - m1 - xhat * m2)
+  // on load (bn_bwd2_kernel's apply arithmetic): y = dyy, dys4 = [mean|invstd|scale|shift],
+  // dycoef = [k|m1|m2] (each Cout floats)
+  const bf16_t* dyy;
+  const float* dys4;
+  const float* dycoef;
 };
 void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st);
 // LDS-DMA variant (1 x TH x 16 pixel tiles of conv3_wgrad2_pt(bco) pixels; 3-D: planes = 3,

@@ -235,7 +235,23 @@ class _DoubleConvFn(torch.autograd.Function):
         # ---- first conv
         w1 = blk.conv1.weight
         padded_in = x2 is None and x1.shape[-1] != w1.shape[1]   # first layer: 3 -> 8 ch
-        if direct:
+        # first block, input gradient not wanted: the weight gradient is BN1 backward's only
+        # consumer, so it applies that backward on load (dY prologue) from dA1 and y1 — the
+        # apply pass (read dA1 + y1, write dY1) is skipped
+        wg_pro = (padded_in and part1 is not None and eng.wgrad_dy_prologue and
+                  not ctx.needs_input_grad[0])
+        if direct and wg_pro:
+            coefs, _, _ = F.bn_grad_coefs(part1, y1, s1, g1, bn1.weight.grad, bn1.bias.grad)
+            with eng.wgrad_stream(da1, y1, x1, coefs, s1):
+                w1.grad.add_(F.conv3_wgrad(da1, x1, None, None, None, None, None, None,
+                                           y1, s1, coefs)[:, :w1.shape[1]])
+                eng.ready(bn1.weight, bn1.bias, w1, blk.conv1.bias)
+            dg1 = dbe1 = dw1 = None
+        elif wg_pro:
+            coefs, dg1, dbe1 = F.bn_grad_coefs(part1, y1, s1, g1)
+            dw1 = F.conv3_wgrad(da1, x1, None, None, None, None, None, None, y1, s1, coefs)
+            dw1 = dw1[:, :w1.shape[1]].reshape(w1.shape)
+        elif direct:
             dy1, _, _ = F.bn_backward(da1, None, y1, s1, g1, None, bn1.weight.grad, bn1.bias.grad,
                                       part1)
             with eng.wgrad_stream(dy1, x1, x2, x2_bn):
@@ -250,7 +266,7 @@ class _DoubleConvFn(torch.autograd.Function):
             dw1 = F.conv3_wgrad(dy1, x1, x2, None, None, None, sc2, sh2)
             dw1 = (dw1[:, :w1.shape[1]] if padded_in else dw1).reshape(w1.shape)
         dx1 = dx2 = None
-        if ctx.needs_input_grad[0] or (x2 is not None and ctx.needs_input_grad[1]):
+        if not wg_pro and (ctx.needs_input_grad[0] or (x2 is not None and ctx.needs_input_grad[1])):
             c_x1 = x1.shape[-1]
             co1 = c_x1 if x2 is not None else 0
             # for a decoder block dx1 is the transposed conv's output gradient: keep the
@@ -496,6 +512,9 @@ class UNetEngine:
         # 64 -> 64-channel transposed conv: data + weight gradient in one kernel
         # (DDLPC_CONVT_FUSED=0: separate kernels, weight gradient on the side stream)
         self.convt_fused = os.environ.get("DDLPC_CONVT_FUSED", "1") != "0"
+        # first block: BN1 backward applied on load by its weight gradient (no apply pass;
+        # DDLPC_WGRAD_DYP=0: separate bn_backward)
+        self.wgrad_dy_prologue = os.environ.get("DDLPC_WGRAD_DYP", "1") != "0"
         self.enc = [_Block(b.double_conv, first=(i == 0), engine=self)
                     for i, b in enumerate(model.down_blocks())]
         self.mid = _Block(model.double_conv, first=False, engine=self)

@@ -440,6 +440,36 @@ def test_trilinear_3d(ops):
     assert rel_err(nchw(dx), gx) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 32, 32), (3, 24, 40), (1, 20, 18)])
+def test_conv3_wgrad_dy_prologue(ops, N, H, W):
+    """First-layer weight gradient with BatchNorm backward applied on load (dY prologue:
+    dy holds dA, the kernel forms k (dA [relu active] - m1 - xhat m2) from y) equals the
+    separate path (bn_backward writing dY, then conv3_wgrad) — same arithmetic, so equal up
+    to fp32 summation order at most; partial 16x16 tiles via odd H/W."""
+    torch.manual_seed(23)
+    Cin, Cout = 8, 32
+    x = torch.randn(N, H, W, Cin, device=DEV).bfloat16()
+    y = torch.randn(N, H, W, Cout, device=DEV).bfloat16()
+    da = torch.randn(N, H, W, Cout, device=DEV).bfloat16()
+    s4 = _bn4(Cout, 9)
+    gamma = torch.rand(Cout, device=DEV) + 0.5
+    # partial rows as the data-gradient epilogue would produce them: one reduction pass
+    ref_dy, ref_dg, ref_db = ops.bn_backward(da, None, y, s4, gamma, None)
+    part = torch.zeros(1, 2, Cout, device=DEV)
+    a = y.float() * s4[2] + s4[3]
+    dyh = torch.where(a > 0, da.float(), torch.zeros_like(a))
+    xh = (y.float() - s4[0]) * s4[1]
+    part[0, 0] = dyh.sum((0, 1, 2))
+    part[0, 1] = (dyh * xh).sum((0, 1, 2))
+    dy_sep, dg, db = ops.bn_backward(da, None, y, s4, gamma, None, None, None, part)
+    coefs, dg2, db2 = ops.bn_grad_coefs(part, y, s4, gamma)
+    assert torch.equal(dg, dg2) and torch.equal(db, db2)
+    w_sep = ops.conv3_wgrad(dy_sep, x, None, None, None)
+    w_pro = ops.conv3_wgrad(da, x, None, None, None, None, None, None, y, s4, coefs)
+    assert rel_err(w_pro, w_sep) < 1e-6, rel_err(w_pro, w_sep)
+    assert rel_err(dy_sep, ref_dy) < 1e-2
+
+
 @pytest.mark.parametrize("N,H,W,bn", [(2, 16, 16, False), (3, 12, 20, True), (1, 40, 24, True),
                                       (4, 8, 8, True)])
 def test_convt_bwd_fused(ops, N, H, W, bn):
