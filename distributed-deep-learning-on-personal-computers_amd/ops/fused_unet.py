@@ -677,7 +677,13 @@ class UNetEngine:
             return [False] * len(self.enc)
         out = []
         w = x.shape[-1]
+        # DDLPC_DEFER_SKIP_LEVELS=0,1: only those encoder levels (0 = full resolution)
+        lv = os.environ.get("DDLPC_DEFER_SKIP_LEVELS", "")
+        only = {int(v) for v in lv.split(",") if v.strip()} if lv else None
         for lvl, blk in enumerate(self.enc):
+            if only is not None and lvl not in only:
+                out.append(False)
+                continue
             ub, _pack, dblk = self.dec[len(self.dec) - 1 - lvl]
             c_up = dblk.conv1.weight.shape[1] - blk.conv2.weight.shape[0]
             c_skip = blk.conv2.weight.shape[0]
