@@ -833,8 +833,11 @@ std::vector<at::Tensor> head_ce_bn_bwd(const at::Tensor& a, const at::Tensor& Wh
                                        const at::Tensor& bn4, const at::Tensor& partial,
                                        const at::Tensor& gamma,
                                        const c10::optional<at::Tensor>& dgamma_out,
-                                       const c10::optional<at::Tensor>& dbeta_out) {
+                                       const c10::optional<at::Tensor>& dbeta_out,
+                                       const c10::optional<at::Tensor>& pscale) {
   CHECK_DEV(a); CHECK_CONTIG(a); CHECK_BF16(a);
+  // pscale: device factor on the partial rows (rows from the fused forward at unit scale)
+  const float* ps = fptr_opt(pscale);
   c10::DeviceGuard guard(a.device());
   const int C = (int)a.size(-1), K = (int)Wh.size(0);
   const float* pbn = bn4_ptr(bn4, C);
@@ -852,18 +855,70 @@ std::vector<at::Tensor> head_ce_bn_bwd(const at::Tensor& a, const at::Tensor& Wh
   if (nb <= 2048) {
     bn_grad_finalize_rows_launch(partial.data_ptr<float>(), nb, C, (double)P, gamma.data_ptr<float>(),
                                  s + C, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
-                                 coefs.data_ptr<float>(), into, cur_stream());
+                                 coefs.data_ptr<float>(), into, cur_stream(), ps);
   } else {
     at::Tensor sums = reduce_rows(partial, nb, 2 * C);
     bn_grad_finalize_launch(sums.data_ptr<double>(), C, (double)P, gamma.data_ptr<float>(), s + C,
                             dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
-                            coefs.data_ptr<float>(), into, cur_stream());
+                            coefs.data_ptr<float>(), into, cur_stream(), ps);
   }
   at::Tensor dY = at::empty_like(a);
   head_bn_apply_launch(bptr(a), Wh.data_ptr<float>(), bh.data_ptr<float>(), labels.data_ptr<int64_t>(),
                        fptr_opt(gscale), out3.data_ptr<float>(), pbn, coefs.data_ptr<float>(),
                        bptr_mut(dY), P, C, K, (int)ignore_index, cur_stream());
   return {dY, dgamma, dbeta};
+}
+
+// Training forward of the head with the deferred BatchNorm, fused with the backward's
+// statistics pass at a unit gradient scale: returns {out3 = (loss, correct, count),
+// dW rows [R][K*C + K], BN partial rows [R][2][C]}.  The backward scales the reductions by
+// dL/count on the device (head_wgrad_from_rows, head_ce_bn_bwd pscale).
+std::vector<at::Tensor> head_ce_fwd_stats(const at::Tensor& a, const at::Tensor& Wh,
+                                          const at::Tensor& bh, const at::Tensor& labels,
+                                          int64_t ignore_index, const at::Tensor& bn4) {
+  CHECK_DEV(a); CHECK_CONTIG(a); CHECK_BF16(a); CHECK_CONTIG(labels);
+  TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
+  c10::DeviceGuard guard(a.device());
+  const int C = (int)a.size(-1), K = (int)Wh.size(0);
+  const float* pbn = bn4_ptr(bn4, C);
+  TORCH_CHECK(head_supported(C, K), "head kernel: unsupported (C, K)");
+  const long long P = a.numel() / C;
+  TORCH_CHECK(labels.numel() == P, "labels / activation pixel count mismatch");
+  const int nb = head_ce_bwd_blocks(C, K, true, P, num_cus());
+  auto fopts = a.options().dtype(at::kFloat);
+  at::Tensor wrows = at::empty({nb, K * C + K}, fopts);
+  at::Tensor brows = at::empty({nb, 2, C}, fopts);
+  at::Tensor lrows = at::empty({nb, 3}, fopts);
+  at::Tensor out3 = at::empty({3}, fopts);
+  head_ce_fwd_stats_launch(bptr(a), Wh.data_ptr<float>(), bh.data_ptr<float>(), labels.data_ptr<int64_t>(),
+                           pbn, wrows.data_ptr<float>(), brows.data_ptr<float>(), lrows.data_ptr<float>(),
+                           out3.data_ptr<float>(), nb, P, C, K, (int)ignore_index, cur_stream());
+  return {out3, wrows, brows};
+}
+
+// dWh, dbh from the fused forward's rows: deterministic fp64 row sums times a device scale
+std::vector<at::Tensor> head_wgrad_from_rows(const at::Tensor& rows, const at::Tensor& scale, int64_t K,
+                                             int64_t C, const c10::optional<at::Tensor>& dw_out,
+                                             const c10::optional<at::Tensor>& db_out) {
+  CHECK_F32(rows); CHECK_CONTIG(rows); CHECK_F32(scale);
+  c10::DeviceGuard guard(rows.device());
+  TORCH_CHECK(rows.dim() == 2 && rows.size(1) == K * C + K, "rows must be [R][K*C + K]");
+  const int R = (int)rows.size(0);
+  at::Tensor sums = reduce_rows(rows, R, K * C + K);
+  auto fopts = rows.options();
+  const bool into = dw_out.has_value() && dw_out->defined();
+  if (into) {
+    TORCH_CHECK(dw_out->is_contiguous() && db_out->is_contiguous(), "grad outs must be contiguous");
+    scatter_sums_dscale_launch(sums.data_ptr<double>(), K * C, dw_out->data_ptr<float>(),
+                               scale.data_ptr<float>(), true, cur_stream());
+    scatter_sums_dscale_launch(sums.data_ptr<double>() + K * C, K, db_out->data_ptr<float>(),
+                               scale.data_ptr<float>(), true, cur_stream());
+    return {at::empty({0}, fopts), at::empty({0}, fopts)};
+  }
+  at::Tensor red = at::empty({K * C + K}, fopts);
+  scatter_sums_dscale_launch(sums.data_ptr<double>(), K * C + K, red.data_ptr<float>(),
+                             scale.data_ptr<float>(), false, cur_stream());
+  return {red.narrow(0, 0, K * C).view({K, C}), red.narrow(0, K * C, K)};
 }
 
 at::Tensor head_logits(const at::Tensor& a, const at::Tensor& Wh, const at::Tensor& bh,
@@ -1088,7 +1143,11 @@ TORCH_LIBRARY(ddlpc, m) {
         "bool store_da=True) -> Tensor[]");
   m.def("head_ce_bn_bwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, Tensor out3, Tensor? gscale, "
         "int ignore_index, Tensor bn4, Tensor partial, Tensor gamma, Tensor(a!)? dgamma_out=None, "
-        "Tensor(b!)? dbeta_out=None) -> Tensor[]");
+        "Tensor(b!)? dbeta_out=None, Tensor? pscale=None) -> Tensor[]");
+  m.def("head_ce_fwd_stats(Tensor a, Tensor Wh, Tensor bh, Tensor labels, int ignore_index, "
+        "Tensor bn4) -> Tensor[]");
+  m.def("head_wgrad_from_rows(Tensor rows, Tensor scale, int K, int C, Tensor(a!)? dw_out=None, "
+        "Tensor(b!)? db_out=None) -> Tensor[]");
   m.def("head_logits(Tensor a, Tensor Wh, Tensor bh, Tensor? bn4=None) -> Tensor");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float eps, "
         "float wd, float step_size, float inv_sqrt_bc2) -> ()");
@@ -1120,6 +1179,8 @@ TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
   m.impl("head_ce_fwd", &ddlpc::head_ce_fwd);
   m.impl("head_ce_bwd", &ddlpc::head_ce_bwd);
   m.impl("head_ce_bn_bwd", &ddlpc::head_ce_bn_bwd);
+  m.impl("head_ce_fwd_stats", &ddlpc::head_ce_fwd_stats);
+  m.impl("head_wgrad_from_rows", &ddlpc::head_wgrad_from_rows);
   m.impl("head_logits", &ddlpc::head_logits);
   m.impl("adam_step", &ddlpc::adam_step);
   m.impl("adam_step_dev", &ddlpc::adam_step_dev);

@@ -173,11 +173,14 @@ __global__ void ce_finalize_kernel(const float* __restrict__ partial, int nb, fl
 // channels av and the label, the activation f (the deferred BN + ReLU, bf16-rounded), the
 // softmax-CE gradient d[K] (identical on the G lanes of the pixel) and the lane's 8
 // channels of dA = d . Wh, rounded to bf16 (pk) exactly as stored.
+// head_pixel with the extras of the fused forward + statistics pass: dA before rounding
+// (o8), the log-sum-exp, the label's logit and the arg-max class
 template <int C, int K, bool DEFER>
-DDLPC_DEVICE void head_pixel(const uint4 av, const int64_t lab, const float* __restrict__ w,
-                             const float (&bk)[K], const float (&sc)[8], const float (&sh)[8],
-                             float gs, int ignore_index, float (&y8)[8], float (&f)[8],
-                             float (&d)[K], uint4& pk) {
+DDLPC_DEVICE void head_pixel_x(const uint4 av, const int64_t lab, const float* __restrict__ w,
+                               const float (&bk)[K], const float (&sc)[8], const float (&sh)[8],
+                               float gs, int ignore_index, float (&y8)[8], float (&f)[8],
+                               float (&d)[K], uint4& pk, float (&o8)[8], float& lse, float& zy,
+                               int& am) {
   constexpr int G = C / 8;
   unpack8(av, y8);
 #pragma unroll
@@ -203,11 +206,18 @@ DDLPC_DEVICE void head_pixel(const uint4 av, const int64_t lab, const float* __r
 #pragma unroll
     for (int k = 0; k < K; ++k) z[k] += __shfl_xor(z[k], o, 64);
   float m = -INFINITY;
+  am = 0;
+  zy = 0.f;
 #pragma unroll
-  for (int k = 0; k < K; ++k) { z[k] += bk[k]; m = fmaxf(m, z[k]); }
+  for (int k = 0; k < K; ++k) {
+    z[k] += bk[k];
+    if (z[k] > m) { m = z[k]; am = k; }              // first maximum (padded classes: -inf)
+    zy = k == lab ? z[k] : zy;
+  }
   float se = 0.f;
 #pragma unroll
   for (int k = 0; k < K; ++k) { z[k] = __expf(z[k] - m); se += z[k]; }
+  lse = m + __logf(se);
   const float inv = 1.f / se;
 #pragma unroll
   for (int k = 0; k < K; ++k) d[k] = lab != ignore_index ? (z[k] * inv - (k == lab ? 1.f : 0.f)) * gs : 0.f;
@@ -219,23 +229,42 @@ DDLPC_DEVICE void head_pixel(const uint4 av, const int64_t lab, const float* __r
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj)
       o2[jj] = __builtin_elementwise_fma(f2_t{d[k], d[k]}, w2[(k * C) / 2 + jj], o2[jj]);
-  const float o8[8] = {o2[0].x, o2[0].y, o2[1].x, o2[1].y, o2[2].x, o2[2].y, o2[3].x, o2[3].y};
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) { o8[2 * jj] = o2[jj].x; o8[2 * jj + 1] = o2[jj].y; }
   pk = pack8(o8);
+}
+
+template <int C, int K, bool DEFER>
+DDLPC_DEVICE void head_pixel(const uint4 av, const int64_t lab, const float* __restrict__ w,
+                             const float (&bk)[K], const float (&sc)[8], const float (&sh)[8],
+                             float gs, int ignore_index, float (&y8)[8], float (&f)[8],
+                             float (&d)[K], uint4& pk) {
+  float o8[8], lse, zy;
+  int am;
+  head_pixel_x<C, K, DEFER>(av, lab, w, bk, sc, sh, gs, ignore_index, y8, f, d, pk, o8, lse, zy, am);
 }
 
 // STORE = false (deferred BN only): the stats pass of the two-pass head backward — dWh,
 // dbh and the BN-backward partials, no dA (head_bn_apply_kernel recomputes it)
-template <int C, int K, bool DEFER, bool STORE = true>
+//
+// LOSS = true (training forward with the deferred BN): the forward itself — loss, pixel hits
+// and valid count per workgroup (lossp rows [nb][3]) — fused with the statistics pass at a
+// UNIT gradient scale: dWh, dbh and the BN partials (from the unrounded dA) are linear in
+// the scale dL/count, which the backward applies on the device (head_wgrad_from_rows,
+// head_ce_bn_bwd's pscale) — one pass over the activation and labels instead of two.
+template <int C, int K, bool DEFER, bool STORE = true, bool LOSS = false>
 __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
     const bf16_t* __restrict__ a, const float* __restrict__ Wh, const float* __restrict__ bh,
     const int64_t* __restrict__ labels, const float* __restrict__ gscale,
     const float* __restrict__ stats3, bf16_t* __restrict__ dA, float* __restrict__ dWp,
     long long P, int ignore_index, const float* __restrict__ bn4, float* __restrict__ bnpart,
-    int Kreal) {
+    int Kreal, float* __restrict__ lossp = nullptr) {
   static_assert(STORE || DEFER, "the stats-only pass exists for the deferred BatchNorm");
+  static_assert(!LOSS || (DEFER && !STORE), "the fused forward is the deferred stats pass");
   constexpr int G = C / 8;                          // lanes per pixel
   constexpr int PPB = 256 / G;                      // pixels per workgroup step
-  constexpr int NACC = 8 * K + K + (DEFER ? 16 : 0);
+  constexpr int NACC = 8 * K + K + (DEFER ? 16 : 0) + (LOSS ? 3 : 0);
+  constexpr int LA = 8 * K + K + (DEFER ? 16 : 0);  // loss | correct | count accumulators
   __shared__ float sred[4][G][NACC];
   __shared__ __attribute__((aligned(16))) float sW[K * C];      // Wh, padded classes zero
   __shared__ __attribute__((aligned(16))) float sXh[2 * C];     // invstd | -mean*invstd
@@ -255,8 +284,8 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
     sh[j] = DEFER ? bn4[3 * C + c8 + j] : 0.f;
   }
   __syncthreads();
-  const float cnt = stats3[2];
-  const float gs = (gscale != nullptr ? gscale[0] : 1.0f) / (cnt > 0.f ? cnt : 1.f);
+  const float cnt = LOSS ? 1.f : stats3[2];
+  const float gs = LOSS ? 1.f : (gscale != nullptr ? gscale[0] : 1.0f) / (cnt > 0.f ? cnt : 1.f);
   float acc[NACC];
 #pragma unroll
   for (int i = 0; i < NACC; ++i) acc[i] = 0.f;
@@ -275,11 +304,16 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
       a_nx = *reinterpret_cast<const uint4*>(a + (px + stride) * C + c8);
       l_nx = labels[px + stride];
     }
-    float y8[8], f[8], d[K];
+    float y8[8], f[8], d[K], o8[8], lse, zy;
+    int am;
     uint4 pk;
-    head_pixel<C, K, DEFER>(a_cur, lab, sW + opaque_zero() + c8, bk, sc, sh, gs, ignore_index,
-                            y8, f, d, pk);
+    head_pixel_x<C, K, DEFER>(a_cur, lab, sW + opaque_zero() + c8, bk, sc, sh, gs, ignore_index,
+                              y8, f, d, pk, o8, lse, zy, am);
     if (STORE) *reinterpret_cast<uint4*>(dA + px * C + c8) = pk;
+    if (LOSS && cg == 0) {
+      if (lab != ignore_index) { acc[LA] += lse - zy; acc[LA + 2] += 1.f; }
+      acc[LA + 1] += am == lab ? 1.f : 0.f;
+    }
     {
       typedef float f2_t __attribute__((ext_vector_type(2)));
 #pragma unroll
@@ -298,7 +332,12 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
     }
     if (DEFER) {
       float r[8];
-      unpack8(pk, r);                                // BN backward sees the stored dA
+      if (LOSS) {                                    // unit scale: the unrounded dA
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = o8[j];
+      } else {
+        unpack8(pk, r);                              // BN backward sees the stored dA
+      }
       const float* xh = sXh + opaque_zero() + c8;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -336,6 +375,11 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
       for (int wv = 0; wv < 4; ++wv) t += sred[wv][c / 8][9 * K + 8 * half + c % 8];
       bnpart[(long long)blockIdx.x * 2 * C + o] = t;
     }
+  if (LOSS && tid < 3) {                             // lanes cg == 0 hold them
+    float t = 0.f;
+    for (int wv = 0; wv < 4; ++wv) t += sred[wv][0][LA + tid];
+    lossp[(long long)blockIdx.x * 3 + tid] = t;
+  }
 }
 
 // Second pass of the two-pass head backward (deferred BatchNorm of the last decoder
@@ -502,6 +546,16 @@ void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
     HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK, false>), dim3(nblocks), dim3(256), 0,
                                          st, a, Wh, bh, labels, gscale, stats3, dA, dW_partial, P,
                                          ignore_index, bn4, bnpart, K));
+}
+
+void head_ce_fwd_stats_launch(const bf16_t* a, const float* Wh, const float* bh,
+                              const int64_t* labels, const float* bn4, float* dW_partial,
+                              float* bnpart, float* loss_partial, float* out3, int nblocks,
+                              long long P, int C, int K, int ignore_index, hipStream_t st) {
+  HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK, true, false, true>), dim3(nblocks),
+                                       dim3(256), 0, st, a, Wh, bh, labels, nullptr, nullptr, nullptr,
+                                       dW_partial, P, ignore_index, bn4, bnpart, K, loss_partial));
+  hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(256), 0, st, loss_partial, nblocks, out3);
 }
 
 int head_bn_apply_blocks(long long P, int C) {

@@ -167,6 +167,12 @@ void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
 // two-pass backward with the deferred BatchNorm of the last decoder block: dA == nullptr in
 // head_ce_bwd_launch runs the stats pass (dWh, dbh, BN partials); this second pass
 // recomputes dA and writes that BatchNorm's dY (coefs = [k | m1 | m2] x C)
+// training forward with the deferred BN: loss rows -> out3 (ce_finalize) plus the backward
+// statistics at a unit gradient scale (head_ce_bwd_kernel LOSS variant)
+void head_ce_fwd_stats_launch(const bf16_t* a, const float* Wh, const float* bh,
+                              const int64_t* labels, const float* bn4, float* dW_partial,
+                              float* bnpart, float* loss_partial, float* out3, int nblocks,
+                              long long P, int C, int K, int ignore_index, hipStream_t st);
 void head_bn_apply_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
                           const float* gscale, const float* stats3, const float* bn4,
                           const float* coefs, bf16_t* dY, long long P, int C, int K,
@@ -209,7 +215,9 @@ void bn_stats_finalize_launch(const double* sums, int C, double count, const flo
                               int64_t* nbt, hipStream_t st);
 void bn_grad_finalize_launch(const double* sums, int C, double count, const float* gamma,
                              const float* invstd, float* dgamma, float* dbeta, float* coefs,
-                             bool accumulate, hipStream_t st);
+                             bool accumulate, hipStream_t st, const float* dscale = nullptr);
+void scatter_sums_dscale_launch(const double* sums, long long N, float* dst, const float* dscale,
+                                bool accumulate, hipStream_t st);
 // single-kernel variants reading the partial rows directly (P small): one block per channel
 void bn_stats_finalize_rows_launch(const float* partial, int P, int C, double count,
                                    const float* gamma, const float* beta, float* running_mean,
@@ -217,7 +225,8 @@ void bn_stats_finalize_rows_launch(const float* partial, int P, int C, double co
                                    bool update_running, int64_t* nbt, hipStream_t st);
 void bn_grad_finalize_rows_launch(const float* partial, int P, int C, double count,
                                   const float* gamma, const float* invstd, float* dgamma,
-                                  float* dbeta, float* coefs, bool accumulate, hipStream_t st);
+                                  float* dbeta, float* coefs, bool accumulate, hipStream_t st,
+                                  const float* dscale = nullptr);
 void reduce_rows_scatter_launch(const float* in, int R, long long N, double* tmp, float* dst,
                                 int mode, int A, int T, int B, bool accumulate, hipStream_t st,
                                 long long ld = -1);

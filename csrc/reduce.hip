@@ -57,13 +57,16 @@ __global__ void bn_stats_finalize_kernel(const double* __restrict__ sums, int C,
 }
 
 // dgamma, dbeta (accumulated if requested) and dY coefficients from fp64 (sum dyh, sum dyh*xhat)
+// (dscale: optional device factor on both sums — partials reduced at a unit gradient scale)
 __global__ void bn_grad_finalize_kernel(const double* __restrict__ sums, int C, double count,
                                         const float* __restrict__ gamma,
                                         const float* __restrict__ invstd, float* dgamma,
-                                        float* dbeta, float* coefs, int accumulate) {
+                                        float* dbeta, float* coefs, int accumulate,
+                                        const float* __restrict__ dscale) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  const double t1 = sums[c], t2 = sums[C + c];
+  const double ds = dscale != nullptr ? (double)dscale[0] : 1.0;
+  const double t1 = sums[c] * ds, t2 = sums[C + c] * ds;
   dbeta[c] = accumulate ? dbeta[c] + (float)t1 : (float)t1;
   dgamma[c] = accumulate ? dgamma[c] + (float)t2 : (float)t2;
   coefs[c] = gamma[c] * invstd[c];
@@ -91,6 +94,17 @@ __global__ void scatter_sums_kernel(const double* __restrict__ sums, long long N
     }
     const float v = (float)sums[j] * scale;
     dst[d] = accumulate ? dst[d] + v : v;
+  }
+}
+
+// dst[j] (+)= sums[j] * dscale[0]  (identity layout; device-side scale)
+__global__ void scatter_sums_dscale_kernel(const double* __restrict__ sums, long long N, float* dst,
+                                           const float* __restrict__ dscale, int accumulate) {
+  const double ds = (double)dscale[0];
+  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < N;
+       j += (long long)gridDim.x * blockDim.x) {
+    const float v = (float)(sums[j] * ds);
+    dst[j] = accumulate ? dst[j] + v : v;
   }
 }
 
@@ -138,7 +152,7 @@ __global__ void bn_stats_rows_kernel(const float* __restrict__ partial, int P, i
 __global__ void bn_grad_rows_kernel(const float* __restrict__ partial, int P, int C, double count,
                                     const float* __restrict__ gamma,
                                     const float* __restrict__ invstd, float* dgamma, float* dbeta,
-                                    float* coefs, int accumulate) {
+                                    float* coefs, int accumulate, const float* __restrict__ dscale) {
   const int c = blockIdx.x;
   double a = 0.0, b = 0.0;
   for (int r = threadIdx.x; r < P; r += 256) {
@@ -147,6 +161,7 @@ __global__ void bn_grad_rows_kernel(const float* __restrict__ partial, int P, in
   }
   block_sum2(a, b);
   if (threadIdx.x != 0) return;
+  if (dscale != nullptr) { a *= (double)dscale[0]; b *= (double)dscale[0]; }
   dbeta[c] = accumulate ? dbeta[c] + (float)a : (float)a;
   dgamma[c] = accumulate ? dgamma[c] + (float)b : (float)b;
   coefs[c] = gamma[c] * invstd[c];
@@ -193,9 +208,10 @@ void bn_stats_finalize_rows_launch(const float* partial, int P, int C, double co
 
 void bn_grad_finalize_rows_launch(const float* partial, int P, int C, double count,
                                   const float* gamma, const float* invstd, float* dgamma,
-                                  float* dbeta, float* coefs, bool accumulate, hipStream_t st) {
+                                  float* dbeta, float* coefs, bool accumulate, hipStream_t st,
+                                  const float* dscale) {
   hipLaunchKernelGGL(bn_grad_rows_kernel, dim3(C), dim3(256), 0, st, partial, P, C, count, gamma,
-                     invstd, dgamma, dbeta, coefs, accumulate ? 1 : 0);
+                     invstd, dgamma, dbeta, coefs, accumulate ? 1 : 0, dscale);
 }
 
 // dst (+)= permute(sum over rows of in[R][N]); one pass when R <= 64, else chunk sums first
@@ -250,9 +266,16 @@ void bn_stats_finalize_launch(const double* sums, int C, double count, const flo
 
 void bn_grad_finalize_launch(const double* sums, int C, double count, const float* gamma,
                              const float* invstd, float* dgamma, float* dbeta, float* coefs,
-                             bool accumulate, hipStream_t st) {
+                             bool accumulate, hipStream_t st, const float* dscale) {
   hipLaunchKernelGGL(bn_grad_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, sums, C,
-                     count, gamma, invstd, dgamma, dbeta, coefs, accumulate ? 1 : 0);
+                     count, gamma, invstd, dgamma, dbeta, coefs, accumulate ? 1 : 0, dscale);
+}
+
+void scatter_sums_dscale_launch(const double* sums, long long N, float* dst, const float* dscale,
+                                bool accumulate, hipStream_t st) {
+  const int grid = (int)std::max<long long>(1, std::min<long long>((N + 255) / 256, 4096));
+  hipLaunchKernelGGL(scatter_sums_dscale_kernel, dim3(grid), dim3(256), 0, st, sums, N, dst, dscale,
+                     accumulate ? 1 : 0);
 }
 
 void scatter_sums_launch(const double* sums, long long N, float* dst, int mode, int A, int T,

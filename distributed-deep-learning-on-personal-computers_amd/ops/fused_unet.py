@@ -210,7 +210,8 @@ class _DoubleConvFn(torch.autograd.Function):
         # ---- second conv: BN2 + ReLU (+ unpool + skip sum) backward, then its gradients
         if direct:
             if head is not None:
-                dy2, _, _ = F.head_ce_bn_bwd(*head, s2, part2, g2, bn2.weight.grad, bn2.bias.grad)
+                dy2, _, _ = F.head_ce_bn_bwd(*head, s2, part2, g2, bn2.weight.grad, bn2.bias.grad,
+                                             getattr(da2, "_ddlpc_bn_pscale", None))
             else:
                 dy2, _, _ = F.bn_backward(da2, dpool, y2, s2, g2, None, bn2.weight.grad,
                                           bn2.bias.grad, part2)
@@ -220,7 +221,8 @@ class _DoubleConvFn(torch.autograd.Function):
             dg2 = dbe2 = dw2 = None
         else:
             if head is not None:
-                dy2, dg2, dbe2 = F.head_ce_bn_bwd(*head, s2, part2, g2, None, None)
+                dy2, dg2, dbe2 = F.head_ce_bn_bwd(*head, s2, part2, g2, None, None,
+                                                  getattr(da2, "_ddlpc_bn_pscale", None))
             else:
                 dy2, dg2, dbe2 = F.bn_backward(da2, dpool, y2, s2, g2, None, None, None, part2)
             dw2 = F.conv3_wgrad(dy2, y1, None, s1[2], s1[3]).view_as(blk.conv2.weight)
@@ -356,7 +358,17 @@ class _HeadCEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, wh, bh, labels, ignore_index: int, engine,
                 bn: Optional[torch.Tensor] = None):
-        out3 = _ops().head_ce_fwd(a, wh, bh, labels, ignore_index, bn)
+        # training with the deferred BN: the forward also runs the backward's statistics
+        # pass (unit gradient scale) — one read of the activation and labels for both
+        ctx.rows = None
+        # (Function.forward runs with grad mode off: needs_input_grad says whether a
+        # backward will follow)
+        if (bn is not None and engine.head_apply and engine.head_fused_fwd
+                and any(ctx.needs_input_grad[:3])):
+            out3, wrows, brows = _ops().head_ce_fwd_stats(a, wh, bh, labels, ignore_index, bn)
+            ctx.rows = (wrows, brows)
+        else:
+            out3 = _ops().head_ce_fwd(a, wh, bh, labels, ignore_index, bn)
         ctx.save_for_backward(a, wh, bh, labels, out3, bn if bn is not None else torch.empty(0))
         ctx.has_bn = bn is not None
         ctx.ignore_index = ignore_index
@@ -377,6 +389,26 @@ class _HeadCEFn(torch.autograd.Function):
         # which recomputes dA and applies the BatchNorm backward in registers (no dA
         # round trip through HBM, no separate BN-apply pass).  DDLPC_HEAD_APPLY=0: one pass
         two_pass = bn is not None and eng.head_apply
+        if ctx.rows is not None:
+            # statistics already reduced by the forward at unit scale: scale = dL / count
+            wrows, brows = ctx.rows
+            cnt = out3[2:3]
+            g = gs if gs is not None else torch.ones_like(cnt)
+            scale = (g / torch.where(cnt > 0, cnt, torch.ones_like(cnt))).contiguous()
+            K, C = wh.shape
+            head = eng.head
+            if eng.direct_grads:
+                _ops().head_wgrad_from_rows(wrows, scale, K, C, head.weight.grad, head.bias.grad)
+                with eng.wgrad_stream():
+                    eng.ready(head.weight, head.bias)
+                dw = db = None
+            else:
+                dw, db = _ops().head_wgrad_from_rows(wrows, scale, K, C)
+            da = torch.zeros((), dtype=a.dtype, device=a.device).expand(a.shape)
+            da._ddlpc_head = (a, wh, bh, labels, out3, gs, ctx.ignore_index)
+            da._ddlpc_bn_partial = brows
+            da._ddlpc_bn_pscale = scale
+            return da, dw, db, None, None, None, None
         if eng.direct_grads:
             head = eng.head
             da, _, _, part = _ops().head_ce_bwd(a, wh, bh, labels, out3, gs, ctx.ignore_index,
@@ -509,6 +541,9 @@ class UNetEngine:
         # two-pass head backward with the last block's BN backward fused into the second
         # pass (see _HeadCEFn.backward; DDLPC_HEAD_APPLY=0: dA stored + separate BN apply)
         self.head_apply = os.environ.get("DDLPC_HEAD_APPLY", "1") != "0"
+        # ... and its statistics pass fused into the training forward (DDLPC_HEAD_FUSED_FWD=0:
+        # separate forward and statistics passes)
+        self.head_fused_fwd = os.environ.get("DDLPC_HEAD_FUSED_FWD", "1") != "0"
         # 64 -> 64-channel transposed conv: data + weight gradient in one kernel
         # (DDLPC_CONVT_FUSED=0: separate kernels, weight gradient on the side stream)
         self.convt_fused = os.environ.get("DDLPC_CONVT_FUSED", "1") != "0"

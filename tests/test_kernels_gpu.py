@@ -440,6 +440,34 @@ def test_trilinear_3d(ops):
     assert rel_err(nchw(dx), gx) < 1e-2
 
 
+@pytest.mark.parametrize("C,K,H", [(32, 6, 12), (16, 3, 9), (64, 2, 8), (8, 16, 5)])
+def test_head_fused_forward_stats(ops, C, K, H):
+    """Training forward fused with the backward's statistics pass (unit gradient scale,
+    scaled on the device in backward) against the separate forward + stats pass: loss /
+    hits / count, dWh, dbh, and the BatchNorm backward (dgamma, dbeta, dY) to fp32 rounding."""
+    torch.manual_seed(8)
+    N, W = 2, H + 5
+    yh = torch.randn(N, H, W, C, device=DEV).bfloat16()
+    bnh = _bn4(C, 4)
+    wh = torch.randn(K, C, device=DEV) * 0.3
+    bh = torch.randn(K, device=DEV) * 0.1
+    lab = torch.randint(0, K, (N, H, W), device=DEV)
+    lab[1, 0, :3] = -100
+    o_ref = ops.head_ce_fwd(yh, wh, bh, lab, -100, bnh)
+    o, wrows, brows = ops.head_ce_fwd_stats(yh, wh, bh, lab, -100, bnh)
+    assert torch.allclose(o, o_ref, rtol=1e-5, atol=0)
+    gs = torch.tensor([0.5], device=DEV)
+    _, dw_ref, db_ref, part_ref = ops.head_ce_bwd(yh, wh, bh, lab, o_ref, gs, -100, None, None, bnh, False)
+    scale = gs / o[2:3]
+    dw, db = ops.head_wgrad_from_rows(wrows, scale, K, C)
+    assert rel_err(dw, dw_ref) < 1e-5 and rel_err(db, db_ref) < 1e-5
+    gamma = torch.rand(C, device=DEV) + 0.5
+    ref = ops.head_ce_bn_bwd(yh, wh, bh, lab, o_ref, gs, -100, bnh, part_ref, gamma)
+    got = ops.head_ce_bn_bwd(yh, wh, bh, lab, o, gs, -100, bnh, brows, gamma, None, None, scale)
+    assert rel_err(got[1], ref[1]) < 5e-3 and rel_err(got[2], ref[2]) < 5e-3
+    assert rel_err(got[0], ref[0]) < 1e-2
+
+
 @pytest.mark.parametrize("N,H,W", [(2, 32, 32), (3, 24, 40), (1, 20, 18)])
 def test_conv3_wgrad_dy_prologue(ops, N, H, W):
     """First-layer weight gradient with BatchNorm backward applied on load (dY prologue:
