@@ -173,6 +173,11 @@ __global__ void ce_finalize_kernel(const float* __restrict__ partial, int nb, fl
 // channels av and the label, the activation f (the deferred BN + ReLU, bf16-rounded), the
 // softmax-CE gradient d[K] (identical on the G lanes of the pixel) and the lane's 8
 // channels of dA = d . Wh, rounded to bf16 (pk) exactly as stored.
+template <int CTRL>
+DDLPC_DEVICE float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+
 // head_pixel with the extras of the fused forward + statistics pass: dA before rounding
 // (o8), the log-sum-exp, the label's logit and the arg-max class
 template <int C, int K, bool DEFER>
@@ -201,10 +206,14 @@ DDLPC_DEVICE void head_pixel_x(const uint4 av, const int64_t lab, const float* _
     for (int jj = 0; jj < 4; ++jj) t2 = __builtin_elementwise_fma(f2[jj], w2[(k * C) / 2 + jj], t2);
     z[k] = t2.x + t2.y;
   }
+  // sum over the G lanes of the pixel: DPP lane swaps (xor 1, xor 2 within quads, then the
+  // half-row mirror — the quads are uniform by then), no LDS-crossbar permutes
 #pragma unroll
-  for (int o = 1; o < G; o <<= 1)
-#pragma unroll
-    for (int k = 0; k < K; ++k) z[k] += __shfl_xor(z[k], o, 64);
+  for (int k = 0; k < K; ++k) {
+    if (G >= 2) z[k] += dpp_f<0xB1>(z[k]);
+    if (G >= 4) z[k] += dpp_f<0x4E>(z[k]);
+    if (G >= 8) z[k] += dpp_f<0x141>(z[k]);
+  }
   float m = -INFINITY;
   am = 0;
   zy = 0.f;
@@ -218,7 +227,7 @@ DDLPC_DEVICE void head_pixel_x(const uint4 av, const int64_t lab, const float* _
 #pragma unroll
   for (int k = 0; k < K; ++k) { z[k] = __expf(z[k] - m); se += z[k]; }
   lse = m + __logf(se);
-  const float inv = 1.f / se;
+  const float inv = __builtin_amdgcn_rcpf(se);      // (se >= 1: the max term is exp(0))
 #pragma unroll
   for (int k = 0; k < K; ++k) d[k] = lab != ignore_index ? (z[k] * inv - (k == lab ? 1.f : 0.f)) * gs : 0.f;
   f2_t o2[4];
@@ -289,9 +298,17 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
   float acc[NACC];
 #pragma unroll
   for (int i = 0; i < NACC; ++i) acc[i] = 0.f;
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  f2_t accw[K][4];                                  // dWh[k][c8 + 2jj, +1] (packed pairs)
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) accw[k][jj] = f2_t{0.f, 0.f};
   const long long stride = (long long)gridDim.x * PPB;
   // software pipeline: the next pixel's activation + label loads are in flight while this
-  // pixel computes (low occupancy: few waves per CU to cover the HBM latency otherwise)
+  // pixel computes.  (Two slots in ping-pong were measured: SQ_WAIT_ANY 0.46 -> 0.25 but
+  // VALU-active 0.37 -> 0.68 with 15% more VALU instructions, 442 -> 475 us — this loop is
+  // VALU-issue bound, not latency bound; profiles/head_pmc_*_s2.txt)
   long long px = (long long)blockIdx.x * PPB + tid / G;
   uint4 a_nx = make_uint4(0, 0, 0, 0);
   int64_t l_nx = 0;
@@ -315,16 +332,13 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
       acc[LA + 1] += am == lab ? 1.f : 0.f;
     }
     {
-      typedef float f2_t __attribute__((ext_vector_type(2)));
+      f2_t f2[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) f2[jj] = f2_t{f[2 * jj], f[2 * jj + 1]};
 #pragma unroll
       for (int k = 0; k < K; ++k)
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const f2_t r = __builtin_elementwise_fma(f2_t{f[2 * jj], f[2 * jj + 1]}, f2_t{d[k], d[k]},
-                                                   f2_t{acc[k * 8 + 2 * jj], acc[k * 8 + 2 * jj + 1]});
-          acc[k * 8 + 2 * jj] = r.x;
-          acc[k * 8 + 2 * jj + 1] = r.y;
-        }
+        for (int jj = 0; jj < 4; ++jj) accw[k][jj] = __builtin_elementwise_fma(f2[jj], f2_t{d[k], d[k]}, accw[k][jj]);
     }
     if (cg == 0) {
 #pragma unroll
@@ -347,6 +361,10 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
       }
     }
   }
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) { acc[k * 8 + 2 * jj] = accw[k][jj].x; acc[k * 8 + 2 * jj + 1] = accw[k][jj].y; }
   // ---- workgroup reduction: lanes with equal c8 (xor over the pixel-slot bits), then waves
 #pragma unroll
   for (int o = G; o < 64; o <<= 1)

@@ -11,7 +11,7 @@ for r in rows:
     k = (int(r["Dispatch_Id"]), r["Kernel_Name"].replace("void ", "").replace("ddlpc::(anonymous namespace)::", "").split("(")[0][:44])
     agg.setdefault(k, defaultdict(float))[r["Counter_Name"]] += float(r["Counter_Value"])
 for (d, name), c in agg.items():
-    if "conv" not in name and "wgrad" not in name:
+    if "conv" not in name and "wgrad" not in name and "head" not in name:
         continue
     wc = c.get("SQ_WAVE_CYCLES", 0) or 1
     parts = [f"{d:5d} {name:44s}"]
