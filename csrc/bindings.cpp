@@ -326,7 +326,9 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
     a.dys4 = dy_s4->data_ptr<float>();
     a.dycoef = dy_coefs->data_ptr<float>();
   }
-  if (v3) { a.TD = 1; a.TW = 16; a.TH = bco == 32 ? 16 : (v3_pt64 == 96 && a.C2 > 0 ? 6 : 8); }
+  // (DDLPC_WGRAD3_RING=1: 32-output-channel layers on 128-pixel tiles with a 3-deep DMA ring)
+  static const int v3_ring = [] { const char* e = getenv("DDLPC_WGRAD3_RING"); return e ? atoi(e) : 0; }();
+  if (v3) { a.TD = 1; a.TW = 16; a.TH = bco == 32 ? (v3_ring ? 8 : 16) : (v3_pt64 == 96 && a.C2 > 0 ? 6 : 8); }
   else if (v2) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad2_pt(bco, a.C2, g.H, g.W) / 16; }
   else if (g.dims == 2) { a.TD = 1; a.TW = g.W >= 16 ? 16 : 8; a.TH = 128 / a.TW; }
   else { a.TW = g.W >= 16 ? 16 : 8; a.TH = 4; a.TD = 128 / (a.TW * a.TH); }

@@ -550,7 +550,10 @@ DDLPC_DEVICE int wg3_yswz(int row) {             // XOR on the 16-B piece index
   return BCO == 64 ? (((row >> 1) & 1) << 2) : 0;
 }
 
-template <int BCO, int PT>
+// NB: stages in the LDS-DMA ring (2: double buffer, one full vmcnt drain per tile; 3: the
+// DMA of tile t + 2 in flight while t computes, counted waits — with 128-pixel tiles so two
+// workgroups still fit per CU)
+template <int BCO, int PT, int NB = 2>
 __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
   using namespace convlds;
   using Cfg = Wg2Cfg<BCO, PT>;                     // DMA geometry / LDS budget as v2
@@ -640,11 +643,20 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
       dma16(rx, sX(buf) + (i * 4 + wave) * 1024, x_pix[i] >= 0 ? (unsigned)(x_pix[i] * Cs + cs0) * 2u : kOOB);
     }
   };
-  auto transform = [&](char* __restrict__ X) __attribute__((always_inline)) {
+  // (ring: the halo validity of `tile` is recomputed here — x_pix already holds a later tile's)
+  auto transform = [&](int tile, char* __restrict__ X) __attribute__((always_inline)) {
+    int t = tile;
+    const int tw_i = t % p.tilesW; t /= p.tilesW;
+    const int th_i = t % p.tilesH; t /= p.tilesH;
+    const int dx = t % p.D + dshift;
+    const bool dok = dx >= 0 && dx < p.D;
+    const int h0 = th_i * TH, w0 = tw_i * 16;
 #pragma unroll
     for (int i = 0; i < Cfg::X_ITERS; ++i) {
       const int e = (i * 4 + wave) * 64 + lane;
-      if ((i * 4 + wave) < Cfg::X_INSTR && x_pix[i] >= 0) {
+      const int gw = w0 + x_dw[i], gh = h0 + x_dh[i];
+      const bool ok = gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && xch_ok && dok;
+      if ((i * 4 + wave) < Cfg::X_INSTR && ok) {
         uint4* q = reinterpret_cast<uint4*>(X + e * 16);
         float f[8];
         unpack8(*q, f);
@@ -693,14 +705,36 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
     }
   };
 
-  if (t_begin < t_end) issue(t_begin, 0);
-  for (int tile = t_begin; tile < t_end; ++tile) {
-    const int buf = (tile - t_begin) & 1;
-    dma_wait<0>();
-    if (second ? has_pro2 : has_pro) transform(sX(buf));
-    lds_sync();
-    if (tile + 1 < t_end) issue(tile + 1, buf ^ 1);
-    compute(sY(buf), sX(buf));
+  if constexpr (NB == 2) {
+    if (t_begin < t_end) issue(t_begin, 0);
+    for (int tile = t_begin; tile < t_end; ++tile) {
+      const int buf = (tile - t_begin) & 1;
+      dma_wait<0>();
+      if (second ? has_pro2 : has_pro) transform(tile, sX(buf));
+      lds_sync();
+      if (tile + 1 < t_end) issue(tile + 1, buf ^ 1);
+      compute(sY(buf), sX(buf));
+    }
+  } else {
+    // this wave's DMA instructions per tile (the counted waits below)
+    int per = 0;
+#pragma unroll
+    for (int i = 0; i < Cfg::Y_ITERS; ++i) per += (i * 4 + wave) < Cfg::Y_INSTR;
+#pragma unroll
+    for (int i = 0; i < Cfg::X_ITERS; ++i) per += (i * 4 + wave) < Cfg::X_INSTR;
+#pragma unroll
+    for (int j = 0; j < NB - 1; ++j)
+      if (t_begin + j < t_end) issue(t_begin + j, j);
+    for (int tile = t_begin; tile < t_end; ++tile) {
+      const int idx = tile - t_begin, buf = idx % NB;
+      const int after = min(NB - 2, t_end - 1 - tile);   // tiles issued after this one
+      vm_wait_dyn(after * per);
+      if (second ? has_pro2 : has_pro) transform(tile, sX(buf));
+      lds_sync();
+      // the buffer of tile - 1 is free (every wave is past its compute): refill it
+      if (tile + NB - 1 < t_end) issue(tile + NB - 1, (idx + NB - 1) % NB);
+      compute(sY(buf), sX(buf));
+    }
   }
 
   // ---- k-split reduction over the KW waves of each co tile (fixed order, in LDS, one tap
@@ -776,7 +810,12 @@ void conv3_wgrad2_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
 void conv3_wgrad3_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
   const int grid = a.coTiles * a.ciChunks * a.planes * a.splits;
   const int pt = a.TH * 16;
-  if (bco == 32)
+  // (32 output channels, 128-pixel tiles: the 3-deep ring variant; LDS = SS + 3 stages)
+  constexpr int SMEM32R = Wg2Cfg<32, 128>::SS_BYTES + 3 * (Wg2Cfg<32, 128>::Y_BYTES + Wg2Cfg<32, 128>::X_BYTES);
+  static_assert(2 * SMEM32R <= 160 * 1024, "two ring workgroups per CU");
+  if (bco == 32 && pt == 128)
+    hipLaunchKernelGGL((conv3_wgrad3_kernel<32, 128, 3>), dim3(grid), dim3(256), SMEM32R, st, a);
+  else if (bco == 32)
     hipLaunchKernelGGL((conv3_wgrad3_kernel<32, 256>), dim3(grid), dim3(256), (Wg2Cfg<32, 256>::SMEM), st, a);
   else if (pt == 256)
     hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 256>), dim3(grid), dim3(256), (Wg2Cfg<64, 256>::SMEM), st, a);
