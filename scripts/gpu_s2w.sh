@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 2 session 2, pass W: does the ~4.5 us floor of every small kernel in the step trace
+# move with kernel arguments in device memory (HIP_FORCE_DEV_KERNARG=1)?  bench A/B/A/B
+set -o pipefail
+cd "$(dirname "$0")/.."
+O=gpurun_out/s2w
+mkdir -p $O
+export TMPDIR=/tmp
+run() { local name=$1 to=$2; shift 2; timeout -k 10 $to "$@" > $O/$name.json 2> $O/$name.err; local rc=$?; echo "== $name rc=$rc"; python scripts/summ_bench.py $O/$name.json | cut -c1-100; [ $rc -eq 0 ] || exit $rc; }
+run def1 200 python -u bench.py
+run dk1 200 env HIP_FORCE_DEV_KERNARG=1 python -u bench.py
+run def2 200 python -u bench.py
+run dk2 200 env HIP_FORCE_DEV_KERNARG=1 python -u bench.py
