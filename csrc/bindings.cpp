@@ -911,16 +911,51 @@ std::vector<at::Tensor> head_wgrad_from_rows(const at::Tensor& rows, const at::T
   const bool into = dw_out.has_value() && dw_out->defined();
   if (into) {
     TORCH_CHECK(dw_out->is_contiguous() && db_out->is_contiguous(), "grad outs must be contiguous");
-    scatter_sums_dscale_launch(sums.data_ptr<double>(), K * C, dw_out->data_ptr<float>(),
-                               scale.data_ptr<float>(), true, cur_stream());
-    scatter_sums_dscale_launch(sums.data_ptr<double>() + K * C, K, db_out->data_ptr<float>(),
-                               scale.data_ptr<float>(), true, cur_stream());
+    if (db_out->data_ptr<float>() == dw_out->data_ptr<float>() + K * C) {
+      // adjacent in the flat gradient buffer (weight then bias): one launch
+      scatter_sums_dscale_launch(sums.data_ptr<double>(), K * C + K, dw_out->data_ptr<float>(),
+                                 scale.data_ptr<float>(), true, cur_stream());
+    } else {
+      scatter_sums_dscale_launch(sums.data_ptr<double>(), K * C, dw_out->data_ptr<float>(),
+                                 scale.data_ptr<float>(), true, cur_stream());
+      scatter_sums_dscale_launch(sums.data_ptr<double>() + K * C, K, db_out->data_ptr<float>(),
+                                 scale.data_ptr<float>(), true, cur_stream());
+    }
     return {at::empty({0}, fopts), at::empty({0}, fopts)};
   }
   at::Tensor red = at::empty({K * C + K}, fopts);
   scatter_sums_dscale_launch(sums.data_ptr<double>(), K * C + K, red.data_ptr<float>(),
                              scale.data_ptr<float>(), false, cur_stream());
   return {red.narrow(0, 0, K * C).view({K, C}), red.narrow(0, K * C, K)};
+}
+
+// dL/count as a device scalar from the loss kernel's out3 = (loss, correct, count) and the
+// incoming dL (absent: 1)
+at::Tensor head_grad_scale(const at::Tensor& out3, const c10::optional<at::Tensor>& gs) {
+  CHECK_F32(out3); CHECK_CONTIG(out3);
+  TORCH_CHECK(out3.numel() >= 3, "out3 must hold (loss, correct, count)");
+  c10::DeviceGuard guard(out3.device());
+  const float* pg = nullptr;
+  if (gs.has_value() && gs->defined()) {
+    CHECK_F32(*gs); CHECK_CONTIG(*gs);
+    TORCH_CHECK(gs->numel() == 1 && gs->device() == out3.device(), "gs must be one float on out3's device");
+    pg = gs->data_ptr<float>();
+  }
+  at::Tensor scale = at::empty({1}, out3.options());
+  head_grad_scale_launch(out3.data_ptr<float>(), pg, scale.data_ptr<float>(), cur_stream());
+  return scale;
+}
+
+// DeviceMeter accumulation in one launch (buf: 4 doubles; loss / correct: one float each)
+void meter_add(at::Tensor& buf, const at::Tensor& loss, const at::Tensor& correct, double pixels) {
+  TORCH_CHECK(buf.scalar_type() == at::kDouble && buf.numel() == 4 && buf.is_contiguous(),
+              "meter buffer must be 4 contiguous doubles");
+  CHECK_F32(loss); CHECK_F32(correct);
+  TORCH_CHECK(loss.numel() == 1 && correct.numel() == 1, "loss / correct must be scalars");
+  TORCH_CHECK(loss.device() == buf.device() && correct.device() == buf.device(), "device mismatch");
+  c10::DeviceGuard guard(buf.device());
+  meter_add_launch(buf.data_ptr<double>(), loss.data_ptr<float>(), correct.data_ptr<float>(), pixels,
+                   cur_stream());
 }
 
 at::Tensor head_logits(const at::Tensor& a, const at::Tensor& Wh, const at::Tensor& bh,
@@ -1150,6 +1185,8 @@ TORCH_LIBRARY(ddlpc, m) {
         "Tensor bn4) -> Tensor[]");
   m.def("head_wgrad_from_rows(Tensor rows, Tensor scale, int K, int C, Tensor(a!)? dw_out=None, "
         "Tensor(b!)? db_out=None) -> Tensor[]");
+  m.def("meter_add(Tensor(a!) buf, Tensor loss, Tensor correct, float pixels) -> ()");
+  m.def("head_grad_scale(Tensor out3, Tensor? gs=None) -> Tensor");
   m.def("head_logits(Tensor a, Tensor Wh, Tensor bh, Tensor? bn4=None) -> Tensor");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float eps, "
         "float wd, float step_size, float inv_sqrt_bc2) -> ()");
@@ -1183,6 +1220,8 @@ TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
   m.impl("head_ce_bn_bwd", &ddlpc::head_ce_bn_bwd);
   m.impl("head_ce_fwd_stats", &ddlpc::head_ce_fwd_stats);
   m.impl("head_wgrad_from_rows", &ddlpc::head_wgrad_from_rows);
+  m.impl("head_grad_scale", &ddlpc::head_grad_scale);
+  m.impl("meter_add", &ddlpc::meter_add);
   m.impl("head_logits", &ddlpc::head_logits);
   m.impl("adam_step", &ddlpc::adam_step);
   m.impl("adam_step_dev", &ddlpc::adam_step_dev);

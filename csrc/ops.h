@@ -216,6 +216,9 @@ void bn_stats_finalize_launch(const double* sums, int C, double count, const flo
 void bn_grad_finalize_launch(const double* sums, int C, double count, const float* gamma,
                              const float* invstd, float* dgamma, float* dbeta, float* coefs,
                              bool accumulate, hipStream_t st, const float* dscale = nullptr);
+void meter_add_launch(double* buf, const float* loss, const float* correct, double pixels,
+                      hipStream_t st);
+void head_grad_scale_launch(const float* out3, const float* gs, float* scale, hipStream_t st);
 void scatter_sums_dscale_launch(const double* sums, long long N, float* dst, const float* dscale,
                                 bool accumulate, hipStream_t st);
 // single-kernel variants reading the partial rows directly (P small): one block per channel

@@ -108,6 +108,25 @@ __global__ void scatter_sums_dscale_kernel(const double* __restrict__ sums, long
   }
 }
 
+// head gradient scale dL/count from the loss kernel's (loss, correct, count) and the incoming
+// dL (null: 1) — one thread; replaces a handful of tiny elementwise launches per step
+__global__ void head_grad_scale_kernel(const float* __restrict__ out3, const float* __restrict__ gs,
+                                       float* __restrict__ scale) {
+  if (threadIdx.x != 0) return;
+  const float cnt = out3[2];
+  scale[0] = (gs != nullptr ? gs[0] : 1.f) / (cnt > 0.f ? cnt : 1.f);
+}
+
+// training meter [sum loss, sum correct, sum pixels, micro-batches] += (loss, correct, pixels, 1)
+__global__ void meter_add_kernel(double* __restrict__ buf, const float* __restrict__ loss,
+                                 const float* __restrict__ correct, double pixels) {
+  const int t = threadIdx.x;
+  if (t == 0) buf[0] += (double)loss[0];
+  else if (t == 1) buf[1] += (double)correct[0];
+  else if (t == 2) buf[2] += pixels;
+  else if (t == 3) buf[3] += 1.0;
+}
+
 // one block per channel: fp64 sum of P partial rows, then finalize (P <= a few thousand)
 DDLPC_DEVICE void block_sum2(double& a, double& b) {
   __shared__ double r1[4], r2[4];
@@ -276,6 +295,15 @@ void scatter_sums_dscale_launch(const double* sums, long long N, float* dst, con
   const int grid = (int)std::max<long long>(1, std::min<long long>((N + 255) / 256, 4096));
   hipLaunchKernelGGL(scatter_sums_dscale_kernel, dim3(grid), dim3(256), 0, st, sums, N, dst, dscale,
                      accumulate ? 1 : 0);
+}
+
+void head_grad_scale_launch(const float* out3, const float* gs, float* scale, hipStream_t st) {
+  hipLaunchKernelGGL(head_grad_scale_kernel, dim3(1), dim3(64), 0, st, out3, gs, scale);
+}
+
+void meter_add_launch(double* buf, const float* loss, const float* correct, double pixels,
+                      hipStream_t st) {
+  hipLaunchKernelGGL(meter_add_kernel, dim3(1), dim3(64), 0, st, buf, loss, correct, pixels);
 }
 
 void scatter_sums_launch(const double* sums, long long N, float* dst, int mode, int A, int T,

@@ -392,9 +392,7 @@ class _HeadCEFn(torch.autograd.Function):
         if ctx.rows is not None:
             # statistics already reduced by the forward at unit scale: scale = dL / count
             wrows, brows = ctx.rows
-            cnt = out3[2:3]
-            g = gs if gs is not None else torch.ones_like(cnt)
-            scale = (g / torch.where(cnt > 0, cnt, torch.ones_like(cnt))).contiguous()
+            scale = _ops().head_grad_scale(out3, gs)       # one launch, on the device
             K, C = wh.shape
             head = eng.head
             if eng.direct_grads:

@@ -22,6 +22,18 @@ import torch
 import torch.distributed as dist
 
 
+_HIP = False
+
+
+def _hip_ops():
+    """``torch.ops.ddlpc`` when the kernel library is built, else None (CPU runs)."""
+    global _HIP
+    if _HIP is False:
+        from ..ops import _ext
+        _HIP = _ext.ops() if _ext.load(strict=False) else None
+    return _HIP
+
+
 class DeviceMeter:
     """Accumulates loss*n, correct pixels, pixel count on the device."""
 
@@ -41,6 +53,11 @@ class DeviceMeter:
 
     def add(self, loss: torch.Tensor, correct: torch.Tensor, pixels: int):
         # [sum loss, sum correct, sum pixels, micro-batches]; no host->device copies per step
+        if (self.buf.is_cuda and loss.dtype == torch.float32 and correct.dtype == torch.float32
+                and loss.numel() == 1 and correct.numel() == 1 and _hip_ops() is not None):
+            # one launch instead of five small elementwise kernels
+            _hip_ops().meter_add(self.buf, loss.detach(), correct.detach(), float(pixels))
+            return
         if self._inc_pixels != pixels:
             self._inc = torch.tensor([float(pixels), 1.0], dtype=torch.float64, device=self.device)
             self._inc_pixels = pixels

@@ -458,9 +458,15 @@ def test_head_fused_forward_stats(ops, C, K, H):
     assert torch.allclose(o, o_ref, rtol=1e-5, atol=0)
     gs = torch.tensor([0.5], device=DEV)
     _, dw_ref, db_ref, part_ref = ops.head_ce_bwd(yh, wh, bh, lab, o_ref, gs, -100, None, None, bnh, False)
-    scale = gs / o[2:3]
+    scale = ops.head_grad_scale(o, gs)
+    assert torch.allclose(scale, gs / o[2:3], rtol=1e-6, atol=0)
+    assert torch.allclose(ops.head_grad_scale(o), 1.0 / o[2:3], rtol=1e-6, atol=0)
     dw, db = ops.head_wgrad_from_rows(wrows, scale, K, C)
     assert rel_err(dw, dw_ref) < 1e-5 and rel_err(db, db_ref) < 1e-5
+    # into adjacent (weight, bias) views of one flat buffer: the single-launch scatter
+    flat = torch.zeros(K * C + K, device=DEV)
+    ops.head_wgrad_from_rows(wrows, scale, K, C, flat[:K * C].view(K, C), flat[K * C:])
+    assert torch.equal(flat[:K * C].view(K, C), dw) and torch.equal(flat[K * C:], db)
     gamma = torch.rand(C, device=DEV) + 0.5
     ref = ops.head_ce_bn_bwd(yh, wh, bh, lab, o_ref, gs, -100, bnh, part_ref, gamma)
     got = ops.head_ce_bn_bwd(yh, wh, bh, lab, o, gs, -100, bnh, brows, gamma, None, None, scale)
@@ -781,3 +787,17 @@ def test_deferred_skip_prologue_matches_materialised(ops, H, C1, C2, Cout):
     dw_mat = ops.conv3_wgrad(dy, up, a, None, None)
     dw_def = ops.conv3_wgrad(dy, up, y, None, None, None, bn4[2], bn4[3])
     assert torch.equal(dw_mat, dw_def)
+
+
+def test_meter_add_single_launch(ops):
+    """DeviceMeter on the HIP path (meter_add: one launch) accumulates exactly what the
+    elementwise path does: fp64 sums of loss, correct, pixels and the micro-batch count."""
+    from ddlpc.utils.metrics import DeviceMeter
+    m = DeviceMeter(DEV)
+    out3 = torch.tensor([0.75, 1000.0, 4096.0], device=DEV)
+    for k in range(3):
+        m.add(out3[0] * (k + 1), out3[1], 4096)
+    torch.cuda.synchronize()
+    assert m.buf.tolist() == [0.75 * 6, 3000.0, 3 * 4096.0, 3.0]
+    r = m.reduce()
+    assert abs(r["loss"] - 1.5) < 1e-12 and abs(r["pixel_acc"] - 1000.0 / 4096.0) < 1e-12
