@@ -590,12 +590,11 @@ std::vector<at::Tensor> convt_dgrad(const at::Tensor& dout, const at::Tensor& wd
   }
   const int res_rows = convt_res_rows(a, num_cus());
   if (a.bn4 != nullptr) {
-    // resident-weight kernel: one fully written row per persistent workgroup; GEMM fallback:
-    // one per workgroup of the widest tiling (128 x 64) — a 128-wide tiling writes fewer
-    // rows, the unused ones stay zero
-    const long long grid = res_rows > 0 ? res_rows : ((a.M + 127) / 128) * (long long)((a.N + 63) / 64);
-    bnpart = res_rows > 0 ? at::empty({(int64_t)grid, 2, (int64_t)cin}, dout.options().dtype(at::kFloat))
-                          : at::zeros({(int64_t)grid, 2, (int64_t)cin}, dout.options().dtype(at::kFloat));
+    // one fully written row per workgroup: the resident-weight kernel's persistent
+    // workgroups, or the GEMM fallback's tiles (each writes its full-width row, zeros
+    // outside its channel tile) — no zero-fill pass
+    const long long grid = res_rows > 0 ? res_rows : gemm_nt_grid(a);
+    bnpart = at::empty({(int64_t)grid, 2, (int64_t)cin}, dout.options().dtype(at::kFloat));
     a.bnpart = bnpart.data_ptr<float>();
   }
   if (res_rows == 0 || !convt_res_launch(a, num_cus(), cur_stream())) gemm_launch(a, cur_stream());

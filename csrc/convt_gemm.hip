@@ -851,6 +851,18 @@ int convt_wgrad2_tiles(const GemmArgs& a) {
   return ((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
 }
 
+int gemm_nt_bn(const GemmArgs& a) {
+  static const int fwd_bn = [] { const char* e = getenv("DDLPC_CONVT_BN"); return e ? atoi(e) : 128; }();
+  static const int dgrad_bn = [] { const char* e = getenv("DDLPC_CONVT_DGRAD_BN"); return e ? atoi(e) : 128; }();
+  return (a.N % 128 == 0 && (a.mode == GEMM_CONVT_FWD ? fwd_bn : dgrad_bn) == 128) ? 128 : 64;
+}
+
+// workgroups of the NT (forward / data-gradient) launch: one BN-partial row each
+long long gemm_nt_grid(const GemmArgs& a) {
+  const int bn = gemm_nt_bn(a);
+  return ((a.M + 127) / 128) * (long long)((a.N + bn - 1) / bn);
+}
+
 void gemm_launch(GemmArgs& a, hipStream_t st) {
   if (a.mode == GEMM_CONVT_WGRAD && a.wg2) {
     const int grid = convt_wgrad2_tiles(a) * a.splits;
@@ -868,10 +880,8 @@ void gemm_launch(GemmArgs& a, hipStream_t st) {
   // measured (B=64 U-Net shapes): the gathered data-gradient A operand gains from wide
   // steps; the forward (contiguous A, K = Cin) runs best at one chunk per step.  The forward
   // uses 128-wide N tiles when N allows (each A tile is read from L2 half as often)
-  static const int fwd_bn = [] { const char* e = getenv("DDLPC_CONVT_BN"); return e ? atoi(e) : 128; }();
-  static const int dgrad_bn = [] { const char* e = getenv("DDLPC_CONVT_DGRAD_BN"); return e ? atoi(e) : 128; }();
-  const int bn = (a.N % 128 == 0 && (a.mode == GEMM_CONVT_FWD ? fwd_bn : dgrad_bn) == 128) ? 128 : 64;
-  const long long grid = ((a.M + 127) / 128) * (long long)((a.N + bn - 1) / bn);
+  const int bn = gemm_nt_bn(a);
+  const long long grid = gemm_nt_grid(a);
   const int kc = a.mode == GEMM_CONVT_FWD ? 1 : a.K <= 64 ? 2 : 4;
   if (a.mode == GEMM_CONVT_FWD) {
     if (bn == 128) hipLaunchKernelGGL((gemm_nt_kernel<GEMM_CONVT_FWD, 1, 128>), dim3((unsigned)grid), dim3(256), 0, st, a);

@@ -124,6 +124,8 @@ enum GemmMode {
   GEMM_CONVT_WGRAD = 2, // TN: dW[ci][(sub, co)] = sum_px x[px][ci] * dOut[up(px, sub)][co]
 };
 void gemm_launch(GemmArgs& a, hipStream_t st);
+int gemm_nt_bn(const GemmArgs& a);            // N tile of the forward / data-gradient GEMM
+long long gemm_nt_grid(const GemmArgs& a);     // its workgroup count (= BN-partial rows)
 int convt_wgrad2_tiles(const GemmArgs& a);
 // fused data + weight gradient of a 2-D 64 -> 64-channel transposed conv (convt_gemm.hip):
 // A = x [px][64], B = dOut, C = dx [px][64] (bf16), Wd2 = packed dgrad weights, partial =

@@ -625,14 +625,16 @@ def _bn4(C, seed):
     return torch.stack([mean, invstd, scale, shift]).contiguous()
 
 
-@pytest.mark.parametrize("Cin,Cout,H", [(64, 64, 16), (128, 64, 12), (128, 128, 8)])
+@pytest.mark.parametrize("Cin,Cout,H", [(64, 64, 16), (128, 64, 12), (128, 128, 8), (512, 256, 8),
+                                        (256, 128, 12)])
 def test_deferred_bn_consumers_match_materialised(ops, Cin, Cout, H):
     """Deferred BatchNorm activations (engine: block output kept pre-BN, BN + ReLU applied
     on load by the transposed-conv / head kernels) equal the materialised path bit for bit,
     and the BN-backward partial sums emitted by the consumers' backward epilogues give the
     same BatchNorm backward as the standalone reduction pass.  (Cin, Cout) cover the
     resident-weight convT kernels' 128- and 64-wide n tiles in both directions; H = 12
-    leaves a partial 128-pixel tile.)"""
+    leaves a partial 128-pixel tile; 512 / 256 input channels take the GEMM data gradient,
+    whose BN-partial rows are one per launched tile, each fully written.)"""
     torch.manual_seed(11)
     N, W, C = 2, H, Cin
     y = torch.randn(N, H, W, C, device=DEV).bfloat16()
