@@ -1,6 +1,7 @@
 #!/bin/bash
 # BN-backward apply pass (bn_bwd2 MODE 1, no pool): loads in flight per lane (2 vs 4) and
 # streaming (nontemporal) dY stores — numerics with the variant, per-kernel time per variant
+# (the DDLPC_BN_APPLY_U / _NT knobs were removed after this measurement: neither helped)
 set -o pipefail
 cd "$(dirname "$0")/.."
 O=gpurun_out/s3a
