@@ -1144,8 +1144,8 @@ std::vector<at::Tensor> tile_gather(const at::Tensor& src, const at::Tensor& lab
   at::Tensor x = at::empty(xs, src.options().dtype(at::kBFloat16));
   if (B > 0)
     tile_gather_launch(src.data_ptr<uint8_t>(), lab.data_ptr<uint8_t>(), idx.data_ptr<int64_t>(),
-                       (int)B, S, (int)in_ch, (int)cpad, bptr_mut(x), y.data_ptr<int64_t>(),
-                       cur_stream());
+                       (int)B, S, (int)in_ch, (int)cpad, (long long)lab.size(0), bptr_mut(x),
+                       y.data_ptr<int64_t>(), cur_stream());
   return {x, y};
 }
 

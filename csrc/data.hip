@@ -94,18 +94,24 @@ __global__ __launch_bounds__(256) void synth_tiles_kernel(
 
 __global__ __launch_bounds__(256) void tile_gather_kernel(
     const uint8_t* __restrict__ src, const uint8_t* __restrict__ lab, const int64_t* __restrict__ idx,
-    int B, long long S, int in_ch, int cpad, bf16_t* __restrict__ x, int64_t* __restrict__ y) {
+    int B, long long S, int in_ch, int cpad, long long N, bf16_t* __restrict__ x,
+    int64_t* __restrict__ y) {
   const long long total = (long long)B * S;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
        e += (long long)gridDim.x * blockDim.x) {
     const int b = (int)(e / S);
     const long long p = e - (long long)b * S;
-    const long long sp = idx[b] * S + p;
-    y[e] = lab[sp];
+    const long long n = idx[b];
+    // an out-of-range sample index reads nothing: zero image, label -100 (CrossEntropy's
+    // ignore_index).  Host indices are range-checked by DeviceTileDataset.get first; device
+    // indices cannot raise without a blocking read-back
+    const bool in_range = n >= 0 && n < N;
+    const long long sp = in_range ? n * S + p : 0;
+    y[e] = in_range ? (int64_t)lab[sp] : (int64_t)-100;
     float f[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c)
-      f[c] = c < in_ch ? __fdiv_rn((float)src[sp * in_ch + c], 255.0f) : 0.f;
+      f[c] = (c < in_ch && in_range) ? __fdiv_rn((float)src[sp * in_ch + c], 255.0f) : 0.f;
     if (cpad == 8) {
       reinterpret_cast<uint4*>(x)[e] = pack8(f);
     } else {
@@ -131,9 +137,10 @@ void synth_tiles_launch(const int64_t* idx, int B, uint32_t seed, int classes, i
 }
 
 void tile_gather_launch(const uint8_t* src, const uint8_t* lab, const int64_t* idx, int B,
-                        long long S, int in_ch, int cpad, bf16_t* x, int64_t* y, hipStream_t st) {
+                        long long S, int in_ch, int cpad, long long N, bf16_t* x, int64_t* y,
+                        hipStream_t st) {
   hipLaunchKernelGGL(tile_gather_kernel, dim3(data_grid(B * S)), dim3(256), 0, st, src, lab, idx, B,
-                     S, in_ch, cpad, x, y);
+                     S, in_ch, cpad, N, x, y);
 }
 
 }  // namespace ddlpc

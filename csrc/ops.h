@@ -253,6 +253,7 @@ void synth_tiles_launch(const int64_t* idx, int B, uint32_t seed, int classes, i
                         int dims, int grid, float k, const float* palette, int cpad, bf16_t* x,
                         int64_t* y, hipStream_t st);
 void tile_gather_launch(const uint8_t* src, const uint8_t* lab, const int64_t* idx, int B,
-                        long long S, int in_ch, int cpad, bf16_t* x, int64_t* y, hipStream_t st);
+                        long long S, int in_ch, int cpad, long long N, bf16_t* x, int64_t* y,
+                        hipStream_t st);
 
 }  // namespace ddlpc

@@ -74,7 +74,8 @@ class TrainConfig:
     betas: tuple = (0.9, 0.999)
     eps: float = 1e-8
     weight_decay: float = 0.0
-    dtype: str = "bf16"                  # compute dtype on GPU (fp32 master weights)
+    dtype: str = "bf16"                  # compute dtype on GPU (fp32 master weights); "fp32"
+                                         # (the reference's precision) = stock ops, no autocast
     seed: int = 0
     # ---- data parallel -----------------------------------------------------------
     backend: Optional[str] = None        # None = nccl(RCCL) on GPU, gloo on CPU
@@ -106,7 +107,8 @@ class TrainConfig:
     profile_dir: Optional[str] = None    # torch.profiler Chrome traces per rank
     profile_steps: int = 5               # active profiler steps (after 2 wait + 2 warm-up)
     # ---- execution -----------------------------------------------------------------
-    impl: str = "auto"                   # auto | hip | torch   (hip = hand-written kernels)
+    impl: str = "auto"                   # auto | hip | torch   (hip = hand-written kernels, bf16;
+                                         # auto = hip on a GPU for bf16, torch for fp32)
     hip_graph: bool = False              # capture the train step in a hipGraph
     recompute: int = 0                   # HIP engine activation recompute in backward (SURVEY 5.7,
                                          # batches beyond HBM): 1 = each block's first conv output,
@@ -124,6 +126,12 @@ class TrainConfig:
                                    ("dtype", self.dtype, ("bf16", "fp32"))):
             if val not in allowed:
                 raise ValueError(f"{name}={val!r} not in {allowed}")
+        if self.impl == "hip" and self.dtype != "bf16":
+            # the hand-written kernels compute in bf16 (fp32 accumulation, fp32 master
+            # weights); fp32 compute — the reference's precision (ref.py:702-704) — runs on
+            # the stock-op path (impl="torch", or impl="auto" with dtype="fp32")
+            raise ValueError("impl='hip' computes in bf16; use dtype='bf16', or impl='torch' / "
+                             "'auto' for fp32 compute")
         if self.accum_steps < 1 or self.batch_per_gpu < 1:
             raise ValueError("accum_steps and batch_per_gpu must be >= 1")
         return self

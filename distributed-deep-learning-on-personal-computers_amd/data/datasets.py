@@ -322,6 +322,14 @@ class DeviceTileDataset:
         return xd, yd
 
     def get(self, idx) -> Tuple[torch.Tensor, torch.Tensor]:
+        if not torch.is_tensor(idx) or idx.device.type == "cpu":
+            # host indices: range-checked here (device indices are not — that would be a
+            # blocking read-back; the gather kernel turns an out-of-range one into a zero
+            # image with ignored labels instead of reading outside the dataset)
+            ii = torch.as_tensor(idx, dtype=torch.int64).reshape(-1)
+            if ii.numel() and (int(ii.min()) < 0 or int(ii.max()) >= len(self)):
+                raise IndexError(f"sample index out of range [0, {len(self)}): "
+                                 f"{int(ii.min())}..{int(ii.max())}")
         if self.resident:
             src, lab = self.x, self.y
             it = device_indices(idx, self.device)

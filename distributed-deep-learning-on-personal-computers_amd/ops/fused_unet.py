@@ -142,7 +142,7 @@ class _DoubleConvFn(torch.autograd.Function):
         # (a deferred block's y2 IS its output, held by the consumer anyway)
         rc = int(blk.engine.recompute) if training else 0
         ctx.recompute = rc
-        ctx.recompute_y2 = rc >= 2 and not defer
+        ctx.recompute_y2 = rc >= 2 and not defer and not defer_skip   # those save y2 anyway
         ctx.b1 = b1 if rc else None
         ctx.b2 = b2 if ctx.recompute_y2 else None
         empty = torch.empty(0, device=y1.device, dtype=y1.dtype)
@@ -189,6 +189,12 @@ class _DoubleConvFn(torch.autograd.Function):
         x2 = x2 if ctx.has_x2 else None
         # head gradient still to be formed (two-pass head backward, see _HeadCEFn)
         head = getattr(da2, "_ddlpc_head", None) if (ctx.defer and da2 is not None) else None
+        if (ctx.defer and head is None and da2 is not None and da2.dim() > 0
+                and all(st == 0 for st in da2.stride())):
+            # the head's zero-stride stand-in lost its attribute: another autograd consumer
+            # of the deferred output summed into it, so the head's gradient would be dropped
+            raise RuntimeError("deferred block output has a second autograd consumer besides "
+                               "the two-pass head; set engine.head_apply = False")
         if da2 is not None and head is None:
             da2 = da2.contiguous()
         if dpool is not None:

@@ -24,11 +24,13 @@ MI355X design:
   reference's skewed weights; for W=2 that is a plain sum, SURVEY.md §2.6);
 * optional lossy codec (fp16/int8 absmax, ref.py:25) as an all-gather of packed payloads
   + scales, decoded and summed in rank order (``parallel.codec``; fused HIP kernels on GPU);
-* optional bf16 wire format (``wire_dtype="bf16"``, lossless codec off): half the bytes of
-  the fp32 all-reduce with fp32 accumulation — an all-to-all of bf16 chunks (the
-  reduce-scatter's transport), a rank-ordered fp32 sum of the owned chunk, and an
-  all-gather of the bf16 result; every rank receives identical bits.  For slow links (the
-  reference's "PCs over Ethernet" setting) this halves the exchange time.
+* optional bf16 wire format (``wire_dtype="bf16"``): half the bytes of the fp32
+  all-reduce — an all-to-all of bf16 chunks (the reduce-scatter's transport) launched
+  asynchronously from backward, then in ``finish()`` a rank-ordered fp32 sum of the owned
+  chunk and an all-gather of the sums.  LOSSY: each rank's gradient is rounded to bf16
+  before the exchange and the reduced gradient is rounded to bf16 again before it is
+  copied back into the fp32 grad buffer (every rank receives identical bits).  For slow
+  links (the reference's "PCs over Ethernet" setting) this halves the bytes on the wire.
 """
 from __future__ import annotations
 
@@ -180,8 +182,9 @@ class GradBucketReducer:
         b.work = (w1, w2)
 
     def _launch_bf16(self, b: _Bucket, g: torch.Tensor):
-        """bf16 transport, fp32 accumulation: all-to-all of bf16 chunks -> each rank sums the
-        chunk it owns in fp32, in rank order -> all-gather of the bf16 sums."""
+        """bf16 transport, first half: the all-to-all of bf16 chunks, left in flight (its
+        wait, the fp32 rank-order sum and the all-gather run in ``finish()``, so backward is
+        never blocked by the exchange — on gloo a wait here would stall the host)."""
         n, W = g.numel(), self.world
         chunk = -(-n // W)
         if b.wire is None:
@@ -191,8 +194,15 @@ class GradBucketReducer:
                       torch.empty_like(send))
         send, recv, own, out = b.wire
         send[:n].copy_(g)
-        dist.all_to_all_single(recv, send, group=self.group, async_op=True).wait()
-        own.copy_(recv.view(W, chunk).float().sum(0))
+        b.work = ("a2a", dist.all_to_all_single(recv, send, group=self.group, async_op=True))
+
+    def _finish_bf16(self, b: _Bucket):
+        """bf16 transport, second half: wait the all-to-all, sum the owned chunk in fp32 in
+        rank order, launch the all-gather of the sums (waited by the caller)."""
+        _, recv, own, out = b.wire
+        chunk = own.numel()
+        b.work[1].wait()
+        own.copy_(recv.view(self.world, chunk).float().sum(0))
         b.work = ("bf16", dist.all_gather_into_tensor(out, own, group=self.group,
                                                       async_op=True))
 
@@ -211,6 +221,9 @@ class GradBucketReducer:
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)
+        for b in self.buckets:                      # bf16 wire: all-gathers in bucket order
+            if isinstance(b.work, tuple) and b.work[0] == "a2a":
+                self._finish_bf16(b)
         for b in self.buckets:
             if b.work is None:
                 continue

@@ -40,13 +40,17 @@ from ..utils.tracing import PhaseTimer, StepProfiler, enable_ranges, trace_range
 from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
 
 
-def resolve_impl(impl: str, device: torch.device) -> str:
+def resolve_impl(impl: str, device: torch.device, dtype: str = "bf16") -> str:
+    """``auto``: the HIP kernels on a GPU for bf16 compute; stock ops for fp32 compute (the
+    reference's precision) or on a CPU.  ``hip`` with fp32 is rejected by the config."""
     if device.type != "cuda":
         if impl == "hip":
             raise RuntimeError("impl='hip' needs a GPU")
         return "torch"
     if impl == "auto":
-        return "hip"
+        return "hip" if dtype == "bf16" else "torch"
+    if impl == "hip" and dtype != "bf16":
+        raise ValueError("impl='hip' computes in bf16 (dtype='fp32' needs impl='torch')")
     return impl
 
 
@@ -59,7 +63,7 @@ class Trainer:
         self.rank, self.world = self.info.rank, self.info.world_size
         torch.manual_seed(cfg.seed)                  # identical init on every rank ...
         model = UNet.from_config(cfg.model).to(self.device)
-        self.impl = resolve_impl(cfg.impl, self.device)
+        self.impl = resolve_impl(cfg.impl, self.device, cfg.dtype)
         self.model = model
         if self.device.type == "cuda" and self.impl == "torch":
             # MIOpen NHWC / NDHWC path (baseline)
@@ -118,6 +122,10 @@ class Trainer:
             path = latest_checkpoint(cfg.ckpt_dir) if cfg.resume == "auto" else cfg.resume
             if path and os.path.exists(path):
                 self.load(path)
+            elif cfg.resume != "auto" and self.rank == 0:
+                # an explicit path must exist on rank 0 (its state is broadcast below); other
+                # ranks may lack the file (no shared filesystem) and receive rank 0's state
+                raise FileNotFoundError(f"resume checkpoint not found: {cfg.resume}")
             # only rank 0 writes checkpoints: on machines without a shared filesystem the
             # other ranks find none, so rank 0's restored state is authoritative
             self._broadcast_state()
