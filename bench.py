@@ -64,6 +64,12 @@ def _parse():
     ap.add_argument("--fixed-batch", type=int, default=0,
                     help="diagnostic: 1 = reuse one rendered batch every step (no per-step "
                          "input pipeline; reported in 'data')")
+    ap.add_argument("--reserve-cus", type=int, default=-1,
+                    help="CUs kept out of persistent kernel grids (-1: 8 under DP, else 0)")
+    ap.add_argument("--comm-proxy", type=int, default=0,
+                    help="1 GPU: stand-in collective per gradient bucket for a world of N "
+                         "(streaming kernel on a third stream; measures launch-to-finish "
+                         "latency during backward)")
     ap.add_argument("--heartbeat", type=float, default=0.0,
                     help="seconds between 'alive' lines on stderr (long first-step autotuning)")
     return ap.parse_args()
@@ -149,7 +155,8 @@ def main():
                       num_samples=1 << 30, test_holdout=0, impl=args.impl,
                       bucket_mb=args.bucket_mb, wire_dtype=args.wire_dtype,
                       grad_codec=args.codec, log_dir=None, hip_graph=bool(args.hip_graph),
-                      recompute=int(args.recompute))
+                      recompute=int(args.recompute), reserve_cus=args.reserve_cus,
+                      comm_proxy=args.comm_proxy)
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     tr = Trainer(cfg, device=dev)
     world, rank = tr.world, tr.rank
@@ -233,7 +240,14 @@ def main():
             sweep[str(mb)] = {"buckets": nb,
                               "ms_per_step": round(timed(args.steps, first) / args.steps * 1e3, 3)}
         tr.set_bucket_mb(args.bucket_mb)
+    proxy = None
+    if tr.reducer is not None and tr.reducer.proxy:
+        proxy = [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in d.items()}
+                 for d in tr.reducer.proxy_times()]
     base = _baseline(args)
+    from ddlpc.utils.flops import PEAK_BF16_TFLOPS, unet_train_flops_per_sample
+    flop_img = unet_train_flops_per_sample(cfg.model, args.tile)
+    tflops = value * flop_img / 1e12                     # whole job
     loss = tr.meter.reduce()
     if args.dims == 2:
         metric = f"images/sec (whole node), U-Net {args.tile}x{args.tile} {args.classes}-class tiles"
@@ -256,6 +270,11 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": (round(value / (base * world), 3) if base else None),
+            # roofline: model-geometry FLOPs (3 x forward conv MACs x 2, utils/flops.py) per
+            # second, and that as a fraction of world x 2.5 PF dense bf16
+            "tflops_per_s": round(tflops, 1),
+            "mfu": round(tflops / (PEAK_BF16_TFLOPS * world), 4),
+            "gflop_per_sample": round(flop_img / 1e9, 2),
             "dtype": "bf16" if dev == "cuda" else "fp32",
             "data": data_desc,
             "config": {"model": f"UNet depth{args.depth} width/{args.width_divisor} "
@@ -264,7 +283,11 @@ def main():
                        "per_gpu_batch": B, "accum_steps": args.accum,
                        "seq_len": None, "tile": args.tile, "dims": args.dims,
                        "classes": args.classes,
-                       "parallelism": f"dp{world}", "impl": tr.impl,
+                       "parallelism": f"dp{world}" + (f"+comm_proxy{args.comm_proxy}"
+                                                       if args.comm_proxy else ""),
+                       "impl": tr.impl,
+                       "reserve_cus": getattr(tr, "reserve_cus", None),
+                       "comm_proxy_last_step": proxy,
                        "optimizer": "Adam(lr=1e-3)", "loss": "CrossEntropy",
                        "train_loss_mean": round(loss["loss"], 4),
                        "recompute": int(args.recompute),

@@ -72,7 +72,7 @@ int pick_bn(int Cout) {
   return 128;
 }
 
-int num_cus() {
+int phys_cus() {
   static int n = -1;
   if (n < 0) {
     hipDeviceProp_t prop;
@@ -82,6 +82,14 @@ int num_cus() {
   }
   return n;
 }
+
+// CUs left out of every persistent / chip-filling grid (set_cu_reserve): under data
+// parallelism an RCCL kernel launched in the middle of backward needs free workgroup slots
+// at once, but the persistent conv / head kernels otherwise hold every CU until they exit
+int g_cu_reserve = 0;
+
+// the CU count grids are sized for
+int num_cus() { return std::max(8, phys_cus() - g_cu_reserve); }
 
 // fp64 column sums of an fp32 [R][N] partial slab (deterministic two-pass reduction)
 at::Tensor reduce_rows(const at::Tensor& partial, int64_t R, int64_t N) {
@@ -199,6 +207,14 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
     if (a.nTilesM * a.nTilesN >= num_cus()) cfg = 4;
     else plan(cfg);
   }
+  // 512-pixel tiles (cfg 5) where they fill the chip without padding (DDLPC_CONV_CFG5=0: off)
+  static const int use_cfg5 = [] { const char* e = getenv("DDLPC_CONV_CFG5"); return e ? atoi(e) : 1; }();
+  if (cfg == 4 && use_cfg5 && a.bnb_y == nullptr) {
+    plan(5);
+    const double w5 = (double)a.nTilesM * 512 / ((double)g.N * g.D * g.H * g.W);
+    if (a.nTilesM * a.nTilesN >= num_cus() && w5 <= 1.05) cfg = 5;
+    else plan(cfg);
+  }
   if (cfg == 2 && a.nTilesM * a.nTilesN < 2 * num_cus()) { cfg = 3; plan(cfg); }
   // small images: a tile larger than the image computes padding (the 8x8 bottleneck layer
   // under a 256-pixel tile is 75% padding: 48.6 -> 32.5 us with 64-pixel tiles, batch 128)
@@ -207,6 +223,8 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
     return (double)a.nTilesM * conv3_fwd_cfg_bm(c) / ((double)g.N * g.D * g.H * g.W);
   };
   while ((cfg == 4 || cfg == 2) && waste(cfg) > 1.3) cfg = cfg == 4 ? 2 : 3;
+  if (cfg == 5 && waste(5) > 1.05) cfg = 4;
+  if (cfg == 5) { plan(5); TORCH_CHECK(a.TW == 16 && g.dims == 2, "cfg 5: 16-wide 2-D tiles"); }
   plan(cfg);
   TORCH_CHECK((g.dims == 3 ? a.TD + 2 : 1) * (a.TH + 2) * (a.TW + 2) <= conv3_fwd_cfg_halo(g.dims, cfg),
               "halo exceeds LDS capacity");
@@ -218,7 +236,7 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   at::Tensor y2;
   if (a.Co1 < a.Cout) y2 = at::empty(shape_with_c(g, a.Cout - a.Co1), opts);
   at::Tensor stats;
-  a.persist_blocks = (cfg == 4 ? 1 : 2) * num_cus();   // cfg 4: one 8-wave workgroup per CU
+  a.persist_blocks = (cfg >= 4 ? 1 : 2) * num_cus();   // cfg 4/5: one 8-wave workgroup per CU
   {
     static const int pb = [] { const char* e = getenv("DDLPC_CONV_PERSIST"); return e ? atoi(e) : -1; }();
     static const int ksx = [] { const char* e = getenv("DDLPC_CONV_KSPLIT"); return e ? atoi(e) : -1; }();
@@ -1149,11 +1167,30 @@ std::vector<at::Tensor> tile_gather(const at::Tensor& src, const at::Tensor& lab
   return {x, y};
 }
 
+// -> the CU count grids are sized for after reserving k CUs (k < 0: query only)
+int64_t set_cu_reserve(int64_t k) {
+  if (k >= 0) g_cu_reserve = (int)std::min<int64_t>(k, std::max(0, phys_cus() - 8));
+  return num_cus();
+}
+
+// single-GPU stand-in for a bucket all-reduce (Trainer comm_proxy): `blocks` workgroups
+// stream the bucket `passes` times (read + write back, values unchanged) on the current
+// stream — RCCL's footprint (a few tens of channels, each a streaming workgroup)
+void comm_proxy(const at::Tensor& g, int64_t blocks, int64_t passes) {
+  CHECK_DEV(g); CHECK_CONTIG(g); CHECK_F32(g);
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0, "comm_proxy: 16-byte aligned buffer");
+  c10::DeviceGuard guard(g.device());
+  if (g.numel() == 0) return;
+  comm_proxy_launch(g.data_ptr<float>(), g.numel(), (int)blocks, (int)passes, cur_stream());
+}
+
 }  // namespace
 
 }  // namespace ddlpc
 
 TORCH_LIBRARY(ddlpc, m) {
+  m.def("set_cu_reserve(int k) -> int", &ddlpc::set_cu_reserve);
+  m.def("comm_proxy(Tensor(a!) g, int blocks, int passes) -> ()");
   m.def("conv3_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, Tensor? pscale, Tensor? pshift, "
         "int cout, int co1, bool stats, Tensor? pscale2=None, Tensor? pshift2=None, Tensor? bnb_y=None, "
         "Tensor? bnb_s4=None) -> Tensor[]");
@@ -1233,4 +1270,5 @@ TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
   m.impl("to_nhwc_bf16", &ddlpc::to_nhwc_bf16);
   m.impl("synth_tiles", &ddlpc::synth_tiles);
   m.impl("tile_gather", &ddlpc::tile_gather);
+  m.impl("comm_proxy", &ddlpc::comm_proxy);
 }

@@ -53,7 +53,12 @@ struct Cfg {
   static constexpr int B_ITERS = (3 * BN * 4 / 64 + NW - 1) / NW;  // DMA instrs / wave / stage
   static constexpr int B_BYTES = B_ITERS * NW * 1024;           // one weight buffer
   static constexpr int SS_BYTES = 2 * 512 * 4;                  // prologue scale/shift
-  static constexpr int SMEM = SS_BYTES + 2 * A_BYTES + NBB * B_BYTES;   // NBB weight buffers
+  // LEAN (accumulator of 32+ tiles per wave): bias and the BN-statistics accumulators live
+  // in LDS instead of 48 VGPRs — per-wave-row slots [WM][2][BN], each (wave, column) owned
+  // by one lane (no atomics: the order of the sums is fixed) + the bias of the n tile
+  static constexpr bool LEAN = MT * NT >= 32;
+  static constexpr int LEAN_BYTES = LEAN ? (WM * 2 * BN + BN) * 4 : 0;
+  static constexpr int SMEM = SS_BYTES + LEAN_BYTES + 2 * A_BYTES + NBB * B_BYTES;   // NBB weight buffers
 };
 
 // Persistent workgroups walk (m tile, n tile) items; the stage stream runs across item
@@ -78,7 +83,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* s_scale = reinterpret_cast<float*>(smem);
   float* s_shift = s_scale + 512;
-  char* base = smem + C::SS_BYTES;
+  char* base = smem + C::SS_BYTES + C::LEAN_BYTES;
+  constexpr bool LEAN = C::LEAN;
+  float* s_red = reinterpret_cast<float*>(smem + C::SS_BYTES);    // LEAN: [WM][2][BN]
+  float* s_bias = s_red + WM * 2 * BN;                             // LEAN: [BN]
+  static_assert(!LEAN || !BNB, "LEAN tiles: no BN-backward epilogue");
   // double buffers addressed arithmetically (a runtime-indexed pointer array would spill)
   auto sA = [&](int b) { return base + b * C::A_BYTES; };
   auto sB = [&](int b) { return base + 2 * C::A_BYTES + b * C::B_BYTES; };
@@ -225,14 +234,17 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 
   // ---- per-lane fragment geometry (item independent)
   const int g = lane >> 4;
-  int hp0[MT];
+  // (LEAN: 16-wide pixel tiles, TW == 16 — launcher-enforced — so the halo pixel of tile mt
+  // is hp_lean + mt * HW2: one register instead of MT)
+  const int hp_lean = (wm * MT) * HW2 + (lane & 15);
+  int hp0[LEAN ? 1 : MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
     const int pw = pix % p.TW;
     const int ph = (pix / p.TW) % p.TH;
     const int pd = DIMS == 3 ? pix / (p.TW * p.TH) : 0;
-    hp0[mt] = (pd * HH2 + ph) * HW2 + pw;
+    if (!LEAN) hp0[LEAN ? 0 : mt] = (pd * HH2 + ph) * HW2 + pw;
   }
 
   f32x4_t acc[MT][NT];
@@ -242,21 +254,29 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   // BN statistics accumulate in registers across all items of this workgroup: every item
   // of a workgroup has the same n tile (grid % nTilesN == 0, enforced by the launcher)
-  float s1[NT][4], s2[NT][4];
+  float s1[NT][4], s2[NT][4];                        // (LEAN: unused)
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int i = 0; i < 4; ++i) { s1[nt][i] = 0.f; s2[nt][i] = 0.f; }
+  if constexpr (LEAN) {
+    // published to every wave by the first stage barrier
+    for (int i = tid; i < WM * 2 * BN; i += C::NTH) s_red[i] = 0.f;
+    for (int i = tid; i < BN; i += C::NTH) {
+      const int co = co0_blk + i;
+      s_bias[i] = (p.bias != nullptr && co < p.Cout) ? p.bias[co] : 0.0f;
+    }
+  }
 
   // bias of this block's channel tile, loaded once (a global load inside the epilogue would
   // make the compiler wait vmcnt(0) — on in-flight stores and DMA — before every use)
-  float bias_r[NT][4];
+  float bias_r[NT][4];                               // (LEAN: unused, bias in LDS)
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int co = co0_blk + wn * (NT * 16) + nt * 16 + 4 * g + i;
-      bias_r[nt][i] = (p.bias != nullptr && co < p.Cout) ? p.bias[co] : 0.0f;
+      bias_r[nt][i] = (!LEAN && p.bias != nullptr && co < p.Cout) ? p.bias[co] : 0.0f;
     }
 
   // ---- epilogue of item k straight from the accumulators:
@@ -304,6 +324,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       const int co = it.co0 + wn * (NT * 16) + nt * 16 + 4 * g;
       BnbC kb;
       if constexpr (BNB) kb = bnb_load(s_scale, BN, wn * (NT * 16) + nt * 16 + 4 * g);
+      // LEAN: this tile's bias from LDS, statistics of its 4 channels summed over the mt
+      // tiles here, then over the 16 pixel lanes into the wave's LDS slot below
+      float bl[4] = {0.f, 0.f, 0.f, 0.f}, t1[4] = {0.f, 0.f, 0.f, 0.f}, t2[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (LEAN) {
+        const float4 b4 = *reinterpret_cast<const float4*>(s_bias + opaque_zero() + wn * (NT * 16) + nt * 16 + 4 * g);
+        bl[0] = b4.x; bl[1] = b4.y; bl[2] = b4.z; bl[3] = b4.w;
+      }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
@@ -324,7 +351,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         }
         float v[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bias_r[nt][i];
+        for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + (LEAN ? bl[i] : bias_r[nt][i]);
         const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         pkv[mt][nt] = pk;
         if (!pairs) {
@@ -339,12 +366,34 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         } else if (ok) {
           // statistics of the stored (bf16-rounded) values
           const float r0 = lo_bf(pk.x), q1 = hi_bf(pk.x), q2 = lo_bf(pk.y), q3 = hi_bf(pk.y);
-          s1[nt][0] += r0; s2[nt][0] += r0 * r0;
-          s1[nt][1] += q1; s2[nt][1] += q1 * q1;
-          s1[nt][2] += q2; s2[nt][2] += q2 * q2;
-          s1[nt][3] += q3; s2[nt][3] += q3 * q3;
+          if constexpr (LEAN) {
+            t1[0] += r0; t2[0] += r0 * r0;
+            t1[1] += q1; t2[1] += q1 * q1;
+            t1[2] += q2; t2[2] += q2 * q2;
+            t1[3] += q3; t2[3] += q3 * q3;
+          } else {
+            s1[nt][0] += r0; s2[nt][0] += r0 * r0;
+            s1[nt][1] += q1; s2[nt][1] += q1 * q1;
+            s1[nt][2] += q2; s2[nt][2] += q2 * q2;
+            s1[nt][3] += q3; s2[nt][3] += q3 * q3;
+          }
         }
         acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+      if constexpr (LEAN) {
+        if (p.stats != nullptr && KS == 1) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float a1 = t1[i], a2 = t2[i];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) { a1 += __shfl_xor(a1, o, 64); a2 += __shfl_xor(a2, o, 64); }
+            if ((lane & 15) == 0) {
+              const int col = wn * (NT * 16) + nt * 16 + 4 * g + i;
+              s_red[(2 * wm) * BN + col] += a1;       // one owner lane per (wave, column)
+              s_red[(2 * wm + 1) * BN + col] += a2;
+            }
+          }
+        }
       }
       if constexpr (BNB) __builtin_amdgcn_sched_barrier(0);
     }
@@ -379,7 +428,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     auto load_frags = [&](int t, uint4 (&xf)[MT], uint4 (&wf)[NT]) __attribute__((always_inline)) {
       const int tapoff = (kd * HH2 + r) * HW2 + t;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) xf[mt] = lds128(A + lds_off(hp0[mt] + tapoff, g));
+      for (int mt = 0; mt < MT; ++mt)
+        xf[mt] = lds128(A + lds_off((LEAN ? hp_lean + mt * HW2 : hp0[LEAN ? 0 : mt]) + tapoff, g));
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
         wf[nt] = lds128(B + lds_off(t * BN + wn * (NT * 16) + nt * 16 + (lane & 15), g));
@@ -408,7 +458,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       const char* B = tt < 3 ? B0 : B1;
       const int tapoff = (tt < 3 ? r0 : r1) * HW2 + t;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) xf[mt] = lds128(A + lds_off(hp0[mt] + tapoff, g));
+      for (int mt = 0; mt < MT; ++mt)
+        xf[mt] = lds128(A + lds_off((LEAN ? hp_lean + mt * HW2 : hp0[LEAN ? 0 : mt]) + tapoff, g));
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
         wf[nt] = lds128(B + lds_off(t * BN + wn * (NT * 16) + nt * 16 + (lane & 15), g));
@@ -613,10 +664,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   if (p.stats != nullptr && KS == 1) {
     dma_wait<0>();
     lds_sync();
-    float* red = reinterpret_cast<float*>(base);          // halo buffers are free now
+    float* red = LEAN ? s_red : reinterpret_cast<float*>(base);   // halo buffers are free now
     const int co0 = my_items > 0 ? item_of(0).co0 : 0;
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
+    for (int nt = 0; nt < (LEAN ? 0 : NT); ++nt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float a1 = s1[nt][i], a2 = s2[nt][i];
@@ -752,7 +803,7 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
       return;
     }
   }
-  if constexpr (DIMS == 2 && NBB != 3) {
+  if constexpr (DIMS == 2 && NBB != 3 && !C::LEAN) {
     if (a.bnb_y != nullptr) {
       hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK, true, false>), dim3(grid),
                          dim3(C::NTH), C::SMEM, st, a);
@@ -765,6 +816,21 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   else
     hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, false, false, false>), dim3(grid),
                        dim3(C::NTH), C::SMEM, st, a);
+}
+
+// cfg 5 without fragment double buffering (never with the BN-backward epilogue: LEAN tiles)
+void launch_cfg5_nofdb(ConvFwdArgs& a, hipStream_t st) {
+  using C = Cfg<2, 4, 2, 8, 4, 640, 2>;
+  const int items = a.nTilesM * a.nTilesN * a.ksplit;
+  int grid = items;
+  if (a.persist_blocks > 0 && grid > a.persist_blocks) {
+    const int q = a.nTilesN * a.ksplit;
+    grid = a.persist_blocks / q * q;
+  }
+  a.stat_rows = grid;
+  a.diag = 0;
+  hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 640, 2, false, false, false>), dim3(grid),
+                     dim3(C::NTH), C::SMEM, st, a);
 }
 
 // super-stages (two kernel rows per barrier) in the 8-wave configuration (DDLPC_CONV_SUPER=0: off)
@@ -781,7 +847,14 @@ int conv_nbb() {
   return v == 3 ? 3 : 2;
 }
 
-int cfg_wm(int cfg) { return cfg <= 1 || cfg == 4 ? 4 : cfg == 2 ? 2 : 1; }
+int cfg_wm(int cfg) { return cfg <= 1 || cfg >= 4 ? 4 : cfg == 2 ? 2 : 1; }
+
+// BM-512 configuration (cfg 5): fragment double buffering off by default (VGPR budget of two
+// waves per SIMD with a 128-register accumulator); DDLPC_CONV5_FDB=1 turns it on
+bool conv5_fdb() {
+  static const int v = [] { const char* e = getenv("DDLPC_CONV5_FDB"); return e ? atoi(e) : 0; }();
+  return v != 0;
+}
 
 }  // namespace
 
@@ -792,12 +865,15 @@ int cfg_wm(int cfg) { return cfg <= 1 || cfg == 4 ? 4 : cfg == 2 ? 2 : 1; }
 //   3: BN 128, BM 64  (1x4 waves, 4x2 tiles)     2-D 4x16 / 8x8     3-D 1x4x16 / 2x4x8
 //   4: BN 128, BM 256 (4x2 waves = 512 threads, 4x4 tiles; 2-D only) 16x16 / 32x8: half the
 //      weight-stream traffic per MFMA of cfg 2 (one workgroup per CU)
+//   5: BN 128, BM 512 (4x2 waves = 512 threads, 8x4 tiles: 128 px x 64 ch per wave; 2-D
+//      only) 32x16: half cfg 4's weight-stream DMA per MFMA and a quarter fewer LDS fragment
+//      reads per MFMA (each wave's weight fragments serve 8 pixel tiles)
 // (halo capacity = DMA instructions per wave x 64 pixels)
 int conv3_fwd_cfg_wm(int cfg) { return cfg_wm(cfg); }
 int conv3_fwd_cfg_bn(int cfg) { return cfg == 0 ? 32 : cfg == 1 ? 64 : 128; }
-int conv3_fwd_cfg_bm(int cfg) { return cfg <= 1 || cfg == 4 ? 256 : cfg == 2 ? 128 : 64; }
+int conv3_fwd_cfg_bm(int cfg) { return cfg == 5 ? 512 : cfg <= 1 || cfg == 4 ? 256 : cfg == 2 ? 128 : 64; }
 int conv3_fwd_cfg_halo(int dims, int cfg) {
-  if (dims == 2) return cfg <= 1 || cfg == 4 ? 384 : cfg == 2 ? 192 : 128;
+  if (dims == 2) return cfg == 5 ? 640 : cfg <= 1 || cfg == 4 ? 384 : cfg == 2 ? 192 : 128;
   return cfg <= 1 ? 704 : cfg == 2 ? 448 : 384;
 }
 
@@ -819,6 +895,10 @@ void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st) {
         else launch_cfg<2, 4, 2, 4, 4, 384, 2>(a, st);
         break;
       }
+      case 5:
+        if (conv5_fdb()) launch_cfg<2, 4, 2, 8, 4, 640, 2>(a, st);
+        else launch_cfg5_nofdb(a, st);
+        break;
       default: launch_cfg<2, 1, 4, 4, 2, 128>(a, st); break;
     }
   } else {

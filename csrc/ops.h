@@ -256,4 +256,7 @@ void tile_gather_launch(const uint8_t* src, const uint8_t* lab, const int64_t* i
                         long long S, int in_ch, int cpad, long long N, bf16_t* x, int64_t* y,
                         hipStream_t st);
 
+// ---------------------------------------------------------------- comm proxy (reduce.hip)
+void comm_proxy_launch(float* g, long long n, int blocks, int passes, hipStream_t st);
+
 }  // namespace ddlpc

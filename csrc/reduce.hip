@@ -301,6 +301,26 @@ void head_grad_scale_launch(const float* out3, const float* gs, float* scale, hi
   hipLaunchKernelGGL(head_grad_scale_kernel, dim3(1), dim3(64), 0, st, out3, gs, scale);
 }
 
+// a bucket all-reduce's memory footprint without a peer: `passes` read + write-back sweeps
+// (values unchanged: the empty asm keeps the compiler from folding the store of a just-
+// loaded value), 16-byte accesses, each workgroup on its own contiguous slice
+__global__ __launch_bounds__(256) void comm_proxy_kernel(float* __restrict__ g, long long n, int passes) {
+  const long long n4 = n / 4;
+  const long long per = (n4 + gridDim.x - 1) / gridDim.x;
+  const long long lo = blockIdx.x * per, hi = lo + per < n4 ? lo + per : n4;
+  for (int p = 0; p < passes; ++p) {
+    for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      float4 v = reinterpret_cast<float4*>(g)[i];
+      asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+      reinterpret_cast<float4*>(g)[i] = v;
+    }
+  }
+}
+
+void comm_proxy_launch(float* g, long long n, int blocks, int passes, hipStream_t st) {
+  hipLaunchKernelGGL(comm_proxy_kernel, dim3(std::max(1, blocks)), dim3(256), 0, st, g, n, passes);
+}
+
 void meter_add_launch(double* buf, const float* loss, const float* correct, double pixels,
                       hipStream_t st) {
   hipLaunchKernelGGL(meter_add_kernel, dim3(1), dim3(64), 0, st, buf, loss, correct, pixels);

@@ -87,6 +87,11 @@ class TrainConfig:
     overlap_comm: bool = True
     broadcast_buffers: bool = False      # BN running stats from rank 0 (reference: off)
     check_consistency_every: int = 0     # debug: all-reduce a param checksum every K steps
+    reserve_cus: int = -1                # CUs kept out of persistent kernel grids so a
+                                         # collective launched mid-backward starts at once
+                                         # (-1 = auto: 8 with data parallelism, else 0)
+    comm_proxy: int = 0                  # single GPU: stand-in collective for a world of N
+                                         # (streaming kernel on a third stream, identity)
     timeout_s: int = 1800
     # fault injection: rank `fault_rank` exits (code 17) right after
     # optimizer step `fault_step`, on the first launch attempt only

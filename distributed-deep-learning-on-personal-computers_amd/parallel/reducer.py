@@ -46,7 +46,7 @@ from .flat import FlatParams
 
 class _Bucket:
     __slots__ = ("idx", "start", "end", "params", "pending", "work", "payload", "scales",
-                 "gathered", "launched", "wire")
+                 "gathered", "launched", "wire", "ev")
 
     def __init__(self, idx, start, end, params):
         self.idx, self.start, self.end, self.params = idx, start, end, params
@@ -55,12 +55,14 @@ class _Bucket:
         self.payload = self.scales = self.gathered = None
         self.launched = False
         self.wire = None                 # bf16 wire buffers (send, recv, owned chunk, out)
+        self.ev = None                   # comm proxy: (ready, start, end) events
 
 
 class GradBucketReducer:
     def __init__(self, flat: FlatParams, group=None, bucket_mb: float = 8.0,
                  reduce: str = "mean", grad_codec: str = "none", codec_scale: str = "bucket",
-                 overlap: bool = True, use_hooks: bool = True, wire_dtype: str = "fp32"):
+                 overlap: bool = True, use_hooks: bool = True, wire_dtype: str = "fp32",
+                 proxy: int = 0):
         if wire_dtype not in ("fp32", "bf16"):
             raise ValueError(f"wire_dtype={wire_dtype!r}")
         self.flat = flat
@@ -69,6 +71,21 @@ class GradBucketReducer:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.backend = dist.get_backend(group) if dist.is_initialized() else None
+        # comm proxy (single GPU; ``proxy`` = the world size it stands in for): every
+        # bucket's collective is replaced by ``comm_proxy`` — 16 streaming workgroups (an
+        # RCCL-like channel count) sweeping the bucket twice (reduce-scatter + all-gather
+        # passes, values unchanged) — on a dedicated comm stream, launched at the same
+        # readiness points as the real collective.  It measures how fast a collective
+        # launched mid-backward gets CUs next to the persistent kernels.
+        self.proxy = int(proxy) if self.world == 1 else 0
+        self.proxy_stream = None
+        self.proxy_log: List[Tuple[int, float, float]] = []
+        if self.proxy:
+            if grad_codec != "none" or wire_dtype != "fp32":
+                raise ValueError("comm proxy: plain fp32 all-reduce only")
+            self.world = 2                       # every rank path below behaves as DP ...
+            reduce = "sum"                       # ... with the identity as the reduction
+            self.proxy_stream = torch.cuda.Stream(flat.grad_buf.device)
         self.reduce, self.codec, self.codec_scale = reduce, grad_codec, codec_scale
         self.overlap = overlap and not (grad_codec != "none" and codec_scale == "global")
         if reduce == "mean":
@@ -92,7 +109,7 @@ class GradBucketReducer:
         # directly (the HIP engine).  Never both: autograd still runs the AccumulateGrad
         # nodes of such parameters (with no gradient), which would count them twice and
         # launch a bucket before its last gradient is written.
-        if self.world > 1 and use_hooks:
+        if self.world > 1 and use_hooks and not self.proxy:
             for p in flat.order:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
         self.stats = {"buckets": len(self.buckets), "launched_in_backward": 0}
@@ -161,6 +178,9 @@ class GradBucketReducer:
     def _launch(self, b: _Bucket):
         b.launched = True
         g = self._seg(b)
+        if self.proxy:
+            self._launch_proxy(b, g)
+            return
         if self.codec == "none":
             # pre-scaled SUM on every backend (exact for power-of-two world sizes; no
             # dependence on the collective library's AVG support)
@@ -180,6 +200,39 @@ class GradBucketReducer:
         w1 = dist.all_gather(b.gathered[0], b.payload, group=self.group, async_op=True)
         w2 = dist.all_gather(b.gathered[1], b.scales, group=self.group, async_op=True)
         b.work = (w1, w2)
+
+    PROXY_BLOCKS = 16                    # RCCL-like channel count
+
+    def _launch_proxy(self, b: _Bucket, g: torch.Tensor):
+        cur = torch.cuda.current_stream(g.device)
+        if b.ev is None:
+            b.ev = tuple(torch.cuda.Event(enable_timing=True) for _ in range(3))
+        ready, start, end = b.ev
+        ready.record(cur)                    # gradients complete on the producing stream
+        st = self.proxy_stream
+        st.wait_stream(cur)                  # as RCCL's stream waits on the caller's
+        with torch.cuda.stream(st):
+            start.record(st)
+            from ..ops import _ext
+            # two sweeps: the reduce-scatter's and the all-gather's pass over the bucket
+            _ext.ops().comm_proxy(g, self.PROXY_BLOCKS, 2)
+            end.record(st)
+        b.work = ("proxy", end)
+
+    def proxy_times(self) -> List[Dict[str, float]]:
+        """Per bucket of the last synchronised step: ms from gradients-ready to the proxy
+        collective's start and end (synchronises on the events)."""
+        out = []
+        for b in self.buckets:
+            if b.ev is None:
+                continue
+            ready, start, end = b.ev
+            end.synchronize()
+            out.append({"bucket": b.idx, "mb": round((b.end - b.start) * 4 / 2**20, 2),
+                        "ready_to_start_ms": ready.elapsed_time(start),
+                        "ready_to_end_ms": ready.elapsed_time(end),
+                        "kernel_ms": start.elapsed_time(end)})
+        return out
 
     def _launch_bf16(self, b: _Bucket, g: torch.Tensor):
         """bf16 transport, first half: the all-to-all of bf16 chunks, left in flight (its
@@ -227,7 +280,9 @@ class GradBucketReducer:
         for b in self.buckets:
             if b.work is None:
                 continue
-            if isinstance(b.work, tuple) and b.work[0] == "bf16":
+            if isinstance(b.work, tuple) and b.work[0] == "proxy":
+                torch.cuda.current_stream(self.flat.grad_buf.device).wait_event(b.work[1])
+            elif isinstance(b.work, tuple) and b.work[0] == "bf16":
                 b.work[1].wait()
                 g = self._seg(b)
                 g.copy_(b.wire[3][:g.numel()])

@@ -80,8 +80,16 @@ class Trainer:
                                   use_hip=(self.impl == "hip"))
         if self.impl == "hip":
             self.optimizer.weight_pack = model._engine.pack_weights
+        # CU reservation for collectives: the persistent kernels otherwise hold every CU
+        # until they exit, and an RCCL kernel launched mid-backward queues behind them
+        if cfg.comm_proxy and (self.impl != "hip" or self.world > 1):
+            raise ValueError("comm_proxy: single-GPU HIP runs only (it stands in for RCCL)")
+        dp = self.world > 1 or cfg.comm_proxy > 0
+        self.reserve_cus = cfg.reserve_cus if cfg.reserve_cus >= 0 else (8 if dp else 0)
+        if self.impl == "hip":
+            self.grid_cus = int(_ext.ops().set_cu_reserve(self.reserve_cus))
         self.reducer = None
-        if self.world > 1:
+        if dp:
             self.reducer = self._make_reducer(cfg.bucket_mb)
         if self.impl == "hip":
             # kernels write gradients straight into the flat grad buffer and trigger the
@@ -110,8 +118,8 @@ class Trainer:
         self._inflight: List[torch.cuda.Event] = []
         self.step_count = 0
         self.micro_count = 0
-        self._graph = None               # hipGraph of the train step (cfg.hip_graph)
-        self._graph_warm = 0
+        self._graphs: Dict[str, "torch.cuda.CUDAGraph"] = {}   # hipGraphs (cfg.hip_graph)
+        self._graph_warm: Dict[str, int] = {}
         self._static = None
         self.epoch = 0
         self.epoch_step = 0              # optimizer steps done in the current epoch
@@ -135,7 +143,8 @@ class Trainer:
         return GradBucketReducer(self.flat, bucket_mb=bucket_mb, reduce=c.reduce,
                                  grad_codec=c.grad_codec, codec_scale=c.codec_scale,
                                  overlap=c.overlap_comm, use_hooks=(self.impl != "hip"),
-                                 wire_dtype=c.wire_dtype)
+                                 wire_dtype=c.wire_dtype,
+                                 proxy=c.comm_proxy if self.world == 1 else 0)
 
     def set_bucket_mb(self, bucket_mb: float) -> int:
         """Re-bucket the gradient reducer between steps (bucket-size sweeps, SURVEY.md §5.8);
@@ -216,45 +225,101 @@ class Trainer:
     # ------------------------------------------------------------------ hipGraph step
     def _graph_ok(self, n_micro: int) -> bool:
         return (self.cfg.hip_graph and self.impl == "hip" and self.device.type == "cuda"
-                and self.reducer is None and n_micro == 1 and not self.cfg.broadcast_buffers
-                and not self.cfg.check_consistency_every)
+                and not self.cfg.broadcast_buffers and not self.cfg.check_consistency_every
+                and (self.reducer is None or n_micro > 1))
 
-    def _graph_body(self):
-        x, y = self._static
+    def _static_in(self, x: torch.Tensor, y: torch.Tensor):
+        """Copy a micro-batch into the graphs' static input buffers (one pair shared by every
+        graph: replays are sequential on one stream).  A device-pipeline batch (padded
+        channel-last bf16, ``data.engine_input``) is copied in that layout, so the captured
+        forward reads it with no layout pass."""
+        from ..data.datasets import engine_input
+        xp = getattr(x, "_ddlpc_nhwc", None)
+        if self._static is None or self._static[1].shape != y.shape:
+            if xp is not None:
+                sp = torch.empty_like(xp)
+                self._static = (engine_input(sp, x.shape[1]), torch.empty_like(y), sp)
+            else:
+                self._static = (torch.empty_like(x), torch.empty_like(y), None)
+        sx, sy, sp = self._static
+        if sp is not None and xp is not None:
+            sp.copy_(xp)
+        else:
+            sx.copy_(x)
+        sy.copy_(y)
+
+    def _graph_body(self, kind: str):
+        x, y = self._static[0], self._static[1]
+        if self.reducer is not None:
+            self.reducer.prepare(sync=False)        # "acc": never a collective in a graph
         loss, correct = self.model.loss_and_correct(x, y)
         loss.backward()
         self.meter.add(loss, correct, y.numel())
-        self.optimizer.step()
-        self.optimizer.zero_grad()
+        if kind == "last":                          # single GPU: the optimizer step too
+            self.optimizer.step()
+            self.optimizer.zero_grad()
 
-    def _graph_step(self, x: torch.Tensor, y: torch.Tensor):
-        """Single-GPU step as ONE hipGraph replay (~250 kernel launches -> 1): the batch
-        is copied into static buffers, the first ``GRAPH_WARMUP`` steps run eagerly on a
-        side stream (allocator + lazy state warm-up), then forward + backward + Adam (with
-        device-side bias corrections) + weight re-pack are captured once and replayed."""
+    def _graph_run(self, kind: str):
+        """Run one captured micro-batch (``kind`` "acc": forward + backward accumulating into
+        the gradient buffer; "last": that + Adam (device-side bias corrections) + zero_grad +
+        weight re-pack).  The first ``GRAPH_WARMUP`` calls per kind run eagerly on a side
+        stream (allocator + lazy state warm-up); the next eager call is followed by the
+        capture (which executes nothing), later calls replay."""
+        g = self._graphs.get(kind)
+        if g is not None:
+            g.replay()
+            if kind == "last":
+                self.optimizer.note_replayed_step()
+            return
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            self._graph_body(kind)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        self._graph_warm[kind] = self._graph_warm.get(kind, 0) + 1
+        if self._graph_warm[kind] >= self.GRAPH_WARMUP:
+            self.model._engine.join()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._graph_body(kind)
+            if kind == "last":
+                self.optimizer.step_count -= 1       # the capture ran step() once in Python
+            self._graphs[kind] = g
+
+    def _graph_step(self, micro_batches: List[Tuple[torch.Tensor, torch.Tensor]]):
+        """One optimizer step with hipGraph-captured micro-batches (~220 kernel launches per
+        micro-batch -> one replay): the reference's regime — batch 1 per GPU, 50
+        accumulated micro-batches per exchange (ref.py:685-687,750-766) — is launch-bound.
+        Accumulation micro-batches replay the "acc" graph; the last one replays "last"
+        (single GPU) or, under data parallelism, runs eagerly so the bucketed collectives
+        launch from backward as usual, followed by the exchange and Adam."""
         self.model.train()
-        if self._static is None:
-            self._static = (torch.empty_like(x), torch.empty_like(y))
-        self._static[0].copy_(x)
-        self._static[1].copy_(y)
-        if self._graph is None:
-            side = torch.cuda.Stream(self.device)
-            side.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(side):
-                self._graph_body()
-            torch.cuda.current_stream(self.device).wait_stream(side)
-            self._graph_warm += 1
-            if self._graph_warm >= self.GRAPH_WARMUP:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    self._graph_body()
-                self.optimizer.step_count -= 1       # capture ran step() once in Python
-                self._graph = g
-                # the capture itself executed nothing: the step above was the real one
-        else:
-            self._graph.replay()
-            self.optimizer.note_replayed_step()
-        self.micro_count += 1
+        ph = self.phases
+        if ph is not None:
+            ph.mark("start")
+        n = len(micro_batches)
+        for i, (x, y) in enumerate(micro_batches):
+            last = i == n - 1
+            if last and self.reducer is not None:
+                self._micro(x, y, sync=True)
+                break
+            self._static_in(x, y)
+            self._graph_run("last" if last else "acc")
+            self.micro_count += 1
+        if self.reducer is not None:
+            if ph is not None:
+                ph.mark("fwd_bwd")
+            with trace_range("ddlpc.grad_sync"):
+                self.reducer.finish()
+            if ph is not None:
+                ph.mark("comm_wait")
+            with trace_range("ddlpc.optimizer"):
+                self.optimizer.step()
+                self.optimizer.zero_grad()
+            if ph is not None:
+                ph.mark("optimizer")
+        if ph is not None:
+            ph.end_step()
         self.step_count += 1
         self.profiler.step()
 
@@ -281,7 +346,7 @@ class Trainer:
 
     def _train_step(self, micro_batches: List[Tuple[torch.Tensor, torch.Tensor]]):
         if self._graph_ok(len(micro_batches)):
-            return self._graph_step(*micro_batches[0])
+            return self._graph_step(micro_batches)
         self.model.train()
         n = len(micro_batches)
         ph = self.phases

@@ -4,7 +4,7 @@
 #   scripts/gpu.sh OUT STEP [STEP ...]
 #
 # OUT is a directory under gpurun_out/.  Each STEP is "name:timeout:command ..." (the command
-# is split on spaces) or one of the shorthands below.  Every GPU step runs under its own
+# runs under `bash -c`, so it may quote: "t:300:pytest -k 'a or b'") or a shorthand below.  Every GPU step runs under its own
 # `timeout -k 10`, writes OUT/name.log, and the first failing step ends the script (no GPU
 # work after a fault, an abort or a time limit).
 #
@@ -49,8 +49,7 @@ for spec in "$@"; do
       head -60 "$OUT/prof_summary.txt" ;;
     *:*:*)
       name=${spec%%:*}; rest=${spec#*:}; t=${rest%%:*}; cmd=${rest#*:}
-      # shellcheck disable=SC2086
-      run_step "$name" "$t" $cmd ;;
+      run_step "$name" "$t" bash -c "$cmd" ;;
     *)
       echo "unknown step: $spec"; exit 2 ;;
   esac

@@ -85,3 +85,43 @@ def test_yaml_config(tmp_path):
     p.write_text("model:\n  depth: 4\n  out_classes: 2\ntile: 128\nbatch_per_gpu: 2\n")
     c = TrainConfig.load(str(p))
     assert c.model.depth == 4 and c.tile == 128 and c.batch_per_gpu == 2
+
+
+def test_config_precision_is_honest():
+    """The HIP kernels compute in bf16: asking them for fp32 (the reference's precision,
+    ref.py:702-704) is an error, not a silent bf16 run; fp32 runs on stock ops."""
+    import pytest
+    import torch
+    from ddlpc.config import TrainConfig
+    from ddlpc.train.trainer import resolve_impl
+    with pytest.raises(ValueError):
+        TrainConfig(impl="hip", dtype="fp32").validate()
+    TrainConfig(impl="torch", dtype="fp32").validate()
+    gpu = torch.device("cuda", 0)
+    assert resolve_impl("auto", gpu, "fp32") == "torch"
+    assert resolve_impl("auto", gpu, "bf16") == "hip"
+    assert resolve_impl("auto", torch.device("cpu"), "bf16") == "torch"
+
+
+def test_resume_missing_explicit_checkpoint_raises(tmp_path):
+    """An explicit resume path that does not exist fails loudly on rank 0 (it would otherwise
+    start from scratch and broadcast that state); resume='auto' tolerates an empty dir."""
+    import pytest
+    from ddlpc.config import ModelConfig, TrainConfig
+    from ddlpc.train.trainer import Trainer
+    kw = dict(model=ModelConfig(out_classes=3, depth=3, width_divisor=8), tile=32,
+              batch_per_gpu=1, num_samples=2, test_holdout=0, impl="torch")
+    with pytest.raises(FileNotFoundError):
+        Trainer(TrainConfig(resume=str(tmp_path / "nope.pt"), **kw), device="cpu")
+    Trainer(TrainConfig(resume="auto", ckpt_dir=str(tmp_path), **kw), device="cpu").close()
+
+
+def test_device_dataset_rejects_out_of_range_host_indices():
+    import pytest
+    import torch
+    from ddlpc.data.datasets import DeviceTileDataset, TileDataset
+    base = TileDataset(torch.zeros(3, 8, 8, 3, dtype=torch.uint8), torch.zeros(3, 8, 8, dtype=torch.uint8))
+    ds = DeviceTileDataset.__new__(DeviceTileDataset)
+    ds.base = base
+    with pytest.raises(IndexError):
+        DeviceTileDataset.get(ds, [0, 3])

@@ -10,7 +10,8 @@ from dist_utils import run
 pytestmark = pytest.mark.gpu
 
 
-def _dp_rank(rank, world, bucket_mb, side, overlap, codec="none", accum=1, wire="fp32"):
+def _dp_rank(rank, world, bucket_mb, side, overlap, codec="none", accum=1, wire="fp32",
+             scale="bucket", reduce="mean"):
     import os
     os.environ["LOCAL_RANK"] = "0"              # both ranks on the box's single GPU
     os.environ["DDLPC_WGRAD_STREAM"] = side
@@ -22,7 +23,7 @@ def _dp_rank(rank, world, bucket_mb, side, overlap, codec="none", accum=1, wire=
     cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=2,
                       num_samples=1, test_holdout=0, impl="hip", backend="gloo",
                       bucket_mb=bucket_mb, overlap_comm=overlap, grad_codec=codec,
-                      accum_steps=accum, wire_dtype=wire)
+                      accum_steps=accum, wire_dtype=wire, codec_scale=scale, reduce=reduce)
     tr = Trainer(cfg, device="cuda")
     red = tr.reducer
     mbs = [device_random_batch(2, 64, 6, tr.device, seed=10 + rank + 100 * j)
@@ -47,10 +48,18 @@ def _dp_rank(rank, world, bucket_mb, side, overlap, codec="none", accum=1, wire=
     tr.optimizer.zero_grad()
     gl = [torch.empty_like(g_local) for _ in range(world)]
     dist.all_gather(gl, g_local)
+    weights = C.reference_weights(world) if reduce == "reference" else [red.weight] * world
     if codec == "none":
-        want = sum(gl) / world
+        want = sum(w * g for w, g in zip(weights, gl))
         if wire == "bf16":       # bf16(g / W) on the wire, fp32 sum in rank order, bf16 result
             want = sum((g * (1.0 / world)).bfloat16().float() for g in gl).bfloat16().float()
+    elif scale == "global":      # reference parity: ONE absmax over the whole gradient
+        want = torch.zeros_like(g_local).cpu()
+        segs = [(0, want.numel())]
+        for w, g in zip(weights, gl):
+            q, sc = C.encode_segments(g.cpu(), segs, codec)
+            C.decode_segments_accumulate(want, q, sc, segs, codec, weight=w)
+        want = want.to(g_red.device)
     else:                        # the CPU codec oracle on every rank's local gradient
         want = torch.zeros_like(g_local).cpu()
         for b in red.buckets:
@@ -102,6 +111,25 @@ def test_dp_hip_codec_accum_wire(codec, accum, wire):
         assert o["replicas_equal"] and o["nonzero"] > 0.01, o
 
 
+@pytest.mark.parametrize("codec,scale,reduce", [("fp16_absmax", "global", "reference"),
+                                                ("int8_absmax", "global", "mean"),
+                                                ("none", "bucket", "reference"),
+                                                ("fp16_absmax", "tensor", "reference")])
+def test_dp_hip_reference_parity_modes(codec, scale, reduce):
+    """The reference's own exchange semantics on the HIP path: one global absmax scale over
+    the whole gradient (ref.py:328-340,451-463; ``_finish_global_codec`` through the HIP
+    codec kernels, exchanged after backward) and its skewed "crooked averaging" weights
+    (ref.py:269-315: a plain SUM at W=2).  Every rank must hold the CPU oracle's gradient and
+    identical replicas."""
+    res = run(_dp_rank, 2, (1.0, "1", True, codec, 1, "fp32", scale, reduce), timeout=200)
+    for r in (0, 1):
+        o = res[r]
+        # the global scale needs the whole gradient: nothing launches during backward
+        assert o["launched"] == (0 if scale == "global" and codec != "none" else o["buckets"]), o
+        assert o["max_err"] <= 1e-6 * max(o["scale"], 1.0), o
+        assert o["replicas_equal"] and o["nonzero"] > 0.0, o
+
+
 def _rccl_one_rank(rank, world):
     """The nccl (= RCCL) code path of the reducer on a 1-rank group: async bucket
     all-reduces launched from the weight-gradient side stream, waits, optimizer step."""
@@ -148,3 +176,33 @@ def test_rccl_reducer_path_one_rank():
     res = run(_rccl_one_rank, 1, (), timeout=150)
     o = res[0]
     assert o["launched"] == o["buckets"] > 1 and o["exact"], o
+
+
+def test_comm_proxy_collective_during_backward():
+    """Single-GPU stand-in for the RCCL exchange (Trainer comm_proxy): one streaming kernel
+    per gradient bucket on a third stream, launched from the reducer's readiness points
+    during backward.  It is the identity, so training is bit-identical to the same CU
+    reservation without it; every bucket's proxy must start and finish inside the step."""
+    from ddlpc.config import ModelConfig, TrainConfig
+    from ddlpc.data import device_random_batch
+    from ddlpc.train.trainer import Trainer
+    out = {}
+    for proxy in (0, 8):
+        cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=8,
+                          num_samples=1, test_holdout=0, impl="hip", comm_proxy=proxy,
+                          reserve_cus=8, bucket_mb=2.0)
+        tr = Trainer(cfg, device="cuda")
+        assert tr.grid_cus == torch.cuda.get_device_properties(0).multi_processor_count - 8
+        batches = [device_random_batch(8, 64, 6, tr.device, seed=s) for s in range(3)]
+        for b in batches:
+            tr.train_step([b])
+        torch.cuda.synchronize()
+        times = tr.reducer.proxy_times() if proxy else []
+        out[proxy] = (tr.flat.param_buf.clone(), times,
+                      tr.reducer.stats["launched_in_backward"] if proxy else 0)
+        tr.close()
+    assert torch.equal(out[0][0], out[8][0])
+    times, launched = out[8][1], out[8][2]
+    assert len(times) > 1 and launched == 3 * len(times), (times, launched)
+    for t in times:
+        assert 0.0 <= t["ready_to_start_ms"] <= t["ready_to_end_ms"] < 50.0, t

@@ -70,6 +70,36 @@ def test_conv3_fwd(ops, N, H, W, C1, C2, Cout):
     assert torch.allclose(s[1], (yf * yf).sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
 
 
+# shapes that fill the chip with 512-pixel (32 x 16) tiles: the BM-512 configuration (cfg 5,
+# bias and BN statistics accumulated in LDS), incl. a concat input, the BN prologue and the
+# split data-gradient output
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout,pro,co1", [
+    (32, 64, 64, 128, 0, 128, True, 0), (32, 64, 64, 256, 128, 128, False, 0),
+    (64, 32, 32, 256, 0, 256, True, 0), (64, 32, 32, 128, 0, 384, False, 256)])
+def test_conv3_fwd_bigtile(ops, N, H, W, C1, C2, Cout, pro, co1):
+    torch.manual_seed(5)
+    x1 = torch.randn(N, C1, H, W, device=DEV).bfloat16()
+    x2 = torch.randn(N, C2, H, W, device=DEV).bfloat16() if C2 else None
+    w = torch.randn(Cout, C1 + C2, 3, 3, device=DEV) * (1.0 / math.sqrt(9 * (C1 + C2)))
+    b = torch.randn(Cout, device=DEV) * 0.1 if not co1 else None
+    scale = torch.rand(C1, device=DEV) + 0.5 if pro else None
+    shift = torch.randn(C1, device=DEV) * 0.5 if pro else None
+    pk = pack_conv(ops, w)
+    y, y2, st = ops.conv3_fwd(nhwc(x1), nhwc(x2) if x2 is not None else None, pk.fwd, b, scale,
+                              shift, Cout, co1, True)
+    a1 = x1.float()
+    if pro:
+        a1 = torch.relu(a1 * scale[None, :, None, None] + shift[None, :, None, None]).bfloat16().float()
+    xin = torch.cat([a1, x2.float()], 1) if x2 is not None else a1
+    ref = F.conv2d(xin, w.bfloat16().float(), b, padding=1)
+    out = torch.cat([nchw(y), nchw(y2)], 1) if co1 else nchw(y)
+    assert rel_err(out, ref) < 1e-2
+    s = st.sum(0)
+    yf = out.float()
+    assert torch.allclose(s[0], yf.sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+    assert torch.allclose(s[1], (yf * yf).sum((0, 2, 3)), rtol=1e-3, atol=1.0)
+
+
 def test_conv3_fwd_prologue(ops):
     torch.manual_seed(1)
     N, H, W, C, Cout = 2, 32, 32, 64, 64
