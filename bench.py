@@ -70,6 +70,11 @@ def _parse():
                     help="1 GPU: stand-in collective per gradient bucket for a world of N "
                          "(streaming kernel on a third stream; measures launch-to-finish "
                          "latency during backward)")
+    ap.add_argument("--ab", default="",
+                    help="diagnostic: KNOB:v0,v1 — after the main timing, alternate a kernel "
+                         "knob (torch.ops.ddlpc.set_knob; CU_RESERVE = set_cu_reserve) over "
+                         "--ab-rounds timed blocks in this process; reported as config.ab")
+    ap.add_argument("--ab-rounds", type=int, default=4)
     ap.add_argument("--heartbeat", type=float, default=0.0,
                     help="seconds between 'alive' lines on stderr (long first-step autotuning)")
     return ap.parse_args()
@@ -240,6 +245,28 @@ def main():
             sweep[str(mb)] = {"buckets": nb,
                               "ms_per_step": round(timed(args.steps, first) / args.steps * 1e3, 3)}
         tr.set_bucket_mb(args.bucket_mb)
+    ab = None
+    if args.ab and tr.impl == "hip":
+        from ddlpc.ops import _ext
+        F = _ext.ops()
+        knob, vals = args.ab.split(":")
+        vals = [int(v) for v in vals.split(",")]
+
+        def setk(v):
+            if knob == "CU_RESERVE":
+                F.set_cu_reserve(v)
+            else:
+                F.set_knob(knob, v)
+        ab = {str(v): [] for v in vals}
+        for r in range(args.ab_rounds):
+            for v in vals:
+                setk(v)
+                first += args.steps + 2
+                step(first - 1)                        # one untimed step with the new setting
+                ab[str(v)].append(round(timed(args.steps, first) / args.steps * 1e3, 3))
+        setk(vals[0])
+        ab = {"knob": knob, "ms_per_step": ab,
+              "median_ms": {v: sorted(x)[len(x) // 2] for v, x in ab.items()}}
     proxy = None
     if tr.reducer is not None and tr.reducer.proxy:
         proxy = [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in d.items()}
@@ -308,6 +335,7 @@ def main():
                        "comm_wait_ms": (round(phases["comm_wait_ms"], 3)
                                         if "comm_wait_ms" in phases else None),
                        "bucket_sweep": sweep or None,
+                       "ab": ab,
                        "alloc_retries": mstats.get("num_alloc_retries"),
                        "side_lag_waits": (getattr(tr.model._engine, "lag_waits", None)
                                           if tr.impl == "hip" else None),

@@ -11,6 +11,9 @@
 #include <torch/library.h>
 
 #include <cstdlib>
+#include <mutex>
+#include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "ops.h"
@@ -70,6 +73,41 @@ int pick_bn(int Cout) {
   if (Cout <= 32) return 32;
   if (Cout <= 64) return 64;
   return 128;
+}
+
+}  // namespace
+
+// ---- tuning knobs: DDLPC_<NAME> environment defaults, overridable in-process
+namespace {
+std::mutex g_knob_mu;
+std::unordered_map<std::string, int>& knob_map() {
+  static std::unordered_map<std::string, int> m;
+  return m;
+}
+}  // namespace
+
+int knob(const char* name, int def) {
+  std::lock_guard<std::mutex> lk(g_knob_mu);
+  auto& m = knob_map();
+  auto it = m.find(name);
+  if (it != m.end()) return it->second;
+  const std::string env = std::string("DDLPC_") + name;
+  const char* e = getenv(env.c_str());
+  const int v = e ? atoi(e) : def;
+  m.emplace(name, v);                   // (cached: the environment is read once per name)
+  return v;
+}
+
+namespace {
+
+// in-process knob override -> the previous value (INT64_MIN: never read or set)
+int64_t set_knob(const std::string& name, int64_t value) {
+  std::lock_guard<std::mutex> lk(g_knob_mu);
+  auto& m = knob_map();
+  auto it = m.find(name);
+  const int64_t prev = it != m.end() ? it->second : INT64_MIN;
+  m[name] = (int)value;
+  return prev;
 }
 
 int phys_cus() {
@@ -171,7 +209,7 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   a.npix = (long long)g.N * g.D * g.H * g.W;
   {
     // high-resolution few-channel layers: resident-weight kernel (conv3x3_res.hip)
-    static const int use_res = [] { const char* e = getenv("DDLPC_CONV_RES"); return e ? atoi(e) : 1; }();
+    const int use_res = knob("CONV_RES", 1);
     int grid = 0, smem = 0;
     const int variant = use_res ? conv3_res_plan(a, num_cus(), grid, smem) : -1;
     if (variant >= 0) {
@@ -201,15 +239,17 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
     a.nTilesN = (a.Cout + conv3_fwd_cfg_bn(c) - 1) / conv3_fwd_cfg_bn(c);
   };
   plan(cfg);
-  static const int use_cfg4 = [] { const char* e = getenv("DDLPC_CONV_CFG4"); return e ? atoi(e) : 1; }();
+  const int use_cfg4 = knob("CONV_CFG4", 1);
   if (cfg == 2 && g.dims == 2 && use_cfg4) {    // 256-pixel tiles on 8 waves if they fill the chip
     plan(4);
     if (a.nTilesM * a.nTilesN >= num_cus()) cfg = 4;
     else plan(cfg);
   }
-  // 512-pixel tiles (cfg 5) where they fill the chip without padding (DDLPC_CONV_CFG5=0: off)
-  static const int use_cfg5 = [] { const char* e = getenv("DDLPC_CONV_CFG5"); return e ? atoi(e) : 1; }();
-  if (cfg == 4 && use_cfg5 && a.bnb_y == nullptr) {
+  // 512-pixel tiles (cfg 5) where they fill the chip without padding and K >= 9 x 256 (same-
+  // process A/B at batch 128, profiles/conv_ab_cfg5_r3d.txt: 3-6% faster on those layers,
+  // 2-4% slower with 128 input channels; DDLPC_CONV_CFG5=0: off, 2: every eligible layer)
+  const int use_cfg5 = knob("CONV_CFG5", 1);
+  if (cfg == 4 && use_cfg5 && a.bnb_y == nullptr && (a.Cin >= 256 || use_cfg5 == 2)) {
     plan(5);
     const double w5 = (double)a.nTilesM * 512 / ((double)g.N * g.D * g.H * g.W);
     if (a.nTilesM * a.nTilesN >= num_cus() && w5 <= 1.05) cfg = 5;
@@ -238,10 +278,8 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   at::Tensor stats;
   a.persist_blocks = (cfg >= 4 ? 1 : 2) * num_cus();   // cfg 4/5: one 8-wave workgroup per CU
   {
-    static const int pb = [] { const char* e = getenv("DDLPC_CONV_PERSIST"); return e ? atoi(e) : -1; }();
-    static const int ksx = [] { const char* e = getenv("DDLPC_CONV_KSPLIT"); return e ? atoi(e) : -1; }();
+    const int pb = knob("CONV_PERSIST", -1);
     if (pb >= 0) a.persist_blocks = pb * num_cus();
-    (void)ksx;
   }
   // small layers: split the input-channel chunks across workgroups so the grid fills the
   // chip; partial sums go through an fp32 buffer and a deterministic finalize
@@ -254,8 +292,8 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
       for (int ks = 2; ks <= 8; ++ks)
         if (nchunks_total % ks == 0 && nchunks_total / ks >= 2 && items * ks <= 2 * num_cus())
           best = ks;
-    const char* e = getenv("DDLPC_CONV_KSPLIT");
-    if (e && atoi(e) >= 1 && nchunks_total % atoi(e) == 0) best = atoi(e);
+    const int kx = knob("CONV_KSPLIT", -1);
+    if (kx >= 1 && nchunks_total % kx == 0) best = kx;
     a.ksplit = best;
   }
   at::Tensor part;
@@ -318,19 +356,19 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   if (a.pscale) TORCH_CHECK(a.C1 <= 512, "prologue supports C1 <= 512");
   if (a.pscale2) TORCH_CHECK(dual && a.pshift2 && a.C1 + a.C2 <= 512, "X2 prologue: x2, pscale2/pshift2, C1 + C2 <= 512");
   const int bco = a.Cout <= 32 ? 32 : 64;
-  static const int use_v2 = [] { const char* e = getenv("DDLPC_WGRAD_V2"); return e ? atoi(e) : 1; }();
+  const int use_v2 = knob("WGRAD_V2", 1);
   // (images narrower than the 16-pixel tile rows run with masked columns: DDLPC_WGRAD_MINW)
   // (8: the 8x8 bottleneck layers, 10% faster than the v1 kernel there)
-  static const int min_w = [] { const char* e = getenv("DDLPC_WGRAD_MINW"); return e ? atoi(e) : 8; }();
+  const int min_w = knob("WGRAD_MINW", 8);
   const bool v2 = use_v2 && (use_v2 != 2 || g.dims == 2) && g.W >= min_w && (a.C2 == 0 || a.C1 % 32 == 0);
   // v3 (32x32x16 MFMA, conflict-free transposed reads): whole 32-channel input chunks
-  static const int use_v3 = [] { const char* e = getenv("DDLPC_WGRAD_V3"); return e ? atoi(e) : 1; }();
+  const int use_v3 = knob("WGRAD_V3", 1);
   // (the large 64-channel concat layers stay on v2's 96-pixel tiles: 4-5% faster there)
   const bool v3 = v2 && use_v3 && a.C1 % 32 == 0 && a.C2 % 32 == 0 &&
                   !(bco == 64 && a.C2 > 0 && g.H * g.W >= 64 * 64);
   // 128-pixel tiles (v2: 16 x conv3_wgrad2_pt/16; v3: 256 for 32 output channels, else 128)
   // (DDLPC_WGRAD3_PT64 = 96 | 128: pixel tile of the 64-channel v3 kernel; default 128)
-  static const int v3_pt64 = [] { const char* e = getenv("DDLPC_WGRAD3_PT64"); return e ? atoi(e) : 128; }();
+  const int v3_pt64 = knob("WGRAD3_PT64", 128);
   if (dy_y.has_value() && dy_y->defined()) {
     // dy holds dA; BN backward applied on load (v2 kernel only)
     CHECK_CONTIG(*dy_y); CHECK_BF16(*dy_y);
@@ -345,7 +383,7 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
     a.dycoef = dy_coefs->data_ptr<float>();
   }
   // (DDLPC_WGRAD3_RING=1: 32-output-channel layers on 128-pixel tiles with a 3-deep DMA ring)
-  static const int v3_ring = [] { const char* e = getenv("DDLPC_WGRAD3_RING"); return e ? atoi(e) : 0; }();
+  const int v3_ring = knob("WGRAD3_RING", 0);
   if (v3) { a.TD = 1; a.TW = 16; a.TH = bco == 32 ? (v3_ring ? 8 : 16) : (v3_pt64 == 96 && a.C2 > 0 ? 6 : 8); }
   else if (v2) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad2_pt(bco, a.C2, g.H, g.W) / 16; }
   else if (g.dims == 2) { a.TD = 1; a.TW = g.W >= 16 ? 16 : 8; a.TH = 128 / a.TW; }
@@ -365,7 +403,7 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   // workgroups per CU to aim for (DDLPC_WGRAD_WG_PER_CU): the weight gradient runs
   // concurrently with the data-gradient chain, and its resident workgroups' LDS decides
   // what else fits on a CU
-  static const int wg_per_cu = [] { const char* e = getenv("DDLPC_WGRAD_WG_PER_CU"); return e ? std::max(1, atoi(e)) : 2; }();
+  const int wg_per_cu = std::max(1, knob("WGRAD_WG_PER_CU", 2));
   const int target = wg_per_cu * num_cus();
   int splits = std::max(1, (target + base - 1) / base);
   splits = std::min(splits, std::max(1, a.nTiles / 8));
@@ -661,7 +699,7 @@ std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
 bool convt_bwd_fused_ok(const at::Tensor& x, const at::Tensor& dout) {
   if (x.dim() != 4 || dout.dim() != 4 || x.size(3) != 64 || dout.size(3) != 64) return false;
   if (dout.size(1) != 2 * x.size(1) || dout.size(2) != 2 * x.size(2)) return false;
-  static const int on = [] { const char* e = getenv("DDLPC_CONVT_FUSED"); return e ? atoi(e) : 1; }();
+  const int on = knob("CONVT_FUSED", 1);
   if (!on) return false;
   const long long K = x.size(0) * x.size(1) * x.size(2);
   if (K * 4 >= (long long)INT32_MAX) return false;
@@ -741,7 +779,7 @@ std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
   a.bn4 = bn4_ptr(bn4, g.C);
   // v2 kernel (64 x 64 wave tiles, LDS-DMA stages): enough 128 x 128 workgroups for two per
   // CU, every split >= 4 stages of 64 pixels; DDLPC_CONVT_WG2=0 keeps the v1 kernel
-  static const int use_wg2 = [] { const char* e = getenv("DDLPC_CONVT_WG2"); return e ? atoi(e) : 1; }();
+  const int use_wg2 = knob("CONVT_WG2", 1);
   int splits;
   a.wg2 = use_wg2 && g.C % 8 == 0 && go.C % 8 == 0 && g.C <= 512;
   if (a.wg2) {
@@ -1190,6 +1228,7 @@ void comm_proxy(const at::Tensor& g, int64_t blocks, int64_t passes) {
 
 TORCH_LIBRARY(ddlpc, m) {
   m.def("set_cu_reserve(int k) -> int", &ddlpc::set_cu_reserve);
+  m.def("set_knob(str name, int value) -> int", &ddlpc::set_knob);
   m.def("comm_proxy(Tensor(a!) g, int blocks, int passes) -> ()");
   m.def("conv3_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, Tensor? pscale, Tensor? pshift, "
         "int cout, int co1, bool stats, Tensor? pscale2=None, Tensor? pshift2=None, Tensor? bnb_y=None, "

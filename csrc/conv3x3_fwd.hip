@@ -768,14 +768,14 @@ __global__ void conv_splitk_finalize_kernel(const float* __restrict__ part, int 
 // fragment double buffering (sched barrier per tap): on by default except the 3-D 4x4-tile
 // configs (VGPR spill); DDLPC_CONV_FDB=0 turns it off for A/B
 bool conv_fdb() {
-  static const int v = [] { const char* e = getenv("DDLPC_CONV_FDB"); return e ? atoi(e) : 1; }();
+  const int v = knob("CONV_FDB", 1);
   return v != 0;
 }
 
 // super-stages: next-stage DMAs interleaved with the MFMAs (DDLPC_CONV_ILV=1).  Measured at
 // batch 128 (conv_micro, same box): 1-2% slower per layer than one burst, so off
 bool conv_ilv() {
-  static const int v = [] { const char* e = getenv("DDLPC_CONV_ILV"); return e ? atoi(e) : 0; }();
+  const int v = knob("CONV_ILV", 0);
   return v != 0;
 }
 
@@ -789,7 +789,7 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
     grid = a.persist_blocks / q * q;
   }
   a.stat_rows = grid;
-  static const int diag = [] { const char* e = getenv("DDLPC_DIAG_CONV"); return e ? atoi(e) : 0; }();
+  const int diag = knob("DIAG_CONV", 0);
   a.diag = diag;
   constexpr bool FDB_OK = !(DIMS == 3 && MT * NT >= 16);
   if constexpr (NBB == 4) {
@@ -835,7 +835,7 @@ void launch_cfg5_nofdb(ConvFwdArgs& a, hipStream_t st) {
 
 // super-stages (two kernel rows per barrier) in the 8-wave configuration (DDLPC_CONV_SUPER=0: off)
 int conv_super() {
-  static const int v = [] { const char* e = getenv("DDLPC_CONV_SUPER"); return e ? atoi(e) : 1; }();
+  const int v = knob("CONV_SUPER", 1);
   return v;
 }
 
@@ -843,7 +843,7 @@ int conv_super() {
 // Measured at batch 128 (conv_micro, same box): the 3-deep ring is 2.8% slower over all
 // layers' forward + data gradient — the weight stream is not what limits this kernel.
 int conv_nbb() {
-  static const int v = [] { const char* e = getenv("DDLPC_CONV_NBB"); return e ? atoi(e) : 2; }();
+  const int v = knob("CONV_NBB", 2);
   return v == 3 ? 3 : 2;
 }
 
@@ -852,7 +852,7 @@ int cfg_wm(int cfg) { return cfg <= 1 || cfg >= 4 ? 4 : cfg == 2 ? 2 : 1; }
 // BM-512 configuration (cfg 5): fragment double buffering off by default (VGPR budget of two
 // waves per SIMD with a 128-register accumulator); DDLPC_CONV5_FDB=1 turns it on
 bool conv5_fdb() {
-  static const int v = [] { const char* e = getenv("DDLPC_CONV5_FDB"); return e ? atoi(e) : 0; }();
+  const int v = knob("CONV5_FDB", 0);
   return v != 0;
 }
 

@@ -553,7 +553,7 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
   const int bn = a.Cout == 96 ? 96 : (a.Cout <= 32 || a.Cout % 64 != 0) ? 32 : 64;
   // preference: 3-deep halo rings (latency hiding) first; DDLPC_RES_DEPTH=2 prefers the
   // 2-deep, two-workgroups-per-CU variants (A/B experiments)
-  static const int depth = [] { const char* e = getenv("DDLPC_RES_DEPTH"); return e ? atoi(e) : 3; }();
+  const int depth = knob("RES_DEPTH", 3);
   int cand[3];
   int nc = 0;
   if (tap8) {

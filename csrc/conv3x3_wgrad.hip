@@ -798,7 +798,7 @@ void launch_wg(ConvWgradArgs& a, hipStream_t st) {
 // 25% faster with 96-pixel tiles (three 46 KB workgroups per CU) and slower elsewhere
 // (conv_micro, batch 128).  DDLPC_WGRAD64_PT = 64 | 96 | 128 | 256 forces one size.
 int conv3_wgrad2_pt(int bco, int C2, int H, int W) {
-  static const int force = [] { const char* e = getenv("DDLPC_WGRAD64_PT"); return e ? atoi(e) : 0; }();
+  const int force = knob("WGRAD64_PT", 0);
   if (bco == 32) return 256;
   if (force == 64 || force == 96 || force == 128 || force == 256) return force;
   return (C2 > 0 && H * W >= 64 * 64) ? 96 : 128;

@@ -852,8 +852,8 @@ int convt_wgrad2_tiles(const GemmArgs& a) {
 }
 
 int gemm_nt_bn(const GemmArgs& a) {
-  static const int fwd_bn = [] { const char* e = getenv("DDLPC_CONVT_BN"); return e ? atoi(e) : 128; }();
-  static const int dgrad_bn = [] { const char* e = getenv("DDLPC_CONVT_DGRAD_BN"); return e ? atoi(e) : 128; }();
+  const int fwd_bn = knob("CONVT_BN", 128);
+  const int dgrad_bn = knob("CONVT_DGRAD_BN", 128);
   return (a.N % 128 == 0 && (a.mode == GEMM_CONVT_FWD ? fwd_bn : dgrad_bn) == 128) ? 128 : 64;
 }
 

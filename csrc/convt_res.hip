@@ -345,7 +345,7 @@ struct ResPlan {
 
 ResPlan plan_of(const GemmArgs& a) {
   ResPlan r;
-  static const int use = [] { const char* e = getenv("DDLPC_CONVT_RES"); return e ? atoi(e) : 1; }();
+  const int use = knob("CONVT_RES", 1);
   if (!use || a.mode == GEMM_CONVT_WGRAD || a.K % BK != 0 || a.Cout % 32 != 0) return r;
   const int S = a.dims == 2 ? 4 : 8;
   int tbn = 0;

@@ -542,7 +542,7 @@ int head_ce_bwd_blocks(int C, int K, bool /*defer*/, long long P, int num_cus) {
   HEAD_SWITCH(C, K, occ(reinterpret_cast<const void*>(&head_ce_bwd_kernel<CC, KK, true>)));
   HEAD_SWITCH(C, K, occ(reinterpret_cast<const void*>(&head_ce_bwd_kernel<CC, KK, false>)));
   // DDLPC_HEAD_BWD_PER_CU: workgroups per CU in the grid (A/B knob; default: resident ones)
-  static const int pc = [] { const char* e = getenv("DDLPC_HEAD_BWD_PER_CU"); return e ? atoi(e) : 0; }();
+  const int pc = knob("HEAD_BWD_PER_CU", 0);
   if (pc > 0) per_cu = pc;
   const long long ppb = 256 / (C / 8);
   return (int)std::max<long long>(1, std::min<long long>((P + ppb - 1) / ppb, (long long)per_cu * num_cus));
@@ -578,7 +578,7 @@ void head_ce_fwd_stats_launch(const bf16_t* a, const float* Wh, const float* bh,
 
 int head_bn_apply_blocks(long long P, int C) {
   const long long ppb = 256 / (C / 8);
-  static const int cap = [] { const char* e = getenv("DDLPC_HEAD_APPLY_BLOCKS"); return e ? atoi(e) : 4096; }();
+  const int cap = knob("HEAD_APPLY_BLOCKS", 4096);
   return (int)std::max<long long>(1, std::min<long long>((P + 2 * ppb - 1) / (2 * ppb), cap));
 }
 

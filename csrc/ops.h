@@ -256,6 +256,11 @@ void tile_gather_launch(const uint8_t* src, const uint8_t* lab, const int64_t* i
                         long long S, int in_ch, int cpad, long long N, bf16_t* x, int64_t* y,
                         hipStream_t st);
 
+// ---------------------------------------------------------------- tuning knobs (bindings.cpp)
+// knob("CONV_CFG5", 1): an in-process override (torch.ops.ddlpc.set_knob, for interleaved
+// same-process A/B runs) or else the environment variable DDLPC_CONV_CFG5, or else the default
+int knob(const char* name, int def);
+
 // ---------------------------------------------------------------- comm proxy (reduce.hip)
 void comm_proxy_launch(float* g, long long n, int blocks, int passes, hipStream_t st);
 

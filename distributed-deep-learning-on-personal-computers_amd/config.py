@@ -89,7 +89,9 @@ class TrainConfig:
     check_consistency_every: int = 0     # debug: all-reduce a param checksum every K steps
     reserve_cus: int = -1                # CUs kept out of persistent kernel grids so a
                                          # collective launched mid-backward starts at once
-                                         # (-1 = auto: 8 with data parallelism, else 0)
+                                         # (-1 = auto = 0: measured, a bucket collective
+                                         # starts within 20 us without it, and 8 reserved
+                                         # CUs cost 5% of the step; docs/PERF.md)
     comm_proxy: int = 0                  # single GPU: stand-in collective for a world of N
                                          # (streaming kernel on a third stream, identity)
     timeout_s: int = 1800

@@ -80,12 +80,15 @@ class Trainer:
                                   use_hip=(self.impl == "hip"))
         if self.impl == "hip":
             self.optimizer.weight_pack = model._engine.pack_weights
-        # CU reservation for collectives: the persistent kernels otherwise hold every CU
-        # until they exit, and an RCCL kernel launched mid-backward queues behind them
+        # optional CU reservation for collectives (persistent grids sized to num_cus - k).
+        # Default 0: the comm proxy measured a bucket collective launched mid-backward
+        # starting within ~20 us without any reservation (the side stream's weight-gradient
+        # workgroups keep releasing slots), while 8 reserved CUs cost 5% of the step
+        # (persistent grids lose their even split of tiles over 256 CUs)
         if cfg.comm_proxy and (self.impl != "hip" or self.world > 1):
             raise ValueError("comm_proxy: single-GPU HIP runs only (it stands in for RCCL)")
         dp = self.world > 1 or cfg.comm_proxy > 0
-        self.reserve_cus = cfg.reserve_cus if cfg.reserve_cus >= 0 else (8 if dp else 0)
+        self.reserve_cus = max(0, cfg.reserve_cus)
         if self.impl == "hip":
             self.grid_cus = int(_ext.ops().set_cu_reserve(self.reserve_cus))
         self.reducer = None

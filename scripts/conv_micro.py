@@ -27,6 +27,17 @@ LAYERS = [  # name, H, C1, C2, Cout, prologue
 ]
 
 
+def _time(fn, iters):
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
@@ -35,6 +46,10 @@ def main():
     ap.add_argument("--passes", default="fwd,dgrad,wgrad")
     ap.add_argument("--dims", type=int, default=2)
     ap.add_argument("--tile", type=int, default=256, help="top-level image size (layer sizes scale)")
+    ap.add_argument("--ab", default="",
+                    help="KNOB:v0,v1[,..] — interleaved same-process A/B of a kernel knob "
+                         "(torch.ops.ddlpc.set_knob), e.g. CONV_CFG5:0,1; medians over --rounds")
+    ap.add_argument("--rounds", type=int, default=5)
     a = ap.parse_args()
     from ddlpc.ops import _ext
     from ddlpc.ops.fused_unet import _ConvPack
@@ -77,15 +92,27 @@ def main():
             if ps == "dgradbn" and (C2 or a.dims != 2):
                 continue
             fn = fns[ps]
+            if a.ab:
+                knob, vals = a.ab.split(":")
+                vals = [int(v) for v in vals.split(",")]
+                samples = {v: [] for v in vals}
+                for v in vals:                       # warm every variant once
+                    F.set_knob(knob, v)
+                    fn()
+                for _ in range(a.rounds):
+                    for v in vals:
+                        F.set_knob(knob, v)
+                        samples[v].append(_time(fn, a.iters))
+                med = {v: sorted(x)[len(x) // 2] for v, x in samples.items()}
+                for v in vals:
+                    tot[f"{ps}@{v}"] = tot.get(f"{ps}@{v}", 0.0) + med[v]
+                print(f"{name:8s} {ps:6s} " + "  ".join(
+                    f"{knob}={v}: {med[v]:8.1f} us {flops / med[v] / 1e6:7.1f} TF/s" for v in vals)
+                    + f"  ({med[vals[1]] / med[vals[0]]:.3f}x)", flush=True)
+                continue
             fn()
             torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(a.iters):
-                fn()
-            e1.record()
-            e1.synchronize()
-            us = e0.elapsed_time(e1) * 1e3 / a.iters
+            us = _time(fn, a.iters)
             tot[ps] += us
             if ps == "dgradbn":
                 tot["dgrad_b_layers"] = tot.get("dgrad_b_layers", 0.0) + fns_ref_us.get(name, 0.0)
