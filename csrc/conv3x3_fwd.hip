@@ -287,7 +287,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   // stores per epilogue: single bf16 output -> 16-byte stores of channel-tile pairs (pair16);
   // split output / split-K fp32 partials -> one store per tile
   static_assert(NT % 2 == 0, "channel tiles come in pairs");
-  const bool pairs = KS == 1 && p.Y2 == nullptr;
+  // (a split output takes pairs too when it splits at a 32-channel boundary: each pair lies
+  // wholly in one output)
+  const bool pairs = KS == 1 && (p.Y2 == nullptr || p.Co1 % 32 == 0);
   const int EPI_STORES = pairs ? MT * NT / 2 : MT * NT;
   // BNB: y at an item's output pixels, loaded into VGPRs at the item's last stage (after that
   // stage's DMA) and consumed by its epilogue after the next stage's full wait
@@ -411,9 +413,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       for (int np = 0; np < NT / 2; ++np) {
         const uint4 q = pair16(pkv[mt][2 * np], pkv[mt][2 * np + 1]);
         const int co = it.co0 + wn * (NT * 16) + np * 32 + pair16_ch(lane);
-        unsigned off = valid && co < p.Cout ? (unsigned)(lpix * p.Cout + co) * 2u : kOOB;
+        const bool in1 = p.Y2 == nullptr || it.co0 + wn * (NT * 16) + np * 32 < p.Co1;   // wave-uniform
+        unsigned off = valid && co < p.Cout ? (unsigned)(in1 ? lpix * p.Co1 + co : lpix * Co2 + co - p.Co1) * 2u
+                                            : kOOB;
         asm volatile("" : "+v"(off));
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, r1, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, in1 ? r1 : r2, off, 0, 0);
       }
     }
   };
@@ -439,10 +443,12 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       if (t + 1 < 3) load_frags(t + 1, xf[(t + 1) & 1], wf[(t + 1) & 1]);
+      if (p.prio & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[t & 1][nt], xf[t & 1][mt], acc[mt][nt]);
+      if (p.prio & 2) __builtin_amdgcn_s_setprio(0);
       if (FRAG_DB) __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -469,10 +475,12 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 #pragma unroll
     for (int tt = 0; tt < 6; ++tt) {
       if (tt + 1 < 6) load_frags(tt + 1, xf[(tt + 1) & 1], wf[(tt + 1) & 1]);
+      if (p.prio & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[tt & 1][nt], xf[tt & 1][mt], acc[mt][nt]);
+      if (p.prio & 2) __builtin_amdgcn_s_setprio(0);
       hook(tt);                                   // ILV: this tap's share of the next DMAs
       if (FRAG_DB) __builtin_amdgcn_sched_barrier(0);
     }
@@ -489,6 +497,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     chunk1 = r1 / NG;
     grp1 = r1 % NG;
   };
+  // wave priorities (MI355X_MICROARCH.md, two waves per SIMD: the second-dispatched half of an
+  // 8-wave workgroup loses VALU / issue arbitration; one s_setprio 1 for it, no flips)
+  if ((p.prio & 1) && C::NW == 8 && __builtin_amdgcn_readfirstlane(tid) >= C::NTH / 2)
+    __builtin_amdgcn_s_setprio(1);
   if constexpr (NBB <= 3) {
     int ops = 0, snap0 = 0, snap1 = 0;           // NBB = 3: ops issued so far; after B(s), B(s+1)
     if (S > 0) {
@@ -791,6 +803,7 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   a.stat_rows = grid;
   const int diag = knob("DIAG_CONV", 0);
   a.diag = diag;
+  a.prio = knob("CONV_PRIO", 2);
   constexpr bool FDB_OK = !(DIMS == 3 && MT * NT >= 16);
   if constexpr (NBB == 4) {
     if (conv_ilv()) {
@@ -829,6 +842,7 @@ void launch_cfg5_nofdb(ConvFwdArgs& a, hipStream_t st) {
   }
   a.stat_rows = grid;
   a.diag = 0;
+  a.prio = knob("CONV_PRIO", 2);
   hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 640, 2, false, false, false>), dim3(grid),
                      dim3(C::NTH), C::SMEM, st, a);
 }

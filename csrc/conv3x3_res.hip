@@ -53,7 +53,10 @@ DDLPC_HOST_DEVICE int res_w_bytes(int Cin, int BN, bool tap8) {
   return tap8 ? 3 * BN * ROWB : ((Cin + BK - 1) / BK) * 9 * BN * ROWB;
 }
 
-template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF, bool SPLIT, bool BNB>
+// SPLIT: 0 = one output; 1 = two outputs (concat data gradient), 8-byte stores; 2 = two
+// outputs split at a 32-channel boundary (Co1 % 32 == 0, launcher-checked): 16-byte pair
+// stores, each pair wholly in one output (a quarter of mode 1's store instructions)
+template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF, int SPLIT, bool BNB>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_kernel(ConvFwdArgs p) {
   using C = RCfg<WM, WN, MT, NT, HALO, TAP8, NBUF>;
   static_assert(NBUF == 2 || NBUF == 3, "halo ring depth");
@@ -275,8 +278,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   // PAIRS: 16-byte stores of channel-tile pairs (pair16).  Measured per layer at batch 128
   // (profiles/conv_micro_b128_pair16_r2.txt): 5-10% faster on the BN 64 and image-layer
   // variants, 4-6% slower on the 32-channel 3x3 layers (BN 32) -> 8-byte stores there
-  constexpr bool PAIRS = !SPLIT && (TAP8 || BN >= 64) && NT % 2 == 0;
-  constexpr int EPI_STORES = SPLIT ? MT * NT * 2 : PAIRS ? MT * NT / 2 : MT * NT;
+  constexpr bool PAIRS = (!SPLIT && (TAP8 || BN >= 64) && NT % 2 == 0) || SPLIT == 2;
+  static_assert(SPLIT != 2 || (NT % 2 == 0 && BN % 32 == 0), "split pairs: 32-channel pairs");
+  constexpr int EPI_STORES = SPLIT == 1 ? MT * NT * 2 : PAIRS ? MT * NT / 2 : MT * NT;
   // BNB: y at this item's output pixels, loaded into VGPRs at the item's last stage (before
   // that stage's halo DMA) and consumed by its epilogue one stage later
   constexpr int YL = BNB ? MT * NT : 0;
@@ -367,9 +371,18 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
         for (int np = 0; np < NT / 2; ++np) {
           const uint4 q = pair16(pkv[mt][2 * np], pkv[mt][2 * np + 1]);
           const int co = co0 + wn * (NT * 16) + np * 32 + pair16_ch(lane);
-          unsigned o1 = valid && co < p.Cout ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
-          asm volatile("" : "+v"(o1));
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, r1, o1, 0, 0);
+          if constexpr (SPLIT == 2) {
+            // the pair's 32 channels lie in one output (wave-uniform choice)
+            const bool in1 = co0 + wn * (NT * 16) + np * 32 < p.Co1;
+            unsigned o = valid && co < p.Cout ? (unsigned)(in1 ? lp * p.Co1 + co : lp * Co2 + co - p.Co1) * 2u
+                                              : kOOB;
+            asm volatile("" : "+v"(o));
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, in1 ? r1 : r2, o, 0, 0);
+          } else {
+            unsigned o1 = valid && co < p.Cout ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
+            asm volatile("" : "+v"(o1));
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, r1, o1, 0, 0);
+          }
         }
       }
     }
@@ -391,6 +404,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     next_of(kp, cp, k1, c1);
     kp = k1; cp = c1;
   }
+  // wave priorities (DDLPC_CONV_PRIO, ConvFwdArgs::prio): bit 0 = s_setprio 1 once for the
+  // second-dispatched half of an 8-wave workgroup, bit 1 = around every MFMA cluster
+  if ((p.prio & 1) && NW == 8 && __builtin_amdgcn_readfirstlane(tid) >= C::NTH / 2)
+    __builtin_amdgcn_s_setprio(1);
   int k = 0, c = 0;
   bool epi_prev = false;                              // stage s-1 ran an epilogue
   for (int s = 0; s < S; ++s) {
@@ -453,11 +470,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
 #pragma unroll
     for (int j = 0; j < KSTEPS; ++j) {
       if (j + 1 < KSTEPS) load_frags(j + 1, xf[(j + 1) & 1], wf[(j + 1) & 1]);
+      if (p.prio & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = mfma16x16x32(wf[j & 1][nt], xf[j & 1][mt], acc[mt][nt]);
+      if (p.prio & 2) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     }
     };
@@ -525,18 +544,28 @@ int res_smem(const ResVariant& v, int Cin, int C1, bool pro, bool bnb) {   // C1
 
 template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF>
 void launch_res(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
-  if (a.Co1 < a.Cout)
-    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, true, false>), dim3(grid),
+  a.prio = knob("CONV_PRIO", 2);
+  constexpr int BNc = WN * NT * 16;
+  if (a.Co1 < a.Cout) {
+    // split output at a 32-channel boundary: 16-byte pair stores (DDLPC_RES_SPLIT_PAIRS=0: off)
+    if constexpr (NT % 2 == 0 && BNc % 32 == 0 && !TAP8) {
+      if (a.Co1 % 32 == 0 && knob("RES_SPLIT_PAIRS", 1)) {
+        hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 2, false>), dim3(grid),
+                           dim3(WM * WN * 64), smem, st, a);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 1, false>), dim3(grid),
                        dim3(WM * WN * 64), smem, st, a);
-  else if constexpr (!TAP8 && WN * NT * 16 != 96) {
+  } else if constexpr (!TAP8 && BNc != 96) {
     if (a.bnb_y != nullptr)
-      hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, false, true>), dim3(grid),
+      hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 0, true>), dim3(grid),
                          dim3(WM * WN * 64), smem, st, a);
     else
-      hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, false, false>), dim3(grid),
+      hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 0, false>), dim3(grid),
                          dim3(WM * WN * 64), smem, st, a);
   } else {
-    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, false, false>), dim3(grid),
+    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 0, false>), dim3(grid),
                        dim3(WM * WN * 64), smem, st, a);
   }
 }

@@ -38,6 +38,9 @@ struct ConvFwdArgs {
   float* part;                    // [ksplit][npix][Cout] fp32 (ksplit > 1)
   long long npix;                 // N * D * H * W
   int diag;                       // diagnostics only (DDLPC_DIAG_CONV): bit 0 skip weight DMA after stage 1, bit 1 skip halo DMA after chunk 1
+  int prio;                       // wave priorities (DDLPC_CONV_PRIO): bit 0 = s_setprio 1 for the
+                                  // second half of an 8-wave workgroup (static form), bit 1 =
+                                  // s_setprio 1 / 0 around every tap's MFMA cluster
   // BN-backward epilogue (data gradient dA of a conv whose input went through BN + ReLU):
   // `stats` rows then hold (sum dyh, sum dyh * xhat) with dyh = [y*scale + shift > 0] * dA,
   // xhat = (y - mean) * invstd — the reduction pass of that BN's backward, fused.  2-D,
