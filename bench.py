@@ -64,6 +64,8 @@ def _parse():
     ap.add_argument("--fixed-batch", type=int, default=0,
                     help="diagnostic: 1 = reuse one rendered batch every step (no per-step "
                          "input pipeline; reported in 'data')")
+    ap.add_argument("--micro-streams", type=int, default=1,
+                    help="accumulation micro-batches in flight on this many HIP streams")
     ap.add_argument("--reserve-cus", type=int, default=-1,
                     help="CUs kept out of persistent kernel grids (-1: 8 under DP, else 0)")
     ap.add_argument("--comm-proxy", type=int, default=0,
@@ -161,7 +163,7 @@ def main():
                       bucket_mb=args.bucket_mb, wire_dtype=args.wire_dtype,
                       grad_codec=args.codec, log_dir=None, hip_graph=bool(args.hip_graph),
                       recompute=int(args.recompute), reserve_cus=args.reserve_cus,
-                      comm_proxy=args.comm_proxy)
+                      comm_proxy=args.comm_proxy, micro_streams=args.micro_streams)
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     tr = Trainer(cfg, device=dev)
     world, rank = tr.world, tr.rank
@@ -318,6 +320,7 @@ def main():
                        "optimizer": "Adam(lr=1e-3)", "loss": "CrossEntropy",
                        "train_loss_mean": round(loss["loss"], 4),
                        "recompute": int(args.recompute),
+                       "micro_streams": args.micro_streams,
                        "peak_mem_gb": (round(torch.cuda.max_memory_allocated(device) / 2**30, 2)
                                        if dev == "cuda" else None),
                        "schedule": ("overlap" if sched.get("side_stream") else "serial") if sched

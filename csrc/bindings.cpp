@@ -459,6 +459,20 @@ at::Tensor bn_finalize(const at::Tensor& partial, double count, const at::Tensor
   return st;
 }
 
+// deferred BatchNorm running-statistics updates, in micro-batch order (see reduce.hip)
+void bn_running_apply(at::Tensor running_mean, at::Tensor running_var, const at::Tensor& slots,
+                      double momentum, const c10::optional<at::Tensor>& nbt) {
+  CHECK_F32(running_mean); CHECK_F32(running_var); CHECK_F32(slots); CHECK_CONTIG(slots);
+  const int C = (int)running_mean.numel();
+  TORCH_CHECK(running_var.numel() == C && slots.numel() % (2 * C) == 0, "slots [K][2][C]");
+  c10::DeviceGuard guard(slots.device());
+  const int K = (int)(slots.numel() / (2 * C));
+  if (K == 0) return;
+  int64_t* nbp = (nbt.has_value() && nbt->defined()) ? nbt->data_ptr<int64_t>() : nullptr;
+  bn_running_apply_launch(running_mean.data_ptr<float>(), running_var.data_ptr<float>(),
+                          slots.data_ptr<float>(), K, C, (float)momentum, nbp, cur_stream());
+}
+
 std::vector<at::Tensor> bn_relu_apply(const at::Tensor& y, const at::Tensor& stats4, bool pool,
                                       bool full) {
   CHECK_DEV(y); CHECK_CONTIG(y); CHECK_BF16(y);
@@ -1239,6 +1253,8 @@ TORCH_LIBRARY(ddlpc, m) {
   m.def("bn_finalize(Tensor partial, float count, Tensor gamma, Tensor beta, Tensor(a!) running_mean, "
         "Tensor(b!) running_var, float momentum, float eps, bool update_running, Tensor(c!)? nbt) -> Tensor");
   m.def("bn_relu_apply(Tensor y, Tensor stats4, bool pool, bool full=True) -> Tensor[]");
+  m.def("bn_running_apply(Tensor(a!) running_mean, Tensor(b!) running_var, Tensor slots, float momentum, "
+        "Tensor(c!)? nbt=None) -> ()");
   m.def("bn_grad_coefs(Tensor partial, Tensor y, Tensor stats4, Tensor gamma, "
         "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None) -> Tensor[]");
   m.def("bn_backward(Tensor? dA, Tensor? dP, Tensor y, Tensor stats4, Tensor gamma, Tensor? gscale, "
@@ -1284,6 +1300,7 @@ TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
   m.impl("conv3_wgrad", &ddlpc::conv3_wgrad);
   m.impl("bn_finalize", &ddlpc::bn_finalize);
   m.impl("bn_relu_apply", &ddlpc::bn_relu_apply);
+  m.impl("bn_running_apply", &ddlpc::bn_running_apply);
   m.impl("bn_grad_coefs", &ddlpc::bn_grad_coefs);
   m.impl("bn_backward", &ddlpc::bn_backward);
   m.impl("convt_fwd", &ddlpc::convt_fwd);

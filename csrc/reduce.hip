@@ -30,6 +30,13 @@ __global__ void rows_chunk_sum_kernel(const T* __restrict__ in, int R, long long
   out[(long long)blockIdx.y * N + j] = s;
 }
 
+// running <- (1 - m) running + m x, in one fixed fp32 form: the deferred (per-micro-batch
+// slot) updates of bn_running_apply_kernel reproduce the in-kernel ones bit for bit; with
+// m = 1 a slot receives x exactly
+DDLPC_DEVICE float bn_momentum_update(float running, float x, float m) {
+  return fmaf(m, x, (1.f - m) * running);
+}
+
 // mean / invstd / scale / shift + running statistics from fp64 (sum, sum^2)
 __global__ void bn_stats_finalize_kernel(const double* __restrict__ sums, int C, double count,
                                          const float* __restrict__ gamma,
@@ -51,8 +58,8 @@ __global__ void bn_stats_finalize_kernel(const double* __restrict__ sums, int C,
   out4[3 * C + c] = beta[c] - (float)mean * sc;
   if (update_running) {
     const double unb = count > 1 ? var * count / (count - 1) : var;
-    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+    running_mean[c] = bn_momentum_update(running_mean[c], (float)mean, momentum);
+    running_var[c] = bn_momentum_update(running_var[c], (float)unb, momentum);
   }
 }
 
@@ -106,6 +113,24 @@ __global__ void scatter_sums_dscale_kernel(const double* __restrict__ sums, long
     const float v = (float)(sums[j] * ds);
     dst[j] = accumulate ? dst[j] + v : v;
   }
+}
+
+// deferred running-statistics updates (concurrent micro-batch streams): slots [K][2][C] of
+// (batch mean, unbiased batch var) written by K forwards with momentum 1, applied here in
+// micro-batch order — the sequence of updates the K forwards would have made one by one
+__global__ void bn_running_apply_kernel(float* __restrict__ running_mean, float* __restrict__ running_var,
+                                        const float* __restrict__ slots, int K, int C, float momentum,
+                                        int64_t* nbt) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt != nullptr) nbt[0] += K;
+  if (c >= C) return;
+  float rm = running_mean[c], rv = running_var[c];
+  for (int k = 0; k < K; ++k) {
+    rm = bn_momentum_update(rm, slots[(2 * k) * C + c], momentum);
+    rv = bn_momentum_update(rv, slots[(2 * k + 1) * C + c], momentum);
+  }
+  running_mean[c] = rm;
+  running_var[c] = rv;
 }
 
 // head gradient scale dL/count from the loss kernel's (loss, correct, count) and the incoming
@@ -163,8 +188,8 @@ __global__ void bn_stats_rows_kernel(const float* __restrict__ partial, int P, i
   out4[3 * C + c] = beta[c] - (float)mean * sc;
   if (update_running) {
     const double unb = count > 1 ? var * count / (count - 1) : var;
-    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+    running_mean[c] = bn_momentum_update(running_mean[c], (float)mean, momentum);
+    running_var[c] = bn_momentum_update(running_var[c], (float)unb, momentum);
   }
 }
 
@@ -295,6 +320,12 @@ void scatter_sums_dscale_launch(const double* sums, long long N, float* dst, con
   const int grid = (int)std::max<long long>(1, std::min<long long>((N + 255) / 256, 4096));
   hipLaunchKernelGGL(scatter_sums_dscale_kernel, dim3(grid), dim3(256), 0, st, sums, N, dst, dscale,
                      accumulate ? 1 : 0);
+}
+
+void bn_running_apply_launch(float* rm, float* rv, const float* slots, int K, int C, float momentum,
+                             int64_t* nbt, hipStream_t st) {
+  hipLaunchKernelGGL(bn_running_apply_kernel, dim3((C + 255) / 256), dim3(256), 0, st, rm, rv, slots, K,
+                     C, momentum, nbt);
 }
 
 void head_grad_scale_launch(const float* out3, const float* gs, float* scale, hipStream_t st) {

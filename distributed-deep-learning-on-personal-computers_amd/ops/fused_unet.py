@@ -93,13 +93,24 @@ class _ConvPack:
 
 
 class _BNState:
-    def __init__(self, bn: nn.Module):
+    def __init__(self, bn: nn.Module, engine=None):
         self.bn = bn
+        self.engine = engine
+        self.index = -1                  # position in engine.bns (deferred running stats)
 
     def finalize(self, stats_partial: torch.Tensor, count: float) -> torch.Tensor:
         bn = self.bn
         if bn.training:
             mom = bn.momentum if bn.momentum is not None else 0.1
+            eng = self.engine
+            j = eng.bn_defer_j if eng is not None else None
+            if j is not None and bn.track_running_stats:
+                # concurrent micro-batch streams: this forward's (mean, unbiased var) go to
+                # its own slot (momentum 1 writes them exactly); the momentum updates are
+                # applied later in micro-batch order (UNetEngine.bn_defer_apply)
+                slot = eng.bn_defer_slot(self.index, j)
+                return _ops().bn_finalize(stats_partial, float(count), bn.weight, bn.bias,
+                                          slot[0], slot[1], 1.0, float(bn.eps), True, None)
             return _ops().bn_finalize(stats_partial, float(count), bn.weight, bn.bias,
                                       bn.running_mean, bn.running_var, float(mom), float(bn.eps),
                                       bool(bn.track_running_stats), bn.num_batches_tracked)
@@ -441,7 +452,7 @@ class _Block:
         self.first = first
         seq = dc.double_conv
         self.conv1, self.conv2 = seq[0], seq[3]
-        self.bn1, self.bn2 = _BNState(seq[1]), _BNState(seq[4])
+        self.bn1, self.bn2 = _BNState(seq[1], engine), _BNState(seq[4], engine)
         self.pack1 = _ConvPack(self.conv1, 0, need_dgrad=not first)
         self.pack2 = _ConvPack(self.conv2, 0, need_dgrad=True)
 
@@ -565,6 +576,14 @@ class UNetEngine:
                                               up_is_convt=pack is not None)))
         head = model.conv_last
         self.head = head
+        # deferred BatchNorm running statistics (concurrent micro-batch streams, Trainer
+        # micro_streams): bn_defer_j = index of the micro-batch whose forward is being queued
+        self.bns = [b for blk in self.enc + [self.mid] + [d[2] for d in self.dec]
+                    for b in (blk.bn1, blk.bn2)]
+        for i, b in enumerate(self.bns):
+            b.index = i
+        self.bn_defer_j: Optional[int] = None
+        self._bn_slots: List[torch.Tensor] = []
         self.packs = [p for b in self.enc + [self.mid] for p in (b.pack1, b.pack2)]
         for _, pk, b in self.dec:
             self.packs += [pk, b.pack1, b.pack2] if pk is not None else [b.pack1, b.pack2]
@@ -572,6 +591,28 @@ class UNetEngine:
         self._entries_key = None
         self._version = None
         self.pack_weights()
+
+    # ------------------------------------------------------------------ deferred BN stats
+    def bn_defer_prepare(self, n: int):
+        """Slots [n][2][C] per BatchNorm for n concurrently queued forwards (zeroed once,
+        reused: a slot only ever holds finite (mean, var) values)."""
+        if not self._bn_slots or self._bn_slots[0].shape[0] < n:
+            self._bn_slots = [torch.zeros(n, 2, b.bn.num_features, dtype=torch.float32,
+                                          device=b.bn.running_mean.device) for b in self.bns]
+
+    def bn_defer_slot(self, index: int, j: int) -> torch.Tensor:
+        return self._bn_slots[index][j]
+
+    def bn_defer_apply(self, n: int):
+        """Apply the n deferred running-statistics updates of every BatchNorm in micro-batch
+        order (one launch per BatchNorm): bit-identical to n sequential forwards."""
+        for b, slots in zip(self.bns, self._bn_slots):
+            bn = b.bn
+            if not bn.track_running_stats:
+                continue
+            mom = bn.momentum if bn.momentum is not None else 0.1
+            _ops().bn_running_apply(bn.running_mean, bn.running_var, slots[:n], float(mom),
+                                    bn.num_batches_tracked)
 
     def enable_direct_grads(self, grad_ready=None):
         for p in self.model.parameters():

@@ -121,6 +121,10 @@ class Trainer:
         self._inflight: List[torch.cuda.Event] = []
         self.step_count = 0
         self.micro_count = 0
+        self._mstreams: List[torch.cuda.Stream] = []     # concurrent micro-batch streams
+        self._mbufs: List[torch.Tensor] = []               # their extra gradient buffers
+        self._mviews: List[list] = []
+        self._flat_views = None
         self._graphs: Dict[str, "torch.cuda.CUDAGraph"] = {}   # hipGraphs (cfg.hip_graph)
         self._graph_warm: Dict[str, int] = {}
         self._static = None
@@ -224,6 +228,89 @@ class Trainer:
         self.meter.add(loss, correct, y.numel())
         self.micro_count += 1
         return loss
+
+    # ------------------------------------------------------------------ concurrent micro-batches
+    def _concurrent_ok(self, n_micro: int) -> bool:
+        return (self.cfg.micro_streams > 1 and n_micro > 1 and self.impl == "hip"
+                and self.device.type == "cuda")
+
+    def _grad_views(self, buf: torch.Tensor):
+        from ..parallel.flat import FlatParams
+        f = self.flat
+        return [FlatParams._view(buf, f.offsets[id(p)], p) for p in f.order]
+
+    def _concurrent_micros(self, mbs: List[Tuple[torch.Tensor, torch.Tensor]]):
+        """Accumulation micro-batches on ``micro_streams`` HIP streams at once.
+
+        The reference's regime (batch 1 per GPU, 50 accumulated micro-batches per exchange,
+        ref.py:685-687,750-766) leaves the GPU mostly idle inside each micro-batch: the deep
+        layers of one 512² image are a few hundred pixels.  Independent micro-batches fill
+        it: micro-batch j runs forward AND backward on stream j % K (autograd keeps a
+        backward on its forward's stream), with
+          * its own gradient buffer per stream (the kernels accumulate into ``.grad``; the
+            parameters' grad views are re-pointed before each backward is queued), summed
+            into the flat gradient in stream order afterwards — deterministic, though not
+            the sequential summation order;
+          * the BatchNorm running-statistics updates deferred to per-micro-batch slots and
+            applied in micro-batch order after the streams join: bit-identical running
+            statistics to one-by-one forwards;
+          * the weight-gradient side stream off (each micro-batch stream is serial).
+        Parameters do not change inside an accumulation window, so every micro-batch sees
+        the same weights as in the sequential loop."""
+        eng = self.model._engine
+        K = min(self.cfg.micro_streams, len(mbs))
+        cur = torch.cuda.current_stream(self.device)
+        # streams: the caller's, the engine's (idle here) weight-gradient stream, then new
+        # ones — GPU_MAX_HW_QUEUES (4) hardware queues per process: streams beyond that share
+        # a queue and serialise, so K <= 4 uses at most 4 streams in all
+        if len(self._mstreams) < K - 1:
+            pool = [eng._side_stream] if eng._side_stream is not None else []
+            while len(pool) < K - 1:
+                pool.append(torch.cuda.Stream(self.device))
+            self._mstreams = pool
+        streams = [cur] + self._mstreams[:K - 1]
+        while len(self._mbufs) < K - 1:
+            self._mbufs.append(torch.zeros_like(self.flat.grad_buf))
+            self._mviews.append(self._grad_views(self._mbufs[-1]))
+        if self._flat_views is None:
+            self._flat_views = self._grad_views(self.flat.grad_buf)
+        views = [self._flat_views] + self._mviews[:K - 1]
+        side_on = eng.side is not None
+        eng.set_side_stream(False)
+        for st in streams[1:]:
+            st.wait_stream(cur)                    # inputs and the previous step are queued
+        eng.bn_defer_prepare(len(mbs))
+        outs = []
+        order = self.flat.order
+        try:
+            for j, (x, y) in enumerate(mbs):
+                s = j % K
+                for p, g in zip(order, views[s]):
+                    p.grad = g
+                eng.bn_defer_j = j
+                st = streams[s]
+                with torch.cuda.stream(st):
+                    loss, correct = self.model.loss_and_correct(x, y)
+                    loss.backward()
+                if st is not cur:
+                    for t in (x, getattr(x, "_ddlpc_nhwc", None), y):
+                        if t is not None and t.is_cuda:
+                            t.record_stream(st)    # allocated on the caller's stream
+                outs.append((loss, correct, y.numel()))
+        finally:
+            eng.bn_defer_j = None
+            for p, g in zip(order, self._flat_views):
+                p.grad = g
+            eng.set_side_stream(side_on)
+        for st in streams[1:]:
+            cur.wait_stream(st)
+        eng.bn_defer_apply(len(mbs))
+        for b in self._mbufs[:K - 1]:
+            self.flat.grad_buf.add_(b)
+            b.zero_()
+        for loss, correct, n in outs:
+            self.meter.add(loss, correct, n)
+        self.micro_count += len(mbs)
 
     # ------------------------------------------------------------------ hipGraph step
     def _graph_ok(self, n_micro: int) -> bool:
@@ -356,8 +443,12 @@ class Trainer:
         if ph is not None:
             ph.mark("start")
         with trace_range("ddlpc.fwd_bwd"):
-            for i, (x, y) in enumerate(micro_batches):
-                self._micro(x, y, sync=(i == n - 1))
+            if self._concurrent_ok(n):
+                self._concurrent_micros(micro_batches[:-1])
+                self._micro(*micro_batches[-1], sync=True)
+            else:
+                for i, (x, y) in enumerate(micro_batches):
+                    self._micro(x, y, sync=(i == n - 1))
         if ph is not None:
             ph.mark("fwd_bwd")
         if self.reducer is not None:
