@@ -64,8 +64,9 @@ def _parse():
     ap.add_argument("--fixed-batch", type=int, default=0,
                     help="diagnostic: 1 = reuse one rendered batch every step (no per-step "
                          "input pipeline; reported in 'data')")
-    ap.add_argument("--micro-streams", type=int, default=1,
-                    help="accumulation micro-batches in flight on this many HIP streams")
+    ap.add_argument("--micro-streams", type=int, default=-1,
+                    help="accumulation micro-batches in flight on this many HIP streams "
+                         "(-1: auto, 3 for small accumulated micro-batches)")
     ap.add_argument("--reserve-cus", type=int, default=-1,
                     help="CUs kept out of persistent kernel grids (-1: 8 under DP, else 0)")
     ap.add_argument("--comm-proxy", type=int, default=0,
@@ -232,8 +233,10 @@ def main():
     if tr.phases is not None:
         tr.phases.read(reset=True)                 # phase means over the timed steps only
     first = args.warmup + 100
+    tr.ms_host_s = 0.0
     dt = timed(args.steps, first)
     phases = tr.phases.read() if tr.phases is not None else {}
+    ms_host = getattr(tr, "ms_host_s", 0.0)
     mstats = torch.cuda.memory_stats(device) if dev == "cuda" else {}
     ms = dt / args.steps * 1e3
     imgs = B * args.accum * world * args.steps
@@ -320,7 +323,10 @@ def main():
                        "optimizer": "Adam(lr=1e-3)", "loss": "CrossEntropy",
                        "train_loss_mean": round(loss["loss"], 4),
                        "recompute": int(args.recompute),
-                       "micro_streams": args.micro_streams,
+                       "micro_streams": getattr(tr, "micro_streams", 1),
+                       "micro_streams_host_ms_per_step": (round(ms_host * 1e3 / args.steps, 2)
+                                                          if getattr(tr, "micro_streams", 1) > 1
+                                                          else None),
                        "peak_mem_gb": (round(torch.cuda.max_memory_allocated(device) / 2**30, 2)
                                        if dev == "cuda" else None),
                        "schedule": ("overlap" if sched.get("side_stream") else "serial") if sched

@@ -1225,6 +1225,22 @@ int64_t set_cu_reserve(int64_t k) {
   return num_cus();
 }
 
+// a HIP stream restricted to CUs {i : i % K == k} (K concurrent micro-batch streams, each on
+// its own slice of the chip, interleaved over the XCDs).  ROCm gives a CU-masked stream its
+// own hardware queue, so K such streams never serialise on a shared queue.  -> the stream
+// handle (never destroyed: the Trainer keeps it for the process lifetime)
+int64_t cu_mask_stream(int64_t k, int64_t K) {
+  TORCH_CHECK(K >= 1 && k >= 0 && k < K, "cu_mask_stream: 0 <= k < K");
+  const int n = phys_cus();
+  std::vector<uint32_t> mask((n + 31) / 32, 0u);
+  for (int i = 0; i < n; ++i)
+    if (i % K == k) mask[i / 32] |= 1u << (i % 32);
+  hipStream_t s = nullptr;
+  TORCH_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) == hipSuccess,
+              "hipExtStreamCreateWithCUMask failed");
+  return reinterpret_cast<int64_t>(s);
+}
+
 // single-GPU stand-in for a bucket all-reduce (Trainer comm_proxy): `blocks` workgroups
 // stream the bucket `passes` times (read + write back, values unchanged) on the current
 // stream — RCCL's footprint (a few tens of channels, each a streaming workgroup)
@@ -1243,6 +1259,7 @@ void comm_proxy(const at::Tensor& g, int64_t blocks, int64_t passes) {
 TORCH_LIBRARY(ddlpc, m) {
   m.def("set_cu_reserve(int k) -> int", &ddlpc::set_cu_reserve);
   m.def("set_knob(str name, int value) -> int", &ddlpc::set_knob);
+  m.def("cu_mask_stream(int k, int K) -> int", &ddlpc::cu_mask_stream);
   m.def("comm_proxy(Tensor(a!) g, int blocks, int passes) -> ()");
   m.def("conv3_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, Tensor? pscale, Tensor? pshift, "
         "int cout, int co1, bool stats, Tensor? pscale2=None, Tensor? pshift2=None, Tensor? bnb_y=None, "

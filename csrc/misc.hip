@@ -82,19 +82,30 @@ __global__ __launch_bounds__(256) void weight_pack_kernel(const PackEntry* __res
     }
     __syncthreads();
     if (e.kind == 0) {
-      // fwd: [co = r0+r][tap][ci = c0 + c]
-      for (int i = tid; i < PT * T * NC; i += 256) {
-        const int c = i % NC, rt = i / NC, tap = rt % T, r = rt / T;
-        if (r < nr && c < nc)
-          e.fwd[((long long)(r0 + r) * T + tap) * e.CinW + c0 + c] = f2bf(tile[r][c * T + tap]);
+      // fwd: [co = r0+r][tap][ci = c0 + c] — a thread writes a (c, c+1) pair as one 4-byte
+      // store (NC, c0, CinW even; a lone last channel of an odd Cin is written alone)
+      for (int i = tid; i < PT * T * (NC / 2); i += 256) {
+        const int c = 2 * (i % (NC / 2)), rt = i / (NC / 2), tap = rt % T, r = rt / T;
+        if (r < nr && c < nc) {
+          bf16_t* d = e.fwd + ((long long)(r0 + r) * T + tap) * e.CinW + c0 + c;
+          if (c + 1 < nc)
+            *reinterpret_cast<uint32_t*>(d) = pack2(tile[r][c * T + tap], tile[r][(c + 1) * T + tap]);
+          else
+            d[0] = f2bf(tile[r][c * T + tap]);
+        }
       }
-      // dgrad: [ci = c0 + c][tp][co = r0 + r], source tap = T-1-tp
+      // dgrad: [ci = c0 + c][tp][co = r0 + r], source tap = T-1-tp (co pairs: r0, CoutW even)
       if (e.dgrad != nullptr)
-        for (int i = tid; i < PT * T * NC; i += 256) {
-          const int r = i % PT, ct = i / PT, tp = ct % T, c = ct / T;
-          if (r < nr && c < nc)
-            e.dgrad[((long long)(c0 + c) * T + tp) * e.CoutW + r0 + r] =
-                f2bf(tile[r][c * T + (T - 1 - tp)]);
+        for (int i = tid; i < (PT / 2) * T * NC; i += 256) {
+          const int r = 2 * (i % (PT / 2)), ct = i / (PT / 2), tp = ct % T, c = ct / T;
+          if (r < nr && c < nc) {
+            bf16_t* d = e.dgrad + ((long long)(c0 + c) * T + tp) * e.CoutW + r0 + r;
+            const int st = c * T + (T - 1 - tp);
+            if (r + 1 < nr)
+              *reinterpret_cast<uint32_t*>(d) = pack2(tile[r][st], tile[r + 1][st]);
+            else
+              d[0] = f2bf(tile[r][st]);
+          }
         }
     } else {
       // fwd: [(sub, co = c0 + c)][ci = r0 + r]

@@ -117,9 +117,10 @@ class TrainConfig:
     impl: str = "auto"                   # auto | hip | torch   (hip = hand-written kernels, bf16;
                                          # auto = hip on a GPU for bf16, torch for fp32)
     hip_graph: bool = False              # capture the train step in a hipGraph
-    micro_streams: int = 1               # accumulation micro-batches queued on this many HIP
-                                         # streams at once (small micro-batches: the
-                                         # reference's batch-1 regime); 1 = one by one
+    micro_streams: int = -1              # accumulation micro-batches in flight on this many
+                                         # HIP streams (each replaying its own graph); -1 =
+                                         # auto: 3 for small accumulated micro-batches (the
+                                         # reference's batch-1 regime), else 1 = one by one
     recompute: int = 0                   # HIP engine activation recompute in backward (SURVEY 5.7,
                                          # batches beyond HBM): 1 = each block's first conv output,
                                          # 2 = both conv outputs of blocks that hand out a

@@ -419,7 +419,7 @@ class _HeadCEFn(torch.autograd.Function):
                 dw = db = None
             else:
                 dw, db = _ops().head_wgrad_from_rows(wrows, scale, K, C)
-            da = torch.zeros((), dtype=a.dtype, device=a.device).expand(a.shape)
+            da = eng.zero_scalar(a).expand(a.shape)
             da._ddlpc_head = (a, wh, bh, labels, out3, gs, ctx.ignore_index)
             da._ddlpc_bn_partial = brows
             da._ddlpc_bn_pscale = scale
@@ -436,7 +436,7 @@ class _HeadCEFn(torch.autograd.Function):
                                                   None, None, bn, not two_pass)
         if two_pass:
             # stand-in gradient of the right shape (no storage); the consumer recognises it
-            da = torch.zeros((), dtype=a.dtype, device=a.device).expand(a.shape)
+            da = eng.zero_scalar(a).expand(a.shape)
             da._ddlpc_head = (a, wh, bh, labels, out3, gs, ctx.ignore_index)
         if bn is not None:
             da._ddlpc_bn_partial = part
@@ -583,6 +583,7 @@ class UNetEngine:
         for i, b in enumerate(self.bns):
             b.index = i
         self.bn_defer_j: Optional[int] = None
+        self._zeros = {}
         self._bn_slots: List[torch.Tensor] = []
         self.packs = [p for b in self.enc + [self.mid] for p in (b.pack1, b.pack2)]
         for _, pk, b in self.dec:
@@ -591,6 +592,15 @@ class UNetEngine:
         self._entries_key = None
         self._version = None
         self.pack_weights()
+
+    def zero_scalar(self, like: torch.Tensor) -> torch.Tensor:
+        """A cached 0-d zero of ``like``'s dtype/device (base of the head's zero-stride
+        stand-in gradient: no fill kernel per step)."""
+        key = (like.dtype, like.device)
+        z = self._zeros.get(key)
+        if z is None:
+            z = self._zeros[key] = torch.zeros((), dtype=like.dtype, device=like.device)
+        return z
 
     # ------------------------------------------------------------------ deferred BN stats
     def bn_defer_prepare(self, n: int):

@@ -121,7 +121,12 @@ class Trainer:
         self._inflight: List[torch.cuda.Event] = []
         self.step_count = 0
         self.micro_count = 0
+        self.micro_streams = self._resolve_micro_streams()
         self._mstreams: List[torch.cuda.Stream] = []     # concurrent micro-batch streams
+        self._ms_mode = None
+        self._ms_meters: List[DeviceMeter] = []
+        self._ms_graphs, self._ms_warm, self._ms_static = [], [], []
+        self.ms_host_s = 0.0
         self._mbufs: List[torch.Tensor] = []               # their extra gradient buffers
         self._mviews: List[list] = []
         self._flat_views = None
@@ -231,13 +236,93 @@ class Trainer:
 
     # ------------------------------------------------------------------ concurrent micro-batches
     def _concurrent_ok(self, n_micro: int) -> bool:
-        return (self.cfg.micro_streams > 1 and n_micro > 1 and self.impl == "hip"
+        return (self.micro_streams > 1 and n_micro > 1 and self.impl == "hip"
                 and self.device.type == "cuda")
+
+    SMALL_MICRO_PIXELS = 4 * 256 * 256          # one 512² image, four 256² ones
+
+    def _resolve_micro_streams(self) -> int:
+        """cfg.micro_streams (-1 = auto): 3 concurrent micro-batch streams when micro-batches
+        are small (<= SMALL_MICRO_PIXELS) and accumulated, else 1.  Measured at 512² batch 1,
+        50 micro-batches, with per-stream graphs: 1 / 2 / 3 / 4 / 6 streams = 356 / 520 /
+        638 / 513 / 646 images/s — 3 streams plus the caller's fill the process's 4 hardware
+        queues (GPU_MAX_HW_QUEUES); a 4th stream shares one and serialises."""
+        c = self.cfg
+        if c.micro_streams >= 0:
+            return max(1, c.micro_streams)
+        px = c.batch_per_gpu * c.tile ** c.model.dims
+        small = px <= self.SMALL_MICRO_PIXELS
+        return 3 if (c.accum_steps > 1 and small and self.impl == "hip"
+                     and self.device.type == "cuda") else 1
 
     def _grad_views(self, buf: torch.Tensor):
         from ..parallel.flat import FlatParams
         f = self.flat
         return [FlatParams._view(buf, f.offsets[id(p)], p) for p in f.order]
+
+    def _ms_streams(self, K: int, cur) -> List[torch.cuda.Stream]:
+        """K micro-batch streams: plain HIP streams (default), or with DDLPC_MS_MODE=2
+        CU-masked ones (stream k on CUs {i : i % K == k}, each its own hardware queue).
+        Measured at 512² batch 1 with graphs (docs/PERF.md): the masked streams run 2-3x
+        SLOWER than plain ones (171 vs 515 images/s at K = 4), so they stay a diagnostic."""
+        mode = int(os.environ.get("DDLPC_MS_MODE", "0"))
+        if len(self._mstreams) != K or self._ms_mode != mode:
+            if mode == 2:
+                F = _ext.ops()
+                self._mstreams = [torch.cuda.ExternalStream(int(F.cu_mask_stream(k, K)),
+                                                            device=self.device)
+                                  for k in range(K)]
+            else:
+                self._mstreams = [torch.cuda.Stream(self.device) for _ in range(K)]
+            self._ms_mode = mode
+            self._ms_graphs, self._ms_warm, self._ms_static = [None] * K, [0] * K, [None] * K
+        return self._mstreams
+
+    def _ms_buffers(self, K: int):
+        while len(self._mbufs) < K - 1:
+            self._mbufs.append(torch.zeros_like(self.flat.grad_buf))
+            self._mviews.append(self._grad_views(self._mbufs[-1]))
+        if self._flat_views is None:
+            self._flat_views = self._grad_views(self.flat.grad_buf)
+        while len(self._ms_meters) < K:
+            self._ms_meters.append(DeviceMeter(self.device))
+        return [self._flat_views] + self._mviews[:K - 1]
+
+    def _ms_enter(self, K: int):
+        """Per-window setup: side stream off; with DDLPC_MS_SPLIT=1 the persistent /
+        chip-filling grids are sized for 1/K of the chip (default: full-chip grids)."""
+        eng = self.model._engine
+        state = (eng.side is not None, os.environ.get("DDLPC_MS_SPLIT", "0") != "0")
+        eng.set_side_stream(False)
+        if state[1]:
+            phys = torch.cuda.get_device_properties(self.device).multi_processor_count
+            _ext.ops().set_cu_reserve(phys - phys // K)
+        return state
+
+    def _ms_exit(self, state):
+        eng = self.model._engine
+        eng.bn_defer_j = None
+        for p, g in zip(self.flat.order, self._flat_views):
+            p.grad = g
+        eng.set_side_stream(state[0])
+        if state[1]:
+            _ext.ops().set_cu_reserve(self.reserve_cus)
+
+    def _ms_finish(self, K: int, n: int):
+        """After the streams joined: extra gradient buffers into the flat one (stream
+        order), per-stream meters into the trainer's."""
+        for b in self._mbufs[:K - 1]:
+            self.flat.grad_buf.add_(b)
+            b.zero_()
+        for m in self._ms_meters[:K]:
+            self.meter.buf += m.buf
+            m.buf.zero_()
+        self.micro_count += n
+
+    def _ms_body(self, k: int, x, y):
+        loss, correct = self.model.loss_and_correct(x, y)
+        loss.backward()
+        self._ms_meters[k].add(loss, correct, y.numel())
 
     def _concurrent_micros(self, mbs: List[Tuple[torch.Tensor, torch.Tensor]]):
         """Accumulation micro-batches on ``micro_streams`` HIP streams at once.
@@ -245,72 +330,91 @@ class Trainer:
         The reference's regime (batch 1 per GPU, 50 accumulated micro-batches per exchange,
         ref.py:685-687,750-766) leaves the GPU mostly idle inside each micro-batch: the deep
         layers of one 512² image are a few hundred pixels.  Independent micro-batches fill
-        it: micro-batch j runs forward AND backward on stream j % K (autograd keeps a
-        backward on its forward's stream), with
+        it.  They are processed in rounds of K: micro-batch rK + k runs forward AND backward
+        on stream k (autograd keeps a backward on its forward's stream), with
           * its own gradient buffer per stream (the kernels accumulate into ``.grad``; the
-            parameters' grad views are re-pointed before each backward is queued), summed
-            into the flat gradient in stream order afterwards — deterministic, though not
+            parameters' grad views are re-pointed before each micro-batch is queued), summed
+            into the flat gradient in stream order at the end — deterministic, though not
             the sequential summation order;
-          * the BatchNorm running-statistics updates deferred to per-micro-batch slots and
-            applied in micro-batch order after the streams join: bit-identical running
-            statistics to one-by-one forwards;
-          * the weight-gradient side stream off (each micro-batch stream is serial).
+          * the BatchNorm running-statistics updates written to per-stream slots and applied
+            in micro-batch order after each round (``UNetEngine.bn_defer_apply``);
+          * its own training meter; the weight-gradient side stream off;
+          * stream k replays its own captured micro-batch graph (own static inputs,
+            activation pool, gradient buffer and slot; eager for the first GRAPH_WARMUP
+            uses) — without graphs the host's ~230 launches per micro-batch are the limit
+            once the GPU work overlaps (measured: 93 of a 100 ms step spent enqueueing).
         Parameters do not change inside an accumulation window, so every micro-batch sees
-        the same weights as in the sequential loop."""
+        the same weights as in the one-by-one loop.  The final micro-batch of the window
+        runs on the caller's stream as usual (it triggers the gradient exchange)."""
         eng = self.model._engine
-        K = min(self.cfg.micro_streams, len(mbs))
+        K = self.micro_streams
         cur = torch.cuda.current_stream(self.device)
-        # streams: the caller's, the engine's (idle here) weight-gradient stream, then new
-        # ones — GPU_MAX_HW_QUEUES (4) hardware queues per process: streams beyond that share
-        # a queue and serialise, so K <= 4 uses at most 4 streams in all
-        if len(self._mstreams) < K - 1:
-            pool = [eng._side_stream] if eng._side_stream is not None else []
-            while len(pool) < K - 1:
-                pool.append(torch.cuda.Stream(self.device))
-            self._mstreams = pool
-        streams = [cur] + self._mstreams[:K - 1]
-        while len(self._mbufs) < K - 1:
-            self._mbufs.append(torch.zeros_like(self.flat.grad_buf))
-            self._mviews.append(self._grad_views(self._mbufs[-1]))
-        if self._flat_views is None:
-            self._flat_views = self._grad_views(self.flat.grad_buf)
-        views = [self._flat_views] + self._mviews[:K - 1]
-        side_on = eng.side is not None
-        eng.set_side_stream(False)
-        for st in streams[1:]:
-            st.wait_stream(cur)                    # inputs and the previous step are queued
-        eng.bn_defer_prepare(len(mbs))
-        outs = []
+        streams = self._ms_streams(K, cur)
+        views = self._ms_buffers(K)
+        # per-stream graphs by default: without them the host's ~230 launches per
+        # micro-batch become the limit once the streams overlap (DDLPC_MS_GRAPH=0: eager)
+        use_graph = os.environ.get("DDLPC_MS_GRAPH", "1") != "0"
+        state = self._ms_enter(K)
+        eng.bn_defer_prepare(K)
         order = self.flat.order
+        t_host = time.perf_counter()
         try:
-            for j, (x, y) in enumerate(mbs):
-                s = j % K
-                for p, g in zip(order, views[s]):
-                    p.grad = g
-                eng.bn_defer_j = j
-                st = streams[s]
-                with torch.cuda.stream(st):
-                    loss, correct = self.model.loss_and_correct(x, y)
-                    loss.backward()
-                if st is not cur:
+            for r0 in range(0, len(mbs), K):
+                chunk = mbs[r0:r0 + K]
+                for k, (x, y) in enumerate(chunk):
+                    st = streams[k]
+                    st.wait_stream(cur)            # inputs, previous round's BN updates
+                    for p, g in zip(order, views[k]):
+                        p.grad = g
+                    eng.bn_defer_j = k
+                    with torch.cuda.stream(st):
+                        if use_graph:
+                            self._ms_graph_micro(k, st, x, y)
+                        else:
+                            self._ms_body(k, x, y)
                     for t in (x, getattr(x, "_ddlpc_nhwc", None), y):
                         if t is not None and t.is_cuda:
                             t.record_stream(st)    # allocated on the caller's stream
-                outs.append((loss, correct, y.numel()))
+                for k in range(len(chunk)):
+                    cur.wait_stream(streams[k])
+                eng.bn_defer_apply(len(chunk))     # this round's running stats, in order
         finally:
-            eng.bn_defer_j = None
-            for p, g in zip(order, self._flat_views):
-                p.grad = g
-            eng.set_side_stream(side_on)
-        for st in streams[1:]:
-            cur.wait_stream(st)
-        eng.bn_defer_apply(len(mbs))
-        for b in self._mbufs[:K - 1]:
-            self.flat.grad_buf.add_(b)
-            b.zero_()
-        for loss, correct, n in outs:
-            self.meter.add(loss, correct, n)
-        self.micro_count += len(mbs)
+            self._ms_exit(state)
+        self.ms_host_s += time.perf_counter() - t_host     # host enqueue time (diagnostic)
+        self._ms_finish(K, len(mbs))
+
+    def _ms_graph_micro(self, k: int, st, x, y):
+        """Stream k's micro-batch as a replay of its own graph (eager for the first
+        GRAPH_WARMUP uses, then captured): the batch is copied into stream k's static
+        buffers on stream k."""
+        from ..data.datasets import engine_input
+        xp = getattr(x, "_ddlpc_nhwc", None)
+        sk = self._ms_static[k]
+        if sk is None or sk[1].shape != y.shape:
+            if xp is not None:
+                sp = torch.empty_like(xp)
+                sk = (engine_input(sp, x.shape[1]), torch.empty_like(y), sp)
+            else:
+                sk = (torch.empty_like(x), torch.empty_like(y), None)
+            self._ms_static[k] = sk
+            self._ms_graphs[k], self._ms_warm[k] = None, 0
+        sx, sy, sp = sk
+        if sp is not None and xp is not None:
+            sp.copy_(xp)
+        else:
+            sx.copy_(x)
+        sy.copy_(y)
+        g = self._ms_graphs[k]
+        if g is not None:
+            g.replay()
+            return
+        self._ms_body(k, sx, sy)
+        self._ms_warm[k] += 1
+        if self._ms_warm[k] >= self.GRAPH_WARMUP:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                self._ms_body(k, sx, sy)
+            self._ms_graphs[k] = g
 
     # ------------------------------------------------------------------ hipGraph step
     def _graph_ok(self, n_micro: int) -> bool:
@@ -387,6 +491,10 @@ class Trainer:
         ph = self.phases
         if ph is not None:
             ph.mark("start")
+        if self._concurrent_ok(len(micro_batches)):
+            # accumulation micro-batches: K streams, each replaying its own graph
+            self._concurrent_micros(micro_batches[:-1])
+            micro_batches = micro_batches[-1:]
         n = len(micro_batches)
         for i, (x, y) in enumerate(micro_batches):
             last = i == n - 1

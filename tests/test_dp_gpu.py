@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _dp_rank(rank, world, bucket_mb, side, overlap, codec="none", accum=1, wire="fp32",
-             scale="bucket", reduce="mean"):
+             scale="bucket", reduce="mean", ms=1):
     import os
     os.environ["LOCAL_RANK"] = "0"              # both ranks on the box's single GPU
     os.environ["DDLPC_WGRAD_STREAM"] = side
@@ -23,7 +23,8 @@ def _dp_rank(rank, world, bucket_mb, side, overlap, codec="none", accum=1, wire=
     cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=2,
                       num_samples=1, test_holdout=0, impl="hip", backend="gloo",
                       bucket_mb=bucket_mb, overlap_comm=overlap, grad_codec=codec,
-                      accum_steps=accum, wire_dtype=wire, codec_scale=scale, reduce=reduce)
+                      accum_steps=accum, wire_dtype=wire, codec_scale=scale, reduce=reduce,
+                      micro_streams=ms)
     tr = Trainer(cfg, device="cuda")
     red = tr.reducer
     mbs = [device_random_batch(2, 64, 6, tr.device, seed=10 + rank + 100 * j)
@@ -37,7 +38,14 @@ def _dp_rank(rank, world, bucket_mb, side, overlap, codec="none", accum=1, wire=
     g_local = tr.flat.grad_buf.clone()
     tr.optimizer.zero_grad()
     # same micro-batches; the bucketed exchange overlaps the LAST micro-batch's backward
-    for j, (x, y) in enumerate(mbs):
+    # (ms > 1: the accumulation micro-batches on concurrent streams first)
+    if ms > 1:
+        red.prepare(sync=False)
+        tr._concurrent_micros(mbs[:-1])
+        mbs_loop = [(accum - 1, mbs[-1])]
+    else:
+        mbs_loop = list(enumerate(mbs))
+    for j, (x, y) in mbs_loop:
         red.prepare(sync=(j == accum - 1))
         loss, _ = tr.model.loss_and_correct(x, y)
         loss.backward()
@@ -92,6 +100,18 @@ def test_dp_two_ranks_hip_engine_gloo(side, overlap):
         o = res[r]
         assert o["buckets"] > 1 and o["launched"] == (o["buckets"] if overlap else 0), o
         assert o["max_err"] <= 1e-6 * max(o["scale"], 1.0), o
+        assert o["replicas_equal"], o
+
+
+def test_dp_concurrent_micro_streams_two_ranks():
+    """Data parallelism with the accumulation micro-batches on 3 concurrent streams per rank
+    (per-stream graphs): the exchanged gradient equals the mean of the ranks' sequentially
+    accumulated local gradients to fp32 summation order, replicas stay bit-identical."""
+    res = run(_dp_rank, 2, (1.0, "1", True, "none", 6, "fp32", "bucket", "mean", 3), timeout=200)
+    for r in (0, 1):
+        o = res[r]
+        assert o["launched"] == o["buckets"] > 1, o
+        assert o["max_err"] <= 1e-5 * max(o["scale"], 1.0), o
         assert o["replicas_equal"], o
 
 
