@@ -462,15 +462,19 @@ at::Tensor bn_finalize(const at::Tensor& partial, double count, const at::Tensor
 // deferred BatchNorm running-statistics updates, in micro-batch order (see reduce.hip)
 void bn_running_apply(at::Tensor running_mean, at::Tensor running_var, const at::Tensor& slots,
                       double momentum, const c10::optional<at::Tensor>& nbt) {
-  CHECK_F32(running_mean); CHECK_F32(running_var); CHECK_F32(slots); CHECK_CONTIG(slots);
+  // slots: [K][2C] rows of (mean | unbiased var), any row stride (a column slice of a
+  // per-micro-batch arena), rows contiguous
+  CHECK_F32(running_mean); CHECK_F32(running_var); CHECK_F32(slots);
   const int C = (int)running_mean.numel();
-  TORCH_CHECK(running_var.numel() == C && slots.numel() % (2 * C) == 0, "slots [K][2][C]");
+  TORCH_CHECK(running_var.numel() == C && slots.dim() == 2 && slots.size(1) == 2 * C &&
+              slots.stride(1) == 1, "slots [K][2C] with contiguous rows");
   c10::DeviceGuard guard(slots.device());
-  const int K = (int)(slots.numel() / (2 * C));
+  const int K = (int)slots.size(0);
   if (K == 0) return;
   int64_t* nbp = (nbt.has_value() && nbt->defined()) ? nbt->data_ptr<int64_t>() : nullptr;
   bn_running_apply_launch(running_mean.data_ptr<float>(), running_var.data_ptr<float>(),
-                          slots.data_ptr<float>(), K, C, (float)momentum, nbp, cur_stream());
+                          slots.data_ptr<float>(), K, C, (long long)slots.stride(0), (float)momentum,
+                          nbp, cur_stream());
 }
 
 std::vector<at::Tensor> bn_relu_apply(const at::Tensor& y, const at::Tensor& stats4, bool pool,

@@ -115,19 +115,19 @@ __global__ void scatter_sums_dscale_kernel(const double* __restrict__ sums, long
   }
 }
 
-// deferred running-statistics updates (concurrent micro-batch streams): slots [K][2][C] of
+// deferred running-statistics updates (concurrent micro-batch streams): K slots of
 // (batch mean, unbiased batch var) written by K forwards with momentum 1, applied here in
 // micro-batch order — the sequence of updates the K forwards would have made one by one
 __global__ void bn_running_apply_kernel(float* __restrict__ running_mean, float* __restrict__ running_var,
-                                        const float* __restrict__ slots, int K, int C, float momentum,
-                                        int64_t* nbt) {
+                                        const float* __restrict__ slots, int K, int C, long long stride,
+                                        float momentum, int64_t* nbt) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c == 0 && nbt != nullptr) nbt[0] += K;
   if (c >= C) return;
   float rm = running_mean[c], rv = running_var[c];
-  for (int k = 0; k < K; ++k) {
-    rm = bn_momentum_update(rm, slots[(2 * k) * C + c], momentum);
-    rv = bn_momentum_update(rv, slots[(2 * k + 1) * C + c], momentum);
+  for (int k = 0; k < K; ++k) {                   // slot k: [mean (C) | var (C)] at k * stride
+    rm = bn_momentum_update(rm, slots[k * stride + c], momentum);
+    rv = bn_momentum_update(rv, slots[k * stride + C + c], momentum);
   }
   running_mean[c] = rm;
   running_var[c] = rv;
@@ -322,10 +322,10 @@ void scatter_sums_dscale_launch(const double* sums, long long N, float* dst, con
                      accumulate ? 1 : 0);
 }
 
-void bn_running_apply_launch(float* rm, float* rv, const float* slots, int K, int C, float momentum,
-                             int64_t* nbt, hipStream_t st) {
+void bn_running_apply_launch(float* rm, float* rv, const float* slots, int K, int C, long long stride,
+                             float momentum, int64_t* nbt, hipStream_t st) {
   hipLaunchKernelGGL(bn_running_apply_kernel, dim3((C + 255) / 256), dim3(256), 0, st, rm, rv, slots, K,
-                     C, momentum, nbt);
+                     C, stride, momentum, nbt);
 }
 
 void head_grad_scale_launch(const float* out3, const float* gs, float* scale, hipStream_t st) {

@@ -577,14 +577,18 @@ class UNetEngine:
         head = model.conv_last
         self.head = head
         # deferred BatchNorm running statistics (concurrent micro-batch streams, Trainer
-        # micro_streams): bn_defer_j = index of the micro-batch whose forward is being queued
+        # micro_streams): bn_defer_j = the stream whose slot vector the forward being queued
+        # writes (None: update the running statistics in place)
         self.bns = [b for blk in self.enc + [self.mid] + [d[2] for d in self.dec]
                     for b in (blk.bn1, blk.bn2)]
         for i, b in enumerate(self.bns):
             b.index = i
         self.bn_defer_j: Optional[int] = None
         self._zeros = {}
-        self._bn_slots: List[torch.Tensor] = []
+        self._bn_streams: List[torch.Tensor] = []
+        self._bn_views: List[List[torch.Tensor]] = []
+        self._bn_offs: List[int] = []
+        self._bn_arena: Optional[torch.Tensor] = None
         self.packs = [p for b in self.enc + [self.mid] for p in (b.pack1, b.pack2)]
         for _, pk, b in self.dec:
             self.packs += [pk, b.pack1, b.pack2] if pk is not None else [b.pack1, b.pack2]
@@ -603,25 +607,44 @@ class UNetEngine:
         return z
 
     # ------------------------------------------------------------------ deferred BN stats
-    def bn_defer_prepare(self, n: int):
-        """Slots [n][2][C] per BatchNorm for n concurrently queued forwards (zeroed once,
-        reused: a slot only ever holds finite (mean, var) values)."""
-        if not self._bn_slots or self._bn_slots[0].shape[0] < n:
-            self._bn_slots = [torch.zeros(n, 2, b.bn.num_features, dtype=torch.float32,
-                                          device=b.bn.running_mean.device) for b in self.bns]
+    def bn_defer_prepare(self, K: int, n: int):
+        """Storage for deferred BatchNorm running statistics: per stream k (K concurrent
+        micro-batch streams) one flat slot vector [sum over BN layers of 2C] written by the
+        forwards queued on that stream (bn_finalize with momentum 1 writes (mean, unbiased
+        var) exactly), and an arena [n][same] that receives stream k's vector after each of
+        its micro-batches (``bn_defer_stash``).  Slots are zeroed once and then only ever
+        hold finite values (the momentum-1 update reads them as 0 * old)."""
+        total = sum(2 * b.bn.num_features for b in self.bns)
+        dev = self.bns[0].bn.running_mean.device
+        if len(self._bn_streams) < K:
+            self._bn_offs, o = [], 0
+            for b in self.bns:
+                self._bn_offs.append(o)
+                o += 2 * b.bn.num_features
+            self._bn_streams = [torch.zeros(total, dtype=torch.float32, device=dev) for _ in range(K)]
+            self._bn_views = [[v[o:o + 2 * b.bn.num_features].view(2, b.bn.num_features)
+                               for o, b in zip(self._bn_offs, self.bns)] for v in self._bn_streams]
+        if self._bn_arena is None or self._bn_arena.shape[0] < n:
+            self._bn_arena = torch.zeros(n, total, dtype=torch.float32, device=dev)
 
-    def bn_defer_slot(self, index: int, j: int) -> torch.Tensor:
-        return self._bn_slots[index][j]
+    def bn_defer_slot(self, index: int, k: int) -> torch.Tensor:
+        return self._bn_views[k][index]
+
+    def bn_defer_stash(self, k: int, j: int):
+        """Micro-batch j (queued on stream k, current stream): its slot vector -> arena row j."""
+        self._bn_arena[j].copy_(self._bn_streams[k])
 
     def bn_defer_apply(self, n: int):
         """Apply the n deferred running-statistics updates of every BatchNorm in micro-batch
         order (one launch per BatchNorm): bit-identical to n sequential forwards."""
-        for b, slots in zip(self.bns, self._bn_slots):
+        for b, off in zip(self.bns, self._bn_offs):
             bn = b.bn
             if not bn.track_running_stats:
                 continue
             mom = bn.momentum if bn.momentum is not None else 0.1
-            _ops().bn_running_apply(bn.running_mean, bn.running_var, slots[:n], float(mom),
+            c2 = 2 * bn.num_features
+            _ops().bn_running_apply(bn.running_mean, bn.running_var,
+                                    self._bn_arena[:n, off:off + c2], float(mom),
                                     bn.num_batches_tracked)
 
     def enable_direct_grads(self, grad_ready=None):

@@ -330,14 +330,16 @@ class Trainer:
         The reference's regime (batch 1 per GPU, 50 accumulated micro-batches per exchange,
         ref.py:685-687,750-766) leaves the GPU mostly idle inside each micro-batch: the deep
         layers of one 512² image are a few hundred pixels.  Independent micro-batches fill
-        it.  They are processed in rounds of K: micro-batch rK + k runs forward AND backward
-        on stream k (autograd keeps a backward on its forward's stream), with
+        it: micro-batch j runs forward AND backward on stream j % K (autograd keeps a
+        backward on its forward's stream; a stream's micro-batches follow each other), with
           * its own gradient buffer per stream (the kernels accumulate into ``.grad``; the
             parameters' grad views are re-pointed before each micro-batch is queued), summed
             into the flat gradient in stream order at the end — deterministic, though not
             the sequential summation order;
-          * the BatchNorm running-statistics updates written to per-stream slots and applied
-            in micro-batch order after each round (``UNetEngine.bn_defer_apply``);
+          * the BatchNorm running-statistics updates written to per-stream slots, copied to
+            a per-micro-batch arena row after each micro-batch and applied in micro-batch
+            order once the streams have joined (``UNetEngine.bn_defer_apply``; training-mode
+            forwards only write running statistics, so nothing waits for them);
           * its own training meter; the weight-gradient side stream off;
           * stream k replays its own captured micro-batch graph (own static inputs,
             activation pool, gradient buffer and slot; eager for the first GRAPH_WARMUP
@@ -355,32 +357,33 @@ class Trainer:
         # micro-batch become the limit once the streams overlap (DDLPC_MS_GRAPH=0: eager)
         use_graph = os.environ.get("DDLPC_MS_GRAPH", "1") != "0"
         state = self._ms_enter(K)
-        eng.bn_defer_prepare(K)
+        eng.bn_defer_prepare(K, len(mbs))
         order = self.flat.order
         t_host = time.perf_counter()
+        for st in streams:
+            st.wait_stream(cur)                    # inputs and the previous step are queued
         try:
-            for r0 in range(0, len(mbs), K):
-                chunk = mbs[r0:r0 + K]
-                for k, (x, y) in enumerate(chunk):
-                    st = streams[k]
-                    st.wait_stream(cur)            # inputs, previous round's BN updates
-                    for p, g in zip(order, views[k]):
-                        p.grad = g
-                    eng.bn_defer_j = k
-                    with torch.cuda.stream(st):
-                        if use_graph:
-                            self._ms_graph_micro(k, st, x, y)
-                        else:
-                            self._ms_body(k, x, y)
-                    for t in (x, getattr(x, "_ddlpc_nhwc", None), y):
-                        if t is not None and t.is_cuda:
-                            t.record_stream(st)    # allocated on the caller's stream
-                for k in range(len(chunk)):
-                    cur.wait_stream(streams[k])
-                eng.bn_defer_apply(len(chunk))     # this round's running stats, in order
+            for j, (x, y) in enumerate(mbs):
+                k = j % K                          # stream k: micro-batches k, k+K, ... in order
+                st = streams[k]
+                for p, g in zip(order, views[k]):
+                    p.grad = g
+                eng.bn_defer_j = k
+                with torch.cuda.stream(st):
+                    if use_graph:
+                        self._ms_graph_micro(k, st, x, y)
+                    else:
+                        self._ms_body(k, x, y)
+                    eng.bn_defer_stash(k, j)       # its running-stat slot -> arena row j
+                for t in (x, getattr(x, "_ddlpc_nhwc", None), y):
+                    if t is not None and t.is_cuda:
+                        t.record_stream(st)        # allocated on the caller's stream
         finally:
             self._ms_exit(state)
         self.ms_host_s += time.perf_counter() - t_host     # host enqueue time (diagnostic)
+        for st in streams:
+            cur.wait_stream(st)
+        eng.bn_defer_apply(len(mbs))               # running statistics, in micro-batch order
         self._ms_finish(K, len(mbs))
 
     def _ms_graph_micro(self, k: int, st, x, y):
