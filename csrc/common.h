@@ -89,6 +89,21 @@ DDLPC_DEVICE f32x16_t mfma32x32x16(const uint4& a, const uint4& b, f32x16_t c) {
                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
 }
 
+// sum over the 16 lanes of each DPP row (lanes 16r .. 16r+15), the same value in all 16
+// lanes: quad xor 1, quad xor 2, half-row mirror, row mirror — VALU DPP moves instead of
+// __shfl_xor's LDS-crossbar ds_bpermute (order fixed: deterministic)
+template <int CTRL>
+DDLPC_DEVICE float dpp_movf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+DDLPC_DEVICE float row16_sum(float v) {
+  v += dpp_movf<0xB1>(v);
+  v += dpp_movf<0x4E>(v);
+  v += dpp_movf<0x141>(v);
+  v += dpp_movf<0x140>(v);
+  return v;
+}
+
 DDLPC_DEVICE float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

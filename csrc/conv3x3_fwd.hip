@@ -56,8 +56,9 @@ struct Cfg {
   // LEAN (accumulator of 32+ tiles per wave): bias and the BN-statistics accumulators live
   // in LDS instead of 48 VGPRs — per-wave-row slots [WM][2][BN], each (wave, column) owned
   // by one lane (no atomics: the order of the sums is fixed) + the bias of the n tile
+  // (the BN-backward epilogue variants keep their partial sums in the same LDS slots: LSTAT)
   static constexpr bool LEAN = MT * NT >= 32;
-  static constexpr int LEAN_BYTES = LEAN ? (WM * 2 * BN + BN) * 4 : 0;
+  static constexpr int LEAN_BYTES = (WM * 2 * BN + BN) * 4;
   static constexpr int SMEM = SS_BYTES + LEAN_BYTES + 2 * A_BYTES + NBB * B_BYTES;   // NBB weight buffers
 };
 
@@ -70,24 +71,25 @@ struct Cfg {
 // operand the pixel tile, so each lane's accumulator holds 4 CONSECUTIVE channels of one
 // pixel -> 8-byte bf16x4 stores; BN statistics are reduced with 4 lane shuffles and
 // written as one partial row per (m tile, wave row).
-template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, bool FDB, bool BNB, bool ILV>
+template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, int FDB, bool BNB, bool ILV>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_kernel(ConvFwdArgs p) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
   static_assert(NBB == 2 || NBB == 3 || (NBB == 4 && DIMS == 2), "2 / 3 weight-stage buffers, or 4 (super-stages)");
   // BN-backward epilogue: 2-D, and not with the counted waits of the 3-deep weight ring
   static_assert(!BNB || (DIMS == 2 && NBB != 3), "BNB: 2-D, NBB 2 or 4");
   static_assert(!ILV || NBB == 4, "DMA issue interleaved with the MFMAs: super-stages only");
-  constexpr bool FRAG_DB = FDB;
+  constexpr bool FRAG_DB = FDB == 1;            // (FDB 2: rolling pipeline, pipe_taps)
   constexpr int BM = C::BM, BN = C::BN;
   constexpr int NG = DIMS == 2 ? 3 : 9;           // (kd, r) kernel rows per chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* s_scale = reinterpret_cast<float*>(smem);
   float* s_shift = s_scale + 512;
   char* base = smem + C::SS_BYTES + C::LEAN_BYTES;
-  constexpr bool LEAN = C::LEAN;
-  float* s_red = reinterpret_cast<float*>(smem + C::SS_BYTES);    // LEAN: [WM][2][BN]
-  float* s_bias = s_red + WM * 2 * BN;                             // LEAN: [BN]
-  static_assert(!LEAN || !BNB, "LEAN tiles: no BN-backward epilogue");
+  constexpr bool LEAN = C::LEAN;                    // hp_lean addressing (TW == 16)
+  constexpr bool LSTAT = C::LEAN || BNB;           // bias + statistics / BN-backward partials in LDS
+  float* s_red = reinterpret_cast<float*>(smem + C::SS_BYTES);    // LSTAT: [WM][2][BN]
+  float* s_bias = s_red + WM * 2 * BN;                             // LSTAT: [BN]
+  static_assert(!LSTAT || C::LEAN_BYTES > 0, "LDS slots for the statistics");
   // double buffers addressed arithmetically (a runtime-indexed pointer array would spill)
   auto sA = [&](int b) { return base + b * C::A_BYTES; };
   auto sB = [&](int b) { return base + 2 * C::A_BYTES + b * C::B_BYTES; };
@@ -133,39 +135,30 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     it.co0 = ntile * BN;
     return it;
   };
-  // ---- per-lane DMA geometry, computed once (no integer division in the stage loop)
-  // A: element e = (i*4 + wave)*64 + lane of a halo buffer -> halo pixel (hd, hh, hw) and
-  //    the swizzled 8-channel sub-chunk it holds
-  int a_dw[C::A_ITERS], a_dh[C::A_ITERS], a_dd[C::A_ITERS], a_sub8[C::A_ITERS];
+  // ---- per-lane DMA geometry.  Element e = (i*NW + wave)*64 + lane of a halo / weight
+  // buffer holds row e >> 2 = (i*NW + wave)*16 + (lane >> 2), so the swizzled 8-channel
+  // sub-chunk ((e & 3) ^ swz(row)) * 8 is the same for every i (swz depends on bit 2 of the
+  // row = bit 4 of the lane): one register, and the halo position of piece i is recomputed
+  // once per item (set_item_pixels) instead of held in 3 x A_ITERS registers (VGPR budget of
+  // two waves per SIMD: the held geometry made the BM-512 / BN-backward variants spill to
+  // scratch, and every scratch reload waits vmcnt(0) on the in-flight operand DMA)
+  const int sub8 = ((lane & 3) ^ (((lane >> 4) & 1) << 1)) << 3;
   int a_pix[C::A_ITERS];       // in-image pixel of the item last issued, -1 = zero padding
 #pragma unroll
-  for (int i = 0; i < C::A_ITERS; ++i) {
-    const int e = (i * C::NW + wave) * 64 + lane;
-    const int px = e >> 2;
-    a_sub8[i] = ((e & 3) ^ swz(px)) << 3;
-    const int hw = px % HW2, hh = (px / HW2) % HH2;
-    const int hd = DIMS == 3 ? px / (HW2 * HH2) : 1;
-    a_dw[i] = px < halo ? hw - 1 : -(1 << 20);       // outside the halo: always padding
-    a_dh[i] = hh - 1;
-    a_dd[i] = hd - 1;
-    a_pix[i] = -1;
-  }
+  for (int i = 0; i < C::A_ITERS; ++i) a_pix[i] = -1;
   // B: row (tap-in-group, channel) -> byte offset without the (chunk, group) term
   // every item of a block has the same n tile (launcher: grid % (KS * nTilesN) == 0)
   const int co0_blk = (int)blockIdx.x / KS % p.nTilesN * BN;
   // BNB (a data gradient: no prologue, so the prologue constants' LDS holds the BN-backward
   // table [4][BN]; published by the first stage barrier)
   if constexpr (BNB) bnb_fill(s_scale, BN, co0_blk, p.Cout, p.bnb_s4, tid, C::NTH);
-  int b_off[C::B_ITERS], b_sub8[C::B_ITERS];
+  int b_off[C::B_ITERS];
 #pragma unroll
   for (int i = 0; i < C::B_ITERS; ++i) {
-    const int e = (i * C::NW + wave) * 64 + lane;
-    const int row = e >> 2;
-    const int sub = (e & 3) ^ swz(row);
+    const int row = ((i * C::NW + wave) * 64 + lane) >> 2;
     const int tl = row / BN, col = row % BN;
     const int co = co0_blk + col;
-    b_sub8[i] = sub * 8;
-    b_off[i] = (tl < 3 && co < p.Cout) ? ((co * p.taps + tl) * p.CinW + sub * 8) * 2 : -1;
+    b_off[i] = (tl < 3 && co < p.Cout) ? ((co * p.taps + tl) * p.CinW + sub8) * 2 : -1;
   }
   int a_item = -1;                 // item whose pixels a_pix currently holds
   int a_nimg = 0;
@@ -175,8 +168,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     a_nimg = it.n_img;
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
-      const int gw = it.w0 + a_dw[i], gh = it.h0 + a_dh[i], gd = it.d0 + a_dd[i];
-      const bool ok = gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && gd >= 0 && gd < p.D;
+      const int px = (i * C::NW + wave) * 16 + (lane >> 2);
+      const int hw = px % HW2, hh = (px / HW2) % HH2;
+      const int hd = DIMS == 3 ? px / (HW2 * HH2) : 1;
+      const int gw = it.w0 + hw - 1, gh = it.h0 + hh - 1, gd = it.d0 + hd - 1;
+      const bool ok = px < halo && gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && gd >= 0 && gd < p.D;
       a_pix[i] = ok ? (gd * p.H + gh) * p.W + gw : -1;
     }
   };
@@ -191,7 +187,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     const auto r = make_rsrc(src + a_nimg * img_px * Cs, (unsigned)(img_px * Cs * 2));
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
-      const int c8 = c0 + a_sub8[i];
+      const int c8 = c0 + sub8;
       unsigned off = (a_pix[i] >= 0 && c8 < Cs) ? (unsigned)(a_pix[i] * Cs + c8) * 2u : kOOB;
       dma16(r, sA(buf) + (i * C::NW + wave) * 1024, off);
     }
@@ -201,7 +197,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     const int soff = (grp * 3 * p.CinW + chunk * BK) * 2;
 #pragma unroll
     for (int i = 0; i < C::B_ITERS; ++i) {
-      const bool ok = b_off[i] >= 0 && chunk * BK + b_sub8[i] < p.CinW;
+      const bool ok = b_off[i] >= 0 && chunk * BK + sub8 < p.CinW;
       dma16(rW, sB(buf) + (i * C::NW + wave) * 1024, ok ? (unsigned)(b_off[i] + soff) : kOOB);
     }
   };
@@ -217,7 +213,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
       const int e = (i * C::NW + wave) * 64 + lane;    // same element this lane DMA'd
-      const int c8 = cbase + a_sub8[i];
+      const int c8 = cbase + sub8;
       if (c8 < climit && a_pix[i] >= 0) {
         uint4* q = reinterpret_cast<uint4*>(Abuf + e * 16);
         float f[8];
@@ -254,12 +250,12 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   // BN statistics accumulate in registers across all items of this workgroup: every item
   // of a workgroup has the same n tile (grid % nTilesN == 0, enforced by the launcher)
-  float s1[NT][4], s2[NT][4];                        // (LEAN: unused)
+  float s1[NT][4], s2[NT][4];                        // (LSTAT: unused)
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int i = 0; i < 4; ++i) { s1[nt][i] = 0.f; s2[nt][i] = 0.f; }
-  if constexpr (LEAN) {
+  if constexpr (LSTAT) {
     // published to every wave by the first stage barrier
     for (int i = tid; i < WM * 2 * BN; i += C::NTH) s_red[i] = 0.f;
     for (int i = tid; i < BN; i += C::NTH) {
@@ -270,13 +266,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 
   // bias of this block's channel tile, loaded once (a global load inside the epilogue would
   // make the compiler wait vmcnt(0) — on in-flight stores and DMA — before every use)
-  float bias_r[NT][4];                               // (LEAN: unused, bias in LDS)
+  float bias_r[NT][4];                               // (LSTAT: unused, bias in LDS)
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int co = co0_blk + wn * (NT * 16) + nt * 16 + 4 * g + i;
-      bias_r[nt][i] = (!LEAN && p.bias != nullptr && co < p.Cout) ? p.bias[co] : 0.0f;
+      bias_r[nt][i] = (!LSTAT && p.bias != nullptr && co < p.Cout) ? p.bias[co] : 0.0f;
     }
 
   // ---- epilogue of item k straight from the accumulators:
@@ -329,7 +325,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       // LEAN: this tile's bias from LDS, statistics of its 4 channels summed over the mt
       // tiles here, then over the 16 pixel lanes into the wave's LDS slot below
       float bl[4] = {0.f, 0.f, 0.f, 0.f}, t1[4] = {0.f, 0.f, 0.f, 0.f}, t2[4] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (LEAN) {
+      if constexpr (LSTAT) {
         const float4 b4 = *reinterpret_cast<const float4*>(s_bias + opaque_zero() + wn * (NT * 16) + nt * 16 + 4 * g);
         bl[0] = b4.x; bl[1] = b4.y; bl[2] = b4.z; bl[3] = b4.w;
       }
@@ -353,7 +349,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         }
         float v[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + (LEAN ? bl[i] : bias_r[nt][i]);
+        for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + (LSTAT ? bl[i] : bias_r[nt][i]);
         const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         pkv[mt][nt] = pk;
         if (!pairs) {
@@ -364,11 +360,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
           __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk.x, pk.y}, in1 ? r1 : r2, off, 0, 0);
         }
         if constexpr (BNB) {
-          bnb_accum(pk, ybuf[mt][nt], ok, kb, s1[nt], s2[nt]);
+          bnb_accum(pk, ybuf[mt][nt], ok, kb, t1, t2);
         } else if (ok) {
           // statistics of the stored (bf16-rounded) values
           const float r0 = lo_bf(pk.x), q1 = hi_bf(pk.x), q2 = lo_bf(pk.y), q3 = hi_bf(pk.y);
-          if constexpr (LEAN) {
+          if constexpr (LSTAT) {
             t1[0] += r0; t2[0] += r0 * r0;
             t1[1] += q1; t2[1] += q1 * q1;
             t1[2] += q2; t2[2] += q2 * q2;
@@ -382,13 +378,12 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         }
         acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       }
-      if constexpr (LEAN) {
+      if constexpr (LSTAT) {
         if (p.stats != nullptr && KS == 1) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             float a1 = t1[i], a2 = t2[i];
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) { a1 += __shfl_xor(a1, o, 64); a2 += __shfl_xor(a2, o, 64); }
+            a1 = row16_sum(a1); a2 = row16_sum(a2);
             if ((lane & 15) == 0) {
               const int col = wn * (NT * 16) + nt * 16 + 4 * g + i;
               s_red[(2 * wm) * BN + col] += a1;       // one owner lane per (wave, column)
@@ -425,7 +420,57 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   // ---- compute one stage: the 3 taps of kernel row (kd, r).  The operand pointers are
   // restrict-qualified so the LDS reads carry alias scopes and the compiler does not make
   // them wait (vmcnt) for the NEXT stage's in-flight LDS-DMA; vmcnt is managed by hand.
+  //
+  // FDB == 2: ROLLING fragment pipeline.  Step s = (tap tt, pixel tile mt) runs the NT MFMAs
+  // of pixel fragment s against the tap's NT weight fragments; pixel fragments rotate through
+  // XD register sets, each read XD-1 steps (>= 96 MFMA cycles) before its use, and a tap's
+  // weight fragments are read one tap ahead.  Live fragment registers: 4 (XD + 2 NT) instead
+  // of the whole-tap double buffer's 8 (MT + NT) — 64 fewer with the BM-512 tiles (MT = 8),
+  // which otherwise spill to scratch (a scratch reload waits vmcnt(0), i.e. on the operand
+  // DMA in flight for the next stage)
+  constexpr int XD = 1 + 12 / NT;
+  auto pipe_taps = [&](auto TTc, const char* __restrict__ A0, const char* __restrict__ B0, int off0,
+                       const char* __restrict__ A1, const char* __restrict__ B1, int off1, auto&& hook)
+      __attribute__((always_inline)) {
+    constexpr int TT = decltype(TTc)::value;
+    constexpr int NS = TT * MT;
+    auto xload = [&](int s) __attribute__((always_inline)) {
+      const int tt = s / MT, mt = s % MT;
+      const char* A = tt < 3 ? A0 : A1;
+      const int row = (LEAN ? hp_lean + mt * HW2 : hp0[LEAN ? 0 : mt]) + (tt < 3 ? off0 : off1) + tt % 3;
+      return lds128(A + lds_off(row, g));
+    };
+    auto wload = [&](int tt, uint4 (&wf)[NT]) __attribute__((always_inline)) {
+      const char* B = tt < 3 ? B0 : B1;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        wf[nt] = lds128(B + lds_off((tt % 3) * BN + wn * (NT * 16) + nt * 16 + (lane & 15), g));
+    };
+    uint4 xf[XD], wf[2][NT];
+    wload(0, wf[0]);
+#pragma unroll
+    for (int s = 0; s < XD - 1; ++s)
+      if (s < NS) xf[s] = xload(s);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int tt = s / MT, mt = s % MT;
+      if (s + XD - 1 < NS) xf[(s + XD - 1) % XD] = xload(s + XD - 1);
+      if (mt == 0 && tt + 1 < TT) wload(tt + 1, wf[(tt + 1) & 1]);
+      if (mt == 0 && (p.prio & 2)) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[tt & 1][nt], xf[s % XD], acc[mt][nt]);
+      if (mt == MT - 1) {
+        if (p.prio & 2) __builtin_amdgcn_s_setprio(0);
+        hook(tt);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   auto compute = [&](const char* __restrict__ A, const char* __restrict__ B, int kd, int r) __attribute__((always_inline)) {
+    if constexpr (FDB == 2) {
+      pipe_taps(std::integral_constant<int, 3>{}, A, B, (kd * HH2 + r) * HW2, A, B, 0, [](int) {});
+      return;
+    }
     // register double buffer: the fragments of tap t+1 are read while the MFMAs of tap t
     // run (the sched barrier keeps the compiler from sinking the reads next to their use,
     // which exposed the LDS latency between every 4 MFMAs: ~31% MFMA busy)
@@ -458,6 +503,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   auto compute2 = [&](const char* __restrict__ A0, const char* __restrict__ B0, int r0,
                       const char* __restrict__ A1, const char* __restrict__ B1, int r1, auto&& hook)
       __attribute__((always_inline)) {
+    if constexpr (FDB == 2) {
+      pipe_taps(std::integral_constant<int, 6>{}, A0, B0, r0 * HW2, A1, B1, r1 * HW2, hook);
+      return;
+    }
     auto load_frags = [&](int tt, uint4 (&xf)[MT], uint4 (&wf)[NT]) __attribute__((always_inline)) {
       const int t = tt % 3;
       const char* A = tt < 3 ? A0 : A1;
@@ -643,7 +692,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
             if (q * 6 / (2 * C::B_ITERS) != tt) continue;
             const int h = q / C::B_ITERS, i = q % C::B_ITERS;
             if (hB[h]) {
-              const bool ok = b_off[i] >= 0 && chB[h] * BK + b_sub8[i] < p.CinW;
+              const bool ok = b_off[i] >= 0 && chB[h] * BK + sub8 < p.CinW;
               dma16(rW, sB(2 * ((j + 1) & 1) + h) + (i * C::NW + wave) * 1024,
                     ok ? (unsigned)(b_off[i] + sB_off[h]) : kOOB);
             }
@@ -652,7 +701,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
           for (int i = 0; i < C::A_ITERS; ++i) {
             if (i * 6 / C::A_ITERS != tt) continue;
             if (doA) {
-              const int c8 = c0A + a_sub8[i];
+              const int c8 = c0A + sub8;
               const unsigned off = (a_pix[i] >= 0 && c8 < CsA) ? (unsigned)(a_pix[i] * CsA + c8) * 2u : kOOB;
               dma16(rA, sA(cA & 1) + (i * C::NW + wave) * 1024, off);
             }
@@ -676,15 +725,14 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   if (p.stats != nullptr && KS == 1) {
     dma_wait<0>();
     lds_sync();
-    float* red = LEAN ? s_red : reinterpret_cast<float*>(base);   // halo buffers are free now
+    float* red = LSTAT ? s_red : reinterpret_cast<float*>(base);   // halo buffers are free now
     const int co0 = my_items > 0 ? item_of(0).co0 : 0;
 #pragma unroll
-    for (int nt = 0; nt < (LEAN ? 0 : NT); ++nt)
+    for (int nt = 0; nt < (LSTAT ? 0 : NT); ++nt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float a1 = s1[nt][i], a2 = s2[nt][i];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) { a1 += __shfl_xor(a1, o, 64); a2 += __shfl_xor(a2, o, 64); }
+        a1 = row16_sum(a1); a2 = row16_sum(a2);
         if ((lane & 15) == 0) {
           const int col = wn * (NT * 16) + nt * 16 + 4 * (lane >> 4) + i;
           red[(2 * wm) * BN + col] = a1;           // one writer per (wave row, column)
@@ -791,6 +839,27 @@ bool conv_ilv() {
   return v != 0;
 }
 
+// rolling fragment pipeline (FDB mode 2, pipe_taps) instead of the whole-tap register double
+// buffer / none (DDLPC_CONV_PIPE=0 for A/B)
+bool conv_pipe() {
+  const int v = knob("CONV_PIPE", 1);
+  return v != 0;
+}
+
+template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, int FDB>
+void launch_mode(ConvFwdArgs& a, int grid, hipStream_t st) {
+  using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
+  if constexpr (DIMS == 2 && NBB != 3 && !C::LEAN) {
+    if (a.bnb_y != nullptr) {
+      hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB, true, false>), dim3(grid),
+                         dim3(C::NTH), C::SMEM, st, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB, false, false>), dim3(grid),
+                     dim3(C::NTH), C::SMEM, st, a);
+}
+
 template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB = 2>
 void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
@@ -804,7 +873,7 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   const int diag = knob("DIAG_CONV", 0);
   a.diag = diag;
   a.prio = knob("CONV_PRIO", 2);
-  constexpr bool FDB_OK = !(DIMS == 3 && MT * NT >= 16);
+  constexpr int FDB_OK = !(DIMS == 3 && MT * NT >= 16) ? 1 : 0;
   if constexpr (NBB == 4) {
     if (conv_ilv()) {
       if (a.bnb_y != nullptr)
@@ -816,23 +885,14 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
       return;
     }
   }
-  if constexpr (DIMS == 2 && NBB != 3 && !C::LEAN) {
-    if (a.bnb_y != nullptr) {
-      hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK, true, false>), dim3(grid),
-                         dim3(C::NTH), C::SMEM, st, a);
-      return;
-    }
-  }
-  if (FDB_OK && conv_fdb())
-    hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK, false, false>), dim3(grid),
-                       dim3(C::NTH), C::SMEM, st, a);
-  else
-    hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, false, false, false>), dim3(grid),
-                       dim3(C::NTH), C::SMEM, st, a);
+  if (conv_pipe()) launch_mode<DIMS, WM, WN, MT, NT, HALO, NBB, 2>(a, grid, st);
+  else if (FDB_OK && conv_fdb()) launch_mode<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK>(a, grid, st);
+  else launch_mode<DIMS, WM, WN, MT, NT, HALO, NBB, 0>(a, grid, st);
 }
 
-// cfg 5 without fragment double buffering (never with the BN-backward epilogue: LEAN tiles)
-void launch_cfg5_nofdb(ConvFwdArgs& a, hipStream_t st) {
+// cfg 5 (BM-512, LEAN tiles: never with the BN-backward epilogue): the rolling pipeline, or
+// no fragment double buffering (the whole-tap double buffer does not fit the VGPR budget)
+void launch_cfg5(ConvFwdArgs& a, hipStream_t st) {
   using C = Cfg<2, 4, 2, 8, 4, 640, 2>;
   const int items = a.nTilesM * a.nTilesN * a.ksplit;
   int grid = items;
@@ -843,8 +903,12 @@ void launch_cfg5_nofdb(ConvFwdArgs& a, hipStream_t st) {
   a.stat_rows = grid;
   a.diag = 0;
   a.prio = knob("CONV_PRIO", 2);
-  hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 640, 2, false, false, false>), dim3(grid),
-                     dim3(C::NTH), C::SMEM, st, a);
+  if (conv_pipe())
+    hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 640, 2, 2, false, false>), dim3(grid),
+                       dim3(C::NTH), C::SMEM, st, a);
+  else
+    hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 640, 2, 0, false, false>), dim3(grid),
+                       dim3(C::NTH), C::SMEM, st, a);
 }
 
 // super-stages (two kernel rows per barrier) in the 8-wave configuration (DDLPC_CONV_SUPER=0: off)
@@ -910,8 +974,8 @@ void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st) {
         break;
       }
       case 5:
-        if (conv5_fdb()) launch_cfg<2, 4, 2, 8, 4, 640, 2>(a, st);
-        else launch_cfg5_nofdb(a, st);
+        if (conv5_fdb() && !conv_pipe()) launch_cfg<2, 4, 2, 8, 4, 640, 2>(a, st);
+        else launch_cfg5(a, st);
         break;
       default: launch_cfg<2, 1, 4, 4, 2, 128>(a, st); break;
     }

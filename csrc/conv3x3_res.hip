@@ -498,8 +498,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float a1 = s1[nt][i], a2 = s2[nt][i];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) { a1 += __shfl_xor(a1, o, 64); a2 += __shfl_xor(a2, o, 64); }
+        a1 = row16_sum(a1); a2 = row16_sum(a2);
         if ((lane & 15) == 0) {
           const int col = wn * (NT * 16) + nt * 16 + 4 * g + i;
           red[(2 * wm) * BN + col] = a1;           // one writer per (wave row, column)

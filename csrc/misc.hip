@@ -383,7 +383,7 @@ void weight_pack_launch(const PackEntry* entries_dev, int n_entries, long long m
 
 void codec_absmax_launch(const float* x, const int64_t* seg, int nseg, float* scales,
                          hipStream_t st) {
-  hipMemsetAsync(scales, 0, sizeof(float) * nseg, st);
+  (void)hipMemsetAsync(scales, 0, sizeof(float) * nseg, st);
   hipLaunchKernelGGL(codec_absmax_kernel, dim3(64, nseg), dim3(256), 0, st, x, seg, scales);
 }
 
@@ -415,7 +415,7 @@ void bilinear_up2_launch(const bf16_t* x, bf16_t* y, int dims, int N, int D, int
 void bilinear_up2_bwd_launch(const bf16_t* dy, float* dx_f32, bf16_t* dx, int dims, int N, int D,
                              int H, int W, int C, hipStream_t st) {
   const long long nin = (long long)N * D * H * W * C;
-  hipMemsetAsync(dx_f32, 0, sizeof(float) * nin, st);
+  (void)hipMemsetAsync(dx_f32, 0, sizeof(float) * nin, st);
   const long long total = (long long)N * (dims == 3 ? 2 * D : 1) * 2 * H * 2 * W * C;
   const int grid = (int)std::min<long long>((total + 255) / 256, 8192);
   if (dims == 2)

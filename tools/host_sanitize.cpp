@@ -16,6 +16,15 @@
 
 using namespace ddlpc;
 
+// the planners read tuning knobs; bindings.cpp (torch-linked) is not part of this harness,
+// so knobs resolve to their DDLPC_<NAME> environment value or the default here
+int ddlpc::knob(const char* name, int def) {
+  char env[128];
+  std::snprintf(env, sizeof(env), "DDLPC_%s", name);
+  const char* e = std::getenv(env);
+  return e ? std::atoi(e) : def;
+}
+
 static long long g_checks = 0;
 #define EXPECT(c, ...)                                                              \
   do {                                                                              \
