@@ -286,7 +286,7 @@ DDLPC_DEVICE int wg2_yswz(int row) {             // XOR on the 16-B piece index
 }
 
 template <int BCO, int PT>
-__global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
+__global__ __launch_bounds__(256, PT <= 96 ? 3 : 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
   using namespace convlds;
   using Cfg = Wg2Cfg<BCO, PT>;
   constexpr int TH = Cfg::TH, HW2 = 18;
@@ -371,6 +371,8 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad2_kernel(ConvWgradArgs p) {
   const int cs0 = second ? c8l - p.C1 : c8l;
   const bf16_t* xsrc = second ? p.X2 : p.X1;
   const bool xch_ok = cs0 < Cs;
+  // (prologue constants stay in LDS here: 16 more live VGPRs would cost the 96-pixel-tile
+  // variant its third workgroup per CU — measured 55% slower on dec3.a / dec2.a)
 
   auto issue = [&](int tile, int buf) {
     int t = tile;
@@ -563,8 +565,6 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
   constexpr int KS16 = PT / 16;                    // 16-pixel k-steps per tile
   static_assert(KS16 % KW == 0, "k-steps must split evenly over the waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* s_scale = reinterpret_cast<float*>(smem);
-  float* s_shift = s_scale + 512;
   char* base = smem + Cfg::SS_BYTES;
   auto sY = [&](int b) { return base + b * (Cfg::Y_BYTES + Cfg::X_BYTES); };
   auto sX = [&](int b) { return base + b * (Cfg::Y_BYTES + Cfg::X_BYTES) + Cfg::Y_BYTES; };
@@ -582,10 +582,6 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
 
   const bool has_pro = p.pscale != nullptr;
   const bool has_pro2 = p.pscale2 != nullptr;           // deferred skip: X2 channels at C1 + c
-  if (has_pro)
-    for (int c = tid; c < p.C1; c += 256) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
-  if (has_pro2)
-    for (int c = tid; c < p.C2; c += 256) { s_scale[p.C1 + c] = p.pscale2[c]; s_shift[p.C1 + c] = p.pshift2[c]; }
   const int t_begin = (int)((long long)p.nTiles * split / p.splits);
   const int t_end = (int)((long long)p.nTiles * (split + 1) / p.splits);
   const long long img_px = (long long)p.H * p.W;
@@ -617,6 +613,9 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
   const int cs0 = second ? c8l - p.C1 : c8l;
   const bf16_t* xsrc = second ? p.X2 : p.X1;
   const bool xch_ok = cs0 < Cs;
+  float psc[8] = {}, psh[8] = {};                    // this lane's prologue constants
+  if (second ? has_pro2 : has_pro)
+    pro8_load(p.pscale, p.pshift, p.pscale2, p.pshift2, p.C1, c8l, second ? p.Cin : p.C1, psc, psh);
 
   auto issue = [&](int tile, int buf) __attribute__((always_inline)) {
     int t = tile;
@@ -672,10 +671,7 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
         float f[8];
         unpack8(*q, f);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int c = min(c8l + j, (second ? p.Cin : p.C1) - 1);
-          f[j] = fmaxf(fmaf(f[j], s_scale[c], s_shift[c]), 0.0f);
-        }
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], psc[j], psh[j]), 0.0f);
         *q = pack8(f);
       }
     }

@@ -76,6 +76,22 @@ DDLPC_DEVICE uint4 pair16(uint2 lo, uint2 hi) {
 }
 DDLPC_DEVICE int pair16_ch(int lane) { return ((lane >> 4) & 1) * 16 + (lane >> 5) * 8; }
 
+// prologue constants (BN scale, shift) of the 8 consecutive input channels c8 .. c8 + 7
+// (clamped to lim - 1) straight from global memory into registers: channels >= C1 belong to
+// the second input tensor (psc2 / psh2).  For kernels whose lanes keep one channel group for
+// the whole launch, so the in-LDS transform needs no per-piece LDS table reads
+DDLPC_DEVICE void pro8_load(const float* psc, const float* psh, const float* psc2, const float* psh2,
+                            int C1, int c8, int lim, float (&sc)[8], float (&sh)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = min(c8 + j, lim - 1);
+    sc[j] = c < C1 ? psc[c] : psc2[c - C1];
+    sh[j] = c < C1 ? psh[c] : psh2[c - C1];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(sc[j]), "v"(sh[j]));   // consumed here: before any DMA
+}
+
 // ---- BN-backward epilogue (ConvFwdArgs::bnb_y): LDS table [4][nb] of (scale, shift,
 // invstd, -mean*invstd) for the channels [co0, co0 + nb) of a workgroup's n tile
 DDLPC_DEVICE void bnb_fill(float* tab, int nb, int co0, int Cout, const float* s4, int tid, int nth) {
