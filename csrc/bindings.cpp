@@ -331,7 +331,7 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
                        const c10::optional<at::Tensor>& pshift2,
                        const c10::optional<at::Tensor>& dy_y,
                        const c10::optional<at::Tensor>& dy_s4,
-                       const c10::optional<at::Tensor>& dy_coefs) {
+                       const c10::optional<at::Tensor>& dy_coefs, int64_t cin_real) {
   CHECK_DEV(dy); CHECK_CONTIG(dy); CHECK_BF16(dy); CHECK_CONTIG(x1); CHECK_BF16(x1);
   c10::DeviceGuard guard(dy.device());
   const Geo g = geo_of(x1);
@@ -384,7 +384,12 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   }
   // (DDLPC_WGRAD3_RING=1: 32-output-channel layers on 128-pixel tiles with a 3-deep DMA ring)
   const int v3_ring = knob("WGRAD3_RING", 0);
-  if (v3) { a.TD = 1; a.TW = 16; a.TH = bco == 32 ? (v3_ring ? 8 : 16) : (v3_pt64 == 96 && a.C2 > 0 ? 6 : 8); }
+  // the image layer: <= 4 real channels (cin_real, from the caller) of an 8-channel padded
+  // input, (tap, channel)-packed kernel (DDLPC_WGRAD_IMG=0: the v2 path)
+  const bool img = cin_real > 0 && cin_real <= 4 && a.C1 == 8 && !dual && g.dims == 2 && g.W >= 16 &&
+                   a.pscale == nullptr && a.pscale2 == nullptr && knob("WGRAD_IMG", 1) != 0;
+  if (img) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad_img_pt(bco) / 16; }
+  else if (v3) { a.TD = 1; a.TW = 16; a.TH = bco == 32 ? (v3_ring ? 8 : 16) : (v3_pt64 == 96 && a.C2 > 0 ? 6 : 8); }
   else if (v2) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad2_pt(bco, a.C2, g.H, g.W) / 16; }
   else if (g.dims == 2) { a.TD = 1; a.TW = g.W >= 16 ? 16 : 8; a.TH = 128 / a.TW; }
   else { a.TW = g.W >= 16 ? 16 : 8; a.TH = 4; a.TD = 128 / (a.TW * a.TH); }
@@ -412,7 +417,8 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   a.partial = part.data_ptr<float>();
   TORCH_CHECK(a.pscale2 == nullptr || v2, "X2 prologue needs the v2/v3 weight-gradient kernels "
               "(2-D or 3-D, W >= 16, C1 % 32 == 0)");
-  if (v3) conv3_wgrad3_launch(a, bco, cur_stream());
+  if (img) conv3_wgrad_img_launch(a, bco, cur_stream());
+  else if (v3) conv3_wgrad3_launch(a, bco, cur_stream());
   else if (v2) conv3_wgrad2_launch(a, bco, cur_stream());
   else conv3_wgrad_launch(a, bco, cur_stream());
   std::vector<int64_t> wshape = {a.Cout, a.Cin, 3, 3};
@@ -1270,7 +1276,7 @@ TORCH_LIBRARY(ddlpc, m) {
         "Tensor? bnb_s4=None) -> Tensor[]");
   m.def("conv3_wgrad(Tensor dy, Tensor x1, Tensor? x2, Tensor? pscale, Tensor? pshift, Tensor(a!)? out=None, "
         "Tensor? pscale2=None, Tensor? pshift2=None, Tensor? dy_y=None, Tensor? dy_s4=None, "
-        "Tensor? dy_coefs=None) -> Tensor");
+        "Tensor? dy_coefs=None, int cin_real=0) -> Tensor");
   m.def("bn_finalize(Tensor partial, float count, Tensor gamma, Tensor beta, Tensor(a!) running_mean, "
         "Tensor(b!) running_var, float momentum, float eps, bool update_running, Tensor(c!)? nbt) -> Tensor");
   m.def("bn_relu_apply(Tensor y, Tensor stats4, bool pool, bool full=True) -> Tensor[]");

@@ -780,6 +780,244 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
   }
 }
 
+// ============================================================================ image layer
+// The first conv's weight gradient (2-D, one 8-channel padded image of which at most 4
+// channels are real: ref.py:588's Conv2d(3, 32)).  v2 runs it as 9 taps x a 16-channel half
+// chunk (9 x 2 MFMA per 32-pixel k-step, 13 of every 16 columns zero).  Here the GEMM's N
+// packs (tap, channel) as n = 4 tap + c (c < 4): three 16-wide MFMA tiles (taps 0-3, 4-7,
+// 8; columns of taps 9-11 are computed from tap 8's pixels and discarded), a third of the
+// MFMA work.  Each lane of a transposed B read supplies its own row address, so a tap's 4
+// channels (8 bytes) are gathered straight from the 16-B-per-pixel halo rows — no im2col.
+// dY arrives and is optionally BN-backward-transformed exactly as in v2 (same layout, same
+// swizzle); the waves split the k-steps and their partials are summed in LDS in a fixed
+// order; the slab keeps the [co][tap][ci] contract with ci >= 4 written as zeros.
+template <int BCO, int PT>
+struct WgImgCfg {
+  using Y = Wg2Cfg<BCO, PT>;                       // dY staging exactly as v2
+  static constexpr int TH = PT / 16;
+  static constexpr int HALO = (TH + 2) * 18;       // one 16-B piece (8 channels) per pixel
+  static constexpr int X_INSTR = (HALO + 63) / 64;
+  static constexpr int X_ITERS = (X_INSTR + 3) / 4;
+  static constexpr int X_BYTES = X_INSTR * 1024;
+  static constexpr int STAGE = Y::Y_BYTES + X_BYTES;
+  static constexpr int RED_BYTES = 3 * (BCO / 16) * 3 * 4 * 64 * 4;   // k-split partials of waves 1-3
+  static constexpr int SMEM = Y::SS_BYTES + (2 * STAGE > RED_BYTES ? 2 * STAGE : RED_BYTES);
+  static constexpr int KSTEPS = PT / 32;
+};
+
+template <int BCO, int PT>
+__global__ __launch_bounds__(256, 2) void conv3_wgrad_img_kernel(ConvWgradArgs p) {
+  using namespace convlds;
+  using Cfg = WgImgCfg<BCO, PT>;
+  using YC = typename Cfg::Y;
+  constexpr int NCO = BCO / 16, HW2 = 18;
+  static_assert(Cfg::KSTEPS % 4 == 0, "k-steps split evenly over the 4 waves");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* s_dy = reinterpret_cast<float*>(smem) + 1024;   // dY-prologue table (v2's offset)
+  char* base = smem + YC::SS_BYTES;
+  auto sY = [&](int b) { return base + b * Cfg::STAGE; };
+  auto sX = [&](int b) { return base + b * Cfg::STAGE + YC::Y_BYTES; };
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int cot = b % p.coTiles; b /= p.coTiles;
+  const int split = b;
+  const int co0 = cot * BCO;
+
+  const bool has_dyp = p.dyy != nullptr;
+  if (has_dyp)
+    for (int i = tid; i < BCO; i += 256) {
+      const int c = co0 + i;
+      const bool ok = c < p.Cout;
+      const float is = ok ? p.dys4[p.Cout + c] : 0.f;
+      s_dy[i] = ok ? p.dys4[2 * p.Cout + c] : 0.f;
+      s_dy[BCO + i] = ok ? p.dys4[3 * p.Cout + c] : 0.f;
+      s_dy[2 * BCO + i] = is;
+      s_dy[3 * BCO + i] = ok ? -p.dys4[c] * is : 0.f;
+      s_dy[4 * BCO + i] = ok ? p.dycoef[c] : 0.f;
+      s_dy[5 * BCO + i] = ok ? p.dycoef[p.Cout + c] : 0.f;
+      s_dy[6 * BCO + i] = ok ? p.dycoef[2 * p.Cout + c] : 0.f;
+    }
+  const int t_begin = (int)((long long)p.nTiles * split / p.splits);
+  const int t_end = (int)((long long)p.nTiles * (split + 1) / p.splits);
+  const long long img_px = (long long)p.H * p.W;
+
+  // ---- tile-independent per-lane DMA geometry
+  int y_pw[YC::Y_ITERS], y_ph[YC::Y_ITERS], y_rel[YC::Y_ITERS];
+  uint4 yv[YC::Y_ITERS];
+  bool y_ok[YC::Y_ITERS];
+#pragma unroll
+  for (int i = 0; i < YC::Y_ITERS; ++i) {
+    const int e = (i * 4 + wave) * 64 + lane;
+    const int row = e / (BCO / 8), pc = e % (BCO / 8);
+    const int sp = pc ^ wg2_yswz<BCO>(row);
+    y_pw[i] = row % 16;
+    y_ph[i] = row / 16;
+    const int co = co0 + sp * 8;
+    y_rel[i] = co < p.Cout ? (y_ph[i] * p.W + y_pw[i]) * p.Cout + co : -1;
+    y_ok[i] = false;
+  }
+  auto issue = [&](int tile, int buf) {
+    int t = tile;
+    const int tw_i = t % p.tilesW; t /= p.tilesW;
+    const int th_i = t % p.tilesH; t /= p.tilesH;
+    const int n = t;
+    const int h0 = th_i * Cfg::TH, w0 = tw_i * 16;
+    const auto ry = make_rsrc(p.dY + n * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
+    const int ybase = (h0 * p.W + w0) * p.Cout;
+#pragma unroll
+    for (int i = 0; i < YC::Y_ITERS; ++i) {
+      if ((i * 4 + wave) >= YC::Y_INSTR) break;
+      const bool ok = y_rel[i] >= 0 && w0 + y_pw[i] < p.W && h0 + y_ph[i] < p.H;
+      dma16(ry, sY(buf) + (i * 4 + wave) * 1024, ok ? (unsigned)(ybase + y_rel[i]) * 2u : kOOB);
+      if (has_dyp) {
+        const auto ryy = make_rsrc(p.dyy + n * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
+        const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(ryy, ok ? (unsigned)(ybase + y_rel[i]) * 2u : kOOB, 0, 0);
+        yv[i] = make_uint4(v.x, v.y, v.z, v.w);
+        y_ok[i] = ok;
+      }
+    }
+    const auto rx = make_rsrc(p.X1 + n * img_px * p.C1, (unsigned)(img_px * p.C1 * 2));
+#pragma unroll
+    for (int i = 0; i < Cfg::X_ITERS; ++i) {
+      if ((i * 4 + wave) >= Cfg::X_INSTR) break;
+      const int px = (i * 4 + wave) * 64 + lane;          // halo pixel (one piece each)
+      const int gw = w0 + px % HW2 - 1, gh = h0 + px / HW2 - 1;
+      const bool ok = px < Cfg::HALO && gw >= 0 && gw < p.W && gh >= 0 && gh < p.H;
+      dma16(rx, sX(buf) + (i * 4 + wave) * 1024, ok ? (unsigned)(gh * p.W + gw) * (unsigned)(p.C1 * 2) : kOOB);
+    }
+  };
+  // dY = k (dA [y*scale + shift > 0] - m1 - xhat m2) on the lane's own landed pieces (v2's)
+  auto transform_dy = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < YC::Y_ITERS; ++i) {
+      if ((i * 4 + wave) < YC::Y_INSTR && y_ok[i]) {
+        const int e = (i * 4 + wave) * 64 + lane;
+        const int row = e / (BCO / 8), pc = e % (BCO / 8);
+        const int cl = (pc ^ wg2_yswz<BCO>(row)) * 8;
+        uint4* qd = reinterpret_cast<uint4*>(sY(buf) + e * 16);
+        float fd[8], fy[8], o[8];
+        unpack8(*qd, fd);
+        unpack8(yv[i], fy);
+        const float* t = s_dy + opaque_zero() + cl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float a = fmaf(fy[j], t[j], t[BCO + j]);
+          const float dyh = a > 0.f ? fd[j] : 0.f;
+          const float xh = fmaf(fy[j], t[2 * BCO + j], t[3 * BCO + j]);
+          o[j] = t[4 * BCO + j] * (dyh - t[5 * BCO + j] - xh * t[6 * BCO + j]);
+        }
+        *qd = pack8(o);
+      }
+    }
+  };
+
+  // ---- transposed-read geometry: 16-lane group g, row q within 4, column quad pp
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  int ya[2][NCO];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < NCO; ++j) {
+      const int row = 8 * g + 4 * h + q;
+      const int pc = 2 * j + (pp >> 1);
+      ya[h][j] = row * YC::Y_ROWB + ((pc ^ wg2_yswz<BCO>(row)) << 4) + (pp & 1) * 8;
+    }
+  // B: column quad pp of tile n = tap 4n + pp (taps past 8 re-read tap 8: discarded columns)
+  int toff[3];
+#pragma unroll
+  for (int n = 0; n < 3; ++n) {
+    const int tap = min(4 * n + pp, 8);
+    toff[n] = ((tap / 3) * HW2 + tap % 3) * 16;
+  }
+  constexpr int KW = Cfg::KSTEPS / 4;              // k-steps per wave per tile
+  int xb[KW][2];
+#pragma unroll
+  for (int kk = 0; kk < KW; ++kk)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int pix = (kk * 4 + wave) * 32 + 8 * g + 4 * h + q;
+      xb[kk][h] = ((pix / 16) * HW2 + pix % 16) * 16;
+    }
+
+  f32x4_t acc[NCO][3];
+#pragma unroll
+  for (int j = 0; j < NCO; ++j)
+#pragma unroll
+    for (int n = 0; n < 3; ++n) acc[j][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](const char* __restrict__ Y, const char* __restrict__ X) {
+#pragma unroll
+    for (int kk = 0; kk < KW; ++kk) {
+      const int ks = kk * 4 + wave;
+      uint4 af[NCO];
+#pragma unroll
+      for (int j = 0; j < NCO; ++j) {
+        const uint2 lo = lds_read_tr16(Y + ks * 32 * YC::Y_ROWB + ya[0][j]);
+        const uint2 hi = lds_read_tr16(Y + ks * 32 * YC::Y_ROWB + ya[1][j]);
+        af[j] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+#pragma unroll
+      for (int n = 0; n < 3; ++n) {
+        const uint2 lo = lds_read_tr16(X + xb[kk][0] + toff[n]);
+        const uint2 hi = lds_read_tr16(X + xb[kk][1] + toff[n]);
+        const uint4 bfr = make_uint4(lo.x, lo.y, hi.x, hi.y);
+#pragma unroll
+        for (int j = 0; j < NCO; ++j) acc[j][n] = mfma16x16x32(af[j], bfr, acc[j][n]);
+      }
+    }
+  };
+
+  if (has_dyp) __syncthreads();                       // s_dy visible
+  if (t_begin < t_end) issue(t_begin, 0);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int buf = (tile - t_begin) & 1;
+    dma_wait<0>();
+    if (has_dyp) transform_dy(buf);
+    lds_sync();
+    if (tile + 1 < t_end) issue(tile + 1, buf ^ 1);
+    compute(sY(buf), sX(buf));
+  }
+
+  // ---- k-split reduction over the 4 waves (fixed order), then the partial slab
+  dma_wait<0>();
+  lds_sync();
+  float* red = reinterpret_cast<float*>(base);        // [3][NCO][3][4][64]
+  if (wave > 0) {
+#pragma unroll
+    for (int j = 0; j < NCO; ++j)
+#pragma unroll
+      for (int n = 0; n < 3; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[((((wave - 1) * NCO + j) * 3 + n) * 4 + i) * 64 + lane] = acc[j][n][i];
+  }
+  lds_sync();
+  float* out = p.partial + (long long)split * p.Cout * p.taps * p.Cin;
+  if (wave == 0) {
+#pragma unroll
+    for (int j = 0; j < NCO; ++j)
+#pragma unroll
+      for (int n = 0; n < 3; ++n) {
+        const int col = 16 * n + (lane & 15);           // n = 4 tap + c
+        const int tap = col >> 2, ci = col & 3;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = acc[j][n][i];
+#pragma unroll
+          for (int w2 = 1; w2 < 4; ++w2) v += red[((((w2 - 1) * NCO + j) * 3 + n) * 4 + i) * 64 + lane];
+          const int co = co0 + j * 16 + 4 * g + i;
+          if (tap < 9 && co < p.Cout && ci < p.Cin) out[((long long)co * p.taps + tap) * p.Cin + ci] = v;
+        }
+      }
+  }
+  // padding input channels (4 .. Cin-1: zero in the image, so their gradient is exactly 0)
+  for (int e = tid; e < BCO * 9 * (p.Cin - 4); e += 256) {
+    const int ci = 4 + e % (p.Cin - 4), tap = (e / (p.Cin - 4)) % 9, co = co0 + e / ((p.Cin - 4) * 9);
+    if (co < p.Cout) out[((long long)co * p.taps + tap) * p.Cin + ci] = 0.f;
+  }
+}
+
 template <int DIMS, int BCO>
 void launch_wg(ConvWgradArgs& a, hipStream_t st) {
   using Cfg = WgCfg<DIMS, BCO>;
@@ -831,6 +1069,15 @@ void conv3_wgrad3_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
   else
     hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 128>), dim3(grid), dim3(256), (Wg2Cfg<64, 128>::SMEM), st, a);
 }
+
+void conv3_wgrad_img_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
+  const int grid = a.coTiles * a.splits;
+  if (bco == 32)
+    hipLaunchKernelGGL((conv3_wgrad_img_kernel<32, 256>), dim3(grid), dim3(256), (WgImgCfg<32, 256>::SMEM), st, a);
+  else
+    hipLaunchKernelGGL((conv3_wgrad_img_kernel<64, 128>), dim3(grid), dim3(256), (WgImgCfg<64, 128>::SMEM), st, a);
+}
+int conv3_wgrad_img_pt(int bco) { return bco == 32 ? 256 : 128; }
 
 void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
   if (a.dims == 2) {

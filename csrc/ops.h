@@ -90,6 +90,11 @@ void conv3_wgrad2_launch(ConvWgradArgs& a, int bco, hipStream_t st);
 int conv3_wgrad2_pt(int bco, int C2, int H, int W);
 // 32x32x16-MFMA variant (conflict-free transposed reads; Cin % 32 == 0, pixel tiles of 128 / 256)
 void conv3_wgrad3_launch(ConvWgradArgs& a, int bco, hipStream_t st);
+// image layer (2-D, X1 = the 8-channel padded image with <= 4 real channels, no X2 / prologue;
+// optional dY prologue): (tap, channel)-packed N, pixel tiles of conv3_wgrad_img_pt(bco);
+// grid = coTiles x splits
+void conv3_wgrad_img_launch(ConvWgradArgs& a, int bco, hipStream_t st);
+int conv3_wgrad_img_pt(int bco);
 
 int conv3_wgrad_halo_cap(int dims);
 

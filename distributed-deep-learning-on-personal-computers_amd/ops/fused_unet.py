@@ -263,26 +263,29 @@ class _DoubleConvFn(torch.autograd.Function):
             coefs, _, _ = F.bn_grad_coefs(part1, y1, s1, g1, bn1.weight.grad, bn1.bias.grad)
             with eng.wgrad_stream(da1, y1, x1, coefs, s1):
                 w1.grad.add_(F.conv3_wgrad(da1, x1, None, None, None, None, None, None,
-                                           y1, s1, coefs)[:, :w1.shape[1]])
+                                           y1, s1, coefs, cin_real=w1.shape[1])[:, :w1.shape[1]])
                 eng.ready(bn1.weight, bn1.bias, w1, blk.conv1.bias)
             dg1 = dbe1 = dw1 = None
         elif wg_pro:
             coefs, dg1, dbe1 = F.bn_grad_coefs(part1, y1, s1, g1)
-            dw1 = F.conv3_wgrad(da1, x1, None, None, None, None, None, None, y1, s1, coefs)
+            dw1 = F.conv3_wgrad(da1, x1, None, None, None, None, None, None, y1, s1, coefs,
+                                cin_real=w1.shape[1])
             dw1 = dw1[:, :w1.shape[1]].reshape(w1.shape)
         elif direct:
             dy1, _, _ = F.bn_backward(da1, None, y1, s1, g1, None, bn1.weight.grad, bn1.bias.grad,
                                       part1)
             with eng.wgrad_stream(dy1, x1, x2, x2_bn):
                 if padded_in:
-                    w1.grad.add_(F.conv3_wgrad(dy1, x1, None, None, None)[:, :w1.shape[1]])
+                    w1.grad.add_(F.conv3_wgrad(dy1, x1, None, None, None,
+                                               cin_real=w1.shape[1])[:, :w1.shape[1]])
                 else:
                     F.conv3_wgrad(dy1, x1, x2, None, None, w1.grad, sc2, sh2)
                 eng.ready(bn1.weight, bn1.bias, w1, blk.conv1.bias)
             dg1 = dbe1 = dw1 = None
         else:
             dy1, dg1, dbe1 = F.bn_backward(da1, None, y1, s1, g1, None, None, None, part1)
-            dw1 = F.conv3_wgrad(dy1, x1, x2, None, None, None, sc2, sh2)
+            dw1 = F.conv3_wgrad(dy1, x1, x2, None, None, None, sc2, sh2,
+                                cin_real=w1.shape[1] if padded_in else 0)
             dw1 = (dw1[:, :w1.shape[1]] if padded_in else dw1).reshape(w1.shape)
         dx1 = dx2 = None
         if not wg_pro and (ctx.needs_input_grad[0] or (x2 is not None and ctx.needs_input_grad[1])):

@@ -77,7 +77,8 @@ def main():
             "fwd": lambda: F.conv3_fwd(x1, x2, pk.fwd, None, sc, sh, Co, 0, True),
             "dgrad": lambda: F.conv3_fwd(dy, None, pk.dgrad, None, None, None, C1 + C2,
                                          C1 if C2 else 0, False),
-            "wgrad": lambda: F.conv3_wgrad(dy, x1, x2, sc, sh),
+            # (the image layer: 3 real channels of the 8-channel padded input)
+            "wgrad": lambda: F.conv3_wgrad(dy, x1, x2, sc, sh, cin_real=3 if C1 == 8 else 0),
             # data gradient with the BN-backward reduction against y fused into its epilogue
             "dgradbn": lambda: F.conv3_fwd(dy, None, pk.dgrad, None, None, None, C1, 0, False,
                                            None, None, x1, bn4),

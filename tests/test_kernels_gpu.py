@@ -542,6 +542,45 @@ def test_conv3_wgrad_dy_prologue(ops, N, H, W):
     assert rel_err(dy_sep, ref_dy) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W,Cout,pro", [(2, 32, 32, 32, False), (3, 40, 24, 32, True),
+                                            (1, 20, 18, 32, True), (2, 36, 52, 64, False),
+                                            (2, 64, 64, 64, True)])
+def test_conv3_wgrad_image_layer(ops, N, H, W, Cout, pro):
+    """First-layer weight gradient on the (tap, channel)-packed image kernel (cin_real = 3 of
+    the 8-channel padded image) against fp32 autograd, against the generic v2 path (cin_real
+    0: same products, different fp32 summation order) and with the BN-backward dY prologue;
+    gradients of the padding channels must be exactly zero.  Partial 16-pixel tiles via odd
+    sizes."""
+    torch.manual_seed(31)
+    x = torch.randn(N, 3, H, W, device=DEV).bfloat16()
+    xin = ops.to_nhwc_bf16(x, 8)
+    if pro:
+        y = torch.randn(N, H, W, Cout, device=DEV).bfloat16()
+        da = torch.randn(N, H, W, Cout, device=DEV).bfloat16()
+        s4 = _bn4(Cout, 5)
+        gamma = torch.rand(Cout, device=DEV) + 0.5
+        part = torch.zeros(1, 2, Cout, device=DEV)
+        a = y.float() * s4[2] + s4[3]
+        dyh = torch.where(a > 0, da.float(), torch.zeros_like(a))
+        part[0, 0] = dyh.sum((0, 1, 2))
+        part[0, 1] = (dyh * (y.float() - s4[0]) * s4[1]).sum((0, 1, 2))
+        dy, _, _ = ops.bn_backward(da, None, y, s4, gamma, None, None, None, part)
+        coefs, _, _ = ops.bn_grad_coefs(part, y, s4, gamma)
+        w_img = ops.conv3_wgrad(da, xin, None, None, None, None, None, None, y, s4, coefs, cin_real=3)
+        w_gen = ops.conv3_wgrad(da, xin, None, None, None, None, None, None, y, s4, coefs)
+    else:
+        dy = torch.randn(N, H, W, Cout, device=DEV).bfloat16()
+        w_img = ops.conv3_wgrad(dy, xin, None, None, None, cin_real=3)
+        w_gen = ops.conv3_wgrad(dy, xin, None, None, None)
+    assert w_img.shape == (Cout, 8, 3, 3)
+    assert torch.count_nonzero(w_img[:, 3:]) == 0
+    assert rel_err(w_img, w_gen) < 1e-5, rel_err(w_img, w_gen)
+    w = torch.zeros(Cout, 3, 3, 3, device=DEV, requires_grad=True)
+    out = F.conv2d(x.float(), w, padding=1)
+    (g,) = torch.autograd.grad(out, w, dy.permute(0, 3, 1, 2).float())
+    assert rel_err(w_img[:, :3], g) < 5e-3
+
+
 @pytest.mark.parametrize("N,H,W,bn", [(2, 16, 16, False), (3, 12, 20, True), (1, 40, 24, True),
                                       (4, 8, 8, True)])
 def test_convt_bwd_fused(ops, N, H, W, bn):
