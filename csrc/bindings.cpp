@@ -245,10 +245,12 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
     if (a.nTilesM * a.nTilesN >= num_cus()) cfg = 4;
     else plan(cfg);
   }
-  // 512-pixel tiles (cfg 5) where they fill the chip without padding and K >= 9 x 256 (same-
-  // process A/B at batch 128, profiles/conv_ab_cfg5_r3d.txt: 3-6% faster on those layers,
-  // 2-4% slower with 128 input channels; DDLPC_CONV_CFG5=0: off, 2: every eligible layer)
-  const int use_cfg5 = knob("CONV_CFG5", 1);
+  // 512-pixel tiles (cfg 5) wherever they fill the chip without padding (DDLPC_CONV_CFG5=0:
+  // off, 1: only K >= 9 x 256).  With the rolling fragment pipeline (no scratch spills) every
+  // eligible layer gains: 128-input-channel layers 8-10%, K >= 9 x 256 layers 1-2% (same-
+  // process A/B at batch 128, profiles/r3s/conv_ab_cfg5_all_r3s7.txt; before the pipeline
+  // the 128-channel layers were 2-4% slower on cfg 5: profiles/conv_ab_cfg5_r3d.txt)
+  const int use_cfg5 = knob("CONV_CFG5", 2);
   if (cfg == 4 && use_cfg5 && a.bnb_y == nullptr && (a.Cin >= 256 || use_cfg5 == 2)) {
     plan(5);
     const double w5 = (double)a.nTilesM * 512 / ((double)g.N * g.D * g.H * g.W);
