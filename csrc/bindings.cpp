@@ -365,9 +365,12 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   const bool v2 = use_v2 && (use_v2 != 2 || g.dims == 2) && g.W >= min_w && (a.C2 == 0 || a.C1 % 32 == 0);
   // v3 (32x32x16 MFMA, conflict-free transposed reads): whole 32-channel input chunks
   const int use_v3 = knob("WGRAD_V3", 1);
-  // (the large 64-channel concat layers stay on v2's 96-pixel tiles: 4-5% faster there)
+  // (the large 64-channel concat layers dec3.a / dec2.a: v3 since round 3 — same-process
+  // bench A/B at batch 256 -0.8% step time, profiles/r3s/bench_ab_wgrad3_concat_r3s9.log;
+  // DDLPC_WGRAD3_CONCAT=0: back on v2's 96-pixel tiles, which were 4-5% faster at batch 128
+  // before the v3 prologue hoist)
   const bool v3 = v2 && use_v3 && a.C1 % 32 == 0 && a.C2 % 32 == 0 &&
-                  !(bco == 64 && a.C2 > 0 && g.H * g.W >= 64 * 64);
+                  (!(bco == 64 && a.C2 > 0 && g.H * g.W >= 64 * 64) || knob("WGRAD3_CONCAT", 1) != 0);
   // 128-pixel tiles (v2: 16 x conv3_wgrad2_pt/16; v3: 256 for 32 output channels, else 128)
   // (DDLPC_WGRAD3_PT64 = 96 | 128: pixel tile of the 64-channel v3 kernel; default 128)
   const int v3_pt64 = knob("WGRAD3_PT64", 128);

@@ -636,8 +636,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       issue_Ac(1);
       issue_Bj(0);
     }
+    // BNB with ylead 2: an item's y is loaded at its second-to-last super-stage (after that
+    // stage's DMAs: the youngest MT * NT loads), so the last super-stage waits for everything
+    // but y and y has two super-stages to arrive from HBM instead of one
+    const bool y2 = BNB && KS == 1 && p.ylead >= 2;
     for (int j = 0; j < J; ++j) {
-      dma_wait<0>();
+      if (y2 && j > 0 && (2 * j + 2) % spi == 0) dma_wait<MT * NT>();
+      else dma_wait<0>();
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int pp = 2 * j + h;
@@ -655,8 +660,14 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         if (j + 1 < J) issue_Bj(j + 1);
         if (cA >= 0) issue_Ac(cA);
       }
-      // BNB: an item's last super-stage loads y for its epilogue (awaited by the next one)
-      if (BNB && KS == 1 && (2 * j + 2) % spi == 0) issue_Y((2 * j + 2) / spi - 1);
+      // BNB: an item's last (ylead 2: second-to-last) super-stage loads y for its epilogue
+      if (BNB && KS == 1) {
+        if (y2) {
+          if ((2 * j + 4) % spi == 0) issue_Y((2 * j + 4) / spi - 1);
+        } else if ((2 * j + 2) % spi == 0) {
+          issue_Y((2 * j + 2) / spi - 1);
+        }
+      }
       // P is even (nchunks even): both pairs exist; one 6-tap fragment pipeline across them
       const int c0 = (2 * j) / NG, c1 = (2 * j + 1) / NG;
       if constexpr (ILV) {
@@ -873,6 +884,7 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   const int diag = knob("DIAG_CONV", 0);
   a.diag = diag;
   a.prio = knob("CONV_PRIO", 2);
+  a.ylead = knob("BNB_YLEAD", 1);      // 2 measured 1-3% slower per layer (profiles/r3s)
   constexpr int FDB_OK = !(DIMS == 3 && MT * NT >= 16) ? 1 : 0;
   if constexpr (NBB == 4) {
     if (conv_ilv()) {
