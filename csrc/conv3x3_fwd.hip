@@ -913,7 +913,7 @@ void launch_cfg5(ConvFwdArgs& a, hipStream_t st) {
     grid = a.persist_blocks / q * q;
   }
   a.stat_rows = grid;
-  a.diag = 0;
+  a.diag = knob("DIAG_CONV", 0);
   a.prio = knob("CONV_PRIO", 2);
   if (conv_pipe())
     hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 640, 2, 2, false, false>), dim3(grid),
