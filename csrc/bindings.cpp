@@ -1282,6 +1282,7 @@ TORCH_LIBRARY(ddlpc, m) {
   m.def("conv3_wgrad(Tensor dy, Tensor x1, Tensor? x2, Tensor? pscale, Tensor? pshift, Tensor(a!)? out=None, "
         "Tensor? pscale2=None, Tensor? pshift2=None, Tensor? dy_y=None, Tensor? dy_s4=None, "
         "Tensor? dy_coefs=None, int cin_real=0) -> Tensor");
+  m.def("reduce_rows(Tensor partial, int R, int N) -> Tensor");
   m.def("bn_finalize(Tensor partial, float count, Tensor gamma, Tensor beta, Tensor(a!) running_mean, "
         "Tensor(b!) running_var, float momentum, float eps, bool update_running, Tensor(c!)? nbt) -> Tensor");
   m.def("bn_relu_apply(Tensor y, Tensor stats4, bool pool, bool full=True) -> Tensor[]");
@@ -1331,6 +1332,7 @@ TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
   m.impl("conv3_fwd", &ddlpc::conv3_fwd);
   m.impl("conv3_wgrad", &ddlpc::conv3_wgrad);
   m.impl("bn_finalize", &ddlpc::bn_finalize);
+  m.impl("reduce_rows", &ddlpc::reduce_rows);
   m.impl("bn_relu_apply", &ddlpc::bn_relu_apply);
   m.impl("bn_running_apply", &ddlpc::bn_running_apply);
   m.impl("bn_grad_coefs", &ddlpc::bn_grad_coefs);

@@ -239,6 +239,48 @@ __global__ void rows_sum_scatter_kernel(const T* __restrict__ in, int R, long lo
   dst[d] = accumulate ? dst[d] + v : v;
 }
 
+// one-launch form for R > 64 rows (the two-pass pair costs a second >= 4.5 us launch): a
+// 1024-thread block owns 64 columns, its 16 waves sum the rows r = w (mod 16) of them
+// (coalesced 256-B row segments), and wave 0 adds the 16 partials in a fixed order
+// (deterministic); optional permuted scatter / accumulate into the fp32 destination
+template <bool SCATTER>
+__global__ __launch_bounds__(1024) void rows_sum_wide_kernel(const float* __restrict__ in, int R, long long N,
+                                                             long long ld, double* __restrict__ sums,
+                                                             float* dst, int mode, int A, int Tt, int B,
+                                                             int accumulate) {
+  __shared__ double red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long j = blockIdx.x * 64LL + lane;
+  double s = 0.0;
+  if (j < N) {
+#pragma unroll 4
+    for (int r = w; r < R; r += 16) s += (double)in[(long long)r * ld + j];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w != 0 || j >= N) return;
+  double t = 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) t += red[k][lane];
+  if (!SCATTER) { sums[j] = t; return; }
+  long long d = j;
+  if (mode == 0) {
+    const int ci = (int)(j % B);
+    const int tap = (int)((j / B) % Tt);
+    const long long co = j / ((long long)B * Tt);
+    d = (co * B + ci) * Tt + tap;
+  } else if (mode == 1) {
+    const int co = (int)(j % B);
+    const int sub = (int)((j / B) % Tt);
+    const long long ci = j / ((long long)B * Tt);
+    d = (ci * B + co) * Tt + sub;
+  }
+  const float v = (float)t;
+  dst[d] = accumulate ? dst[d] + v : v;
+}
+
+constexpr int kWideMaxRows = 4096;
+
 }  // namespace
 
 void bn_stats_finalize_rows_launch(const float* partial, int P, int C, double count,
@@ -269,6 +311,11 @@ void reduce_rows_scatter_launch(const float* in, int R, long long N, double* tmp
                        mode, A, T, B, accumulate ? 1 : 0, ld);
     return;
   }
+  if (R <= kWideMaxRows) {
+    hipLaunchKernelGGL(rows_sum_wide_kernel<true>, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, st, in,
+                       R, N, ld, nullptr, dst, mode, A, T, B, accumulate ? 1 : 0);
+    return;
+  }
   const int RC = (R + RB - 1) / RB;
   hipLaunchKernelGGL(rows_chunk_sum_kernel<float>, dim3(gx, RC), dim3(256), 0, st, in, R, N, tmp, ld);
   hipLaunchKernelGGL(rows_sum_scatter_kernel<double>, dim3(gx), dim3(256), 0, st, tmp, RC, N, dst,
@@ -284,6 +331,11 @@ void reduce_rows_launch(const float* in, int R, long long N, double* tmp, double
   const unsigned gx = (unsigned)((N + 255) / 256);
   if (RC == 1) {
     hipLaunchKernelGGL(rows_chunk_sum_kernel<float>, dim3(gx, 1), dim3(256), 0, st, in, R, N, sums, -1LL);
+    return;
+  }
+  if (R <= kWideMaxRows) {
+    hipLaunchKernelGGL(rows_sum_wide_kernel<false>, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, st, in,
+                       R, N, N, sums, nullptr, 2, 0, 0, 0, 0);
     return;
   }
   hipLaunchKernelGGL(rows_chunk_sum_kernel<float>, dim3(gx, RC), dim3(256), 0, st, in, R, N, tmp, -1LL);

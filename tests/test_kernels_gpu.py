@@ -233,7 +233,8 @@ def test_conv3_dgrad_split(ops, C1, C2, Cout):
     (2, 16, 16, 32, 0, 32, False), (2, 32, 32, 64, 0, 64, True), (1, 16, 16, 64, 64, 128, False),
     (4, 8, 8, 256, 0, 256, True), (2, 32, 32, 3, 0, 32, False), (1, 16, 16, 64, 32, 32, False),
     (2, 64, 64, 64, 32, 32, True), (2, 72, 40, 32, 0, 64, True), (1, 128, 128, 128, 64, 64, False),
-    (2, 48, 48, 128, 0, 96, True)])
+    (2, 48, 48, 128, 0, 96, True),
+    (4, 256, 256, 32, 0, 32, True)])     # > 64 split-K rows: the one-launch wide reduction
 def test_conv3_wgrad(ops, N, H, W, C1, C2, Cout, pro):
     torch.manual_seed(3)
     x1 = torch.randn(N, C1, H, W, device=DEV).bfloat16()
@@ -254,6 +255,20 @@ def test_conv3_wgrad(ops, N, H, W, C1, C2, Cout, pro):
     (g,) = torch.autograd.grad(out, w, dy.float())
     assert dw.shape == g.shape
     assert rel_err(dw, g) < 5e-3
+
+
+@pytest.mark.parametrize("R,N", [(1, 100), (64, 9216), (65, 37), (300, 9216), (4096, 130),
+                                 (5000, 70)])
+def test_reduce_rows(ops, R, N):
+    """Deterministic fp64 column sums of an fp32 [R][N] slab (single pass for R <= 64, the
+    one-launch 16-wave form up to 4096 rows, the two-pass chunk form beyond)."""
+    torch.manual_seed(R)
+    x = torch.randn(R, N, device=DEV)
+    got = ops.reduce_rows(x, R, N)
+    ref = x.double().sum(0)
+    assert got.dtype == torch.float64
+    assert float((got - ref).abs().max()) < 1e-9 * max(1.0, float(ref.abs().max())) + 1e-9
+    assert torch.equal(got, ops.reduce_rows(x, R, N))        # run to run: bit for bit
 
 
 @pytest.mark.parametrize("N,H,W,C,pool", [
