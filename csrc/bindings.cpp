@@ -357,7 +357,7 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   a.pshift2 = fptr_opt(pshift2);
   if (a.pscale) TORCH_CHECK(a.C1 <= 512, "prologue supports C1 <= 512");
   if (a.pscale2) TORCH_CHECK(dual && a.pshift2 && a.C1 + a.C2 <= 512, "X2 prologue: x2, pscale2/pshift2, C1 + C2 <= 512");
-  const int bco = a.Cout <= 32 ? 32 : 64;
+  int bco = a.Cout <= 32 ? 32 : 64;
   const int use_v2 = knob("WGRAD_V2", 1);
   // (images narrower than the 16-pixel tile rows run with masked columns: DDLPC_WGRAD_MINW)
   // (8: the 8x8 bottleneck layers, 10% faster than the v1 kernel there)
@@ -393,7 +393,14 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   // input, (tap, channel)-packed kernel (DDLPC_WGRAD_IMG=0: the v2 path)
   const bool img = cin_real > 0 && cin_real <= 4 && a.C1 == 8 && !dual && g.dims == 2 && g.W >= 16 &&
                    a.pscale == nullptr && a.pscale2 == nullptr && knob("WGRAD_IMG", 1) != 0;
+  // v3 with 128 output channels per workgroup (every wave a 32-channel quarter, no k-split;
+  // 96-pixel tiles): each staged input halo feeds twice the MFMAs of the 64-channel tiles
+  // (DDLPC_WGRAD3_BCO128=0: 64-channel tiles)
+  // (>= 32x32 images: on the 16^2 / 8^2 levels the 96-pixel tiles are mostly masked columns,
+  // measured 3-21% slower there)
+  if (v3 && !img && a.Cout >= 128 && g.H * g.W >= 32 * 32 && knob("WGRAD3_BCO128", 1) != 0) bco = 128;
   if (img) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad_img_pt(bco) / 16; }
+  else if (v3 && bco == 128) { a.TD = 1; a.TW = 16; a.TH = 6; }
   else if (v3) { a.TD = 1; a.TW = 16; a.TH = bco == 32 ? (v3_ring ? 8 : 16) : (v3_pt64 == 96 && a.C2 > 0 ? 6 : 8); }
   else if (v2) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad2_pt(bco, a.C2, g.H, g.W) / 16; }
   else if (g.dims == 2) { a.TD = 1; a.TW = g.W >= 16 ? 16 : 8; a.TH = 128 / a.TW; }

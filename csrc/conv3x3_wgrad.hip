@@ -549,7 +549,9 @@ __global__ __launch_bounds__(256, PT <= 96 ? 3 : 2) void conv3_wgrad2_kernel(Con
 // in a fixed order at the end (deterministic).
 template <int BCO>
 DDLPC_DEVICE int wg3_yswz(int row) {             // XOR on the 16-B piece index
-  return BCO == 64 ? (((row >> 1) & 1) << 2) : 0;
+  // (256-B rows, 128 channels: the 64-B quarter XOR row bits 0-1 — the 4 consecutive rows a
+  // 32-lane half-wave reads land in 4 different quarters of the bank row)
+  return BCO == 128 ? ((row & 3) << 2) : BCO == 64 ? (((row >> 1) & 1) << 2) : 0;
 }
 
 // NB: stages in the LDS-DMA ring (2: double buffer, one full vmcnt drain per tile; 3: the
@@ -1062,6 +1064,8 @@ void conv3_wgrad3_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
     hipLaunchKernelGGL((conv3_wgrad3_kernel<32, 128, 3>), dim3(grid), dim3(256), SMEM32R, st, a);
   else if (bco == 32)
     hipLaunchKernelGGL((conv3_wgrad3_kernel<32, 256>), dim3(grid), dim3(256), (Wg2Cfg<32, 256>::SMEM), st, a);
+  else if (bco == 128)   // 96-pixel tiles: two 74 KB workgroups per CU
+    hipLaunchKernelGGL((conv3_wgrad3_kernel<128, 96>), dim3(grid), dim3(256), (Wg2Cfg<128, 96>::SMEM), st, a);
   else if (pt == 256)
     hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 256>), dim3(grid), dim3(256), (Wg2Cfg<64, 256>::SMEM), st, a);
   else if (pt == 96)
