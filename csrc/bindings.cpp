@@ -977,7 +977,7 @@ std::vector<at::Tensor> head_ce_fwd_stats(const at::Tensor& a, const at::Tensor&
   TORCH_CHECK(head_supported(C, K), "head kernel: unsupported (C, K)");
   const long long P = a.numel() / C;
   TORCH_CHECK(labels.numel() == P, "labels / activation pixel count mismatch");
-  const int nb = head_ce_bwd_blocks(C, K, true, P, num_cus());
+  const int nb = head_fwd_stats_blocks(C, K, P, num_cus());
   auto fopts = a.options().dtype(at::kFloat);
   at::Tensor wrows = at::empty({nb, K * C + K}, fopts);
   at::Tensor brows = at::empty({nb, 2, C}, fopts);

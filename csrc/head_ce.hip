@@ -400,6 +400,168 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
   }
 }
 
+// The fused training forward + statistics pass for the flagship head (C = 32, deferred
+// BatchNorm) with dWh on the matrix cores.  head_ce_bwd_kernel<.., LOSS> keeps the K x 8
+// dWh accumulators of each lane's channels in registers (48 VGPRs at K = 6: 200 in all, two
+// waves per SIMD, ~1.5 TB/s — latency-bound on its one-pixel prefetch).  Here each wave
+// stages its 16 pixels' activation [16 px][32 ch] and dlogits [16 px][16 classes] (split
+// into bf16 hi + lo parts: products exact to ~2^-17) in LDS and accumulates
+//   dWh^T[class][ch] += dlogits^T[class][px] . act[px][ch]
+// with v_mfma_f32_16x16x16_bf16 (the transposed ds_read_b64_tr_b16 gives both operands in
+// MFMA layout): 8 accumulator VGPRs instead of 48.  Everything else is head_pixel_x's
+// arithmetic.  The pixel loop is wave-uniform (the transposed reads need EXEC all ones):
+// tail lanes run with zeroed contributions.
+DDLPC_DEVICE f32x4_t mfma16x16x16(const uint2& a, const uint2& b, f32x4_t c) {
+  typedef short s4_t __attribute__((ext_vector_type(4)));
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s4_t, a), __builtin_bit_cast(s4_t, b),
+                                                   c, 0, 0, 0);
+}
+
+template <int K>
+__global__ __launch_bounds__(256, 3) void head_fwd_stats_mdw_kernel(
+    const bf16_t* __restrict__ a, const float* __restrict__ Wh, const float* __restrict__ bh,
+    const int64_t* __restrict__ labels, float* __restrict__ dWp, long long P, int ignore_index,
+    const float* __restrict__ bn4, float* __restrict__ bnpart, int Kreal, float* __restrict__ lossp) {
+  constexpr int C = 32, G = 4, PPB = 64;
+  static_assert(K <= 16, "one 16-class MFMA tile");
+  constexpr int NACC = K + 16 + 3;                  // db | BN partials (8 + 8) | loss, hits, count
+  constexpr int LB = K + 16;                        // loss accumulators at LB, LB + 1, LB + 2
+  __shared__ float sred[4][G][NACC];
+  __shared__ __attribute__((aligned(16))) float sW[K * C];      // Wh, padded classes zero
+  __shared__ __attribute__((aligned(16))) float sXh[2 * C];     // invstd | -mean*invstd
+  // per wave: act [16][32] bf16 (1 KB) | dlogits hi [16][16] (512 B) | lo [16][16]; the end
+  // of the kernel reuses it as the wave's dWh^T [16][32] fp32 (2 KB)
+  __shared__ __attribute__((aligned(16))) char sT[4][2048];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cg = lane % G, c8 = cg * 8;
+  for (int i = tid; i < K * C; i += 256) sW[i] = i < Kreal * C ? Wh[i] : 0.f;
+  for (int i = tid; i < C; i += 256) { sXh[i] = bn4[C + i]; sXh[C + i] = -bn4[i] * bn4[C + i]; }
+  float bk[K], sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < K; ++k) bk[k] = k < Kreal ? bh[k] : -INFINITY;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = bn4[2 * C + c8 + j]; sh[j] = bn4[3 * C + c8 + j]; }
+  __syncthreads();
+  char* tA = sT[wave];
+  char* tDh = tA + 1024;
+  char* tDl = tA + 1536;
+  float acc[NACC];
+#pragma unroll
+  for (int i = 0; i < NACC; ++i) acc[i] = 0.f;
+  f32x4_t dw[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+  // transposed-read geometry: 16-lane group g reads pixel rows 4g..4g+3, lane 4q + p of the
+  // group supplies row 4g + q, columns 4p..4p+3 (+16 for the second channel tile)
+  const int g = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
+  const int rA = (4 * g + q) * 64 + pq * 8;          // act row: 32 ch x 2 B
+  const int rD = (4 * g + q) * 32 + pq * 8;          // dlogit row: 16 classes x 2 B
+  const int p16 = lane >> 2;                         // this lane's pixel within the wave's 16
+  const long long stride = (long long)gridDim.x * PPB;
+  long long base = (long long)blockIdx.x * PPB;
+  long long px = base + tid / G;
+  uint4 a_nx = make_uint4(0, 0, 0, 0);
+  int64_t l_nx = ignore_index;
+  if (px < P) { a_nx = *reinterpret_cast<const uint4*>(a + px * C + c8); l_nx = labels[px]; }
+#pragma unroll 1
+  for (; base < P; base += stride, px += stride) {   // wave-uniform trip count
+    const bool valid = px < P;
+    const uint4 a_cur = a_nx;
+    const int64_t lab = l_nx;
+    if (px + stride < P) {
+      a_nx = *reinterpret_cast<const uint4*>(a + (px + stride) * C + c8);
+      l_nx = labels[px + stride];
+    }
+    float y8[8], f[8], d[K], o8[8], lse, zy;
+    int am;
+    uint4 pk;
+    head_pixel_x<C, K, true>(a_cur, lab, sW + opaque_zero() + c8, bk, sc, sh, 1.f, ignore_index,
+                             y8, f, d, pk, o8, lse, zy, am);
+    if (!valid) {                                     // tail lane: contributes nothing
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { f[j] = 0.f; o8[j] = 0.f; }
+#pragma unroll
+      for (int k = 0; k < K; ++k) d[k] = 0.f;
+    }
+    // stage: act row (this lane's 8 channels), dlogit hi / lo (classes 4 cg .. 4 cg + 3)
+    *reinterpret_cast<uint4*>(tA + p16 * 64 + cg * 16) = pack8(f);
+    {
+      float dh[4], dl[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) v = (4 * cg + i == k) ? d[k] : v;
+        const uint32_t h2 = pack2(v, 0.f);
+        dh[i] = lo_bf(h2);
+        dl[i] = v - dh[i];
+      }
+      *reinterpret_cast<uint2*>(tDh + p16 * 32 + cg * 8) = make_uint2(pack2(dh[0], dh[1]), pack2(dh[2], dh[3]));
+      *reinterpret_cast<uint2*>(tDl + p16 * 32 + cg * 8) = make_uint2(pack2(dl[0], dl[1]), pack2(dl[2], dl[3]));
+    }
+    const uint2 ah = lds_read_tr16(tDh + rD);
+    const uint2 al = lds_read_tr16(tDl + rD);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const uint2 b = lds_read_tr16(tA + rA + nt * 32);
+      dw[nt] = mfma16x16x16(ah, b, dw[nt]);
+      dw[nt] = mfma16x16x16(al, b, dw[nt]);
+    }
+    if (valid) {
+      if (cg == 0) {
+        if (lab != ignore_index) { acc[LB] += lse - zy; acc[LB + 2] += 1.f; }
+        acc[LB + 1] += am == lab ? 1.f : 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[k] += d[k];
+      }
+      const float* xh = sXh + opaque_zero() + c8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {                   // unit scale: the unrounded dA
+        const float dyh = fmaf(y8[j], sc[j], sh[j]) > 0.f ? o8[j] : 0.f;
+        acc[K + j] += dyh;
+        acc[K + 8 + j] = fmaf(dyh, fmaf(y8[j], xh[j], xh[C + j]), acc[K + 8 + j]);
+      }
+    }
+  }
+  // ---- workgroup reduction.  dWh: each wave's D (lane: class 4g + i, channel 16 nt + (lane & 15))
+  // to its LDS slot, then the 4 waves summed in a fixed order
+  float* wd = reinterpret_cast<float*>(tA);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wd[(4 * g + i) * 32 + nt * 16 + (lane & 15)] = dw[nt][i];
+  // db / BN partials / loss: lanes with equal cg (xor over the pixel-slot bits), then waves
+#pragma unroll
+  for (int o = G; o < 64; o <<= 1)
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) acc[i] += __shfl_xor(acc[i], o, 64);
+  if (lane < G)
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) sred[wave][lane][i] = acc[i];
+  __syncthreads();
+  const int nout = Kreal * C + Kreal;
+  for (int o = tid; o < nout; o += 256) {            // [dW (k, c) | db (k)]
+    float t = 0.f;
+    if (o < Kreal * C) {
+      const int k = o / C, c = o % C;
+      for (int wv = 0; wv < 4; ++wv) t += reinterpret_cast<const float*>(sT[wv])[k * 32 + c];
+    } else {
+      const int k = o - Kreal * C;
+      for (int wv = 0; wv < 4; ++wv) t += sred[wv][0][k];
+    }
+    dWp[(long long)blockIdx.x * nout + o] = t;
+  }
+  for (int o = tid; o < 2 * C; o += 256) {           // [sum dyh (c) | sum dyh*xhat (c)]
+    const int half = o / C, c = o % C;
+    float t = 0.f;
+    for (int wv = 0; wv < 4; ++wv) t += sred[wv][c / 8][K + 8 * half + c % 8];
+    bnpart[(long long)blockIdx.x * 2 * C + o] = t;
+  }
+  if (tid < 3) {                                     // lanes cg == 0 hold them
+    float t = 0.f;
+    for (int wv = 0; wv < 4; ++wv) t += sred[wv][0][LB + tid];
+    lossp[(long long)blockIdx.x * 3 + tid] = t;
+  }
+}
+
 // Second pass of the two-pass head backward (deferred BatchNorm of the last decoder
 // block): recomputes dA exactly as head_ce_bwd_kernel stores it (head_pixel) and applies
 // that BatchNorm's backward to it in registers,
@@ -566,13 +728,42 @@ void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
                                          ignore_index, bn4, bnpart, K));
 }
 
+// the fused forward + statistics pass on the matrix-core dWh kernel (C = 32; DDLPC_HEAD_MDW=0:
+// the register-accumulator kernel)
+// (K <= 6: the 8- and 16-class instantiations exceed the 168-VGPR budget of three
+// workgroups per CU and spill)
+bool head_mdw(int C, int K) { return C == 32 && K <= 6 && knob("HEAD_MDW", 1) != 0; }
+
+int head_fwd_stats_blocks(int C, int K, long long P, int num_cus) {
+  if (!head_mdw(C, K)) return head_ce_bwd_blocks(C, K, true, P, num_cus);
+  int per_cu = 8;
+  HEAD_SWITCH(C, K, if constexpr (KK <= 6) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&head_fwd_stats_mdw_kernel<KK>),
+                                                     256, 0) == hipSuccess && n > 0)
+      per_cu = std::min(per_cu, n);
+    else
+      per_cu = 1;
+  });
+  const int pc = knob("HEAD_BWD_PER_CU", 0);
+  if (pc > 0) per_cu = pc;
+  const long long ppb = 64;
+  return (int)std::max<long long>(1, std::min<long long>((P + ppb - 1) / ppb, (long long)per_cu * num_cus));
+}
+
 void head_ce_fwd_stats_launch(const bf16_t* a, const float* Wh, const float* bh,
                               const int64_t* labels, const float* bn4, float* dW_partial,
                               float* bnpart, float* loss_partial, float* out3, int nblocks,
                               long long P, int C, int K, int ignore_index, hipStream_t st) {
-  HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK, true, false, true>), dim3(nblocks),
-                                       dim3(256), 0, st, a, Wh, bh, labels, nullptr, nullptr, nullptr,
-                                       dW_partial, P, ignore_index, bn4, bnpart, K, loss_partial));
+  if (head_mdw(C, K))
+    HEAD_SWITCH(C, K, if constexpr (KK <= 6) {
+      hipLaunchKernelGGL((head_fwd_stats_mdw_kernel<KK>), dim3(nblocks), dim3(256), 0, st, a, Wh, bh, labels,
+                         dW_partial, P, ignore_index, bn4, bnpart, K, loss_partial);
+    });
+  else
+    HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK, true, false, true>), dim3(nblocks),
+                                         dim3(256), 0, st, a, Wh, bh, labels, nullptr, nullptr, nullptr,
+                                         dW_partial, P, ignore_index, bn4, bnpart, K, loss_partial));
   hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(256), 0, st, loss_partial, nblocks, out3);
 }
 

@@ -173,6 +173,7 @@ void head_ce_fwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
 // bnpart (with bn4): [nblocks][2][C] BatchNorm-backward partial rows of the stored dA;
 // nblocks from head_ce_bwd_blocks (one persistent wave of workgroups)
 int head_ce_bwd_blocks(int C, int K, bool defer, long long P, int num_cus);
+int head_fwd_stats_blocks(int C, int K, long long P, int num_cus);
 void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
                         const float* gscale, const float* stats3, int unused, bf16_t* dA,
                         float* dW_partial, int nblocks, long long P, int C, int K,
