@@ -261,6 +261,154 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
   }
 }
 
+// ---------------------------------------------------------------- NT forward v2
+// The transposed-conv forward GEMM (M = input pixels, N = S*Cout, K = Cin) restructured like
+// the 3x3 conv kernels: 8 waves on a 256-pixel x 128-column tile (4 x 2 waves of 64 x 64),
+// both operands by LDS-DMA (buffer_load ... lds) into double-buffered swizzled LDS, KS
+// 32-channel sub-chunks per stage behind ONE barrier (v1: register staging, two barriers
+// per 32 channels, LDS-staged scalar epilogue), the deferred BN + ReLU of x applied in LDS
+// by the lane that DMA'd each piece.  The MFMA computes D^T (weights as the A operand), so
+// every lane holds 4 consecutive output channels of one pixel; one v_permlane16_swap per
+// dword pairs two 16-column tiles into 8 channels and the result leaves as 16-byte stores
+// at the pixel-shuffled output position (+ bias), straight from the accumulators.
+// Requires Cin % 32 == 0, (S*Cout) % 128 == 0 and Cout % 32 == 0 (launcher-checked).
+template <int KS>
+struct Nt2Cfg {
+  static constexpr int BM = 256, BN = 128;
+  static constexpr int A_BYTES = KS * BM * 64, B_BYTES = KS * BN * 64;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int SMEM = 2 * 512 * 4 + 2 * STAGE;           // BN constants | 2 stages
+  static constexpr int A_IT = KS * BM * 4 / 512;                 // DMA pieces per thread
+  static constexpr int B_IT = KS * BN * 4 / 512;
+};
+
+template <int KS>
+__global__ __launch_bounds__(512, KS == 1 ? 2 : 1) void gemm_nt_fwd2_kernel(GemmArgs p) {
+  using C = Nt2Cfg<KS>;
+  constexpr int BM = C::BM, BN = C::BN;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* s_bn = reinterpret_cast<float*>(smem);                   // scale [512] | shift [512]
+  char* base = smem + 2 * 512 * 4;
+  auto sA = [&](int b) { return base + b * C::STAGE; };
+  auto sB = [&](int b) { return base + b * C::STAGE + C::A_BYTES; };
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const bool bn = p.bn4 != nullptr;
+  if (bn)
+    for (int i = tid; i < p.K; i += 512) { s_bn[i] = p.bn4[2 * p.K + i]; s_bn[512 + i] = p.bn4[3 * p.K + i]; }
+  const int nTilesN = p.N / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / nTilesN) * BM, n0 = (bid % nTilesN) * BN;
+  // per-lane DMA geometry: piece e = i * 512 + tid -> row e >> 2, source piece swizzled
+  const int sub8 = ((lane & 3) ^ (((lane >> 4) & 1) << 1)) << 3;   // same for every i
+  const auto rA = convlds::make_rsrc(p.A + (long long)m0 * p.K,
+                                     (unsigned)((long long)(p.M - m0 < BM ? p.M - m0 : BM) * p.K * 2));
+  const auto rB = convlds::make_rsrc(p.B + (long long)n0 * p.K, (unsigned)((long long)BN * p.K * 2));
+  const int nk = p.K / (32 * KS);
+  auto issue = [&](int kc, int b) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < C::A_IT; ++i) {
+      const int e = i * 512 + tid, row = (e >> 2) % BM, sc = (e >> 2) / BM;
+      convlds::dma16(rA, sA(b) + (i * 8 + wave) * 1024,
+                     (unsigned)((row * p.K + (kc * KS + sc) * 32 + sub8) * 2));
+    }
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i) {
+      const int e = i * 512 + tid, row = (e >> 2) % BN, sc = (e >> 2) / BN;
+      convlds::dma16(rB, sB(b) + (i * 8 + wave) * 1024,
+                     (unsigned)((row * p.K + (kc * KS + sc) * 32 + sub8) * 2));
+    }
+  };
+  // deferred BN + ReLU of x on this lane's landed A pieces (rows past M stay zero)
+  auto transform = [&](int kc, char* __restrict__ A) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < C::A_IT; ++i) {
+      const int e = i * 512 + tid, row = (e >> 2) % BM, sc = (e >> 2) / BM;
+      if (m0 + row < p.M) {
+        const int c8 = (kc * KS + sc) * 32 + sub8;
+        uint4* q = reinterpret_cast<uint4*>(A + e * 16);
+        float f[8];
+        unpack8(*q, f);
+        // (the 8 constants as two 16-B LDS reads each, not 16 scalar reads)
+        const float4* vs = reinterpret_cast<const float4*>(s_bn + c8);
+        const float4* vh = reinterpret_cast<const float4*>(s_bn + 512 + c8);
+        const float4 s0 = vs[0], s1 = vs[1], h0 = vh[0], h1 = vh[1];
+        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
+        *q = pack8(f);
+      }
+    }
+  };
+  const int g = lane >> 4;
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](const char* __restrict__ A, const char* __restrict__ B) __attribute__((always_inline)) {
+#pragma unroll
+    for (int sc = 0; sc < KS; ++sc) {
+      uint4 af[4], bf[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        af[mt] = *reinterpret_cast<const uint4*>(A + sc * BM * 64 + lds_off(wm * 64 + mt * 16 + (lane & 15), g));
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        bf[nt] = *reinterpret_cast<const uint4*>(B + sc * BN * 64 + lds_off(wn * 64 + nt * 16 + (lane & 15), g));
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16x16x32(bf[nt], af[mt], acc[mt][nt]);
+    }
+  };
+  if (bn) __syncthreads();                                        // s_bn visible
+  issue(0, 0);
+  for (int kc = 0; kc < nk; ++kc) {
+    const int b = kc & 1;
+    convlds::dma_wait<0>();
+    if (bn) transform(kc, sA(b));
+    convlds::lds_sync();
+    if (kc + 1 < nk) issue(kc + 1, b ^ 1);
+    compute(sA(b), sB(b));
+  }
+  // ---- epilogue: lane holds columns n0 + wn*64 + nt*16 + 4g .. +3 of pixel wm*64 + mt*16 + (lane & 15)
+  bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C);
+#pragma unroll
+  for (int np = 0; np < 2; ++np) {
+    const int c0 = n0 + wn * 64 + np * 32;                        // 32 columns in one sub-position
+    const int sub = c0 / p.Cout, cob = c0 - sub * p.Cout;
+    float b0[4] = {0.f, 0.f, 0.f, 0.f}, b1[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias != nullptr)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { b0[i] = p.bias[cob + 4 * g + i]; b1[i] = p.bias[cob + 16 + 4 * g + i]; }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int m = m0 + wm * 64 + mt * 16 + (lane & 15);
+      const f32x4_t& a0 = acc[mt][2 * np];
+      const f32x4_t& a1 = acc[mt][2 * np + 1];
+      const uint2 lo = make_uint2(pack2(a0[0] + b0[0], a0[1] + b0[1]), pack2(a0[2] + b0[2], a0[3] + b0[3]));
+      const uint2 hi = make_uint2(pack2(a1[0] + b1[0], a1[1] + b1[1]), pack2(a1[2] + b1[2], a1[3] + b1[3]));
+      const uint4 q = convlds::pair16(lo, hi);
+      if (m < p.M) {
+        const int up = up_pixel(m, sub, p.dims, p.D, p.H, p.W);
+        *reinterpret_cast<uint4*>(Cp + (long long)up * p.Cout + cob + convlds::pair16_ch(lane)) = q;
+      }
+    }
+  }
+}
+
+// DDLPC_CONVT_FWD2: 0 = v1 kernel, 1 = v2 with one 32-channel chunk per stage (two
+// workgroups per CU), 2 = v2 with two chunks per stage (one workgroup per CU)
+int gemm_nt_fwd2_mode(const GemmArgs& a) {
+  const int v = knob("CONVT_FWD2", 1);
+  const bool ok = a.mode == GEMM_CONVT_FWD && a.K % (v == 2 ? 64 : 32) == 0 && a.K <= 512 &&
+                  a.N % 128 == 0 && a.Cout % 32 == 0;
+  return ok ? v : 0;
+}
+
 // ---------------------------------------------------------------- TN (weight gradient)
 // C[m = ci][n = (sub, co)] = sum_px x[px][ci] * dOut[up(px, sub)][co]
 __global__ __launch_bounds__(256, 2) void gemm_tn_wgrad_kernel(GemmArgs p) {
@@ -880,6 +1028,12 @@ void gemm_launch(GemmArgs& a, hipStream_t st) {
   // measured (B=64 U-Net shapes): the gathered data-gradient A operand gains from wide
   // steps; the forward (contiguous A, K = Cin) runs best at one chunk per step.  The forward
   // uses 128-wide N tiles when N allows (each A tile is read from L2 half as often)
+  if (const int v2 = gemm_nt_fwd2_mode(a)) {
+    const unsigned grid2 = (unsigned)(((a.M + 255) / 256) * (long long)(a.N / 128));
+    if (v2 == 2) hipLaunchKernelGGL((gemm_nt_fwd2_kernel<2>), dim3(grid2), dim3(512), Nt2Cfg<2>::SMEM, st, a);
+    else hipLaunchKernelGGL((gemm_nt_fwd2_kernel<1>), dim3(grid2), dim3(512), Nt2Cfg<1>::SMEM, st, a);
+    return;
+  }
   const int bn = gemm_nt_bn(a);
   const long long grid = gemm_nt_grid(a);
   const int kc = a.mode == GEMM_CONVT_FWD ? 1 : a.K <= 64 ? 2 : 4;
