@@ -399,8 +399,15 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   // (>= 32x32 images: on the 16^2 / 8^2 levels the 96-pixel tiles are mostly masked columns,
   // measured 3-21% slower there)
   if (v3 && !img && a.Cout >= 128 && g.H * g.W >= 32 * 32 && knob("WGRAD3_BCO128", 1) != 0) bco = 128;
+  // v3 with two 32-channel input chunks per 64-output-channel workgroup (each staged dY tile
+  // feeds both halos; 96-pixel tiles) on the >= 64x64 layers with >= 2 input chunks: dec2.a
+  // -13%, enc2.b / dec2.b -5% in isolation; the 8^2 / 16^2 layers lose 3-23% (masked tile
+  // columns): profiles/r3s/wgrad_ab_ciw_b256_r3s21.txt.  DDLPC_WGRAD3_CIW=1: off
+  a.ciw = 1;
+  if (v3 && !img && bco == 64 && knob("WGRAD3_CIW", 2) == 2 && a.Cin >= 64 && g.H * g.W >= 64 * 64)
+    a.ciw = 2;
   if (img) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad_img_pt(bco) / 16; }
-  else if (v3 && bco == 128) { a.TD = 1; a.TW = 16; a.TH = 6; }
+  else if (v3 && (bco == 128 || a.ciw == 2)) { a.TD = 1; a.TW = 16; a.TH = 6; }
   else if (v3) { a.TD = 1; a.TW = 16; a.TH = bco == 32 ? (v3_ring ? 8 : 16) : (v3_pt64 == 96 && a.C2 > 0 ? 6 : 8); }
   else if (v2) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad2_pt(bco, a.C2, g.H, g.W) / 16; }
   else if (g.dims == 2) { a.TD = 1; a.TW = g.W >= 16 ? 16 : 8; a.TH = 128 / a.TW; }
@@ -412,7 +419,7 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   a.tilesW = (g.W + a.TW - 1) / a.TW;
   a.nTiles = g.N * a.tilesD * a.tilesH * a.tilesW;
   a.coTiles = (a.Cout + bco - 1) / bco;
-  a.ciChunks = (a.Cin + 31) / 32;
+  a.ciChunks = (a.Cin + 32 * a.ciw - 1) / (32 * a.ciw);
   a.planes = g.dims == 2 ? 1 : 3;
   // split-K over pixel tiles: enough blocks to fill the chip, but every block keeps >= 8
   // tiles so the fp32 partial slab stays small next to the MFMA work

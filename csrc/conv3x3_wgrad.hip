@@ -557,29 +557,35 @@ DDLPC_DEVICE int wg3_yswz(int row) {             // XOR on the 16-B piece index
 // NB: stages in the LDS-DMA ring (2: double buffer, one full vmcnt drain per tile; 3: the
 // DMA of tile t + 2 in flight while t computes, counted waits — with 128-pixel tiles so two
 // workgroups still fit per CU)
-template <int BCO, int PT, int NB = 2>
+// CIW: 32-channel input chunks per workgroup (2: each staged dY tile feeds two X halos — the
+// concat layers' many input chunks re-read dY half as often; the waves split (co tile, chunk)
+// instead of the k-steps)
+template <int BCO, int PT, int NB = 2, int CIW = 1>
 __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
   using namespace convlds;
   using Cfg = Wg2Cfg<BCO, PT>;                     // DMA geometry / LDS budget as v2
   constexpr int TH = Cfg::TH, HW2 = 18;
   constexpr int NJ = BCO / 32;                     // 32-channel co tiles
-  constexpr int KW = 4 / NJ;                       // waves sharing a co tile (k-split)
+  constexpr int KW = 4 / (NJ * CIW);               // waves sharing a (co tile, chunk) (k-split)
+  static_assert(NJ * CIW * KW == 4, "4 waves = co tiles x input chunks x k phases");
+  static_assert(CIW == 1 || NB == 2, "two input chunks: double buffer only");
   constexpr int KS16 = PT / 16;                    // 16-pixel k-steps per tile
   static_assert(KS16 % KW == 0, "k-steps must split evenly over the waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* base = smem + Cfg::SS_BYTES;
-  auto sY = [&](int b) { return base + b * (Cfg::Y_BYTES + Cfg::X_BYTES); };
-  auto sX = [&](int b) { return base + b * (Cfg::Y_BYTES + Cfg::X_BYTES) + Cfg::Y_BYTES; };
+  constexpr int STAGE = Cfg::Y_BYTES + CIW * Cfg::X_BYTES;
+  auto sY = [&](int b) { return base + b * STAGE; };
+  auto sX = [&](int b) { return base + b * STAGE + Cfg::Y_BYTES; };   // + cw * X_BYTES: chunk cw
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wj = wave % NJ, wk = wave / NJ;        // co tile, k-step phase
+  const int wj = wave % NJ, wc = (wave / NJ) % CIW, wk = wave / (NJ * CIW);   // co tile, chunk, k phase
   int b = xcd_remap(blockIdx.x, gridDim.x);
   const int cic = b % p.ciChunks; b /= p.ciChunks;
   const int cot = b % p.coTiles; b /= p.coTiles;
   const int plane = b % p.planes; b /= p.planes;
   const int split = b;
-  const int co0 = cot * BCO, ci0 = cic * BK;
+  const int co0 = cot * BCO, ci0 = cic * BK * CIW;
   const int dshift = p.planes == 3 ? plane - 1 : 0;
 
   const bool has_pro = p.pscale != nullptr;
@@ -609,15 +615,24 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
     x_dh[i] = px / HW2 - 1;
     x_pix[i] = -1;
   }
-  const int c8l = ci0 + (lane & 3) * 8;
-  const bool second = ci0 >= p.C1;
-  const int Cs = second ? p.C2 : p.C1;
-  const int cs0 = second ? c8l - p.C1 : c8l;
-  const bf16_t* xsrc = second ? p.X2 : p.X1;
-  const bool xch_ok = cs0 < Cs;
-  float psc[8] = {}, psh[8] = {};                    // this lane's prologue constants
-  if (second ? has_pro2 : has_pro)
-    pro8_load(p.pscale, p.pshift, p.pscale2, p.pshift2, p.C1, c8l, second ? p.Cin : p.C1, psc, psh);
+  // per input chunk cw: source tensor, channel offset, validity, prologue constants
+  bool second[CIW], xch_ok[CIW], xpro[CIW];
+  int Cs[CIW], cs0[CIW];
+  const bf16_t* xsrc[CIW];
+  float psc[CIW][8] = {}, psh[CIW][8] = {};          // this lane's prologue constants
+#pragma unroll
+  for (int cw = 0; cw < CIW; ++cw) {
+    const int cc = ci0 + cw * BK;
+    const int c8l = cc + (lane & 3) * 8;
+    second[cw] = cc >= p.C1;
+    Cs[cw] = second[cw] ? p.C2 : p.C1;
+    cs0[cw] = second[cw] ? c8l - p.C1 : c8l;
+    xsrc[cw] = second[cw] ? p.X2 : p.X1;
+    xch_ok[cw] = cs0[cw] < Cs[cw];
+    xpro[cw] = second[cw] ? has_pro2 : has_pro;
+    if (xpro[cw])
+      pro8_load(p.pscale, p.pshift, p.pscale2, p.pshift2, p.C1, c8l, second[cw] ? p.Cin : p.C1, psc[cw], psh[cw]);
+  }
 
   auto issue = [&](int tile, int buf) __attribute__((always_inline)) {
     int t = tile;
@@ -635,19 +650,29 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
       const bool ok = y_rel[i] >= 0 && w0 + y_pw[i] < p.W && h0 + y_ph[i] < p.H;
       dma16(ry, sY(buf) + (i * 4 + wave) * 1024, ok ? (unsigned)(ybase + y_rel[i]) * 2u : kOOB);
     }
-    const auto rx = make_rsrc(xsrc + (n + (dok ? dshift : 0)) * img_px * Cs, (unsigned)(img_px * Cs * 2));
 #pragma unroll
     for (int i = 0; i < Cfg::X_ITERS; ++i) {
       if ((i * 4 + wave) >= Cfg::X_INSTR) break;
       const int gw = w0 + x_dw[i], gh = h0 + x_dh[i];
-      x_pix[i] = (gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && xch_ok && dok) ? gh * p.W + gw : -1;
-      dma16(rx, sX(buf) + (i * 4 + wave) * 1024, x_pix[i] >= 0 ? (unsigned)(x_pix[i] * Cs + cs0) * 2u : kOOB);
+      x_pix[i] = (gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && dok) ? gh * p.W + gw : -1;
+    }
+#pragma unroll
+    for (int cw = 0; cw < CIW; ++cw) {
+      const auto rx = make_rsrc(xsrc[cw] + (n + (dok ? dshift : 0)) * img_px * Cs[cw],
+                                (unsigned)(img_px * Cs[cw] * 2));
+#pragma unroll
+      for (int i = 0; i < Cfg::X_ITERS; ++i) {
+        if ((i * 4 + wave) >= Cfg::X_INSTR) break;
+        const bool ok = x_pix[i] >= 0 && xch_ok[cw];
+        dma16(rx, sX(buf) + cw * Cfg::X_BYTES + (i * 4 + wave) * 1024,
+              ok ? (unsigned)(x_pix[i] * Cs[cw] + cs0[cw]) * 2u : kOOB);
+      }
     }
   };
   // (ring: the halo validity of `tile` is recomputed here — x_pix already holds a later tile's)
   // (double buffer: x_pix still holds this tile's validity; the integer divisions of the
   // recomputation measured 6-8% on the weight gradient, so only the ring pays for them)
-  auto transform = [&](int tile, char* __restrict__ X) __attribute__((always_inline)) {
+  auto transform = [&](int tile, char* __restrict__ X0) __attribute__((always_inline)) {
     int h0 = 0, w0 = 0;
     bool dok = true;
     if constexpr (NB != 2) {
@@ -659,25 +684,33 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
       h0 = th_i * TH; w0 = tw_i * 16;
     }
 #pragma unroll
-    for (int i = 0; i < Cfg::X_ITERS; ++i) {
-      const int e = (i * 4 + wave) * 64 + lane;
-      bool ok;
-      if constexpr (NB == 2) {
-        ok = x_pix[i] >= 0;
-      } else {
-        const int gw = w0 + x_dw[i], gh = h0 + x_dh[i];
-        ok = gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && xch_ok && dok;
-      }
-      if ((i * 4 + wave) < Cfg::X_INSTR && ok) {
-        uint4* q = reinterpret_cast<uint4*>(X + e * 16);
-        float f[8];
-        unpack8(*q, f);
+    for (int cw = 0; cw < CIW; ++cw) {
+      if (!xpro[cw]) continue;
+      char* X = X0 + cw * Cfg::X_BYTES;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], psc[j], psh[j]), 0.0f);
-        *q = pack8(f);
+      for (int i = 0; i < Cfg::X_ITERS; ++i) {
+        const int e = (i * 4 + wave) * 64 + lane;
+        bool ok;
+        if constexpr (NB == 2) {
+          ok = x_pix[i] >= 0 && xch_ok[cw];
+        } else {
+          const int gw = w0 + x_dw[i], gh = h0 + x_dh[i];
+          ok = gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && xch_ok[cw] && dok;
+        }
+        if ((i * 4 + wave) < Cfg::X_INSTR && ok) {
+          uint4* q = reinterpret_cast<uint4*>(X + e * 16);
+          float f[8];
+          unpack8(*q, f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], psc[cw][j], psh[cw][j]), 0.0f);
+          *q = pack8(f);
+        }
       }
     }
   };
+  bool any_pro = false;
+#pragma unroll
+  for (int cw = 0; cw < CIW; ++cw) any_pro = any_pro || xpro[cw];
 
   // ---- per-lane transposed-read geometry.  16-lane group g4 = lane >> 4: columns
   // (g4 & 1) * 16 + 4 * pq, pixel rows (g4 >> 1) * 8 + 4 * h + q within the 16-pixel k-step
@@ -697,7 +730,8 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
 
-  auto compute = [&](const char* __restrict__ Y, const char* __restrict__ X) __attribute__((always_inline)) {
+  auto compute = [&](const char* __restrict__ Y, const char* __restrict__ X0) __attribute__((always_inline)) {
+    const char* X = X0 + wc * Cfg::X_BYTES;          // this wave's input chunk
 #pragma unroll
     for (int kk = 0; kk < KS16 / KW; ++kk) {
       const int ks = kk * KW + wk;
@@ -719,7 +753,7 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
     for (int tile = t_begin; tile < t_end; ++tile) {
       const int buf = (tile - t_begin) & 1;
       dma_wait<0>();
-      if (second ? has_pro2 : has_pro) transform(tile, sX(buf));
+      if (any_pro) transform(tile, sX(buf));
       lds_sync();
       if (tile + 1 < t_end) issue(tile + 1, buf ^ 1);
       compute(sY(buf), sX(buf));
@@ -738,7 +772,7 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
       const int idx = tile - t_begin, buf = idx % NB;
       const int after = min(NB - 2, t_end - 1 - tile);   // tiles issued after this one
       vm_wait_dyn(after * per);
-      if (second ? has_pro2 : has_pro) transform(tile, sX(buf));
+      if (any_pro) transform(tile, sX(buf));
       lds_sync();
       // the buffer of tile - 1 is free (every wave is past its compute): refill it
       if (tile + NB - 1 < t_end) issue(tile + NB - 1, (idx + NB - 1) % NB);
@@ -750,7 +784,8 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
   // group at a time), then the partial slab part[split][co][tap][ci]
   dma_wait<0>();
   lds_sync();
-  float* red = reinterpret_cast<float*>(base);     // [KW-1][NJ][3 taps][16][64] floats
+  float* red = reinterpret_cast<float*>(base);     // [KW-1][NJ * CIW][3 taps][16][64] floats
+  const int wjc = wc * NJ + wj;                    // (chunk, co tile) of this wave
   float* out = p.partial + (long long)split * p.Cout * p.taps * p.Cin;
 #pragma unroll
   for (int tg = 0; tg < 3; ++tg) {
@@ -759,7 +794,7 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
       for (int t3 = 0; t3 < 3; ++t3)
 #pragma unroll
         for (int i = 0; i < 16; ++i)
-          red[((((wk - 1) * NJ + wj) * 3 + t3) * 16 + i) * 64 + lane] = acc[tg * 3 + t3][i];
+          red[((((wk - 1) * NJ * CIW + wjc) * 3 + t3) * 16 + i) * 64 + lane] = acc[tg * 3 + t3][i];
     }
     lds_sync();
     if (wk == 0) {
@@ -770,10 +805,10 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
         for (int i = 0; i < 16; ++i) {
           float v = acc[tg * 3 + t3][i];
 #pragma unroll
-          for (int w2 = 1; w2 < KW; ++w2) v += red[((((w2 - 1) * NJ + wj) * 3 + t3) * 16 + i) * 64 + lane];
+          for (int w2 = 1; w2 < KW; ++w2) v += red[((((w2 - 1) * NJ * CIW + wjc) * 3 + t3) * 16 + i) * 64 + lane];
           // D layout of 32x32: column n = lane & 31 (ci), row m = 8 (i / 4) + 4 (lane >> 5) + i % 4
           const int co = co0 + wj * 32 + 8 * (i >> 2) + 4 * (lane >> 5) + (i & 3);
-          const int ci = ci0 + (lane & 31);
+          const int ci = ci0 + wc * BK + (lane & 31);
           if (co < p.Cout && ci < p.Cin) out[((long long)co * p.taps + tap) * p.Cin + ci] = v;
         }
       }
@@ -1060,10 +1095,15 @@ void conv3_wgrad3_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
   // (32 output channels, 128-pixel tiles: the 3-deep ring variant; LDS = SS + 3 stages)
   constexpr int SMEM32R = Wg2Cfg<32, 128>::SS_BYTES + 3 * (Wg2Cfg<32, 128>::Y_BYTES + Wg2Cfg<32, 128>::X_BYTES);
   static_assert(2 * SMEM32R <= 160 * 1024, "two ring workgroups per CU");
+  // (64 output channels x two input chunks, 96-pixel tiles: dY + two halos per stage)
+  constexpr int SMEM64C2 = Wg2Cfg<64, 96>::SS_BYTES + 2 * (Wg2Cfg<64, 96>::Y_BYTES + 2 * Wg2Cfg<64, 96>::X_BYTES);
+  static_assert(2 * SMEM64C2 <= 160 * 1024, "two workgroups per CU");
   if (bco == 32 && pt == 128)
     hipLaunchKernelGGL((conv3_wgrad3_kernel<32, 128, 3>), dim3(grid), dim3(256), SMEM32R, st, a);
   else if (bco == 32)
     hipLaunchKernelGGL((conv3_wgrad3_kernel<32, 256>), dim3(grid), dim3(256), (Wg2Cfg<32, 256>::SMEM), st, a);
+  else if (bco == 64 && a.ciw == 2)   // two input chunks per workgroup, 96-pixel tiles
+    hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 96, 2, 2>), dim3(grid), dim3(256), SMEM64C2, st, a);
   else if (bco == 128)   // 96-pixel tiles: two 74 KB workgroups per CU
     hipLaunchKernelGGL((conv3_wgrad3_kernel<128, 96>), dim3(grid), dim3(256), (Wg2Cfg<128, 96>::SMEM), st, a);
   else if (pt == 256)

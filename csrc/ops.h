@@ -85,6 +85,7 @@ struct ConvWgradArgs {
   const bf16_t* dyy;
   const float* dys4;
   const float* dycoef;
+  int ciw;                        // v3: 32-channel input chunks per workgroup (1 or 2)
 };
 void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st);
 // LDS-DMA variant (1 x TH x 16 pixel tiles of conv3_wgrad2_pt(bco) pixels; 3-D: planes = 3,
