@@ -275,8 +275,12 @@ def main():
                 step(first - 1)                        # one untimed step with the new setting
                 ab[str(v)].append(round(timed(args.steps, first) / args.steps * 1e3, 3))
         setk(vals[0])
+        # (per-round ratios against the first value cancel clock / thermal drifts across rounds)
+        v0 = str(vals[0])
+        paired = {v: sorted(a / b for a, b in zip(x, ab[v0]))[len(x) // 2] for v, x in ab.items()}
         ab = {"knob": knob, "ms_per_step": ab,
-              "median_ms": {v: sorted(x)[len(x) // 2] for v, x in ab.items()}}
+              "median_ms": {v: sorted(x)[len(x) // 2] for v, x in ab.items()},
+              "median_paired_ratio": {v: round(r, 4) for v, r in paired.items()}}
     proxy = None
     if tr.reducer is not None and tr.reducer.proxy:
         proxy = [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in d.items()}

@@ -56,9 +56,16 @@ DDLPC_HOST_DEVICE int res_w_bytes(int Cin, int BN, bool tap8) {
 // SPLIT: 0 = one output; 1 = two outputs (concat data gradient), 8-byte stores; 2 = two
 // outputs split at a 32-channel boundary (Co1 % 32 == 0, launcher-checked): 16-byte pair
 // stores, each pair wholly in one output (a quarter of mode 1's store instructions)
-template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF, int SPLIT, bool BNB>
+// EPI (non-BNB epilogue form): 0 = one block, tiles channel-outer (the round-2 form); 1 = by
+// 16-pixel rows of MFMA tiles with item-independent pixel geometry and packed fp32 bias /
+// statistics; 2 = form 1 interleaved between the tap steps of the next stage's MFMAs from a
+// second accumulator set (measured 10-20% slower: the VALU delays the wave's next MFMAs).
+// BNB keeps form 0.
+template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF, int SPLIT, bool BNB, int EPI = 1>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_kernel(ConvFwdArgs p) {
   using C = RCfg<WM, WN, MT, NT, HALO, TAP8, NBUF>;
+  constexpr bool ILV = EPI == 2;
+  static_assert(!(ILV && BNB), "interleaved epilogue: not with the BN-backward epilogue");
   static_assert(NBUF == 2 || NBUF == 3, "halo ring depth");
   static_assert(!BNB || (!SPLIT && !TAP8), "BN-backward epilogue: single output, no image layer");
   constexpr int NW = C::NW, BN = C::BN;
@@ -197,7 +204,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     const int s0 = a_base * Cs + c0;                   // scalar part of the element offset
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
-      const bool ok = ((a_valid >> i) & 1u) && (full || c0 + a_sub8[i] < Cs);
+      const bool ok = ((a_valid >> i) & 1u) && (full || c0 + a_sub8[i] < Cs) && !(p.diag & 1);
       const unsigned off = ok ? (unsigned)(a_rel[i] * Cs + a_sub8[i] + s0) * 2u : kOOB;
       dma16(r, sA(buf) + (i * NW + wave) * 1024, off);
     }
@@ -239,7 +246,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   auto transform_A = [&](int chunk, int buf) {
     const int cbase = chunk * BK;
     const bool x2ch = cbase >= p.C1;                   // X2 chunk: prologue only if deferred
-    if (x2ch ? !has_pro2 : !has_pro) return;
+    if ((x2ch ? !has_pro2 : !has_pro) || (p.diag & 4)) return;
     transform_body(sA(buf), s_scale, s_shift, cbase, get_vmask(buf), x2ch ? p.Cin : p.C1);
   };
 
@@ -281,6 +288,87 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   constexpr bool PAIRS = (!SPLIT && (TAP8 || BN >= 64) && NT % 2 == 0) || SPLIT == 2;
   static_assert(SPLIT != 2 || (NT % 2 == 0 && BN % 32 == 0), "split pairs: 32-channel pairs");
   constexpr int EPI_STORES = SPLIT == 1 ? MT * NT * 2 : PAIRS ? MT * NT / 2 : MT * NT;
+  // (non-BNB) epilogue by 16-pixel rows of MFMA tiles, from accumulator set A: the per-lane
+  // pixel geometry is item-independent (no division in the loop), bias add and statistics
+  // run as packed fp32 pairs
+  int prow[MT], pcol[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
+    prow[mt] = pix / p.TW;
+    pcol[mt] = pix % p.TW;
+  }
+  struct EpiCtx { __amdgpu_buffer_rsrc_t r1, r2; int h0, w0; };
+  auto epi_ctx = [&](int kk) __attribute__((always_inline)) {
+    const Item it = item_of(kk);
+    EpiCtx e;
+    const int Co2 = p.Cout - p.Co1;
+    e.r1 = make_rsrc(p.Y1 + (long long)it.n_img * img_px * p.Co1, (unsigned)(img_px * p.Co1 * 2));
+    e.r2 = SPLIT ? make_rsrc(p.Y2 + (long long)it.n_img * img_px * Co2, (unsigned)(img_px * Co2 * 2)) : e.r1;
+    e.h0 = it.h0; e.w0 = it.w0;
+    return e;
+  };
+  auto epi_unit = [&](const EpiCtx& e, int mt, f32x4_t (&A)[MT][NT]) __attribute__((always_inline)) {
+    const int Co2 = p.Cout - p.Co1;
+    const int gw = e.w0 + pcol[mt], gh = e.h0 + prow[mt];
+    const bool pv = gw < p.W && gh < p.H;
+    const bool st_on = !(p.diag & 2);
+    const int lp = gh * p.W + gw;
+    uint2 pkv[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * g;
+      const bool ok = pv && co < p.Cout;
+      const f32x2_t b01 = {bias_r[nt][0], bias_r[nt][1]}, b23 = {bias_r[nt][2], bias_r[nt][3]};
+      const f32x2_t v01 = f32x2_t{A[mt][nt][0], A[mt][nt][1]} + b01;
+      const f32x2_t v23 = f32x2_t{A[mt][nt][2], A[mt][nt][3]} + b23;
+      const uint2 pk = make_uint2(pack2(v01.x, v01.y), pack2(v23.x, v23.y));
+      pkv[nt] = pk;
+      if constexpr (!PAIRS) {
+        const u32x2_t d = u32x2_t{pk.x, pk.y};
+        if constexpr (!SPLIT) {
+          unsigned o1 = ok && st_on ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
+          asm volatile("" : "+v"(o1));
+          __builtin_amdgcn_raw_buffer_store_b64(d, e.r1, o1, 0, 0);
+        } else {
+          const bool in1 = co < p.Co1;
+          unsigned o1 = (ok && st_on && in1) ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
+          unsigned o2 = (ok && st_on && !in1) ? (unsigned)(lp * Co2 + co - p.Co1) * 2u : kOOB;
+          asm volatile("" : "+v"(o1), "+v"(o2));
+          __builtin_amdgcn_raw_buffer_store_b64(d, e.r1, o1, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(d, e.r2, o2, 0, 0);
+        }
+      }
+      // statistics of the stored (bf16-rounded) values; masked lanes add zeros
+      const f32x2_t r01 = {ok ? lo_bf(pk.x) : 0.f, ok ? hi_bf(pk.x) : 0.f};
+      const f32x2_t r23 = {ok ? lo_bf(pk.y) : 0.f, ok ? hi_bf(pk.y) : 0.f};
+      f32x2_t a01 = {s1[nt][0], s1[nt][1]}, a23 = {s1[nt][2], s1[nt][3]};
+      f32x2_t q01 = {s2[nt][0], s2[nt][1]}, q23 = {s2[nt][2], s2[nt][3]};
+      a01 += r01; a23 += r23;
+      q01 = __builtin_elementwise_fma(r01, r01, q01);
+      q23 = __builtin_elementwise_fma(r23, r23, q23);
+      s1[nt][0] = a01.x; s1[nt][1] = a01.y; s1[nt][2] = a23.x; s1[nt][3] = a23.y;
+      s2[nt][0] = q01.x; s2[nt][1] = q01.y; s2[nt][2] = q23.x; s2[nt][3] = q23.y;
+    }
+    if constexpr (PAIRS) {
+#pragma unroll
+      for (int np = 0; np < NT / 2; ++np) {
+        const uint4 q = pair16(pkv[2 * np], pkv[2 * np + 1]);
+        const int co = co0 + wn * (NT * 16) + np * 32 + pair16_ch(lane);
+        if constexpr (SPLIT == 2) {
+          const bool in1 = co0 + wn * (NT * 16) + np * 32 < p.Co1;
+          unsigned o = pv && st_on && co < p.Cout ? (unsigned)(in1 ? lp * p.Co1 + co : lp * Co2 + co - p.Co1) * 2u
+                                                 : kOOB;
+          asm volatile("" : "+v"(o));
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, in1 ? e.r1 : e.r2, o, 0, 0);
+        } else {
+          unsigned o1 = pv && st_on && co < p.Cout ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
+          asm volatile("" : "+v"(o1));
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, e.r1, o1, 0, 0);
+        }
+      }
+    }
+  };
   // BNB: y at this item's output pixels, loaded into VGPRs at the item's last stage (before
   // that stage's halo DMA) and consumed by its epilogue one stage later
   constexpr int YL = BNB ? MT * NT : 0;
@@ -301,9 +389,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
       }
     }
   };
-  auto epilogue = [&](int k) {
+  auto epilogue_blk = [&](int k) {
     const Item it = item_of(k);
     const int Co2 = p.Cout - p.Co1;
+    const bool st_on = !(p.diag & 2);
     const auto r1 = make_rsrc(p.Y1 + (long long)it.n_img * img_px * p.Co1, (unsigned)(img_px * p.Co1 * 2));
     const auto r2 = SPLIT ? make_rsrc(p.Y2 + (long long)it.n_img * img_px * Co2, (unsigned)(img_px * Co2 * 2)) : r1;
     // pass 1, channel tiles outer: bias, bf16 rounding, statistics (the BNB constants of one
@@ -320,6 +409,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
         const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
         const int gw = it.w0 + pix % p.TW, gh = it.h0 + pix / p.TW;
         const bool ok = gw < p.W && gh < p.H && co < p.Cout;
+        const bool okst = ok && st_on;
         float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bias_r[nt][i];
@@ -330,13 +420,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
           const int lp = gh * p.W + gw;
           const u32x2_t d = u32x2_t{pk.x, pk.y};
           if constexpr (!SPLIT) {
-            unsigned o1 = ok ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
+            unsigned o1 = okst ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
             asm volatile("" : "+v"(o1));
             __builtin_amdgcn_raw_buffer_store_b64(d, r1, o1, 0, 0);
           } else {
             const bool in1 = co < p.Co1;
-            unsigned o1 = (ok && in1) ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
-            unsigned o2 = (ok && !in1) ? (unsigned)(lp * Co2 + co - p.Co1) * 2u : kOOB;
+            unsigned o1 = (okst && in1) ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
+            unsigned o2 = (okst && !in1) ? (unsigned)(lp * Co2 + co - p.Co1) * 2u : kOOB;
             asm volatile("" : "+v"(o1), "+v"(o2));
             __builtin_amdgcn_raw_buffer_store_b64(d, r1, o1, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b64(d, r2, o2, 0, 0);
@@ -365,7 +455,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
       for (int mt = 0; mt < MT; ++mt) {
         const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
         const int gw = it.w0 + pix % p.TW, gh = it.h0 + pix / p.TW;
-        const bool valid = gw < p.W && gh < p.H;
+        const bool valid = gw < p.W && gh < p.H && st_on;
         const int lp = gh * p.W + gw;                   // pixel within the image (32-bit)
 #pragma unroll
         for (int np = 0; np < NT / 2; ++np) {
@@ -385,6 +475,20 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
           }
         }
       }
+    }
+  };
+
+  auto epilogue = [&](int kk) __attribute__((always_inline)) {
+    if constexpr (BNB || EPI == 0) {
+      epilogue_blk(kk);
+    } else {
+      const EpiCtx e = epi_ctx(kk);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) epi_unit(e, mt, acc);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     }
   };
 
@@ -410,8 +514,17 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     __builtin_amdgcn_s_setprio(1);
   int k = 0, c = 0;
   bool epi_prev = false;                              // stage s-1 ran an epilogue
+  bool epi_prev2 = false;                             // stage s-2 ran an epilogue (ILV)
   for (int s = 0; s < S; ++s) {
-    if (NBUF == 2) {
+    if constexpr (ILV) {
+      // a stage issues [DMA(s+NBUF-1)] then, inside its compute, [its epilogue's stores]:
+      // younger than DMA(s) are stores(s-2), DMA(s+1), stores(s-1) (NBUF 3) / stores(s-1)
+      if (NBUF == 2) {
+        if (epi_prev) vm_wait<EPI_STORES>(); else vm_wait<0>();
+      } else {
+        vm_wait_dyn((epi_prev2 ? EPI_STORES : 0) + (s + 1 < S ? C::A_ITERS : 0) + (epi_prev ? EPI_STORES : 0));
+      }
+    } else if (NBUF == 2) {
       vm_wait<0>();                                   // DMA(s) is the youngest op
     } else {
       // younger than DMA(s): s == 0 -> DMA(1); s >= 1 -> [stores(s-1)] + [DMA(s+1)]
@@ -431,8 +544,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     const int buf = s % NBUF;
     if (!TAP8 && (has_pro || has_pro2)) transform_A(c, buf);
     lds_sync();
+    epi_prev2 = epi_prev;
     epi_prev = (c == 0 && s > 0);
-    if (epi_prev) {
+    if (epi_prev && !ILV) {
       // BNB, 3-deep ring: the y loads (issued before DMA(s+1)) must have landed
       if (BNB && NBUF == 3) { if (s + 1 < S) vm_wait<C::A_ITERS>(); else vm_wait<0>(); }
       epilogue(k - 1);
@@ -451,7 +565,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     // (restrict-qualified operand pointers give the LDS reads alias scopes, so the compiler
     // does not make them wait for the next stage's in-flight LDS-DMA: vmcnt is managed by
     // hand above)
-    auto compute = [&](const char* __restrict__ A, const char* __restrict__ Wc) {
+    auto compute = [&](const char* __restrict__ A, const char* __restrict__ Wc, auto hook) {
     constexpr int KSTEPS = TAP8 ? 3 : 9;
     auto load_frags = [&](int j, uint4 (&xf)[MT], uint4 (&wf)[NT]) {
       if (TAP8) {
@@ -477,10 +591,37 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = mfma16x16x32(wf[j & 1][nt], xf[j & 1][mt], acc[mt][nt]);
       if (p.prio & 2) __builtin_amdgcn_s_setprio(0);
+      hook(j);
       __builtin_amdgcn_sched_barrier(0);
     }
     };
-    compute(sA(buf), TAP8 ? sW : sW + c * 9 * BN * ROWB);
+    const char* Wst = TAP8 ? sW : sW + c * 9 * BN * ROWB;
+    auto no_hook = [](int) {};
+    if constexpr (ILV) {
+      if (epi_prev) {
+        // item k-1's epilogue from a copy of its accumulators, one MFMA-tile row after every
+        // (8 / MT)-th tap step (VALU work under the MFMA stream)
+        const EpiCtx e = epi_ctx(k - 1);
+        f32x4_t accP[MT][NT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) { accP[mt][nt] = acc[mt][nt]; acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f}; }
+        constexpr int STEP = 8 / MT;
+        if (!(p.diag & 8)) {
+          compute(sA(buf), Wst, [&](int j) __attribute__((always_inline)) {
+            if (j % STEP == 0 && j / STEP < MT) epi_unit(e, j / STEP, accP);
+          });
+        } else {
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) epi_unit(e, mt, accP);
+        }
+      } else if (!(p.diag & 8)) {
+        compute(sA(buf), Wst, no_hook);
+      }
+    } else if (!(p.diag & 8)) {
+      compute(sA(buf), Wst, no_hook);
+    }
     k = k1; c = c1;
   }
   if (S > 0) {
@@ -541,32 +682,51 @@ int res_smem(const ResVariant& v, int Cin, int C1, bool pro, bool bnb) {   // C1
   return (bnb ? 16 * bn : res_ss_bytes(C1, pro)) + res_w_bytes(Cin, bn, v.tap8) + v.nbuf * a_bytes;
 }
 
-template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF>
-void launch_res(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
+template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF, int EPIc>
+void launch_res_i(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
   a.prio = knob("CONV_PRIO", 2);
+  // diagnostics only (results wrong): bit 0 no halo DMA, 1 no output stores, 2 no prologue
+  // transform, 3 no MFMA stage compute
+  a.diag = knob("DIAG_RES", 0);
   constexpr int BNc = WN * NT * 16;
   if (a.Co1 < a.Cout) {
     // split output at a 32-channel boundary: 16-byte pair stores (DDLPC_RES_SPLIT_PAIRS=0: off)
     if constexpr (NT % 2 == 0 && BNc % 32 == 0 && !TAP8) {
       if (a.Co1 % 32 == 0 && knob("RES_SPLIT_PAIRS", 1)) {
-        hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 2, false>), dim3(grid),
+        hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 2, false, EPIc>), dim3(grid),
                            dim3(WM * WN * 64), smem, st, a);
         return;
       }
     }
-    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 1, false>), dim3(grid),
+    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 1, false, (EPIc == 2 && !TAP8) ? 1 : EPIc>), dim3(grid),
                        dim3(WM * WN * 64), smem, st, a);
   } else if constexpr (!TAP8 && BNc != 96) {
     if (a.bnb_y != nullptr)
       hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 0, true>), dim3(grid),
                          dim3(WM * WN * 64), smem, st, a);
     else
-      hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 0, false>), dim3(grid),
+      hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 0, false, EPIc>), dim3(grid),
                          dim3(WM * WN * 64), smem, st, a);
   } else {
-    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 0, false>), dim3(grid),
+    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 0, false, EPIc>), dim3(grid),
                        dim3(WM * WN * 64), smem, st, a);
   }
+}
+
+// DDLPC_RES_EPI: non-BNB epilogue form (kernel EPI above; form 2 only on the 3-deep MT-4
+// variants, the others would need more than 256 VGPRs: scratch spills)
+template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF>
+void launch_res(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
+  // default: form 0 on the 8-wave 32-channel tiles (form 1 measured 1-1.5% slower there),
+  // form 1 elsewhere (image layer -19%, 64/96-channel tiles -6..-11%; same-process A/B at
+  // batch 256, profiles/r3s/res_epi_ab_b256_r3s25.txt)
+  const int epi_auto = (WM == 8 && WN == 1 && NT == 2 && !TAP8) ? 0 : 1;
+  const int epi = a.bnb_y != nullptr ? 0 : knob("RES_EPI", -1) < 0 ? epi_auto : knob("RES_EPI", -1);
+  if constexpr (NBUF == 3 && MT == 4) {
+    if (epi == 2) { launch_res_i<WM, WN, MT, NT, HALO, TAP8, NBUF, 2>(a, grid, smem, st); return; }
+  }
+  if (epi == 0) launch_res_i<WM, WN, MT, NT, HALO, TAP8, NBUF, 0>(a, grid, smem, st);
+  else launch_res_i<WM, WN, MT, NT, HALO, TAP8, NBUF, 1>(a, grid, smem, st);
 }
 
 }  // namespace
