@@ -241,13 +241,51 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
       }
     }
   };
+  // batched form: a lane's 8-channel group is the same in every piece it DMAs (the XOR
+  // swizzle flips bit 1 of the piece index by bit 4 of the lane only), so the chunk's 16
+  // constants are read once per stage instead of once per piece, all A_ITERS piece reads
+  // issue before any math, and padding / masked pieces are re-zeroed by a select instead of
+  // a branch around each piece
+  const int sub8_l = TAP8 ? 0 : ((lane & 3) ^ (((lane >> 4) & 1) << 1)) << 3;
+  auto transform_batched = [&](char* __restrict__ Ab, const float* __restrict__ scl,
+                               const float* __restrict__ shf_, int cbase, uint32_t vm, int climit) {
+    const int c8 = cbase + sub8_l;
+    const bool cok = c8 < climit;
+    const float4* scp = reinterpret_cast<const float4*>(scl + (cok ? c8 : 0));
+    const float4* shp = reinterpret_cast<const float4*>(shf_ + (cok ? c8 : 0));
+    const float4 sa = scp[0], sb = scp[1], ha = shp[0], hb = shp[1];
+    const float scf[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+    const float shf[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
+    uint4 v[C::A_ITERS];
+#pragma unroll
+    for (int i = 0; i < C::A_ITERS; ++i)
+      v[i] = *reinterpret_cast<const uint4*>(Ab + ((i * NW + wave) * 64 + lane) * 16);
+#pragma unroll
+    for (int i = 0; i < C::A_ITERS; ++i) {
+      const bool ok = ((vm >> i) & 1u) && cok;
+      const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+      uint32_t o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x2_t x = {lo_bf(w[j]), hi_bf(w[j])};
+        const f32x2_t sc2 = {scf[2 * j], scf[2 * j + 1]};
+        const f32x2_t sh2 = {shf[2 * j], shf[2 * j + 1]};
+        const f32x2_t y2 = __builtin_elementwise_fma(x, sc2, sh2);
+        const uint32_t pk = __builtin_bit_cast(uint32_t, __builtin_convertvector(y2, bf16x2_t));
+        const i16x2_t m = __builtin_elementwise_max(__builtin_bit_cast(i16x2_t, pk), i16x2_t{0, 0});
+        o[j] = ok ? __builtin_bit_cast(uint32_t, m) : 0u;
+      }
+      *reinterpret_cast<uint4*>(Ab + ((i * NW + wave) * 64 + lane) * 16) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  };
   // (restrict-qualified LDS pointers: alias scopes keep the compiler from waiting on the
   // in-flight halo DMAs of later ring slots before these reads)
   auto transform_A = [&](int chunk, int buf) {
     const int cbase = chunk * BK;
     const bool x2ch = cbase >= p.C1;                   // X2 chunk: prologue only if deferred
     if ((x2ch ? !has_pro2 : !has_pro) || (p.diag & 4)) return;
-    transform_body(sA(buf), s_scale, s_shift, cbase, get_vmask(buf), x2ch ? p.Cin : p.C1);
+    if (p.rxf) transform_batched(sA(buf), s_scale, s_shift, cbase, get_vmask(buf), x2ch ? p.Cin : p.C1);
+    else transform_body(sA(buf), s_scale, s_shift, cbase, get_vmask(buf), x2ch ? p.Cin : p.C1);
   };
 
   // ---- per-lane fragment geometry
@@ -378,8 +416,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     const auto ry = make_rsrc(p.bnb_y + (long long)it.n_img * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
-      const int gw = it.w0 + pix % p.TW, gh = it.h0 + pix / p.TW;
+      const int gw = it.w0 + pcol[mt], gh = it.h0 + prow[mt];
       const bool valid = gw < p.W && gh < p.H;
       const int lp = gh * p.W + gw;
 #pragma unroll
@@ -406,8 +443,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
       if constexpr (BNB) kb = bnb_load(s_bnb, BN, wn * (NT * 16) + nt * 16 + 4 * g);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
-        const int gw = it.w0 + pix % p.TW, gh = it.h0 + pix / p.TW;
+        const int gw = it.w0 + pcol[mt], gh = it.h0 + prow[mt];
         const bool ok = gw < p.W && gh < p.H && co < p.Cout;
         const bool okst = ok && st_on;
         float v[4];
@@ -453,8 +489,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     if constexpr (PAIRS) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
-        const int gw = it.w0 + pix % p.TW, gh = it.h0 + pix / p.TW;
+        const int gw = it.w0 + pcol[mt], gh = it.h0 + prow[mt];
         const bool valid = gw < p.W && gh < p.H && st_on;
         const int lp = gh * p.W + gw;                   // pixel within the image (32-bit)
 #pragma unroll
@@ -688,6 +723,7 @@ void launch_res_i(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
   // diagnostics only (results wrong): bit 0 no halo DMA, 1 no output stores, 2 no prologue
   // transform, 3 no MFMA stage compute
   a.diag = knob("DIAG_RES", 0);
+  a.rxf = knob("RES_XFORM", 1);
   constexpr int BNc = WN * NT * 16;
   if (a.Co1 < a.Cout) {
     // split output at a 32-channel boundary: 16-byte pair stores (DDLPC_RES_SPLIT_PAIRS=0: off)

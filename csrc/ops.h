@@ -37,6 +37,7 @@ struct ConvFwdArgs {
   int ksplit;                     // >1: split the channel chunks, fp32 partials to `part`
   float* part;                    // [ksplit][npix][Cout] fp32 (ksplit > 1)
   long long npix;                 // N * D * H * W
+  int rxf;                        // resident kernel prologue transform: 1 = batched, branchless (DDLPC_RES_XFORM)
   int diag;                       // diagnostics only (DDLPC_DIAG_CONV): bit 0 skip weight DMA after stage 1, bit 1 skip halo DMA after chunk 1
   int prio;                       // wave priorities (DDLPC_CONV_PRIO): bit 0 = s_setprio 1 for the
                                   // second half of an 8-wave workgroup (static form), bit 1 =
