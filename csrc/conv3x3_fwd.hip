@@ -210,6 +210,42 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     const bool x2ch = cbase >= p.C1;                // X2 channels: prologue only if deferred
     if (x2ch ? !has_pro2 : !has_pro) return;
     const int climit = x2ch ? p.Cin : p.C1;
+    // batched form (DDLPC_CONV_XFORM=1; <= 6 pieces per lane — the 3-D halos' 11 would spill):
+    // the lane's 8-channel group is the same in every piece, so its 16 constants are read
+    // once; all piece reads issue before the math, and padding is re-zeroed by a select
+    // instead of a branch around each piece
+    if (C::A_ITERS <= 6 && p.rxf) {
+      const int c8 = cbase + sub8;
+      const bool cok = c8 < climit;
+      const float4* scp = reinterpret_cast<const float4*>(s_scale + (cok ? c8 : 0));
+      const float4* shp = reinterpret_cast<const float4*>(s_shift + (cok ? c8 : 0));
+      const float4 sa = scp[0], sb = scp[1], ha = shp[0], hb = shp[1];
+      const float scf[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+      const float shf[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
+      constexpr int NI = C::A_ITERS <= 6 ? C::A_ITERS : 1;
+      uint4 v[NI];
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        v[i] = *reinterpret_cast<const uint4*>(Abuf + ((i * C::NW + wave) * 64 + lane) * 16);
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const bool ok = cok && a_pix[i] >= 0;
+        const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x2_t x = {lo_bf(w[j]), hi_bf(w[j])};
+          const f32x2_t sc2 = {scf[2 * j], scf[2 * j + 1]};
+          const f32x2_t sh2 = {shf[2 * j], shf[2 * j + 1]};
+          const f32x2_t y2 = __builtin_elementwise_fma(x, sc2, sh2);
+          const uint32_t pk = __builtin_bit_cast(uint32_t, __builtin_convertvector(y2, bf16x2_t));
+          const i16x2_t m = __builtin_elementwise_max(__builtin_bit_cast(i16x2_t, pk), i16x2_t{0, 0});
+          o[j] = ok ? __builtin_bit_cast(uint32_t, m) : 0u;
+        }
+        *reinterpret_cast<uint4*>(Abuf + ((i * C::NW + wave) * 64 + lane) * 16) = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
       const int e = (i * C::NW + wave) * 64 + lane;    // same element this lane DMA'd
@@ -885,6 +921,7 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   a.diag = diag;
   a.prio = knob("CONV_PRIO", 2);
   a.ylead = knob("BNB_YLEAD", 1);      // 2 measured 1-3% slower per layer (profiles/r3s)
+  a.rxf = knob("CONV_XFORM", 1);
   constexpr int FDB_OK = !(DIMS == 3 && MT * NT >= 16) ? 1 : 0;
   if constexpr (NBB == 4) {
     if (conv_ilv()) {
@@ -915,6 +952,7 @@ void launch_cfg5(ConvFwdArgs& a, hipStream_t st) {
   a.stat_rows = grid;
   a.diag = knob("DIAG_CONV", 0);
   a.prio = knob("CONV_PRIO", 2);
+  a.rxf = knob("CONV_XFORM", 1);
   if (conv_pipe())
     hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 640, 2, 2, false, false>), dim3(grid),
                        dim3(C::NTH), C::SMEM, st, a);
