@@ -777,7 +777,11 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
   const int bn = a.Cout == 96 ? 96 : (a.Cout <= 32 || a.Cout % 64 != 0) ? 32 : 64;
   // preference: 3-deep halo rings (latency hiding) first; DDLPC_RES_DEPTH=2 prefers the
   // 2-deep, two-workgroups-per-CU variants (A/B experiments)
-  const int depth = knob("RES_DEPTH", 3);
+  // default (-1): 2-deep for the 64-channel tiles (variant 6: BN-backward data gradients
+  // 9-11% faster, the others 1-3.5%), 3-deep for the 32-channel tiles (the 2-deep 4-wave
+  // variant is 5-11% slower forward): profiles/r3s/res_depth_ab_b256_r3s33.txt
+  const int depth_k = knob("RES_DEPTH", -1);
+  const int depth = depth_k > 0 ? depth_k : (bn == 64 ? 2 : 3);
   int cand[3];
   int nc = 0;
   if (tap8) {
