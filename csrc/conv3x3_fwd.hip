@@ -266,6 +266,14 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 
   // ---- per-lane fragment geometry (item independent)
   const int g = lane >> 4;
+  // tile pixel -> (w, h, d) without integer division: TW is 8 or 16 and TW * TH (2-D) /
+  // TW * TH * TD with TH = 4 (3-D) is the tile (bindings.cpp conv_tile)
+  const int tw_sh = p.TW == 16 ? 4 : 3;
+  auto pix_geo = [&](int pix, int& pw, int& ph, int& pd) __attribute__((always_inline)) {
+    pw = pix & (p.TW - 1);
+    ph = DIMS == 3 ? (pix >> tw_sh) & 3 : pix >> tw_sh;
+    pd = DIMS == 3 ? pix >> (tw_sh + 2) : 0;
+  };
   // (LEAN: 16-wide pixel tiles, TW == 16 — launcher-enforced — so the halo pixel of tile mt
   // is hp_lean + mt * HW2: one register instead of MT)
   const int hp_lean = (wm * MT) * HW2 + (lane & 15);
@@ -332,7 +340,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
-      const int gw = it.w0 + pix % p.TW, gh = it.h0 + (pix / p.TW) % p.TH;
+      int pw, ph, pd;
+      pix_geo(pix, pw, ph, pd);
+      const int gw = it.w0 + pw, gh = it.h0 + ph;
       const bool valid = gw < p.W && gh < p.H;
       const int lpix = gh * p.W + gw;
 #pragma unroll
@@ -368,8 +378,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
-        const int pw = pix % p.TW, ph = (pix / p.TW) % p.TH;
-        const int pd = DIMS == 3 ? pix / (p.TW * p.TH) : 0;
+        int pw, ph, pd;
+        pix_geo(pix, pw, ph, pd);
         const int gw = it.w0 + pw, gh = it.h0 + ph, gd = it.d0 + pd;
         const bool valid = gw < p.W && gh < p.H && gd < p.D;
         const int lpix = (gd * p.H + gh) * p.W + gw;        // pixel within the image (32-bit)
@@ -435,8 +445,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
-      const int pw = pix % p.TW, ph = (pix / p.TW) % p.TH;
-      const int pd = DIMS == 3 ? pix / (p.TW * p.TH) : 0;
+      int pw, ph, pd;
+      pix_geo(pix, pw, ph, pd);
       const int gw = it.w0 + pw, gh = it.h0 + ph, gd = it.d0 + pd;
       const bool valid = gw < p.W && gh < p.H && gd < p.D;
       const int lpix = (gd * p.H + gh) * p.W + gw;

@@ -683,6 +683,39 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
       dok = dx >= 0 && dx < p.D;
       h0 = th_i * TH; w0 = tw_i * 16;
     }
+    if (NB == 2 && Cfg::X_ITERS <= 6 && p.xf) {
+      // batched form: all piece reads issue before the math (packed fp32 FMA, bf16 rounding,
+      // ReLU as a packed 16-bit max), padding re-zeroed by a select instead of a branch
+      constexpr int NI = Cfg::X_ITERS <= 6 ? Cfg::X_ITERS : 1;
+#pragma unroll
+      for (int cw = 0; cw < CIW; ++cw) {
+        if (!xpro[cw]) continue;
+        char* X = X0 + cw * Cfg::X_BYTES;
+        uint4 v[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+          if ((i * 4 + wave) < Cfg::X_INSTR) v[i] = *reinterpret_cast<const uint4*>(X + ((i * 4 + wave) * 64 + lane) * 16);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          if ((i * 4 + wave) >= Cfg::X_INSTR) break;
+          const bool ok = x_pix[i] >= 0 && xch_ok[cw];
+          const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+          uint32_t o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x2_t x = {lo_bf(w[j]), hi_bf(w[j])};
+            const f32x2_t sc2 = {psc[cw][2 * j], psc[cw][2 * j + 1]};
+            const f32x2_t sh2 = {psh[cw][2 * j], psh[cw][2 * j + 1]};
+            const f32x2_t y2 = __builtin_elementwise_fma(x, sc2, sh2);
+            const uint32_t pk = __builtin_bit_cast(uint32_t, __builtin_convertvector(y2, bf16x2_t));
+            const i16x2_t m = __builtin_elementwise_max(__builtin_bit_cast(i16x2_t, pk), i16x2_t{0, 0});
+            o[j] = ok ? __builtin_bit_cast(uint32_t, m) : 0u;
+          }
+          *reinterpret_cast<uint4*>(X + ((i * 4 + wave) * 64 + lane) * 16) = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int cw = 0; cw < CIW; ++cw) {
       if (!xpro[cw]) continue;
