@@ -70,7 +70,8 @@ def _parse():
                     help="accumulation micro-batches in flight on this many HIP streams "
                          "(-1: auto, 3 for small accumulated micro-batches)")
     ap.add_argument("--reserve-cus", type=int, default=-1,
-                    help="CUs kept out of persistent kernel grids (-1: 8 under DP, else 0)")
+                    help="CUs kept out of persistent kernel grids (-1: auto = 0, measured: "
+                         "see docs/PERF.md 'Data-parallel overlap')")
     ap.add_argument("--comm-proxy", type=int, default=0,
                     help="1 GPU: stand-in collective per gradient bucket for a world of N "
                          "(streaming kernel on a third stream; measures launch-to-finish "
@@ -262,11 +263,15 @@ def main():
         knob, vals = args.ab.split(":")
         vals = [int(v) for v in vals.split(",")]
 
+        prev = []
+
         def setk(v):
             if knob == "CU_RESERVE":
                 F.set_cu_reserve(v)
             else:
-                F.set_knob(knob, v)
+                p = F.set_knob(knob, v)
+                if not prev:
+                    prev.append(p)                     # the value before the A/B
         ab = {str(v): [] for v in vals}
         for r in range(args.ab_rounds):
             for v in vals:
@@ -274,7 +279,11 @@ def main():
                 first += args.steps + 2
                 step(first - 1)                        # one untimed step with the new setting
                 ab[str(v)].append(round(timed(args.steps, first) / args.steps * 1e3, 3))
-        setk(vals[0])
+        # restore the pre-A/B state (INT64_MIN clears the override: environment / default)
+        if knob == "CU_RESERVE":
+            F.set_cu_reserve(tr.reserve_cus)
+        elif prev:
+            F.set_knob(knob, prev[0])
         # (per-round ratios against the first value cancel clock / thermal drifts across rounds)
         v0 = str(vals[0])
         paired = {v: sorted(a / b for a, b in zip(x, ab[v0]))[len(x) // 2] for v, x in ab.items()}

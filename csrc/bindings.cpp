@@ -106,7 +106,11 @@ int64_t set_knob(const std::string& name, int64_t value) {
   auto& m = knob_map();
   auto it = m.find(name);
   const int64_t prev = it != m.end() ? it->second : INT64_MIN;
-  m[name] = (int)value;
+  if (value == INT64_MIN) {             // clear: the next knob() re-reads the environment
+    if (it != m.end()) m.erase(it);
+  } else {
+    m[name] = (int)value;
+  }
   return prev;
 }
 

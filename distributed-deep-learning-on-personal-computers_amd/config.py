@@ -121,6 +121,12 @@ class TrainConfig:
                                          # HIP streams (each replaying its own graph); -1 =
                                          # auto: 3 for small accumulated micro-batches (the
                                          # reference's batch-1 regime), else 1 = one by one
+    bn_window: int = -1                  # accumulation micro-batches run as ONE batched pass with
+                                         # per-micro-batch BatchNorm groups (same math as the
+                                         # micro-batches one by one: weights are fixed inside
+                                         # the window, train-mode BN normalises per micro-batch):
+                                         # 0 = off, k >= 2 = up to k micro-batches per pass,
+                                         # -1 = auto (small accumulated micro-batches, HIP engine)
     recompute: int = 0                   # HIP engine activation recompute in backward (SURVEY 5.7,
                                          # batches beyond HBM): 1 = each block's first conv output,
                                          # 2 = both conv outputs of blocks that hand out a

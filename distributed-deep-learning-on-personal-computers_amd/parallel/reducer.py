@@ -101,7 +101,11 @@ class GradBucketReducer:
         for b in self.buckets:
             for p in b.params:
                 self._bucket_of[id(p)] = b
-        self._sync = True
+        # readiness is armed explicitly per accumulation window: only ``prepare(sync=True)``
+        # (the window's last micro-batch) arms it and ``finish()`` disarms it, so a fresh
+        # reducer — or one between windows — never launches a collective on a partially
+        # accumulated gradient (ref.py:756-766: no exchange until the 50th micro-batch)
+        self._sync = False
         self._seen = set()
         self._hooks = []
         # readiness: autograd post-accumulate hooks (stock PyTorch modules), or — with
@@ -146,7 +150,8 @@ class GradBucketReducer:
             self._sync = prev
 
     def prepare(self, sync: bool = True):
-        """Call before each micro-batch backward: ``sync`` only on the last one."""
+        """Call before each micro-batch backward: ``sync`` only on the last one of the
+        accumulation window (arms the bucket launches; ``finish()`` disarms them)."""
         self._sync = sync
         if sync:
             self._seen = set()
@@ -270,6 +275,7 @@ class GradBucketReducer:
             return
         if self.codec != "none" and self.codec_scale == "global":
             self._finish_global_codec()
+            self._sync = False
             return
         for b in self.buckets:
             if not b.launched:
@@ -293,7 +299,7 @@ class GradBucketReducer:
             else:
                 b.work.wait()
             b.work = None
-        self._sync = True
+        self._sync = False                          # disarmed until the next window's last micro-batch
 
     def _decode_bucket(self, b: _Bucket):
         from ..ops import codec_ops

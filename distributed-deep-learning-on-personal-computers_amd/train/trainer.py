@@ -140,12 +140,19 @@ class Trainer:
                                       shard=cfg.shard_data, shuffle=cfg.shuffle, seed=cfg.seed)
         if cfg.resume:
             path = latest_checkpoint(cfg.ckpt_dir) if cfg.resume == "auto" else cfg.resume
-            if path and os.path.exists(path):
-                self.load(path)
-            elif cfg.resume != "auto" and self.rank == 0:
+            exists = bool(path) and os.path.exists(path)
+            if cfg.resume != "auto":
                 # an explicit path must exist on rank 0 (its state is broadcast below); other
-                # ranks may lack the file (no shared filesystem) and receive rank 0's state
-                raise FileNotFoundError(f"resume checkpoint not found: {cfg.resume}")
+                # ranks may lack the file (no shared filesystem) and receive rank 0's state.
+                # Every rank learns rank 0's verdict, so a bad path fails the whole job at
+                # once instead of leaving ranks > 0 blocked in the state broadcast
+                found = torch.tensor([1.0 if exists else 0.0], device=self.device)
+                if self.world > 1:
+                    dist.broadcast(found, src=0)
+                if found.item() == 0.0:
+                    raise FileNotFoundError(f"resume checkpoint not found on rank 0: {cfg.resume}")
+            if exists:
+                self.load(path)
             # only rank 0 writes checkpoints: on machines without a shared filesystem the
             # other ranks find none, so rank 0's restored state is authoritative
             self._broadcast_state()
@@ -349,6 +356,10 @@ class Trainer:
         the same weights as in the one-by-one loop.  The final micro-batch of the window
         runs on the caller's stream as usual (it triggers the gradient exchange)."""
         eng = self.model._engine
+        if self.reducer is not None:
+            # accumulation micro-batches: no collective (the readiness callbacks of their
+            # backwards must not launch bucket all-reduces on a partial gradient)
+            self.reducer.prepare(sync=False)
         K = self.micro_streams
         cur = torch.cuda.current_stream(self.device)
         streams = self._ms_streams(K, cur)

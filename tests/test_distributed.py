@@ -132,3 +132,55 @@ def _fault(rank, world):
 def test_fault_injection_dead_peer_raises_not_hangs():
     out = run(_fault, 2, timeout=120, allow_fail=True)
     assert 0 in out and out[0][0] == "err", out      # rank 0 errors out instead of hanging
+
+
+def _fresh_reducer_arming(rank, world):
+    """A fresh reducer (and one after ``finish()``) is disarmed: readiness reports from an
+    accumulation micro-batch's backward launch nothing; only ``prepare(sync=True)`` arms."""
+    import torch.nn.functional as F
+    from ddlpc.parallel import GradBucketReducer, broadcast_module, flatten_module, init_distributed
+    init_distributed(device="cpu")
+    m = _small_model().eval()
+    flat = flatten_module(m)
+    broadcast_module(m)
+    red = GradBucketReducer(flat, bucket_mb=0.01)
+    x, y = _batch(100 + rank)
+    F.cross_entropy(m(x), y).backward()              # no prepare(): accumulation
+    n_fresh = red.stats["launched_in_backward"]
+    red.prepare(sync=True)
+    F.cross_entropy(m(x), y).backward()
+    n_armed = red.stats["launched_in_backward"]
+    red.finish()
+    F.cross_entropy(m(x), y).backward()              # after the exchange: disarmed again
+    return {"fresh": n_fresh, "armed": n_armed, "after": red.stats["launched_in_backward"],
+            "buckets": len(red.buckets)}
+
+
+def test_fresh_reducer_is_disarmed():
+    res = run(_fresh_reducer_arming, 2)
+    for r in (0, 1):
+        o = res[r]
+        assert o["fresh"] == 0 and o["armed"] == o["buckets"] > 1 and o["after"] == o["armed"], o
+
+
+def _resume_missing(rank, world, tmp):
+    from ddlpc.config import ModelConfig, TrainConfig
+    from ddlpc.train.trainer import Trainer
+    cfg = TrainConfig(model=ModelConfig(out_classes=2, depth=2, width_divisor=16), tile=16,
+                      num_samples=4, test_holdout=0, timeout_s=600,
+                      resume=tmp + "/no_such_ckpt.pt")
+    try:
+        Trainer(cfg, device="cpu")
+    except FileNotFoundError as e:
+        return f"raised: {e}"
+    return "no error"
+
+
+def test_missing_resume_path_fails_every_rank_fast(tmp_path):
+    """An explicit resume path missing on rank 0 raises on EVERY rank at once (ranks > 0
+    must not block in the state broadcast until the 30-minute collective timeout)."""
+    import time
+    t0 = time.time()
+    res = run(_resume_missing, 2, (str(tmp_path),), timeout=120)
+    assert all(str(v).startswith("raised") for v in res.values()), res
+    assert time.time() - t0 < 100

@@ -40,8 +40,7 @@ def _dp_rank(rank, world, bucket_mb, side, overlap, codec="none", accum=1, wire=
     # same micro-batches; the bucketed exchange overlaps the LAST micro-batch's backward
     # (ms > 1: the accumulation micro-batches on concurrent streams first)
     if ms > 1:
-        red.prepare(sync=False)
-        tr._concurrent_micros(mbs[:-1])
+        tr._concurrent_micros(mbs[:-1])        # must disarm the reducer by itself
         mbs_loop = [(accum - 1, mbs[-1])]
     else:
         mbs_loop = list(enumerate(mbs))
@@ -113,6 +112,85 @@ def test_dp_concurrent_micro_streams_two_ranks():
         assert o["launched"] == o["buckets"] > 1, o
         assert o["max_err"] <= 1e-5 * max(o["scale"], 1.0), o
         assert o["replicas_equal"], o
+
+
+def _dp_fresh_trainer_steps(rank, world, reduce, window):
+    """Fresh Trainer, first optimizer step through ``train_step`` (accumulation 6, 3 concurrent
+    micro-batch streams — the auto schedule of the reference's regime — or one batched window
+    with per-image BatchNorm groups).  The gradient handed to Adam must equal the rank-weighted
+    sum of every rank's sequentially accumulated local gradient; again after re-bucketing."""
+    import os
+    os.environ["LOCAL_RANK"] = "0"
+    import torch.distributed as dist
+    from ddlpc.config import ModelConfig, TrainConfig
+    from ddlpc.data import device_random_batch
+    from ddlpc.parallel import codec as C
+    from ddlpc.train.trainer import Trainer
+    accum = 6
+    cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=1,
+                      num_samples=1, test_holdout=0, impl="hip", backend="gloo",
+                      bucket_mb=1.0, accum_steps=accum, reduce=reduce, micro_streams=3,
+                      bn_window=window)
+    tr = Trainer(cfg, device="cuda")
+    eng = tr.model._engine
+    captured = []
+    step0 = tr.optimizer.step
+
+    def step_capture(*a, **k):
+        captured.append(tr.flat.grad_buf.clone())
+        return step0(*a, **k)
+    tr.optimizer.step = step_capture
+    out = []
+    for rnd, bucket_mb in enumerate((None, 0.5)):
+        if bucket_mb is not None:
+            tr.set_bucket_mb(bucket_mb)            # a fresh reducer again
+        red = tr.reducer
+        mbs = [device_random_batch(1, 64, 6, tr.device, seed=7 + rank + 100 * j + 1000 * rnd)
+               for j in range(accum)]
+        # the local accumulated gradient, sequentially, without touching the reducer
+        ready = eng.grad_ready
+        eng.grad_ready = None
+        for x, y in mbs:
+            loss, _ = tr.model.loss_and_correct(x, y)
+            loss.backward()
+        eng.grad_ready = ready
+        torch.cuda.synchronize()
+        g_local = tr.flat.grad_buf.clone()
+        tr.optimizer.zero_grad()
+        n0 = red.stats["launched_in_backward"]
+        tr.train_step(mbs)
+        torch.cuda.synchronize()
+        gl = [torch.empty_like(g_local) for _ in range(world)]
+        dist.all_gather(gl, g_local)
+        weights = C.reference_weights(world) if reduce == "reference" else [red.weight] * world
+        want = sum(w * g for w, g in zip(weights, gl))
+        got = captured[-1]
+        out.append({"max_err": float((got - want).abs().max()),
+                    "scale": float(want.abs().max()),
+                    "launched": red.stats["launched_in_backward"] - n0,
+                    "buckets": len(red.buckets)})
+    p = tr.flat.param_buf.clone()
+    ps = [torch.empty_like(p) for _ in range(world)]
+    dist.all_gather(ps, p)
+    tr.close()
+    return {"rounds": out, "replicas_equal": all(torch.equal(ps[0], q) for q in ps)}
+
+
+@pytest.mark.parametrize("reduce,window", [("mean", 0), ("reference", 0), ("mean", 6), ("reference", 3)])
+def test_dp_first_step_from_fresh_trainer(reduce, window):
+    """Regression (round-3 review): the concurrent micro-batch path entered a fresh reducer
+    armed, so the first accumulation window launched bucket all-reduces on a partial
+    gradient.  Step 1 and the step after ``set_bucket_mb`` must exchange exactly the
+    accumulated gradient, with every bucket launched once, from the last micro-batch."""
+    res = run(_dp_fresh_trainer_steps, 2, (reduce, window), timeout=240)
+    for r in (0, 1):
+        o = res[r]
+        assert o["replicas_equal"], o
+        for rd in o["rounds"]:
+            assert rd["launched"] == rd["buckets"] > 1, o
+            # window: batched convs sum in another order than batch-1 micro-batches
+            tol = (2e-3 if window else 1e-5) * max(rd["scale"], 1.0)
+            assert rd["max_err"] <= tol, o
 
 
 @pytest.mark.parametrize("codec,accum,wire", [("fp16_absmax", 1, "fp32"), ("int8_absmax", 1, "fp32"),
