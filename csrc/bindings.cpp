@@ -632,6 +632,102 @@ std::vector<at::Tensor> bn_grad_coefs(const at::Tensor& partial, const at::Tenso
   return {coefs, dgamma, dbeta};
 }
 
+// ------------------------------------------------------------------------ BatchNorm groups
+// per-micro-batch statistics groups (Trainer bn_window): y holds `groups` micro-batches one
+// after another; -> stats4 [groups][4][C]; with an arena [rows][...] the group's
+// (mean | unbiased var) goes to arena row g at column aoff (in-order running-stat update)
+at::Tensor bn_group_finalize(const at::Tensor& y, int64_t groups, const at::Tensor& gamma,
+                             const at::Tensor& beta, double eps,
+                             const c10::optional<at::Tensor>& arena, int64_t aoff) {
+  CHECK_DEV(y); CHECK_CONTIG(y); CHECK_BF16(y); CHECK_F32(gamma); CHECK_F32(beta);
+  c10::DeviceGuard guard(y.device());
+  const Geo g = geo_of(y);
+  TORCH_CHECK(groups >= 1 && groups <= 1024 && g.N % groups == 0,
+              "bn_group_finalize: 1 <= groups <= 1024 dividing the batch");
+  TORCH_CHECK(bn_group_supported(g.dims, false, g.D, g.H, g.W, g.C),
+              "bn_group_finalize: C / 8 must be a power of two <= 256");
+  const long long gpix = (long long)(g.N / groups) * g.D * g.H * g.W;
+  const int nb = bn_group_stats_rows(gpix, g.C, (int)groups);
+  auto fopts = y.options().dtype(at::kFloat);
+  at::Tensor part = at::empty({groups, nb, 2, g.C}, fopts);
+  at::Tensor st = at::empty({groups, 4, g.C}, fopts);
+  float* ap = nullptr;
+  long long astride = 0;
+  if (arena.has_value() && arena->defined()) {
+    CHECK_F32(*arena);
+    TORCH_CHECK(arena->dim() == 2 && arena->size(0) >= groups && arena->stride(1) == 1 &&
+                aoff + 2 * g.C <= arena->size(1), "arena [rows >= groups][>= aoff + 2C]");
+    ap = arena->data_ptr<float>() + aoff;
+    astride = arena->stride(0);
+  }
+  bn_group_stats_finalize_launch(bptr(y), (int)groups, gpix, g.C, gamma.data_ptr<float>(),
+                                 beta.data_ptr<float>(), (float)eps, st.data_ptr<float>(), ap,
+                                 astride, part.data_ptr<float>(), nb, cur_stream());
+  return st;
+}
+
+std::vector<at::Tensor> bn_group_apply(const at::Tensor& y, const at::Tensor& stats4,
+                                       int64_t groups, bool pool) {
+  CHECK_DEV(y); CHECK_CONTIG(y); CHECK_BF16(y); CHECK_F32(stats4); CHECK_CONTIG(stats4);
+  c10::DeviceGuard guard(y.device());
+  const Geo g = geo_of(y);
+  TORCH_CHECK(groups >= 1 && g.N % groups == 0 && stats4.numel() == groups * 4 * g.C,
+              "bn_group_apply: stats4 [groups][4][C], groups dividing the batch");
+  TORCH_CHECK(g.C % 8 == 0, "C must be a multiple of 8");
+  at::Tensor a = at::empty_like(y);
+  at::Tensor p;
+  if (pool) {
+    TORCH_CHECK(g.H % 2 == 0 && g.W % 2 == 0 && (g.dims == 2 || g.D % 2 == 0), "pool needs even dims");
+    std::vector<int64_t> ps = g.dims == 2 ? std::vector<int64_t>{g.N, g.H / 2, g.W / 2, g.C}
+                                          : std::vector<int64_t>{g.N, g.D / 2, g.H / 2, g.W / 2, g.C};
+    p = at::empty(ps, y.options());
+  }
+  const float* s = stats4.data_ptr<float>();
+  bn_relu_apply_launch(bptr(y), s + 2 * g.C, s + 3 * g.C, bptr_mut(a), pool ? bptr_mut(p) : nullptr,
+                       g.dims, g.N / (int)groups, g.D, g.H, g.W, g.C, cur_stream(), (int)groups,
+                       4LL * g.C);
+  return {a, p.defined() ? p : at::empty({0}, y.options())};
+}
+
+// dY (+ dgamma, dbeta summed over the groups, accumulated into the outs when given)
+std::vector<at::Tensor> bn_group_backward(const c10::optional<at::Tensor>& dA,
+                                          const c10::optional<at::Tensor>& dP, const at::Tensor& y,
+                                          const at::Tensor& stats4, const at::Tensor& gamma,
+                                          int64_t groups,
+                                          const c10::optional<at::Tensor>& dgamma_out,
+                                          const c10::optional<at::Tensor>& dbeta_out) {
+  CHECK_DEV(y); CHECK_CONTIG(y); CHECK_BF16(y); CHECK_F32(stats4); CHECK_CONTIG(stats4);
+  c10::DeviceGuard guard(y.device());
+  const Geo g = geo_of(y);
+  const int C = g.C;
+  const bool hasA = dA.has_value() && dA->defined();
+  const bool hasP = dP.has_value() && dP->defined();
+  TORCH_CHECK(hasA || hasP, "bn_group_backward needs dA or dP");
+  if (hasA) { CHECK_CONTIG(*dA); CHECK_BF16(*dA); TORCH_CHECK(dA->numel() == y.numel(), "dA shape"); }
+  if (hasP) { CHECK_CONTIG(*dP); CHECK_BF16(*dP); TORCH_CHECK(dP->numel() * (g.dims == 3 ? 8 : 4) == y.numel(), "dP shape"); }
+  TORCH_CHECK(groups >= 1 && groups <= 1024 && g.N % groups == 0 && stats4.numel() == groups * 4 * C,
+              "bn_group_backward: stats4 [groups][4][C], 1 <= groups <= 1024 dividing the batch");
+  TORCH_CHECK(bn_group_supported(g.dims, hasP, g.D, g.H, g.W, C),
+              "bn_group_backward: C / 8 a power of two (<= 32 with pool), even dims with pool");
+  const int Ng = g.N / (int)groups;
+  const long long items = (long long)Ng * (hasP ? (g.dims == 3 ? g.D / 2 : 1) * (g.H / 2) * (g.W / 2)
+                                                : (long long)g.D * g.H * g.W);
+  const int nb = bn_group_bwd_rows(items, (int)groups);
+  auto fopts = y.options().dtype(at::kFloat);
+  at::Tensor part = at::empty({groups, nb, 2, C}, fopts);
+  at::Tensor coefs = at::empty({groups, 3, C}, fopts);
+  const bool into = dgamma_out.has_value() && dgamma_out->defined();
+  at::Tensor dgamma = into ? *dgamma_out : at::empty({C}, fopts);
+  at::Tensor dbeta = into ? *dbeta_out : at::empty({C}, fopts);
+  at::Tensor dY = at::empty_like(y);
+  bn_group_backward_launch(hasA ? bptr(*dA) : nullptr, hasP ? bptr(*dP) : nullptr, bptr(y),
+                           stats4.data_ptr<float>(), gamma.data_ptr<float>(), dgamma.data_ptr<float>(),
+                           dbeta.data_ptr<float>(), into, coefs.data_ptr<float>(),
+                           part.data_ptr<float>(), nb, bptr_mut(dY), g.dims, (int)groups, Ng, g.D,
+                           g.H, g.W, C, cur_stream());
+  return {dY, dgamma, dbeta};
+}
+
 static const float* bn4_ptr(const c10::optional<at::Tensor>& bn4, int C) {
   if (!(bn4.has_value() && bn4->defined())) return nullptr;
   CHECK_F32(*bn4); CHECK_CONTIG(*bn4);
@@ -1055,7 +1151,8 @@ at::Tensor head_grad_scale(const at::Tensor& out3, const c10::optional<at::Tenso
 }
 
 // DeviceMeter accumulation in one launch (buf: 4 doubles; loss / correct: one float each)
-void meter_add(at::Tensor& buf, const at::Tensor& loss, const at::Tensor& correct, double pixels) {
+void meter_add(at::Tensor& buf, const at::Tensor& loss, const at::Tensor& correct, double pixels,
+               double count) {
   TORCH_CHECK(buf.scalar_type() == at::kDouble && buf.numel() == 4 && buf.is_contiguous(),
               "meter buffer must be 4 contiguous doubles");
   CHECK_F32(loss); CHECK_F32(correct);
@@ -1063,7 +1160,7 @@ void meter_add(at::Tensor& buf, const at::Tensor& loss, const at::Tensor& correc
   TORCH_CHECK(loss.device() == buf.device() && correct.device() == buf.device(), "device mismatch");
   c10::DeviceGuard guard(buf.device());
   meter_add_launch(buf.data_ptr<double>(), loss.data_ptr<float>(), correct.data_ptr<float>(), pixels,
-                   cur_stream());
+                   count, cur_stream());
 }
 
 at::Tensor head_logits(const at::Tensor& a, const at::Tensor& Wh, const at::Tensor& bh,
@@ -1314,6 +1411,11 @@ TORCH_LIBRARY(ddlpc, m) {
         "Tensor(c!)? nbt=None) -> ()");
   m.def("bn_grad_coefs(Tensor partial, Tensor y, Tensor stats4, Tensor gamma, "
         "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None) -> Tensor[]");
+  m.def("bn_group_finalize(Tensor y, int groups, Tensor gamma, Tensor beta, float eps, "
+        "Tensor(a!)? arena=None, int aoff=0) -> Tensor");
+  m.def("bn_group_apply(Tensor y, Tensor stats4, int groups, bool pool) -> Tensor[]");
+  m.def("bn_group_backward(Tensor? dA, Tensor? dP, Tensor y, Tensor stats4, Tensor gamma, int groups, "
+        "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None) -> Tensor[]");
   m.def("bn_backward(Tensor? dA, Tensor? dP, Tensor y, Tensor stats4, Tensor gamma, Tensor? gscale, "
         "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None, Tensor? partial=None) -> Tensor[]");
   m.def("convt_fwd(Tensor x, Tensor wt, Tensor? bias, int cout, Tensor? bn4=None) -> Tensor");
@@ -1333,7 +1435,7 @@ TORCH_LIBRARY(ddlpc, m) {
         "Tensor bn4) -> Tensor[]");
   m.def("head_wgrad_from_rows(Tensor rows, Tensor scale, int K, int C, Tensor(a!)? dw_out=None, "
         "Tensor(b!)? db_out=None) -> Tensor[]");
-  m.def("meter_add(Tensor(a!) buf, Tensor loss, Tensor correct, float pixels) -> ()");
+  m.def("meter_add(Tensor(a!) buf, Tensor loss, Tensor correct, float pixels, float count=1.) -> ()");
   m.def("head_grad_scale(Tensor out3, Tensor? gs=None) -> Tensor");
   m.def("head_logits(Tensor a, Tensor Wh, Tensor bh, Tensor? bn4=None) -> Tensor");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, float b1, float b2, float eps, "
@@ -1361,6 +1463,9 @@ TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
   m.impl("bn_running_apply", &ddlpc::bn_running_apply);
   m.impl("bn_grad_coefs", &ddlpc::bn_grad_coefs);
   m.impl("bn_backward", &ddlpc::bn_backward);
+  m.impl("bn_group_finalize", &ddlpc::bn_group_finalize);
+  m.impl("bn_group_apply", &ddlpc::bn_group_apply);
+  m.impl("bn_group_backward", &ddlpc::bn_group_backward);
   m.impl("convt_fwd", &ddlpc::convt_fwd);
   m.impl("convt_dgrad", &ddlpc::convt_dgrad);
   m.impl("convt_wgrad", &ddlpc::convt_wgrad);

@@ -27,8 +27,19 @@ template <int DIMS, bool POOL>
 __global__ void bn_relu_apply_kernel(const bf16_t* __restrict__ y, const float* __restrict__ scale,
                                      const float* __restrict__ shift, bf16_t* __restrict__ out,
                                      bf16_t* __restrict__ pooled, int N, int D, int H, int W,
-                                     int C) {
+                                     int C, long long sstride) {
   const int G = C / 8;
+  // per-micro-batch BatchNorm groups (bn_group_apply): blockIdx.y = group, N = its images
+  // and the group's (scale, shift) rows sstride floats apart; one group: blockIdx.y = 0
+  {
+    const long long gpix = (long long)N * D * H * W;
+    const int grp = blockIdx.y;
+    y += grp * gpix * C;
+    if (out != nullptr) out += grp * gpix * C;
+    if (POOL) pooled += grp * (gpix / (DIMS == 3 ? 8 : 4)) * C;
+    scale += grp * sstride;
+    shift += grp * sstride;
+  }
   if (!POOL) {
     const long long total = (long long)N * D * H * W * G;
     for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
@@ -218,9 +229,25 @@ __global__ __launch_bounds__(256) void bn_bwd2_kernel(
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ coefs, const float* __restrict__ gscale,
-    float* __restrict__ partial, bf16_t* __restrict__ dY, int N, int H, int W, int C) {
+    float* __restrict__ partial, bf16_t* __restrict__ dY, int N, int H, int W, int C,
+    long long sstride) {
   constexpr int UNROLL = 2;
   const int G = C / 8;
+  // per-micro-batch BatchNorm groups (bn_group_backward): blockIdx.y = group of N slices,
+  // its statistics rows sstride floats apart, its coefficients [3][C] and partial rows
+  // (gridDim.x per group) in group order; one group: blockIdx.y = 0
+  {
+    const int grp = blockIdx.y;
+    const long long gel = (long long)N * H * W * C;
+    y += grp * gel;
+    if (dA != nullptr) dA += grp * gel;
+    if (dY != nullptr) dY += grp * gel;
+    if (POOL) dP += grp * (gel / (DIMS == 3 ? 8 : 4));
+    scale += grp * sstride; shift += grp * sstride;
+    mean += grp * sstride; invstd += grp * sstride;
+    if (MODE == 1) coefs += grp * 3LL * C;
+    if (MODE == 0) partial += (long long)grp * gridDim.x * 2 * C;
+  }
   const int L = POOL ? 2 * G : G;                 // lanes per unit (divides 256)
   const int tid = threadIdx.x;
   const int cg = tid % G, c8 = cg * 8;
@@ -367,43 +394,48 @@ template <int MODE>
 void bn_bwd2_launch(int grid, int dims, bool pool, const bf16_t* dA, const bf16_t* dP,
                     const bf16_t* y, const float* scale, const float* shift, const float* mean,
                     const float* invstd, const float* coefs, const float* gscale, float* partial,
-                    bf16_t* dY, int N, int D, int H, int W, int C, hipStream_t st) {
+                    bf16_t* dY, int N, int D, int H, int W, int C, hipStream_t st,
+                    int groups = 1, long long sstride = 0) {
+  // (groups > 1: N = images per group, the groups' tensors follow each other)
   const int ND = N * (dims == 3 ? D : 1);
+  const dim3 gr(grid, groups);
   if (dims == 3 && pool)
-    hipLaunchKernelGGL((bn_bwd2_kernel<3, true, MODE>), dim3(grid), dim3(256), 0, st, dA, dP, y,
-                       scale, shift, mean, invstd, coefs, gscale, partial, dY, ND, H, W, C);
+    hipLaunchKernelGGL((bn_bwd2_kernel<3, true, MODE>), gr, dim3(256), 0, st, dA, dP, y,
+                       scale, shift, mean, invstd, coefs, gscale, partial, dY, ND, H, W, C, sstride);
   else if (pool)
-    hipLaunchKernelGGL((bn_bwd2_kernel<2, true, MODE>), dim3(grid), dim3(256), 0, st, dA, dP, y,
-                       scale, shift, mean, invstd, coefs, gscale, partial, dY, ND, H, W, C);
+    hipLaunchKernelGGL((bn_bwd2_kernel<2, true, MODE>), gr, dim3(256), 0, st, dA, dP, y,
+                       scale, shift, mean, invstd, coefs, gscale, partial, dY, ND, H, W, C, sstride);
   else
-    hipLaunchKernelGGL((bn_bwd2_kernel<2, false, MODE>), dim3(grid), dim3(256), 0, st, dA, dP, y,
-                       scale, shift, mean, invstd, coefs, gscale, partial, dY, ND, H, W, C);
+    hipLaunchKernelGGL((bn_bwd2_kernel<2, false, MODE>), gr, dim3(256), 0, st, dA, dP, y,
+                       scale, shift, mean, invstd, coefs, gscale, partial, dY, ND, H, W, C, sstride);
 }
 }  // namespace
 
 void bn_relu_apply_launch(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
                           bf16_t* pooled, int dims, int N, int D, int H, int W, int C,
-                          hipStream_t st) {
+                          hipStream_t st, int groups, long long sstride) {
+  // groups > 1: N = images per group (per-micro-batch BatchNorm, statistics rows sstride apart)
   const long long G = C / 8;
+  const int cap = std::max(1, 8192 / groups);
   if (pooled == nullptr) {
     const long long items = (long long)N * D * H * W * G;
-    const int grid = grid_for(items, 256) * 1;
+    const dim3 gr(std::min(grid_for(items, 256), cap), groups);
     if (dims == 2)
-      hipLaunchKernelGGL((bn_relu_apply_kernel<2, false>), dim3(std::min(grid, 8192)), dim3(256), 0,
-                         st, y, scale, shift, out, pooled, N, D, H, W, C);
+      hipLaunchKernelGGL((bn_relu_apply_kernel<2, false>), gr, dim3(256), 0,
+                         st, y, scale, shift, out, pooled, N, D, H, W, C, sstride);
     else
-      hipLaunchKernelGGL((bn_relu_apply_kernel<3, false>), dim3(std::min(grid, 8192)), dim3(256), 0,
-                         st, y, scale, shift, out, pooled, N, D, H, W, C);
+      hipLaunchKernelGGL((bn_relu_apply_kernel<3, false>), gr, dim3(256), 0,
+                         st, y, scale, shift, out, pooled, N, D, H, W, C, sstride);
     return;
   }
   const long long items = (long long)N * (dims == 3 ? D / 2 : 1) * (H / 2) * (W / 2) * G;
-  const int grid = std::min(grid_for(items, 256), 8192);
+  const dim3 gr(std::min(grid_for(items, 256), cap), groups);
   if (dims == 2)
-    hipLaunchKernelGGL((bn_relu_apply_kernel<2, true>), dim3(grid), dim3(256), 0, st, y, scale,
-                       shift, out, pooled, N, D, H, W, C);
+    hipLaunchKernelGGL((bn_relu_apply_kernel<2, true>), gr, dim3(256), 0, st, y, scale,
+                       shift, out, pooled, N, D, H, W, C, sstride);
   else
-    hipLaunchKernelGGL((bn_relu_apply_kernel<3, true>), dim3(grid), dim3(256), 0, st, y, scale,
-                       shift, out, pooled, N, D, H, W, C);
+    hipLaunchKernelGGL((bn_relu_apply_kernel<3, true>), gr, dim3(256), 0, st, y, scale,
+                       shift, out, pooled, N, D, H, W, C, sstride);
 }
 
 #define BN_BWD_DISPATCH(MODE, grid)                                                         \
@@ -459,6 +491,188 @@ void bn_bwd_apply_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y, co
   }
   const int grid = std::min(grid_for(items, per), 16384);
   BN_BWD_DISPATCH(1, grid);
+}
+
+// ===================================================================== per-micro-batch groups
+// A window of accumulation micro-batches run as ONE batched pass (Trainer bn_window): the
+// weights are fixed inside the window and a train-mode BatchNorm normalises over its own
+// micro-batch (ref.py:580,583 with batch_size 1, ref.py:686), so every BatchNorm keeps one
+// statistics group per micro-batch.  The batch is the groups' tensors one after another;
+// statistics are [groups][4][C] (mean | invstd | scale | shift), coefficients [groups][3][C].
+namespace {
+
+// per-group channel (sum, sum^2) of y: grid (nb, groups), a thread keeps one 8-channel group
+// (C / 8 lanes per pixel, a power of two dividing 256); partial rows [groups][nb][2][C]
+__global__ __launch_bounds__(256) void bn_group_stats_kernel(const bf16_t* __restrict__ y,
+                                                             long long gpix, int C,
+                                                             float* __restrict__ partial) {
+  const int G8 = C / 8;
+  const int tid = threadIdx.x;
+  const int c8 = (tid % G8) * 8;
+  const int upb = 256 / G8;
+  const int grp = blockIdx.y;
+  y += grp * gpix * C;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  const long long stride = (long long)gridDim.x * upb;
+  long long p = (long long)blockIdx.x * upb + tid / G8;
+  for (; p + stride < gpix; p += 2 * stride) {     // two pixels' loads in flight
+    const uint4 v0 = *reinterpret_cast<const uint4*>(y + p * C + c8);
+    const uint4 v1 = *reinterpret_cast<const uint4*>(y + (p + stride) * C + c8);
+    float f0[8], f1[8];
+    unpack8(v0, f0);
+    unpack8(v1, f1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s1[j] += f0[j] + f1[j];
+      s2[j] = fmaf(f0[j], f0[j], fmaf(f1[j], f1[j], s2[j]));
+    }
+  }
+  if (p < gpix) {
+    float f0[8];
+    unpack8(*reinterpret_cast<const uint4*>(y + p * C + c8), f0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s1[j] += f0[j]; s2[j] = fmaf(f0[j], f0[j], s2[j]); }
+  }
+  __shared__ float red[256 * 8];
+  float* out = partial + ((long long)grp * gridDim.x + blockIdx.x) * 2 * C;
+  for (int half = 0; half < 2; ++half) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[j * 256 + tid] = half ? s2[j] : s1[j];
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+      const int g2 = c / 8, j = c % 8;
+      float t = 0.f;
+      for (int k = g2; k < 256; k += G8) t += red[j * 256 + k];
+      out[half * C + c] = t;
+    }
+  }
+}
+
+// one workgroup per channel; wave w finalizes groups w, w + 4, ... (fp64 sums of the group's
+// nb partial rows): stats4 per group, and the group's (mean, unbiased var) into its arena row
+// (the running statistics are then updated in micro-batch order: bn_running_apply)
+__global__ __launch_bounds__(256) void bn_group_finalize_kernel(
+    const float* __restrict__ partial, int nb, int groups, int C, double count,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+    float* __restrict__ out4, float* __restrict__ arena, long long astride) {
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int g = w; g < groups; g += 4) {
+    const float* rows = partial + (long long)g * nb * 2 * C;
+    double a = 0.0, b = 0.0;
+    for (int r = lane; r < nb; r += 64) {
+      a += rows[(long long)r * 2 * C + c];
+      b += rows[(long long)r * 2 * C + C + c];
+    }
+    a = wave_sum_d(a);
+    b = wave_sum_d(b);
+    if (lane != 0) continue;
+    const double mean = a / count;
+    double var = b / count - mean * mean;
+    if (var < 0) var = 0;
+    const float inv = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = gamma[c] * inv;
+    float* o = out4 + (long long)g * 4 * C;
+    o[c] = (float)mean;
+    o[C + c] = inv;
+    o[2 * C + c] = sc;
+    o[3 * C + c] = beta[c] - (float)mean * sc;
+    if (arena != nullptr) {
+      const double unb = count > 1 ? var * count / (count - 1) : var;
+      arena[g * astride + c] = (float)mean;
+      arena[g * astride + C + c] = (float)unb;
+    }
+  }
+}
+
+// BatchNorm-backward finalize per group: coefficients [k | m1 | m2] of every group, and
+// dgamma / dbeta = the fp64 sums over groups in group order (deterministic)
+__global__ __launch_bounds__(256) void bn_group_grad_finalize_kernel(
+    const float* __restrict__ partial, int nb, int groups, int C, double count,
+    const float* __restrict__ gamma, const float* __restrict__ stats4, float* dgamma, float* dbeta,
+    float* __restrict__ coefs, int accumulate) {
+  __shared__ double t1s[1024], t2s[1024];
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int g = w; g < groups; g += 4) {
+    const float* rows = partial + (long long)g * nb * 2 * C;
+    double a = 0.0, b = 0.0;
+    for (int r = lane; r < nb; r += 64) {
+      a += rows[(long long)r * 2 * C + c];
+      b += rows[(long long)r * 2 * C + C + c];
+    }
+    a = wave_sum_d(a);
+    b = wave_sum_d(b);
+    if (lane != 0) continue;
+    t1s[g] = a;
+    t2s[g] = b;
+    float* k = coefs + (long long)g * 3 * C;
+    k[c] = gamma[c] * stats4[(long long)g * 4 * C + C + c];
+    k[C + c] = (float)(a / count);
+    k[2 * C + c] = (float)(b / count);
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double a = 0.0, b = 0.0;
+  for (int g = 0; g < groups; ++g) { a += t1s[g]; b += t2s[g]; }
+  dbeta[c] = accumulate ? dbeta[c] + (float)a : (float)a;
+  dgamma[c] = accumulate ? dgamma[c] + (float)b : (float)b;
+}
+
+int bn_group_rows(long long gpix, int C, int groups) {
+  // rows per group: enough workgroups over all groups to fill the chip, each >= 16 steps
+  const long long units = gpix * (C / 8);
+  long long nb = (units + 256 * 16 - 1) / (256 * 16);
+  nb = std::min<long long>(nb, std::max(1, 4096 / groups));
+  return (int)std::max<long long>(1, std::min<long long>(nb, 256));
+}
+
+}  // namespace
+
+bool bn_group_supported(int dims, bool pool, int D, int H, int W, int C) {
+  const int G8 = C / 8;
+  return C % 8 == 0 && (G8 & (G8 - 1)) == 0 && G8 <= 256 && bn_bwd2_ok(dims, pool, D, H, W, C);
+}
+
+void bn_group_stats_finalize_launch(const bf16_t* y, int groups, long long gpix, int C,
+                                    const float* gamma, const float* beta, float eps, float* out4,
+                                    float* arena, long long astride, float* partial_scratch,
+                                    int nb, hipStream_t st) {
+  hipLaunchKernelGGL(bn_group_stats_kernel, dim3(nb, groups), dim3(256), 0, st, y, gpix, C,
+                     partial_scratch);
+  hipLaunchKernelGGL(bn_group_finalize_kernel, dim3(C), dim3(256), 0, st, partial_scratch, nb,
+                     groups, C, (double)gpix, gamma, beta, eps, out4, arena, astride);
+}
+
+int bn_group_stats_rows(long long gpix, int C, int groups) { return bn_group_rows(gpix, C, groups); }
+
+void bn_group_backward_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y,
+                              const float* stats4, const float* gamma, float* dgamma, float* dbeta,
+                              bool accumulate, float* coefs, float* partial_scratch, int nb,
+                              bf16_t* dY, int dims, int groups, int N, int D, int H, int W, int C,
+                              hipStream_t st) {
+  const bool pool = dP != nullptr;
+  const long long sstride = 4LL * C;
+  const float* s = stats4;
+  bn_bwd2_launch<0>(nb, dims, pool, dA, dP, y, s + 2 * C, s + 3 * C, s, s + C, nullptr, nullptr,
+                    partial_scratch, nullptr, N, D, H, W, C, st, groups, sstride);
+  const double count = (double)N * D * H * W;
+  hipLaunchKernelGGL(bn_group_grad_finalize_kernel, dim3(C), dim3(256), 0, st, partial_scratch, nb,
+                     groups, C, count, gamma, stats4, dgamma, dbeta, coefs, accumulate ? 1 : 0);
+  const long long items = (long long)N * (pool ? (dims == 3 ? D / 2 : 1) * (H / 2) * (W / 2)
+                                                : (long long)D * H * W);
+  const int upb = 256 / (pool ? 2 * (C / 8) : C / 8);
+  const int grid2 = (int)std::max<long long>(
+      1, std::min<long long>((items + 2 * upb - 1) / (2 * upb), std::max(1, 8192 / groups)));
+  bn_bwd2_launch<1>(grid2, dims, pool, dA, dP, y, s + 2 * C, s + 3 * C, s, s + C, coefs, nullptr,
+                    nullptr, dY, N, D, H, W, C, st, groups, sstride);
+}
+
+int bn_group_bwd_rows(long long items, int groups) {
+  return (int)std::max<long long>(1, std::min<long long>((items + 255) / 256, std::max(1, 4096 / groups)));
 }
 
 }  // namespace ddlpc

@@ -155,7 +155,7 @@ bool convt_res_launch(GemmArgs& a, int num_cus, hipStream_t st);
 // out may be null with pool (deferred skip: only the pooled tensor is materialised)
 void bn_relu_apply_launch(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
                           bf16_t* pooled, int dims, int N, int D, int H, int W, int C,
-                          hipStream_t st);
+                          hipStream_t st, int groups = 1, long long sstride = 0);
 void bn_bwd_reduce_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y,
                           const float* scale, const float* shift, const float* mean,
                           const float* invstd, const float* gscale, float* partial, int nblocks,
@@ -165,6 +165,23 @@ void bn_bwd_apply_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y, co
                          const float* coefs, const float* gscale, bf16_t* dY, int dims, int N,
                          int D, int H, int W, int C, hipStream_t st);
 int bn_bwd_reduce_blocks(long long pixels_or_quads);
+// per-micro-batch BatchNorm groups (bn.hip): `groups` statistics groups of gpix pixels each,
+// the batch = the groups' tensors one after another; stats4 [groups][4][C]
+bool bn_group_supported(int dims, bool pool, int D, int H, int W, int C);
+int bn_group_stats_rows(long long gpix, int C, int groups);
+// partial_scratch: [groups][nb][2][C]; arena (optional): row g at g * astride gets the
+// group's (mean | unbiased var) for the in-order running-statistics update
+void bn_group_stats_finalize_launch(const bf16_t* y, int groups, long long gpix, int C,
+                                    const float* gamma, const float* beta, float eps, float* out4,
+                                    float* arena, long long astride, float* partial_scratch,
+                                    int nb, hipStream_t st);
+int bn_group_bwd_rows(long long items_per_group, int groups);
+// dY per group (N = images per group), coefs [groups][3][C], dgamma / dbeta summed over groups
+void bn_group_backward_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y,
+                              const float* stats4, const float* gamma, float* dgamma, float* dbeta,
+                              bool accumulate, float* coefs, float* partial_scratch, int nb,
+                              bf16_t* dY, int dims, int groups, int N, int D, int H, int W, int C,
+                              hipStream_t st);
 
 // ---------------------------------------------------------------- head + cross-entropy
 bool head_supported(int C, int K);
@@ -234,7 +251,7 @@ void bn_grad_finalize_launch(const double* sums, int C, double count, const floa
                              const float* invstd, float* dgamma, float* dbeta, float* coefs,
                              bool accumulate, hipStream_t st, const float* dscale = nullptr);
 void meter_add_launch(double* buf, const float* loss, const float* correct, double pixels,
-                      hipStream_t st);
+                      double n, hipStream_t st);
 void head_grad_scale_launch(const float* out3, const float* gs, float* scale, hipStream_t st);
 void scatter_sums_dscale_launch(const double* sums, long long N, float* dst, const float* dscale,
                                 bool accumulate, hipStream_t st);

@@ -142,14 +142,15 @@ __global__ void head_grad_scale_kernel(const float* __restrict__ out3, const flo
   scale[0] = (gs != nullptr ? gs[0] : 1.f) / (cnt > 0.f ? cnt : 1.f);
 }
 
-// training meter [sum loss, sum correct, sum pixels, micro-batches] += (loss, correct, pixels, 1)
+// training meter [sum loss, sum correct, sum pixels, micro-batches] += (loss * n, correct,
+// pixels, n): n micro-batches whose mean loss is `loss` (a batched window counts n)
 __global__ void meter_add_kernel(double* __restrict__ buf, const float* __restrict__ loss,
-                                 const float* __restrict__ correct, double pixels) {
+                                 const float* __restrict__ correct, double pixels, double n) {
   const int t = threadIdx.x;
-  if (t == 0) buf[0] += (double)loss[0];
+  if (t == 0) buf[0] += (double)loss[0] * n;
   else if (t == 1) buf[1] += (double)correct[0];
   else if (t == 2) buf[2] += pixels;
-  else if (t == 3) buf[3] += 1.0;
+  else if (t == 3) buf[3] += n;
 }
 
 // one block per channel: fp64 sum of P partial rows, then finalize (P <= a few thousand)
@@ -407,8 +408,8 @@ void comm_proxy_launch(float* g, long long n, int blocks, int passes, hipStream_
 }
 
 void meter_add_launch(double* buf, const float* loss, const float* correct, double pixels,
-                      hipStream_t st) {
-  hipLaunchKernelGGL(meter_add_kernel, dim3(1), dim3(64), 0, st, buf, loss, correct, pixels);
+                      double n, hipStream_t st) {
+  hipLaunchKernelGGL(meter_add_kernel, dim3(1), dim3(64), 0, st, buf, loss, correct, pixels, n);
 }
 
 void scatter_sums_launch(const double* sums, long long N, float* dst, int mode, int A, int T,

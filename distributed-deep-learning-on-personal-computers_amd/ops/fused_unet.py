@@ -116,6 +116,16 @@ class _BNState:
                                       bool(bn.track_running_stats), bn.num_batches_tracked)
         return self.eval_stats()
 
+    def finalize_groups(self, y: torch.Tensor, groups: int) -> torch.Tensor:
+        """Per-micro-batch statistics of a batched window (``UNetEngine.bn_groups``):
+        -> [groups][4][C]; each group's (mean, unbiased var) goes to its row of the engine's
+        running-statistics arena, applied in micro-batch order after the forward."""
+        bn = self.bn
+        eng = self.engine
+        arena = eng._bn_arena if (bn.track_running_stats and eng._bn_arena is not None) else None
+        off = eng._bn_offs[self.index] if arena is not None else 0
+        return _ops().bn_group_finalize(y, groups, bn.weight, bn.bias, float(bn.eps), arena, off)
+
     def eval_stats(self) -> torch.Tensor:
         bn = self.bn
         inv = torch.rsqrt(bn.running_var.float() + bn.eps)
@@ -135,6 +145,11 @@ class _DoubleConvFn(torch.autograd.Function):
         F = _ops()
         p1, p2 = blk.pack1, blk.pack2
         training = blk.bn1.bn.training
+        G = blk.engine.bn_groups if training else 0
+        if G > 1:
+            assert not defer and not defer_skip and x2_bn is None, "BN groups: no deferred BN"
+            return _DoubleConvFn._group_forward(ctx, x1, x2, b1, b2, g1, g2, blk, pool, G)
+        ctx.groups = 0
         c1 = p1.cout
         sc2 = x2_bn[2] if x2_bn is not None else None
         sh2 = x2_bn[3] if x2_bn is not None else None
@@ -192,7 +207,91 @@ class _DoubleConvFn(torch.autograd.Function):
         return a2, None, None
 
     @staticmethod
+    def _group_forward(ctx, x1, x2, b1, b2, g1, g2, blk, pool: bool, G: int):
+        """A batched window of G micro-batches (``UNetEngine.bn_groups``): the convolutions
+        run over the whole batch, every BatchNorm normalises each micro-batch with its own
+        statistics (ref.py:580,583 at batch_size 1).  BN + ReLU is materialised per group
+        (a1, a2) and the convs read it without a prologue; y1 / y2 stay for the backward."""
+        F = _ops()
+        p1, p2 = blk.pack1, blk.pack2
+        y1 = F.conv3_fwd(x1, x2, p1.fwd, b1, None, None, p1.cout, 0, False)[0]
+        s1 = blk.bn1.finalize_groups(y1, G)
+        a1 = F.bn_group_apply(y1, s1, G, False)[0]
+        y2 = F.conv3_fwd(a1, None, p2.fwd, b2, None, None, p2.cout, 0, False)[0]
+        s2 = blk.bn2.finalize_groups(y2, G)
+        a2, pooled = F.bn_group_apply(y2, s2, G, pool)
+        ctx.groups = G
+        ctx.blk, ctx.pool, ctx.defer = blk, pool, False
+        ctx.has_x2 = x2 is not None
+        ctx.save_for_backward(x1, x2 if x2 is not None else torch.empty(0), y1, y2, s1, s2, g1,
+                              g2, a1)
+        ctx.set_materialize_grads(False)
+        return a2, (pooled if pool else None), None
+
+    @staticmethod
+    def _group_backward(ctx, da2, dpool):
+        F = _ops()
+        x1, x2, y1, y2, s1, s2, g1, g2, a1 = ctx.saved_tensors
+        blk = ctx.blk
+        eng = blk.engine
+        G = ctx.groups
+        x2 = x2 if ctx.has_x2 else None
+        if da2 is None and dpool is None:
+            return (None,) * 15
+        da2 = da2.contiguous() if da2 is not None else None
+        dpool = dpool.contiguous() if dpool is not None else None
+        bn1, bn2 = blk.bn1.bn, blk.bn2.bn
+        p1, p2 = blk.pack1, blk.pack2
+        w1 = blk.conv1.weight
+        direct = eng.direct_grads
+        # ---- second conv: per-group BN2 + ReLU (+ unpool + skip sum) backward, its gradients
+        if direct:
+            dy2 = F.bn_group_backward(da2, dpool, y2, s2, g2, G, bn2.weight.grad, bn2.bias.grad)[0]
+            with eng.wgrad_stream(dy2, a1):
+                F.conv3_wgrad(dy2, a1, None, None, None, blk.conv2.weight.grad)
+                eng.ready(bn2.weight, bn2.bias, blk.conv2.weight, blk.conv2.bias)
+            dg2 = dbe2 = dw2 = None
+        else:
+            dy2, dg2, dbe2 = F.bn_group_backward(da2, dpool, y2, s2, g2, G, None, None)
+            dw2 = F.conv3_wgrad(dy2, a1, None, None, None).view_as(blk.conv2.weight)
+        da1 = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False)[0]
+        # ---- first conv
+        padded_in = x2 is None and x1.shape[-1] != w1.shape[1]     # first layer: 3 -> 8 ch
+        if direct:
+            dy1 = F.bn_group_backward(da1, None, y1, s1, g1, G, bn1.weight.grad, bn1.bias.grad)[0]
+            with eng.wgrad_stream(dy1, x1, x2):
+                if padded_in:
+                    w1.grad.add_(F.conv3_wgrad(dy1, x1, None, None, None,
+                                               cin_real=w1.shape[1])[:, :w1.shape[1]])
+                else:
+                    F.conv3_wgrad(dy1, x1, x2, None, None, w1.grad)
+                eng.ready(bn1.weight, bn1.bias, w1, blk.conv1.bias)
+            dg1 = dbe1 = dw1 = None
+        else:
+            dy1, dg1, dbe1 = F.bn_group_backward(da1, None, y1, s1, g1, G, None, None)
+            dw1 = F.conv3_wgrad(dy1, x1, x2, None, None, None,
+                                cin_real=w1.shape[1] if padded_in else 0)
+            dw1 = (dw1[:, :w1.shape[1]] if padded_in else dw1).reshape(w1.shape)
+        dx1 = dx2 = None
+        if ctx.needs_input_grad[0] or (x2 is not None and ctx.needs_input_grad[1]):
+            co1 = x1.shape[-1] if x2 is not None else 0
+            want_sums = x2 is not None and blk.up_is_convt
+            dx1, dx2, sums = F.conv3_fwd(dy1, None, p1.dgrad, None, None, None, p1.cin, co1,
+                                         want_sums)
+            if want_sums:
+                dx1._ddlpc_colsum_rows = sums
+            if x2 is None:
+                dx2 = None
+        if blk.first:
+            eng.join()
+        zb1 = torch.zeros_like(g1) if (not direct and ctx.needs_input_grad[3]) else None
+        zb2 = torch.zeros_like(g2) if (not direct and ctx.needs_input_grad[7]) else None
+        return (dx1, dx2, dw1, zb1, dg1, dbe1, dw2, zb2, dg2, dbe2, None, None, None, None, None)
+
+    @staticmethod
     def backward(ctx, da2, dpool, _ds2):
+        if ctx.groups:
+            return _DoubleConvFn._group_backward(ctx, da2, dpool)
         F = _ops()
         x1, x2, y1, y2, s1, s2, g1, g2 = ctx.saved_tensors
         blk = ctx.blk
@@ -550,6 +649,10 @@ class UNetEngine:
         # transposed-conv weight gradients on the side stream too (DDLPC_SIDE_CONVT=0: main)
         self.side_convt = os.environ.get("DDLPC_SIDE_CONVT", "1") != "0"
         self.recompute = 0               # Trainer sets cfg.recompute: 0 / 1 (y1) / 2 (y1, y2)
+        # per-micro-batch BatchNorm groups of a batched accumulation window (Trainer
+        # bn_window): > 1 = the training batch is that many micro-batches, each normalised
+        # with its own statistics (no deferred BN / prologue fusion in this mode)
+        self.bn_groups = 0
         # encoder skips handed out pre-BN (see ``defer_skip_levels``): saves ~1 GB at
         # 256^2 x 128 but measured ~1.2% slower end to end (docs/PERF.md), so opt-in
         self.defer_skip = os.environ.get("DDLPC_DEFER_SKIP", "0") != "0"
@@ -766,12 +869,13 @@ class UNetEngine:
         self._ensure_packed()
         h = self.to_nhwc(x)
         skips = []
-        dskip = self.defer_skip_levels(x)
+        grouped = self.bn_groups > 1 and self.enc[0].bn1.bn.training
+        dskip = self.defer_skip_levels(x) if not grouped else [False] * len(self.enc)
         for lvl, blk in enumerate(self.enc):
             skip, h, s_skip = blk(h, None, True, defer_skip=dskip[lvl])
             skips.append((skip, s_skip))
         n = len(self.dec)
-        mode = self.defer_mode                       # "all" | "convt" | "none"
+        mode = self.defer_mode if not grouped else "none"    # "all" | "convt" | "none"
         feeds_convt = [pack is not None and mode != "none" for _, pack, _ in self.dec]
         defer_last = defer_last and mode == "all"
         h, _, s = self.mid(h, None, False, defer=n > 0 and feeds_convt[0])
@@ -823,6 +927,18 @@ class UNetEngine:
         return _ops().head_logits(a, wh.detach().contiguous(), bh.detach(), s)
 
     def loss_and_correct(self, x: torch.Tensor, y: torch.Tensor, ignore_index: int = -100):
+        """-> (mean cross-entropy over the batch's pixels, correct-pixel count).  With
+        ``bn_groups`` = G > 1 (training) the batch is G equal micro-batches with their own
+        BatchNorm statistics; the running statistics are updated once per micro-batch, in
+        order, after the forward (bit-for-bit the update sequence of G forwards)."""
+        G = self.bn_groups if self.enc[0].bn1.bn.training else 0
+        if G > 1:
+            if x.shape[0] % G:
+                raise ValueError(f"bn_groups={G} must divide the batch ({x.shape[0]})")
+            self.bn_defer_prepare(1, G)
         a, s = self.features(x, defer_last=True)
         wh, bh = self._head_params()
-        return _HeadCEFn.apply(a, wh, bh, y.contiguous(), ignore_index, self, s)
+        out = _HeadCEFn.apply(a, wh, bh, y.contiguous(), ignore_index, self, s)
+        if G > 1:
+            self.bn_defer_apply(G)
+        return out

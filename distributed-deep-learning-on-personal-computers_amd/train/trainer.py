@@ -556,8 +556,62 @@ class Trainer:
             self._inflight.append(ev)
         return out
 
+    # ------------------------------------------------------------------ batched BN-group windows
+    WINDOW_PIXELS = 64 * 512 * 512          # auto window: up to 64 512^2 images per pass
+
+    def _window_size(self, n_micro: int) -> int:
+        """Micro-batches per batched pass (0: off).  cfg.bn_window: 0 off, k >= 2 up to k,
+        -1 auto = as many as fit WINDOW_PIXELS when micro-batches are small and accumulated
+        (the reference's regime: batch 1, 50 micro-batches, ref.py:685-687)."""
+        c = self.cfg
+        if (n_micro < 2 or self.impl != "hip" or self.device.type != "cuda"
+                or c.bn_window in (0, 1)):
+            return 0
+        if c.bn_window > 1:
+            return min(c.bn_window, n_micro)
+        px = c.batch_per_gpu * c.tile ** c.model.dims
+        if px > self.SMALL_MICRO_PIXELS:
+            return 0
+        return min(n_micro, max(2, self.WINDOW_PIXELS // px))
+
+    @staticmethod
+    def _cat_window(mbs: List[Tuple[torch.Tensor, torch.Tensor]]):
+        """The window's micro-batches as one batch (engine-layout inputs stay in that layout)."""
+        from ..data.datasets import engine_input
+        xps = [getattr(x, "_ddlpc_nhwc", None) for x, _ in mbs]
+        if all(xp is not None for xp in xps):
+            x = engine_input(torch.cat(xps), mbs[0][0].shape[1])
+        else:
+            x = torch.cat([x for x, _ in mbs])
+        return x, torch.cat([y for _, y in mbs])
+
+    def _window_step(self, micro_batches: List[Tuple[torch.Tensor, torch.Tensor]], W: int):
+        """The accumulation window as batched passes of up to W micro-batches, each micro-batch
+        its own BatchNorm group (``UNetEngine.bn_groups``).  The weights do not change inside
+        the window and a train-mode BatchNorm normalises over its own micro-batch, so this is
+        the computation of the micro-batches one by one (ref.py:750-766) up to the convs'
+        summation order: the loss of a pass is the mean over its micro-batches' pixels, so
+        its gradient is scaled by the number of micro-batches (the reference sums the
+        micro-batch gradients).  Only the last pass arms the gradient exchange."""
+        eng = self.model._engine
+        n = len(micro_batches)
+        chunks = [micro_batches[i:i + W] for i in range(0, n, W)]
+        for ci, ch in enumerate(chunks):
+            x, y = self._cat_window(ch) if len(ch) > 1 else ch[0]
+            if self.reducer is not None:
+                self.reducer.prepare(sync=ci == len(chunks) - 1)
+            eng.bn_groups = len(ch)
+            try:
+                loss, correct = self.model.loss_and_correct(x, y)
+                (loss * float(len(ch)) if len(ch) > 1 else loss).backward()
+            finally:
+                eng.bn_groups = 0
+            self.meter.add(loss, correct, y.numel(), n=len(ch))
+            self.micro_count += len(ch)
+
     def _train_step(self, micro_batches: List[Tuple[torch.Tensor, torch.Tensor]]):
-        if self._graph_ok(len(micro_batches)):
+        W = self._window_size(len(micro_batches))
+        if W == 0 and self._graph_ok(len(micro_batches)):
             return self._graph_step(micro_batches)
         self.model.train()
         n = len(micro_batches)
@@ -565,7 +619,9 @@ class Trainer:
         if ph is not None:
             ph.mark("start")
         with trace_range("ddlpc.fwd_bwd"):
-            if self._concurrent_ok(n):
+            if W:
+                self._window_step(micro_batches, W)
+            elif self._concurrent_ok(n):
                 self._concurrent_micros(micro_batches[:-1])
                 self._micro(*micro_batches[-1], sync=True)
             else:

@@ -51,17 +51,19 @@ class DeviceMeter:
         else:
             self.buf.zero_()
 
-    def add(self, loss: torch.Tensor, correct: torch.Tensor, pixels: int):
-        # [sum loss, sum correct, sum pixels, micro-batches]; no host->device copies per step
+    def add(self, loss: torch.Tensor, correct: torch.Tensor, pixels: int, n: int = 1):
+        # [sum loss, sum correct, sum pixels, micro-batches]; no host->device copies per step.
+        # n > 1: a batched window of n micro-batches whose mean per-micro-batch loss is `loss`
         if (self.buf.is_cuda and loss.dtype == torch.float32 and correct.dtype == torch.float32
                 and loss.numel() == 1 and correct.numel() == 1 and _hip_ops() is not None):
             # one launch instead of five small elementwise kernels
-            _hip_ops().meter_add(self.buf, loss.detach(), correct.detach(), float(pixels))
+            _hip_ops().meter_add(self.buf, loss.detach(), correct.detach(), float(pixels), float(n))
             return
-        if self._inc_pixels != pixels:
-            self._inc = torch.tensor([float(pixels), 1.0], dtype=torch.float64, device=self.device)
-            self._inc_pixels = pixels
-        self.buf[:2] += torch.stack([loss.detach().double(), correct.detach().double()])
+        if self._inc_pixels != (pixels, n):
+            self._inc = torch.tensor([float(pixels), float(n)], dtype=torch.float64,
+                                     device=self.device)
+            self._inc_pixels = (pixels, n)
+        self.buf[:2] += torch.stack([loss.detach().double() * n, correct.detach().double()])
         self.buf[2:] += self._inc
 
     def reduce(self, group=None) -> Dict[str, float]:
