@@ -234,7 +234,12 @@ def test_conv3_dgrad_split(ops, C1, C2, Cout):
     (4, 8, 8, 256, 0, 256, True), (2, 32, 32, 3, 0, 32, False), (1, 16, 16, 64, 32, 32, False),
     (2, 64, 64, 64, 32, 32, True), (2, 72, 40, 32, 0, 64, True), (1, 128, 128, 128, 64, 64, False),
     (2, 48, 48, 128, 0, 96, True),
-    (4, 256, 256, 32, 0, 32, True)])     # > 64 split-K rows: the one-launch wide reduction
+    (4, 256, 256, 32, 0, 32, True),      # > 64 split-K rows: the one-launch wide reduction
+    # the 128-output-channel v3 tiles (Cout >= 128, H*W >= 32^2: the default for the deep
+    # layers, ref.py:579,582 at C_out >= 128), with and without the prologue / a concat input
+    (4, 32, 32, 256, 0, 256, True), (2, 64, 64, 128, 0, 128, False),
+    (2, 32, 32, 256, 256, 256, False), (1, 64, 64, 256, 256, 256, True),
+    (2, 64, 64, 128, 128, 128, True), (2, 40, 56, 128, 0, 128, True)])
 def test_conv3_wgrad(ops, N, H, W, C1, C2, Cout, pro):
     torch.manual_seed(3)
     x1 = torch.randn(N, C1, H, W, device=DEV).bfloat16()
@@ -895,3 +900,60 @@ def test_meter_add_single_launch(ops):
     assert m.buf.tolist() == [0.75 * 6, 3000.0, 3 * 4096.0, 3.0]
     r = m.reduce()
     assert abs(r["loss"] - 1.5) < 1e-12 and abs(r["pixel_acc"] - 1000.0 / 4096.0) < 1e-12
+
+
+# ------------------------------------------------------------------ per-micro-batch BN groups
+@pytest.mark.parametrize("G,n,H,W,C,pool", [(5, 1, 32, 32, 32, True), (3, 2, 16, 16, 256, False),
+                                            (4, 1, 64, 64, 64, False), (50, 1, 16, 16, 128, True),
+                                            (2, 1, 8, 8, 256, False)])
+def test_bn_group_kernels(ops, G, n, H, W, C, pool):
+    """bn_group_finalize / bn_group_apply / bn_group_backward (a batched window of G
+    micro-batches, each its own BatchNorm statistics group) against the fp32 per-group
+    oracle and the single-group kernels run group by group."""
+    torch.manual_seed(G * 7 + C)
+    N = G * n
+    y = (torch.randn(N, H, W, C, device=DEV) * 2 + 0.5).bfloat16()
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.3
+    eps = 1e-5
+    arena = torch.zeros(G, 3 * C + 16, device=DEV)
+    s4 = ops.bn_group_finalize(y, G, gamma, beta, eps, arena, 16)
+    assert s4.shape == (G, 4, C)
+    yg = y.float().view(G, n * H * W, C).double()
+    mean = yg.mean(1)
+    var = yg.var(1, unbiased=False)
+    inv = 1.0 / torch.sqrt(var + eps)
+    assert torch.allclose(s4[:, 0].double(), mean, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(s4[:, 1].double(), inv, rtol=1e-5)
+    sc = gamma.double() * inv
+    assert torch.allclose(s4[:, 2].double(), sc, rtol=1e-5)
+    assert torch.allclose(s4[:, 3].double(), beta.double() - mean * sc, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(arena[:, 16:16 + C].double(), mean, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(arena[:, 16 + C:16 + 2 * C].double(), yg.var(1, unbiased=True), rtol=1e-5)
+    # apply (+ pool)
+    a, p = ops.bn_group_apply(y, s4, G, pool)
+    ref = torch.relu(y.float().view(G, -1, C) * s4[:, 2][:, None] + s4[:, 3][:, None])
+    ref = ref.view(N, H, W, C)
+    # (the kernel rounds fma(y, scale, shift) once; the oracle rounds the product first)
+    assert float((a.float() - ref).abs().max()) <= 1e-2 * float(ref.abs().max())
+    assert rel_err(a, ref) < 3e-3
+    if pool:
+        pr = F.max_pool2d(nchw(a).float(), 2)        # max over the stored activations
+        assert torch.equal(nchw(p).float(), pr)
+    # backward vs the single-group kernel per group
+    dA = torch.randn(N, H, W, C, device=DEV).bfloat16()
+    dP = torch.randn(N, H // 2, W // 2, C, device=DEV).bfloat16() if pool else None
+    dg = torch.zeros(C, device=DEV)
+    db = torch.zeros(C, device=DEV)
+    dY, _, _ = ops.bn_group_backward(dA, dP, y, s4, gamma, G, dg, db)
+    dg_ref = torch.zeros(C, device=DEV, dtype=torch.float64)
+    db_ref = torch.zeros(C, device=DEV, dtype=torch.float64)
+    for g in range(G):
+        sl = slice(g * n, (g + 1) * n)
+        dYg, dgg, dbg = ops.bn_backward(dA[sl].contiguous(), dP[sl].contiguous() if pool else None,
+                                        y[sl].contiguous(), s4[g].contiguous(), gamma, None)
+        assert rel_err(dY[sl], dYg) < 2e-3, g
+        dg_ref += dgg.double()
+        db_ref += dbg.double()
+    assert torch.allclose(dg.double(), dg_ref, rtol=1e-4, atol=1e-3)
+    assert torch.allclose(db.double(), db_ref, rtol=1e-4, atol=1e-3)
