@@ -213,9 +213,8 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   a.npix = (long long)g.N * g.D * g.H * g.W;
   {
     // high-resolution few-channel layers: resident-weight kernel (conv3x3_res.hip)
-    const int use_res = knob("CONV_RES", 1);
     int grid = 0, smem = 0;
-    const int variant = use_res ? conv3_res_plan(a, num_cus(), grid, smem) : -1;
+    const int variant = conv3_res_plan(a, num_cus(), grid, smem);
     if (variant >= 0) {
       at::Tensor y1 = at::empty(shape_with_c(g, a.Co1), opts);
       at::Tensor y2;
@@ -243,19 +242,16 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
     a.nTilesN = (a.Cout + conv3_fwd_cfg_bn(c) - 1) / conv3_fwd_cfg_bn(c);
   };
   plan(cfg);
-  const int use_cfg4 = knob("CONV_CFG4", 1);
-  if (cfg == 2 && g.dims == 2 && use_cfg4) {    // 256-pixel tiles on 8 waves if they fill the chip
+  if (cfg == 2 && g.dims == 2) {    // 256-pixel tiles on 8 waves if they fill the chip
     plan(4);
     if (a.nTilesM * a.nTilesN >= num_cus()) cfg = 4;
     else plan(cfg);
   }
-  // 512-pixel tiles (cfg 5) wherever they fill the chip without padding (DDLPC_CONV_CFG5=0:
-  // off, 1: only K >= 9 x 256).  With the rolling fragment pipeline (no scratch spills) every
-  // eligible layer gains: 128-input-channel layers 8-10%, K >= 9 x 256 layers 1-2% (same-
-  // process A/B at batch 128, profiles/r3s/conv_ab_cfg5_all_r3s7.txt; before the pipeline
-  // the 128-channel layers were 2-4% slower on cfg 5: profiles/conv_ab_cfg5_r3d.txt)
-  const int use_cfg5 = knob("CONV_CFG5", 2);
-  if (cfg == 4 && use_cfg5 && a.bnb_y == nullptr && (a.Cin >= 256 || use_cfg5 == 2)) {
+  // 512-pixel tiles (cfg 5) wherever they fill the chip without padding.  With the rolling
+  // fragment pipeline (no scratch spills) every eligible layer gains: 128-input-channel layers
+  // 8-10%, K >= 9 x 256 layers 1-2% (same-process A/B at batch 128,
+  // profiles/r3s/conv_ab_cfg5_all_r3s7.txt)
+  if (cfg == 4 && a.bnb_y == nullptr) {
     plan(5);
     const double w5 = (double)a.nTilesM * 512 / ((double)g.N * g.D * g.H * g.W);
     if (a.nTilesM * a.nTilesN >= num_cus() && w5 <= 1.05) cfg = 5;
@@ -283,10 +279,6 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   if (a.Co1 < a.Cout) y2 = at::empty(shape_with_c(g, a.Cout - a.Co1), opts);
   at::Tensor stats;
   a.persist_blocks = (cfg >= 4 ? 1 : 2) * num_cus();   // cfg 4/5: one 8-wave workgroup per CU
-  {
-    const int pb = knob("CONV_PERSIST", -1);
-    if (pb >= 0) a.persist_blocks = pb * num_cus();
-  }
   // small layers: split the input-channel chunks across workgroups so the grid fills the
   // chip; partial sums go through an fp32 buffer and a deterministic finalize
   const int nchunks_total = (a.Cin + 31) / 32;
@@ -298,8 +290,6 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
       for (int ks = 2; ks <= 8; ++ks)
         if (nchunks_total % ks == 0 && nchunks_total / ks >= 2 && items * ks <= 2 * num_cus())
           best = ks;
-    const int kx = knob("CONV_KSPLIT", -1);
-    if (kx >= 1 && nchunks_total % kx == 0) best = kx;
     a.ksplit = best;
   }
   at::Tensor part;
@@ -362,22 +352,13 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   if (a.pscale) TORCH_CHECK(a.C1 <= 512, "prologue supports C1 <= 512");
   if (a.pscale2) TORCH_CHECK(dual && a.pshift2 && a.C1 + a.C2 <= 512, "X2 prologue: x2, pscale2/pshift2, C1 + C2 <= 512");
   int bco = a.Cout <= 32 ? 32 : 64;
-  const int use_v2 = knob("WGRAD_V2", 1);
-  // (images narrower than the 16-pixel tile rows run with masked columns: DDLPC_WGRAD_MINW)
-  // (8: the 8x8 bottleneck layers, 10% faster than the v1 kernel there)
-  const int min_w = knob("WGRAD_MINW", 8);
-  const bool v2 = use_v2 && (use_v2 != 2 || g.dims == 2) && g.W >= min_w && (a.C2 == 0 || a.C1 % 32 == 0);
-  // v3 (32x32x16 MFMA, conflict-free transposed reads): whole 32-channel input chunks
-  const int use_v3 = knob("WGRAD_V3", 1);
-  // (the large 64-channel concat layers dec3.a / dec2.a: v3 since round 3 — same-process
-  // bench A/B at batch 256 -0.8% step time, profiles/r3s/bench_ab_wgrad3_concat_r3s9.log;
-  // DDLPC_WGRAD3_CONCAT=0: back on v2's 96-pixel tiles, which were 4-5% faster at batch 128
-  // before the v3 prologue hoist)
-  const bool v3 = v2 && use_v3 && a.C1 % 32 == 0 && a.C2 % 32 == 0 &&
-                  (!(bco == 64 && a.C2 > 0 && g.H * g.W >= 64 * 64) || knob("WGRAD3_CONCAT", 1) != 0);
-  // 128-pixel tiles (v2: 16 x conv3_wgrad2_pt/16; v3: 256 for 32 output channels, else 128)
-  // (DDLPC_WGRAD3_PT64 = 96 | 128: pixel tile of the 64-channel v3 kernel; default 128)
-  const int v3_pt64 = knob("WGRAD3_PT64", 128);
+  // v2 / v3 (LDS-DMA pixel tiles 16 wide; narrower images run with masked columns: the 8x8
+  // bottleneck layers are 10% faster there than on the v1 kernel)
+  const bool v2 = g.W >= 8 && (a.C2 == 0 || a.C1 % 32 == 0);
+  // v3 (32x32x16 MFMA, conflict-free transposed reads): whole 32-channel input chunks,
+  // concat layers included (same-process bench A/B at batch 256: -0.8% step time,
+  // profiles/r3s/bench_ab_wgrad3_concat_r3s9.log)
+  const bool v3 = v2 && a.C1 % 32 == 0 && a.C2 % 32 == 0;
   if (dy_y.has_value() && dy_y->defined()) {
     // dy holds dA; BN backward applied on load (v2 kernel only)
     CHECK_CONTIG(*dy_y); CHECK_BF16(*dy_y);
@@ -391,34 +372,28 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
     a.dys4 = dy_s4->data_ptr<float>();
     a.dycoef = dy_coefs->data_ptr<float>();
   }
-  // (DDLPC_WGRAD3_RING=1: 32-output-channel layers on 128-pixel tiles with a 3-deep DMA ring)
-  const int v3_ring = knob("WGRAD3_RING", 0);
   // the image layer: <= 4 real channels (cin_real, from the caller) of an 8-channel padded
-  // input, (tap, channel)-packed kernel (DDLPC_WGRAD_IMG=0: the v2 path)
+  // input, (tap, channel)-packed kernel
   const bool img = cin_real > 0 && cin_real <= 4 && a.C1 == 8 && !dual && g.dims == 2 && g.W >= 16 &&
-                   a.pscale == nullptr && a.pscale2 == nullptr && knob("WGRAD_IMG", 1) != 0;
+                   a.pscale == nullptr && a.pscale2 == nullptr;
   // v3 with 128 output channels per workgroup (every wave a 32-channel quarter, no k-split;
   // 96-pixel tiles): each staged input halo feeds twice the MFMAs of the 64-channel tiles
-  // (DDLPC_WGRAD3_BCO128=0: 64-channel tiles)
   // (>= 32x32 images: on the 16^2 / 8^2 levels the 96-pixel tiles are mostly masked columns,
   // measured 3-21% slower there)
-  if (v3 && !img && a.Cout >= 128 && g.H * g.W >= 32 * 32 && knob("WGRAD3_BCO128", 1) != 0) bco = 128;
+  if (v3 && !img && a.Cout >= 128 && g.H * g.W >= 32 * 32) bco = 128;
   // v3 with two 32-channel input chunks per 64-output-channel workgroup (each staged dY tile
   // feeds both halos; 96-pixel tiles) on the >= 64x64 layers with >= 2 input chunks: dec2.a
   // -13%, enc2.b / dec2.b -5% in isolation; the 8^2 / 16^2 layers lose 3-23% (masked tile
-  // columns): profiles/r3s/wgrad_ab_ciw_b256_r3s21.txt.  DDLPC_WGRAD3_CIW=1: off
+  // columns): profiles/r3s/wgrad_ab_ciw_b256_r3s21.txt
   a.ciw = 1;
-  if (v3 && !img && bco == 64 && knob("WGRAD3_CIW", 2) == 2 && a.Cin >= 64 && g.H * g.W >= 64 * 64)
+  if (v3 && !img && bco == 64 && a.Cin >= 64 && g.H * g.W >= 64 * 64)
     a.ciw = 2;
   // batched prologue transform (v3): on the 32-output-channel tiles (enc1.b / dec1.b -7%);
   // the 64 / 128-channel tiles measured 0-2% slower with it (profiles/r3s/wgrad_xform_ab_b256_r3s36.txt)
-  {
-    const int xk = knob("WGRAD_XFORM", -1);
-    a.xf = xk >= 0 ? xk : (bco == 32 ? 1 : 0);
-  }
+  a.xf = bco == 32 ? 1 : 0;
   if (img) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad_img_pt(bco) / 16; }
   else if (v3 && (bco == 128 || a.ciw == 2)) { a.TD = 1; a.TW = 16; a.TH = 6; }
-  else if (v3) { a.TD = 1; a.TW = 16; a.TH = bco == 32 ? (v3_ring ? 8 : 16) : (v3_pt64 == 96 && a.C2 > 0 ? 6 : 8); }
+  else if (v3) { a.TD = 1; a.TW = 16; a.TH = bco == 32 ? 16 : 8; }
   else if (v2) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad2_pt(bco, a.C2, g.H, g.W) / 16; }
   else if (g.dims == 2) { a.TD = 1; a.TW = g.W >= 16 ? 16 : 8; a.TH = 128 / a.TW; }
   else { a.TW = g.W >= 16 ? 16 : 8; a.TH = 4; a.TD = 128 / (a.TW * a.TH); }
@@ -436,8 +411,8 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   const int base = a.coTiles * a.ciChunks * a.planes;
   // workgroups per CU to aim for (DDLPC_WGRAD_WG_PER_CU): the weight gradient runs
   // concurrently with the data-gradient chain, and its resident workgroups' LDS decides
-  // what else fits on a CU
-  const int wg_per_cu = std::max(1, knob("WGRAD_WG_PER_CU", 2));
+  // what else fits on a CU (two: 1 / 3 / 4 measured -7 / -1.5 / -1.9%, profiles/bench_s2k_*.json)
+  const int wg_per_cu = 2;
   const int target = wg_per_cu * num_cus();
   int splits = std::max(1, (target + base - 1) / base);
   splits = std::min(splits, std::max(1, a.nTiles / 8));
@@ -848,8 +823,6 @@ std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
 bool convt_bwd_fused_ok(const at::Tensor& x, const at::Tensor& dout) {
   if (x.dim() != 4 || dout.dim() != 4 || x.size(3) != 64 || dout.size(3) != 64) return false;
   if (dout.size(1) != 2 * x.size(1) || dout.size(2) != 2 * x.size(2)) return false;
-  const int on = knob("CONVT_FUSED", 1);
-  if (!on) return false;
   const long long K = x.size(0) * x.size(1) * x.size(2);
   if (K * 4 >= (long long)INT32_MAX) return false;
   // one buffer descriptor per split over its dOut rows (32-bit offsets)
@@ -927,10 +900,9 @@ std::vector<at::Tensor> convt_wgrad(const at::Tensor& x, const at::Tensor& dout,
   a.Cin = g.C; a.Cout = go.C;
   a.bn4 = bn4_ptr(bn4, g.C);
   // v2 kernel (64 x 64 wave tiles, LDS-DMA stages): enough 128 x 128 workgroups for two per
-  // CU, every split >= 4 stages of 64 pixels; DDLPC_CONVT_WG2=0 keeps the v1 kernel
-  const int use_wg2 = knob("CONVT_WG2", 1);
+  // CU, every split >= 4 stages of 64 pixels (other shapes: the v1 kernel)
   int splits;
-  a.wg2 = use_wg2 && g.C % 8 == 0 && go.C % 8 == 0 && g.C <= 512;
+  a.wg2 = g.C % 8 == 0 && go.C % 8 == 0 && g.C <= 512;
   if (a.wg2) {
     const int tiles = convt_wgrad2_tiles(a);
     splits = std::max(1, (2 * num_cus() + tiles - 1) / tiles);
@@ -1361,22 +1333,6 @@ int64_t set_cu_reserve(int64_t k) {
   return num_cus();
 }
 
-// a HIP stream restricted to CUs {i : i % K == k} (K concurrent micro-batch streams, each on
-// its own slice of the chip, interleaved over the XCDs).  ROCm gives a CU-masked stream its
-// own hardware queue, so K such streams never serialise on a shared queue.  -> the stream
-// handle (never destroyed: the Trainer keeps it for the process lifetime)
-int64_t cu_mask_stream(int64_t k, int64_t K) {
-  TORCH_CHECK(K >= 1 && k >= 0 && k < K, "cu_mask_stream: 0 <= k < K");
-  const int n = phys_cus();
-  std::vector<uint32_t> mask((n + 31) / 32, 0u);
-  for (int i = 0; i < n; ++i)
-    if (i % K == k) mask[i / 32] |= 1u << (i % 32);
-  hipStream_t s = nullptr;
-  TORCH_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) == hipSuccess,
-              "hipExtStreamCreateWithCUMask failed");
-  return reinterpret_cast<int64_t>(s);
-}
-
 // single-GPU stand-in for a bucket all-reduce (Trainer comm_proxy): `blocks` workgroups
 // stream the bucket `passes` times (read + write back, values unchanged) on the current
 // stream — RCCL's footprint (a few tens of channels, each a streaming workgroup)
@@ -1395,7 +1351,6 @@ void comm_proxy(const at::Tensor& g, int64_t blocks, int64_t passes) {
 TORCH_LIBRARY(ddlpc, m) {
   m.def("set_cu_reserve(int k) -> int", &ddlpc::set_cu_reserve);
   m.def("set_knob(str name, int value) -> int", &ddlpc::set_knob);
-  m.def("cu_mask_stream(int k, int K) -> int", &ddlpc::cu_mask_stream);
   m.def("comm_proxy(Tensor(a!) g, int blocks, int passes) -> ()");
   m.def("conv3_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, Tensor? pscale, Tensor? pshift, "
         "int cout, int co1, bool stats, Tensor? pscale2=None, Tensor? pshift2=None, Tensor? bnb_y=None, "

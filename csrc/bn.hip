@@ -382,9 +382,7 @@ int bn_bwd_reduce_blocks(long long items) {
 
 namespace {
 bool bn_bwd2_ok(int dims, bool pool, int D, int H, int W, int C) {
-  const int v2 = knob("BN_BWD_V2", 1);
   const int G = C / 8;
-  if (!v2 || (v2 == 2 && dims == 3)) return false;
   if (C % 8 != 0 || (G & (G - 1)) != 0 || G > 256) return false;
   if (pool && (G > 32 || H % 2 != 0 || W % 2 != 0 || (dims == 3 && D % 2 != 0))) return false;
   return true;

@@ -71,13 +71,12 @@ struct Cfg {
 // operand the pixel tile, so each lane's accumulator holds 4 CONSECUTIVE channels of one
 // pixel -> 8-byte bf16x4 stores; BN statistics are reduced with 4 lane shuffles and
 // written as one partial row per (m tile, wave row).
-template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, int FDB, bool BNB, bool ILV>
+template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, int FDB, bool BNB>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_kernel(ConvFwdArgs p) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
   static_assert(NBB == 2 || NBB == 3 || (NBB == 4 && DIMS == 2), "2 / 3 weight-stage buffers, or 4 (super-stages)");
   // BN-backward epilogue: 2-D, and not with the counted waits of the 3-deep weight ring
   static_assert(!BNB || (DIMS == 2 && NBB != 3), "BNB: 2-D, NBB 2 or 4");
-  static_assert(!ILV || NBB == 4, "DMA issue interleaved with the MFMAs: super-stages only");
   constexpr bool FRAG_DB = FDB == 1;            // (FDB 2: rolling pipeline, pipe_taps)
   constexpr int BM = C::BM, BN = C::BN;
   constexpr int NG = DIMS == 2 ? 3 : 9;           // (kd, r) kernel rows per chunk
@@ -576,7 +575,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[tt & 1][nt], xf[tt & 1][mt], acc[mt][nt]);
       if (p.prio & 2) __builtin_amdgcn_s_setprio(0);
-      hook(tt);                                   // ILV: this tap's share of the next DMAs
+      hook(tt);
       if (FRAG_DB) __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -702,10 +701,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       if ((2 * j) % spi == 0 && j > 0) epilogue(k0 - 1);
       // chunk whose halo is issued at this super-stage (-1: none)
       const int cA = j % 3 == 2 ? 2 * ((j + 1) / 3) : (j % 3 == 0 && j > 0) ? 2 * (j / 3) + 1 : -1;
-      if constexpr (!ILV) {
-        if (j + 1 < J) issue_Bj(j + 1);
-        if (cA >= 0) issue_Ac(cA);
-      }
+      if (j + 1 < J) issue_Bj(j + 1);
+      if (cA >= 0) issue_Ac(cA);
       // BNB: an item's last (ylead 2: second-to-last) super-stage loads y for its epilogue
       if (BNB && KS == 1) {
         if (y2) {
@@ -716,60 +713,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       }
       // P is even (nchunks even): both pairs exist; one 6-tap fragment pipeline across them
       const int c0 = (2 * j) / NG, c1 = (2 * j + 1) / NG;
-      if constexpr (ILV) {
-        // ILV: the next super-stage's DMAs (2 x B_ITERS weight pieces, A_ITERS halo pieces)
-        // issued between the taps' MFMAs instead of in one burst before them: every wave of
-        // the workgroup left the barrier together, so a burst stalls both waves of a SIMD
-        // in their issue at once (an LDS-DMA instruction costs ~60-185 issue cycles)
-        bool hB[2];
-        int sB_off[2], chB[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int pp = 2 * (j + 1) + h;
-          hB[h] = j + 1 < J && pp < P;
-          const int cs = hB[h] ? pp / NG : 0;
-          chB[h] = chunk0_of(cs / nchunks) + cs % nchunks;
-          sB_off[h] = ((pp % NG) * 3 * p.CinW + chB[h] * BK) * 2;
-        }
-        const bool doA = cA >= 0 && cA < total_chunks;
-        int c0A = 0, CsA = p.C1;
-        __amdgpu_buffer_rsrc_t rA = rW;
-        if (doA) {
-          const int kA = cA / nchunks;
-          if (kA != a_item) set_item_pixels(kA);
-          const int cbase = (chunk0_of(kA) + cA % nchunks) * BK;
-          const bool second = cbase >= p.C1;
-          CsA = second ? p.C2 : p.C1;
-          c0A = second ? cbase - p.C1 : cbase;
-          rA = make_rsrc((second ? p.X2 : p.X1) + a_nimg * img_px * CsA, (unsigned)(img_px * CsA * 2));
-        }
-        auto hook = [&](int tt) __attribute__((always_inline)) {
-#pragma unroll
-          for (int q = 0; q < 2 * C::B_ITERS; ++q) {
-            if (q * 6 / (2 * C::B_ITERS) != tt) continue;
-            const int h = q / C::B_ITERS, i = q % C::B_ITERS;
-            if (hB[h]) {
-              const bool ok = b_off[i] >= 0 && chB[h] * BK + sub8 < p.CinW;
-              dma16(rW, sB(2 * ((j + 1) & 1) + h) + (i * C::NW + wave) * 1024,
-                    ok ? (unsigned)(b_off[i] + sB_off[h]) : kOOB);
-            }
-          }
-#pragma unroll
-          for (int i = 0; i < C::A_ITERS; ++i) {
-            if (i * 6 / C::A_ITERS != tt) continue;
-            if (doA) {
-              const int c8 = c0A + sub8;
-              const unsigned off = (a_pix[i] >= 0 && c8 < CsA) ? (unsigned)(a_pix[i] * CsA + c8) * 2u : kOOB;
-              dma16(rA, sA(cA & 1) + (i * C::NW + wave) * 1024, off);
-            }
-          }
-        };
-        compute2(sA(c0 & 1), sB(2 * (j & 1)), (2 * j) % NG, sA(c1 & 1), sB(2 * (j & 1) + 1),
-                 (2 * j + 1) % NG, hook);
-      } else {
-        compute2(sA(c0 & 1), sB(2 * (j & 1)), (2 * j) % NG, sA(c1 & 1), sB(2 * (j & 1) + 1),
-                 (2 * j + 1) % NG, [](int) {});
-      }
+      compute2(sA(c0 & 1), sB(2 * (j & 1)), (2 * j) % NG, sA(c1 & 1), sB(2 * (j & 1) + 1),
+               (2 * j + 1) % NG, [](int) {});
     }
   }
   if (S > 0) {
@@ -882,38 +827,17 @@ __global__ void conv_splitk_finalize_kernel(const float* __restrict__ part, int 
     }
 }
 
-// fragment double buffering (sched barrier per tap): on by default except the 3-D 4x4-tile
-// configs (VGPR spill); DDLPC_CONV_FDB=0 turns it off for A/B
-bool conv_fdb() {
-  const int v = knob("CONV_FDB", 1);
-  return v != 0;
-}
-
-// super-stages: next-stage DMAs interleaved with the MFMAs (DDLPC_CONV_ILV=1).  Measured at
-// batch 128 (conv_micro, same box): 1-2% slower per layer than one burst, so off
-bool conv_ilv() {
-  const int v = knob("CONV_ILV", 0);
-  return v != 0;
-}
-
-// rolling fragment pipeline (FDB mode 2, pipe_taps) instead of the whole-tap register double
-// buffer / none (DDLPC_CONV_PIPE=0 for A/B)
-bool conv_pipe() {
-  const int v = knob("CONV_PIPE", 1);
-  return v != 0;
-}
-
 template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, int FDB>
 void launch_mode(ConvFwdArgs& a, int grid, hipStream_t st) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
   if constexpr (DIMS == 2 && NBB != 3 && !C::LEAN) {
     if (a.bnb_y != nullptr) {
-      hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB, true, false>), dim3(grid),
+      hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB, true>), dim3(grid),
                          dim3(C::NTH), C::SMEM, st, a);
       return;
     }
   }
-  hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB, false, false>), dim3(grid),
+  hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB, false>), dim3(grid),
                      dim3(C::NTH), C::SMEM, st, a);
 }
 
@@ -929,28 +853,16 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   a.stat_rows = grid;
   const int diag = knob("DIAG_CONV", 0);
   a.diag = diag;
-  a.prio = knob("CONV_PRIO", 2);
-  a.ylead = knob("BNB_YLEAD", 1);      // 2 measured 1-3% slower per layer (profiles/r3s)
-  a.rxf = knob("CONV_XFORM", 1);
-  constexpr int FDB_OK = !(DIMS == 3 && MT * NT >= 16) ? 1 : 0;
-  if constexpr (NBB == 4) {
-    if (conv_ilv()) {
-      if (a.bnb_y != nullptr)
-        hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK, true, true>), dim3(grid),
-                           dim3(C::NTH), C::SMEM, st, a);
-      else
-        hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK, false, true>), dim3(grid),
-                           dim3(C::NTH), C::SMEM, st, a);
-      return;
-    }
-  }
-  if (conv_pipe()) launch_mode<DIMS, WM, WN, MT, NT, HALO, NBB, 2>(a, grid, st);
-  else if (FDB_OK && conv_fdb()) launch_mode<DIMS, WM, WN, MT, NT, HALO, NBB, FDB_OK>(a, grid, st);
-  else launch_mode<DIMS, WM, WN, MT, NT, HALO, NBB, 0>(a, grid, st);
+  a.prio = 2;       // s_setprio around every tap's MFMA cluster (profiles/conv_ab_prio_r3e.txt)
+  a.ylead = 1;      // (y two super-stages ahead: 1-3% slower per layer, profiles/r3s)
+  // batched prologue transform where a lane holds <= 6 halo pieces (the 3-D halos' 11 spill)
+  a.rxf = 1;
+  // rolling fragment pipeline (pipe_taps): every configuration (the whole-tap register
+  // double buffer and no buffering measured slower: profiles/r3s/conv_ab_pipe_r3s1.txt)
+  launch_mode<DIMS, WM, WN, MT, NT, HALO, NBB, 2>(a, grid, st);
 }
 
-// cfg 5 (BM-512, LEAN tiles: never with the BN-backward epilogue): the rolling pipeline, or
-// no fragment double buffering (the whole-tap double buffer does not fit the VGPR budget)
+// cfg 5 (BM-512, LEAN tiles: never with the BN-backward epilogue) on the rolling pipeline
 void launch_cfg5(ConvFwdArgs& a, hipStream_t st) {
   using C = Cfg<2, 4, 2, 8, 4, 640, 2>;
   const int items = a.nTilesM * a.nTilesN * a.ksplit;
@@ -961,38 +873,13 @@ void launch_cfg5(ConvFwdArgs& a, hipStream_t st) {
   }
   a.stat_rows = grid;
   a.diag = knob("DIAG_CONV", 0);
-  a.prio = knob("CONV_PRIO", 2);
-  a.rxf = knob("CONV_XFORM", 1);
-  if (conv_pipe())
-    hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 640, 2, 2, false, false>), dim3(grid),
-                       dim3(C::NTH), C::SMEM, st, a);
-  else
-    hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 640, 2, 0, false, false>), dim3(grid),
-                       dim3(C::NTH), C::SMEM, st, a);
-}
-
-// super-stages (two kernel rows per barrier) in the 8-wave configuration (DDLPC_CONV_SUPER=0: off)
-int conv_super() {
-  const int v = knob("CONV_SUPER", 1);
-  return v;
-}
-
-// weight-stage buffers of the 8-wave configuration: 2 (default) or 3 (DDLPC_CONV_NBB=3).
-// Measured at batch 128 (conv_micro, same box): the 3-deep ring is 2.8% slower over all
-// layers' forward + data gradient — the weight stream is not what limits this kernel.
-int conv_nbb() {
-  const int v = knob("CONV_NBB", 2);
-  return v == 3 ? 3 : 2;
+  a.prio = 2;
+  a.rxf = 1;
+  hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 640, 2, 2, false>), dim3(grid),
+                     dim3(C::NTH), C::SMEM, st, a);
 }
 
 int cfg_wm(int cfg) { return cfg <= 1 || cfg >= 4 ? 4 : cfg == 2 ? 2 : 1; }
-
-// BM-512 configuration (cfg 5): fragment double buffering off by default (VGPR budget of two
-// waves per SIMD with a 128-register accumulator); DDLPC_CONV5_FDB=1 turns it on
-bool conv5_fdb() {
-  const int v = knob("CONV5_FDB", 0);
-  return v != 0;
-}
 
 }  // namespace
 
@@ -1026,17 +913,13 @@ void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st) {
       case 0: launch_cfg<2, 4, 1, 4, 2, 384>(a, st); break;
       case 1: launch_cfg<2, 4, 1, 4, 4, 384>(a, st); break;
       case 2: launch_cfg<2, 2, 2, 4, 4, 192>(a, st); break;
-      case 4: {  // one workgroup per CU: room for 3 weight-stage buffers or 2 super-stages
+      case 4: {  // one workgroup per CU: super-stages (two kernel rows per barrier)
         const int nch = (a.Cin + 31) / 32 / a.ksplit;
-        if (conv_super() && nch % 2 == 0) launch_cfg<2, 4, 2, 4, 4, 384, 4>(a, st);
-        else if (conv_nbb() == 3 && a.bnb_y == nullptr) launch_cfg<2, 4, 2, 4, 4, 384, 3>(a, st);
+        if (nch % 2 == 0) launch_cfg<2, 4, 2, 4, 4, 384, 4>(a, st);
         else launch_cfg<2, 4, 2, 4, 4, 384, 2>(a, st);
         break;
       }
-      case 5:
-        if (conv5_fdb() && !conv_pipe()) launch_cfg<2, 4, 2, 8, 4, 640, 2>(a, st);
-        else launch_cfg5(a, st);
-        break;
+      case 5: launch_cfg5(a, st); break;
       default: launch_cfg<2, 1, 4, 4, 2, 128>(a, st); break;
     }
   } else {

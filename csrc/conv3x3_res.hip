@@ -58,14 +58,11 @@ DDLPC_HOST_DEVICE int res_w_bytes(int Cin, int BN, bool tap8) {
 // stores, each pair wholly in one output (a quarter of mode 1's store instructions)
 // EPI (non-BNB epilogue form): 0 = one block, tiles channel-outer (the round-2 form); 1 = by
 // 16-pixel rows of MFMA tiles with item-independent pixel geometry and packed fp32 bias /
-// statistics; 2 = form 1 interleaved between the tap steps of the next stage's MFMAs from a
-// second accumulator set (measured 10-20% slower: the VALU delays the wave's next MFMAs).
-// BNB keeps form 0.
+// statistics.  BNB keeps form 0.  (Rejected: form 1 interleaved between the next stage's
+// tap steps from a second accumulator set, 10-20% slower: profiles/r3s/res_ilv_ab_b256_r3s24.txt)
 template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF, int SPLIT, bool BNB, int EPI = 1>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_kernel(ConvFwdArgs p) {
   using C = RCfg<WM, WN, MT, NT, HALO, TAP8, NBUF>;
-  constexpr bool ILV = EPI == 2;
-  static_assert(!(ILV && BNB), "interleaved epilogue: not with the BN-backward epilogue");
   static_assert(NBUF == 2 || NBUF == 3, "halo ring depth");
   static_assert(!BNB || (!SPLIT && !TAP8), "BN-backward epilogue: single output, no image layer");
   constexpr int NW = C::NW, BN = C::BN;
@@ -549,17 +546,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     __builtin_amdgcn_s_setprio(1);
   int k = 0, c = 0;
   bool epi_prev = false;                              // stage s-1 ran an epilogue
-  bool epi_prev2 = false;                             // stage s-2 ran an epilogue (ILV)
   for (int s = 0; s < S; ++s) {
-    if constexpr (ILV) {
-      // a stage issues [DMA(s+NBUF-1)] then, inside its compute, [its epilogue's stores]:
-      // younger than DMA(s) are stores(s-2), DMA(s+1), stores(s-1) (NBUF 3) / stores(s-1)
-      if (NBUF == 2) {
-        if (epi_prev) vm_wait<EPI_STORES>(); else vm_wait<0>();
-      } else {
-        vm_wait_dyn((epi_prev2 ? EPI_STORES : 0) + (s + 1 < S ? C::A_ITERS : 0) + (epi_prev ? EPI_STORES : 0));
-      }
-    } else if (NBUF == 2) {
+    if (NBUF == 2) {
       vm_wait<0>();                                   // DMA(s) is the youngest op
     } else {
       // younger than DMA(s): s == 0 -> DMA(1); s >= 1 -> [stores(s-1)] + [DMA(s+1)]
@@ -579,9 +567,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     const int buf = s % NBUF;
     if (!TAP8 && (has_pro || has_pro2)) transform_A(c, buf);
     lds_sync();
-    epi_prev2 = epi_prev;
     epi_prev = (c == 0 && s > 0);
-    if (epi_prev && !ILV) {
+    if (epi_prev) {
       // BNB, 3-deep ring: the y loads (issued before DMA(s+1)) must have landed
       if (BNB && NBUF == 3) { if (s + 1 < S) vm_wait<C::A_ITERS>(); else vm_wait<0>(); }
       epilogue(k - 1);
@@ -632,31 +619,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     };
     const char* Wst = TAP8 ? sW : sW + c * 9 * BN * ROWB;
     auto no_hook = [](int) {};
-    if constexpr (ILV) {
-      if (epi_prev) {
-        // item k-1's epilogue from a copy of its accumulators, one MFMA-tile row after every
-        // (8 / MT)-th tap step (VALU work under the MFMA stream)
-        const EpiCtx e = epi_ctx(k - 1);
-        f32x4_t accP[MT][NT];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt) { accP[mt][nt] = acc[mt][nt]; acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f}; }
-        constexpr int STEP = 8 / MT;
-        if (!(p.diag & 8)) {
-          compute(sA(buf), Wst, [&](int j) __attribute__((always_inline)) {
-            if (j % STEP == 0 && j / STEP < MT) epi_unit(e, j / STEP, accP);
-          });
-        } else {
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) epi_unit(e, mt, accP);
-        }
-      } else if (!(p.diag & 8)) {
-        compute(sA(buf), Wst, no_hook);
-      }
-    } else if (!(p.diag & 8)) {
-      compute(sA(buf), Wst, no_hook);
-    }
+    if (!(p.diag & 8)) compute(sA(buf), Wst, no_hook);
     k = k1; c = c1;
   }
   if (S > 0) {
@@ -719,22 +682,22 @@ int res_smem(const ResVariant& v, int Cin, int C1, bool pro, bool bnb) {   // C1
 
 template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF, int EPIc>
 void launch_res_i(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
-  a.prio = knob("CONV_PRIO", 2);
+  a.prio = 2;       // s_setprio around every tap's MFMA cluster (profiles/conv_ab_prio_r3e.txt)
   // diagnostics only (results wrong): bit 0 no halo DMA, 1 no output stores, 2 no prologue
   // transform, 3 no MFMA stage compute
   a.diag = knob("DIAG_RES", 0);
-  a.rxf = knob("RES_XFORM", 1);
+  a.rxf = 1;        // batched prologue transform (profiles/r3s/res_xform_ab_b256_r3s27.txt)
   constexpr int BNc = WN * NT * 16;
   if (a.Co1 < a.Cout) {
-    // split output at a 32-channel boundary: 16-byte pair stores (DDLPC_RES_SPLIT_PAIRS=0: off)
+    // split output at a 32-channel boundary: 16-byte pair stores
     if constexpr (NT % 2 == 0 && BNc % 32 == 0 && !TAP8) {
-      if (a.Co1 % 32 == 0 && knob("RES_SPLIT_PAIRS", 1)) {
+      if (a.Co1 % 32 == 0) {
         hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 2, false, EPIc>), dim3(grid),
                            dim3(WM * WN * 64), smem, st, a);
         return;
       }
     }
-    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 1, false, (EPIc == 2 && !TAP8) ? 1 : EPIc>), dim3(grid),
+    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 1, false, EPIc>), dim3(grid),
                        dim3(WM * WN * 64), smem, st, a);
   } else if constexpr (!TAP8 && BNc != 96) {
     if (a.bnb_y != nullptr)
@@ -749,19 +712,13 @@ void launch_res_i(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
   }
 }
 
-// DDLPC_RES_EPI: non-BNB epilogue form (kernel EPI above; form 2 only on the 3-deep MT-4
-// variants, the others would need more than 256 VGPRs: scratch spills)
+// non-BNB epilogue form (kernel EPI above): form 0 on the 8-wave 32-channel tiles (form 1
+// measured 1-1.5% slower there), form 1 elsewhere (image layer -19%, 64/96-channel tiles
+// -6..-11%; same-process A/B at batch 256, profiles/r3s/res_epi_ab_b256_r3s25.txt)
 template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF>
 void launch_res(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
-  // default: form 0 on the 8-wave 32-channel tiles (form 1 measured 1-1.5% slower there),
-  // form 1 elsewhere (image layer -19%, 64/96-channel tiles -6..-11%; same-process A/B at
-  // batch 256, profiles/r3s/res_epi_ab_b256_r3s25.txt)
-  const int epi_auto = (WM == 8 && WN == 1 && NT == 2 && !TAP8) ? 0 : 1;
-  const int epi = a.bnb_y != nullptr ? 0 : knob("RES_EPI", -1) < 0 ? epi_auto : knob("RES_EPI", -1);
-  if constexpr (NBUF == 3 && MT == 4) {
-    if (epi == 2) { launch_res_i<WM, WN, MT, NT, HALO, TAP8, NBUF, 2>(a, grid, smem, st); return; }
-  }
-  if (epi == 0) launch_res_i<WM, WN, MT, NT, HALO, TAP8, NBUF, 0>(a, grid, smem, st);
+  constexpr bool form0 = WM == 8 && WN == 1 && NT == 2 && !TAP8;
+  if (form0 || a.bnb_y != nullptr) launch_res_i<WM, WN, MT, NT, HALO, TAP8, NBUF, 0>(a, grid, smem, st);
   else launch_res_i<WM, WN, MT, NT, HALO, TAP8, NBUF, 1>(a, grid, smem, st);
 }
 
@@ -775,13 +732,10 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
   const bool pro = a.pscale != nullptr;
   const bool tap8 = a.Cin <= 8 && a.C2 == 0 && a.CinW == 8 && !pro;
   const int bn = a.Cout == 96 ? 96 : (a.Cout <= 32 || a.Cout % 64 != 0) ? 32 : 64;
-  // preference: 3-deep halo rings (latency hiding) first; DDLPC_RES_DEPTH=2 prefers the
-  // 2-deep, two-workgroups-per-CU variants (A/B experiments)
-  // default (-1): 2-deep for the 64-channel tiles (variant 6: BN-backward data gradients
-  // 9-11% faster, the others 1-3.5%), 3-deep for the 32-channel tiles (the 2-deep 4-wave
-  // variant is 5-11% slower forward): profiles/r3s/res_depth_ab_b256_r3s33.txt
-  const int depth_k = knob("RES_DEPTH", -1);
-  const int depth = depth_k > 0 ? depth_k : (bn == 64 ? 2 : 3);
+  // halo ring depth: 2 for the 64-channel tiles (variant 6: BN-backward data gradients 9-11%
+  // faster, the others 1-3.5%), 3 for the 32-channel tiles (the 2-deep 4-wave variant is
+  // 5-11% slower forward): profiles/r3s/res_depth_ab_b256_r3s33.txt
+  const int depth = bn == 64 ? 2 : 3;
   int cand[3];
   int nc = 0;
   if (tap8) {

@@ -19,6 +19,8 @@
 #include "conv_lds.h"
 #include "ops.h"
 
+#include <stdexcept>
+
 namespace ddlpc {
 
 namespace {
@@ -1097,14 +1099,12 @@ void launch_wg(ConvWgradArgs& a, hipStream_t st) {
 
 }  // namespace
 
-// pixel-tile size of the 2-D kernel.  BCO 64: 128-pixel tiles (two 60 KB workgroups per CU)
-// except for the large concat layers (two input tensors, >= 64x64 images), which measured
+// pixel-tile size of the 2-D v2 kernel.  BCO 64: 128-pixel tiles (two 60 KB workgroups per
+// CU) except for the large concat layers (two input tensors, >= 64x64 images), which measured
 // 25% faster with 96-pixel tiles (three 46 KB workgroups per CU) and slower elsewhere
-// (conv_micro, batch 128).  DDLPC_WGRAD64_PT = 64 | 96 | 128 | 256 forces one size.
+// (conv_micro, batch 128)
 int conv3_wgrad2_pt(int bco, int C2, int H, int W) {
-  const int force = knob("WGRAD64_PT", 0);
   if (bco == 32) return 256;
-  if (force == 64 || force == 96 || force == 128 || force == 256) return force;
   return (C2 > 0 && H * W >= 64 * 64) ? 96 : 128;
 }
 void conv3_wgrad2_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
@@ -1112,37 +1112,29 @@ void conv3_wgrad2_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
   const int pt = a.TH * 16;
   if (bco == 32)
     hipLaunchKernelGGL((conv3_wgrad2_kernel<32, 256>), dim3(grid), dim3(256), (Wg2Cfg<32, 256>::SMEM), st, a);
-  else if (pt == 256)
-    hipLaunchKernelGGL((conv3_wgrad2_kernel<64, 256>), dim3(grid), dim3(256), (Wg2Cfg<64, 256>::SMEM), st, a);
   else if (pt == 96)
     hipLaunchKernelGGL((conv3_wgrad2_kernel<64, 96>), dim3(grid), dim3(256), (Wg2Cfg<64, 96>::SMEM), st, a);
-  else if (pt == 64)
-    hipLaunchKernelGGL((conv3_wgrad2_kernel<64, 64>), dim3(grid), dim3(256), (Wg2Cfg<64, 64>::SMEM), st, a);
   else
     hipLaunchKernelGGL((conv3_wgrad2_kernel<64, 128>), dim3(grid), dim3(256), (Wg2Cfg<64, 128>::SMEM), st, a);
 }
 
+// v3 tiles: 32 output channels on 256-pixel tiles; 64 on 128-pixel tiles, or two 32-channel
+// input chunks per workgroup on 96-pixel tiles (ciw 2); 128 on 96-pixel tiles.  (Rejected:
+// 128-pixel 32-channel tiles with a 3-deep ring, 12-18% slower per layer:
+// profiles/wgrad_micro_b128_ring*_s2.txt.)
 void conv3_wgrad3_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
   const int grid = a.coTiles * a.ciChunks * a.planes * a.splits;
-  const int pt = a.TH * 16;
-  // (32 output channels, 128-pixel tiles: the 3-deep ring variant; LDS = SS + 3 stages)
-  constexpr int SMEM32R = Wg2Cfg<32, 128>::SS_BYTES + 3 * (Wg2Cfg<32, 128>::Y_BYTES + Wg2Cfg<32, 128>::X_BYTES);
-  static_assert(2 * SMEM32R <= 160 * 1024, "two ring workgroups per CU");
   // (64 output channels x two input chunks, 96-pixel tiles: dY + two halos per stage)
   constexpr int SMEM64C2 = Wg2Cfg<64, 96>::SS_BYTES + 2 * (Wg2Cfg<64, 96>::Y_BYTES + 2 * Wg2Cfg<64, 96>::X_BYTES);
   static_assert(2 * SMEM64C2 <= 160 * 1024, "two workgroups per CU");
-  if (bco == 32 && pt == 128)
-    hipLaunchKernelGGL((conv3_wgrad3_kernel<32, 128, 3>), dim3(grid), dim3(256), SMEM32R, st, a);
-  else if (bco == 32)
+  if (a.TH * 16 != (bco == 32 ? 256 : (bco == 128 || a.ciw == 2) ? 96 : 128))
+    throw std::runtime_error("conv3_wgrad3_launch: pixel tile does not match the v3 variant");
+  if (bco == 32)
     hipLaunchKernelGGL((conv3_wgrad3_kernel<32, 256>), dim3(grid), dim3(256), (Wg2Cfg<32, 256>::SMEM), st, a);
   else if (bco == 64 && a.ciw == 2)   // two input chunks per workgroup, 96-pixel tiles
     hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 96, 2, 2>), dim3(grid), dim3(256), SMEM64C2, st, a);
   else if (bco == 128)   // 96-pixel tiles: two 74 KB workgroups per CU
     hipLaunchKernelGGL((conv3_wgrad3_kernel<128, 96>), dim3(grid), dim3(256), (Wg2Cfg<128, 96>::SMEM), st, a);
-  else if (pt == 256)
-    hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 256>), dim3(grid), dim3(256), (Wg2Cfg<64, 256>::SMEM), st, a);
-  else if (pt == 96)
-    hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 96>), dim3(grid), dim3(256), (Wg2Cfg<64, 96>::SMEM), st, a);
   else
     hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 128>), dim3(grid), dim3(256), (Wg2Cfg<64, 128>::SMEM), st, a);
 }

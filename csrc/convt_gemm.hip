@@ -403,7 +403,7 @@ __global__ __launch_bounds__(512, KS == 1 ? 2 : 1) void gemm_nt_fwd2_kernel(Gemm
 // DDLPC_CONVT_FWD2: 0 = v1 kernel, 1 = v2 with one 32-channel chunk per stage (two
 // workgroups per CU), 2 = v2 with two chunks per stage (one workgroup per CU)
 int gemm_nt_fwd2_mode(const GemmArgs& a) {
-  const int v = knob("CONVT_FWD2", 1);
+  const int v = 1;
   const bool ok = a.mode == GEMM_CONVT_FWD && a.K % (v == 2 ? 64 : 32) == 0 && a.K <= 512 &&
                   a.N % 128 == 0 && a.Cout % 32 == 0;
   return ok ? v : 0;
@@ -1000,9 +1000,7 @@ int convt_wgrad2_tiles(const GemmArgs& a) {
 }
 
 int gemm_nt_bn(const GemmArgs& a) {
-  const int fwd_bn = knob("CONVT_BN", 128);
-  const int dgrad_bn = knob("CONVT_DGRAD_BN", 128);
-  return (a.N % 128 == 0 && (a.mode == GEMM_CONVT_FWD ? fwd_bn : dgrad_bn) == 128) ? 128 : 64;
+  return a.N % 128 == 0 ? 128 : 64;      // 128-wide N tiles (fwd -9%, dgrad -7%: docs/PERF.md)
 }
 
 // workgroups of the NT (forward / data-gradient) launch: one BN-partial row each

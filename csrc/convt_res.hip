@@ -345,8 +345,7 @@ struct ResPlan {
 
 ResPlan plan_of(const GemmArgs& a) {
   ResPlan r;
-  const int use = knob("CONVT_RES", 1);
-  if (!use || a.mode == GEMM_CONVT_WGRAD || a.K % BK != 0 || a.Cout % 32 != 0) return r;
+  if (a.mode == GEMM_CONVT_WGRAD || a.K % BK != 0 || a.Cout % 32 != 0) return r;
   const int S = a.dims == 2 ? 4 : 8;
   int tbn = 0;
   if (a.N % 128 == 0 && 128 * a.K * 2 <= 64 * 1024) tbn = 128;

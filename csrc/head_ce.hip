@@ -703,9 +703,7 @@ int head_ce_bwd_blocks(int C, int K, bool /*defer*/, long long P, int num_cus) {
   };
   HEAD_SWITCH(C, K, occ(reinterpret_cast<const void*>(&head_ce_bwd_kernel<CC, KK, true>)));
   HEAD_SWITCH(C, K, occ(reinterpret_cast<const void*>(&head_ce_bwd_kernel<CC, KK, false>)));
-  // DDLPC_HEAD_BWD_PER_CU: workgroups per CU in the grid (A/B knob; default: resident ones)
-  const int pc = knob("HEAD_BWD_PER_CU", 0);
-  if (pc > 0) per_cu = pc;
+  // (the resident workgroups per CU: 4 / 6 / 8 / 12 measured 3-4% slower, docs/PERF.md)
   const long long ppb = 256 / (C / 8);
   return (int)std::max<long long>(1, std::min<long long>((P + ppb - 1) / ppb, (long long)per_cu * num_cus));
 }
@@ -732,7 +730,7 @@ void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
 // the register-accumulator kernel)
 // (K <= 6: the 8- and 16-class instantiations exceed the 168-VGPR budget of three
 // workgroups per CU and spill)
-bool head_mdw(int C, int K) { return C == 32 && K <= 6 && knob("HEAD_MDW", 1) != 0; }
+bool head_mdw(int C, int K) { return C == 32 && K <= 6; }
 
 int head_fwd_stats_blocks(int C, int K, long long P, int num_cus) {
   if (!head_mdw(C, K)) return head_ce_bwd_blocks(C, K, true, P, num_cus);
@@ -745,8 +743,6 @@ int head_fwd_stats_blocks(int C, int K, long long P, int num_cus) {
     else
       per_cu = 1;
   });
-  const int pc = knob("HEAD_BWD_PER_CU", 0);
-  if (pc > 0) per_cu = pc;
   const long long ppb = 64;
   return (int)std::max<long long>(1, std::min<long long>((P + ppb - 1) / ppb, (long long)per_cu * num_cus));
 }
@@ -769,7 +765,7 @@ void head_ce_fwd_stats_launch(const bf16_t* a, const float* Wh, const float* bh,
 
 int head_bn_apply_blocks(long long P, int C) {
   const long long ppb = 256 / (C / 8);
-  const int cap = knob("HEAD_APPLY_BLOCKS", 4096);
+  const int cap = 4096;
   return (int)std::max<long long>(1, std::min<long long>((P + 2 * ppb - 1) / (2 * ppb), cap));
 }
 

@@ -506,7 +506,7 @@ class _HeadCEFn(torch.autograd.Function):
         # two-pass backward with the deferred BatchNorm: this pass reduces dWh, dbh and the
         # BN partials without storing dA; the block's backward then runs head_ce_bn_bwd,
         # which recomputes dA and applies the BatchNorm backward in registers (no dA
-        # round trip through HBM, no separate BN-apply pass).  DDLPC_HEAD_APPLY=0: one pass
+        # round trip through HBM, no separate BN-apply pass).  engine.head_apply = False: one pass
         two_pass = bn is not None and eng.head_apply
         if ctx.rows is not None:
             # statistics already reduced by the forward at unit scale: scale = dL / count
@@ -629,10 +629,8 @@ class UNetEngine:
         # two chains are independent until the optimizer step, and the small deep-layer
         # kernels of one fill the CUs the other leaves idle.  DDLPC_WGRAD_STREAM=0 disables.
         use_side = os.environ.get("DDLPC_WGRAD_STREAM", "1") != "0"
-        # low priority: when both streams have work queued, the critical data-gradient
-        # chain is dispatched first and the weight gradients fill what is left
-        prio = int(os.environ.get("DDLPC_SIDE_PRIORITY", "1"))
-        self.side = torch.cuda.Stream(dev, priority=prio) if use_side else None
+        # (stream priorities measured within +-0.3%: a plain stream)
+        self.side = torch.cuda.Stream(dev) if use_side else None
         self._side_stream = self.side
         self._side_used = False
         # memory the side stream's lag may hold back (see ``wgrad_stream``): default 6% of
@@ -644,10 +642,10 @@ class UNetEngine:
         self._lag: List[Tuple[torch.cuda.Event, int]] = []
         self._lag_bytes = 0
         self.lag_waits = 0
-        # deferred BatchNorm activations (see ``features``): DDLPC_DEFER_BN=all|convt|none
-        self.defer_mode = os.environ.get("DDLPC_DEFER_BN", "all")
-        # transposed-conv weight gradients on the side stream too (DDLPC_SIDE_CONVT=0: main)
-        self.side_convt = os.environ.get("DDLPC_SIDE_CONVT", "1") != "0"
+        # deferred BatchNorm activations (see ``features``): "all" | "convt" | "none"
+        self.defer_mode = "all"
+        # transposed-conv weight gradients on the side stream too
+        self.side_convt = True
         self.recompute = 0               # Trainer sets cfg.recompute: 0 / 1 (y1) / 2 (y1, y2)
         # per-micro-batch BatchNorm groups of a batched accumulation window (Trainer
         # bn_window): > 1 = the training batch is that many micro-batches, each normalised
@@ -655,22 +653,22 @@ class UNetEngine:
         self.bn_groups = 0
         # encoder skips handed out pre-BN (see ``defer_skip_levels``): saves ~1 GB at
         # 256^2 x 128 but measured ~1.2% slower end to end (docs/PERF.md), so opt-in
-        self.defer_skip = os.environ.get("DDLPC_DEFER_SKIP", "0") != "0"
+        self.defer_skip = False
         # BN1 backward's reduction pass fused into the epilogue of the data gradient that
-        # produces its input gradient (2-D; DDLPC_BNB_EPI=0: separate reduction kernel)
-        self.bnb_epilogue = os.environ.get("DDLPC_BNB_EPI", "1") != "0"
+        # produces its input gradient (2-D; False: separate reduction kernel)
+        self.bnb_epilogue = True
         # two-pass head backward with the last block's BN backward fused into the second
-        # pass (see _HeadCEFn.backward; DDLPC_HEAD_APPLY=0: dA stored + separate BN apply)
-        self.head_apply = os.environ.get("DDLPC_HEAD_APPLY", "1") != "0"
-        # ... and its statistics pass fused into the training forward (DDLPC_HEAD_FUSED_FWD=0:
-        # separate forward and statistics passes)
-        self.head_fused_fwd = os.environ.get("DDLPC_HEAD_FUSED_FWD", "1") != "0"
+        # pass (see _HeadCEFn.backward; False: dA stored + separate BN apply)
+        self.head_apply = True
+        # ... and its statistics pass fused into the training forward (False: separate
+        # forward and statistics passes)
+        self.head_fused_fwd = True
         # 64 -> 64-channel transposed conv: data + weight gradient in one kernel
-        # (DDLPC_CONVT_FUSED=0: separate kernels, weight gradient on the side stream)
-        self.convt_fused = os.environ.get("DDLPC_CONVT_FUSED", "1") != "0"
+        # (False: separate kernels, weight gradient on the side stream)
+        self.convt_fused = True
         # first block: BN1 backward applied on load by its weight gradient (no apply pass;
-        # DDLPC_WGRAD_DYP=0: separate bn_backward)
-        self.wgrad_dy_prologue = os.environ.get("DDLPC_WGRAD_DYP", "1") != "0"
+        # False: separate bn_backward)
+        self.wgrad_dy_prologue = True
         self.enc = [_Block(b.double_conv, first=(i == 0), engine=self)
                     for i, b in enumerate(model.down_blocks())]
         self.mid = _Block(model.double_conv, first=False, engine=self)
@@ -892,18 +890,12 @@ class UNetEngine:
         """Encoder levels whose skip tensor stays pre-BN (BN + ReLU applied on load by the
         decoder's concat conv, forward and weight gradient): 2-D, the skip image at least 16
         wide (the weight-gradient kernels with the X2 prologue) and the concat at most 512
-        channels (prologue constants in LDS).  Opt-in with DDLPC_DEFER_SKIP=1 (or engine.defer_skip)."""
+        channels (prologue constants in LDS).  Opt-in: ``engine.defer_skip = True``."""
         if not self.defer_skip or x.dim() != 4:
             return [False] * len(self.enc)
         out = []
         w = x.shape[-1]
-        # DDLPC_DEFER_SKIP_LEVELS=0,1: only those encoder levels (0 = full resolution)
-        lv = os.environ.get("DDLPC_DEFER_SKIP_LEVELS", "")
-        only = {int(v) for v in lv.split(",") if v.strip()} if lv else None
         for lvl, blk in enumerate(self.enc):
-            if only is not None and lvl not in only:
-                out.append(False)
-                continue
             ub, _pack, dblk = self.dec[len(self.dec) - 1 - lvl]
             c_up = dblk.conv1.weight.shape[1] - blk.conv2.weight.shape[0]
             c_skip = blk.conv2.weight.shape[0]

@@ -107,11 +107,6 @@ class Trainer:
             enable_ranges(True)
         self.phases = PhaseTimer(self.device) if cfg.phase_timers else None
         self.profiler = StepProfiler(cfg.profile_dir, self.rank, active=cfg.profile_steps)
-        # optional dedicated compute stream for the train step (DDLPC_STEP_PRIORITY=<int>; the
-        # default runs on the current stream: measured, priorities did not change the overlap)
-        sp = os.environ.get("DDLPC_STEP_PRIORITY", "none")
-        self.stream = (torch.cuda.Stream(self.device, priority=int(sp))
-                       if self.device.type == "cuda" and sp not in ("", "none") else None)
         # host run-ahead bound: before queueing a step the host waits until the step
         # ``max_inflight`` steps back has finished on the GPU.  Unbounded run-ahead queues
         # thousands of cross-stream barrier packets (weight-gradient side stream); measured:
@@ -123,7 +118,7 @@ class Trainer:
         self.micro_count = 0
         self.micro_streams = self._resolve_micro_streams()
         self._mstreams: List[torch.cuda.Stream] = []     # concurrent micro-batch streams
-        self._ms_mode = None
+        self.ms_graph = True                               # ... each replaying its own graph
         self._ms_meters: List[DeviceMeter] = []
         self._ms_graphs, self._ms_warm, self._ms_static = [], [], []
         self.ms_host_s = 0.0
@@ -268,20 +263,10 @@ class Trainer:
         return [FlatParams._view(buf, f.offsets[id(p)], p) for p in f.order]
 
     def _ms_streams(self, K: int, cur) -> List[torch.cuda.Stream]:
-        """K micro-batch streams: plain HIP streams (default), or with DDLPC_MS_MODE=2
-        CU-masked ones (stream k on CUs {i : i % K == k}, each its own hardware queue).
-        Measured at 512² batch 1 with graphs (docs/PERF.md): the masked streams run 2-3x
-        SLOWER than plain ones (171 vs 515 images/s at K = 4), so they stay a diagnostic."""
-        mode = int(os.environ.get("DDLPC_MS_MODE", "0"))
-        if len(self._mstreams) != K or self._ms_mode != mode:
-            if mode == 2:
-                F = _ext.ops()
-                self._mstreams = [torch.cuda.ExternalStream(int(F.cu_mask_stream(k, K)),
-                                                            device=self.device)
-                                  for k in range(K)]
-            else:
-                self._mstreams = [torch.cuda.Stream(self.device) for _ in range(K)]
-            self._ms_mode = mode
+        """K plain HIP micro-batch streams.  (CU-masked streams, one chip slice each, were
+        measured 2-3x slower than plain ones: 171 vs 515 images/s at K = 4, docs/PERF.md.)"""
+        if len(self._mstreams) != K:
+            self._mstreams = [torch.cuda.Stream(self.device) for _ in range(K)]
             self._ms_graphs, self._ms_warm, self._ms_static = [None] * K, [0] * K, [None] * K
         return self._mstreams
 
@@ -296,14 +281,10 @@ class Trainer:
         return [self._flat_views] + self._mviews[:K - 1]
 
     def _ms_enter(self, K: int):
-        """Per-window setup: side stream off; with DDLPC_MS_SPLIT=1 the persistent /
-        chip-filling grids are sized for 1/K of the chip (default: full-chip grids)."""
+        """Per-window setup: the weight-gradient side stream off (returns its state)."""
         eng = self.model._engine
-        state = (eng.side is not None, os.environ.get("DDLPC_MS_SPLIT", "0") != "0")
+        state = eng.side is not None
         eng.set_side_stream(False)
-        if state[1]:
-            phys = torch.cuda.get_device_properties(self.device).multi_processor_count
-            _ext.ops().set_cu_reserve(phys - phys // K)
         return state
 
     def _ms_exit(self, state):
@@ -311,9 +292,7 @@ class Trainer:
         eng.bn_defer_j = None
         for p, g in zip(self.flat.order, self._flat_views):
             p.grad = g
-        eng.set_side_stream(state[0])
-        if state[1]:
-            _ext.ops().set_cu_reserve(self.reserve_cus)
+        eng.set_side_stream(state)
 
     def _ms_finish(self, K: int, n: int):
         """After the streams joined: extra gradient buffers into the flat one (stream
@@ -365,8 +344,8 @@ class Trainer:
         streams = self._ms_streams(K, cur)
         views = self._ms_buffers(K)
         # per-stream graphs by default: without them the host's ~230 launches per
-        # micro-batch become the limit once the streams overlap (DDLPC_MS_GRAPH=0: eager)
-        use_graph = os.environ.get("DDLPC_MS_GRAPH", "1") != "0"
+        # micro-batch become the limit once the streams overlap (ms_graph = False: eager)
+        use_graph = self.ms_graph
         state = self._ms_enter(K)
         eng.bn_defer_prepare(K, len(mbs))
         order = self.flat.order
@@ -542,14 +521,7 @@ class Trainer:
         if self.max_inflight > 0 and self.device.type == "cuda":
             while len(self._inflight) >= self.max_inflight:
                 self._inflight.pop(0).synchronize()
-        if self.stream is None:
-            out = self._train_step(micro_batches)
-        else:
-            cur = torch.cuda.current_stream(self.device)
-            self.stream.wait_stream(cur)             # inputs produced on the caller's stream
-            with torch.cuda.stream(self.stream):
-                out = self._train_step(micro_batches)
-            cur.wait_stream(self.stream)             # caller sees the finished step
+        out = self._train_step(micro_batches)
         if self.max_inflight > 0 and self.device.type == "cuda":
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))

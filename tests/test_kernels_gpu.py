@@ -78,14 +78,6 @@ def test_conv3_fwd(ops, N, H, W, C1, C2, Cout):
     (64, 32, 32, 256, 0, 256, True, 0), (64, 32, 32, 128, 0, 384, False, 256)])
 def test_conv3_fwd_bigtile(ops, N, H, W, C1, C2, Cout, pro, co1):
     torch.manual_seed(5)
-    prev = ops.set_knob("CONV_CFG5", 2)        # every eligible shape (default: K >= 9 x 256)
-    try:
-        _bigtile(ops, N, H, W, C1, C2, Cout, pro, co1)
-    finally:
-        ops.set_knob("CONV_CFG5", 1 if prev < -2**62 else prev)
-
-
-def _bigtile(ops, N, H, W, C1, C2, Cout, pro, co1):
     x1 = torch.randn(N, C1, H, W, device=DEV).bfloat16()
     x2 = torch.randn(N, C2, H, W, device=DEV).bfloat16() if C2 else None
     w = torch.randn(Cout, C1 + C2, 3, 3, device=DEV) * (1.0 / math.sqrt(9 * (C1 + C2)))

@@ -303,7 +303,7 @@ def test_recompute_matches_stored_activations():
 
 
 def test_deferred_skips_match_materialised_engine():
-    """Engine level: with the encoder skips handed out pre-BN (DDLPC_DEFER_SKIP=1, opt-in)
+    """Engine level: with the encoder skips handed out pre-BN (engine.defer_skip = True, opt-in)
     a training step gives bit-identical loss and gradients to materialised skips."""
     from ddlpc.models.unet import UNet
     torch.manual_seed(3)
@@ -361,24 +361,20 @@ def test_bf16_hip_training_curve_tracks_fp32_reference():
     assert abs(mh - mf) <= 0.08, res
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
-def test_concurrent_micro_streams_match_sequential_accumulation(monkeypatch, split):
+def test_concurrent_micro_streams_match_sequential_accumulation():
     """micro_streams > 1 (accumulation micro-batches on several HIP streams at once, the
-    batch-1 reference regime).  With full-chip grids (DDLPC_MS_SPLIT=0, default) the
-    per-micro-batch losses and the BatchNorm running statistics are bit-identical to the
-    one-by-one loop (deferred running-stat updates applied in order) and the accumulated
-    gradient equals the sequential one up to fp32 summation order.  With split grids
-    (DDLPC_MS_SPLIT=1: 1/K of the chip per stream) the BatchNorm partial sums are grouped
-    differently: everything agrees to fp32 rounding."""
+    batch-1 reference regime): the per-micro-batch losses and the BatchNorm running
+    statistics are bit-identical to the one-by-one loop (deferred running-stat updates
+    applied in order) and the accumulated gradient equals the sequential one up to fp32
+    summation order."""
     from ddlpc.config import ModelConfig, TrainConfig
     from ddlpc.data import device_random_batch
     from ddlpc.train.trainer import Trainer
-    monkeypatch.setenv("DDLPC_MS_SPLIT", split)
     res = {}
     for ms in (1, 3):
         cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=2,
                           num_samples=1, test_holdout=0, impl="hip", micro_streams=ms,
-                          accum_steps=7)
+                          accum_steps=7, bn_window=0)
         tr = Trainer(cfg, device="cuda")
         mbs = [device_random_batch(2, 64, 6, tr.device, seed=100 + j) for j in range(6)]
         tr.optimizer.zero_grad()
@@ -398,16 +394,10 @@ def test_concurrent_micro_streams_match_sequential_accumulation(monkeypatch, spl
         tr.close()
     (g1, m1, b1), (g3, m3, b3) = res[1], res[3]
     scale = float(g1.abs().max())
-    if split == "0":
-        assert torch.equal(m1, m3), (m1, m3)             # identical per-micro-batch losses
-        for k in b1:
-            assert torch.equal(b1[k], b3[k]), k          # running stats / counters
-        assert float((g1 - g3).abs().max()) <= 1e-5 * scale, float((g1 - g3).abs().max())
-    else:
-        assert torch.allclose(m1, m3, rtol=1e-4), (m1, m3)
-        for k in b1:
-            assert torch.allclose(b1[k].double(), b3[k].double(), rtol=1e-3, atol=1e-4), k
-        assert float((g1 - g3).abs().max()) <= 2e-2 * scale, float((g1 - g3).abs().max())
+    assert torch.equal(m1, m3), (m1, m3)                 # identical per-micro-batch losses
+    for k in b1:
+        assert torch.equal(b1[k], b3[k]), k              # running stats / counters
+    assert float((g1 - g3).abs().max()) <= 1e-5 * scale, float((g1 - g3).abs().max())
 
 
 def test_concurrent_micro_stream_graphs():
