@@ -146,7 +146,7 @@ class _DoubleConvFn(torch.autograd.Function):
         p1, p2 = blk.pack1, blk.pack2
         training = blk.bn1.bn.training
         G = blk.engine.bn_groups if training else 0
-        if G > 1:
+        if G >= 1:
             assert not defer and not defer_skip and x2_bn is None, "BN groups: no deferred BN"
             return _DoubleConvFn._group_forward(ctx, x1, x2, b1, b2, g1, g2, blk, pool, G)
         ctx.groups = 0
@@ -648,8 +648,9 @@ class UNetEngine:
         self.side_convt = True
         self.recompute = 0               # Trainer sets cfg.recompute: 0 / 1 (y1) / 2 (y1, y2)
         # per-micro-batch BatchNorm groups of a batched accumulation window (Trainer
-        # bn_window): > 1 = the training batch is that many micro-batches, each normalised
-        # with its own statistics (no deferred BN / prologue fusion in this mode)
+        # bn_window): G >= 1 = the training batch is G micro-batches, each normalised with
+        # its own statistics (no deferred BN / prologue fusion in this mode; G = 1 runs one
+        # micro-batch through the same unfused kernels); 0 = the fused path
         self.bn_groups = 0
         # encoder skips handed out pre-BN (see ``defer_skip_levels``): saves ~1 GB at
         # 256^2 x 128 but measured ~1.2% slower end to end (docs/PERF.md), so opt-in
@@ -867,7 +868,7 @@ class UNetEngine:
         self._ensure_packed()
         h = self.to_nhwc(x)
         skips = []
-        grouped = self.bn_groups > 1 and self.enc[0].bn1.bn.training
+        grouped = self.bn_groups >= 1 and self.enc[0].bn1.bn.training
         dskip = self.defer_skip_levels(x) if not grouped else [False] * len(self.enc)
         for lvl, blk in enumerate(self.enc):
             skip, h, s_skip = blk(h, None, True, defer_skip=dskip[lvl])
@@ -920,17 +921,17 @@ class UNetEngine:
 
     def loss_and_correct(self, x: torch.Tensor, y: torch.Tensor, ignore_index: int = -100):
         """-> (mean cross-entropy over the batch's pixels, correct-pixel count).  With
-        ``bn_groups`` = G > 1 (training) the batch is G equal micro-batches with their own
+        ``bn_groups`` = G >= 1 (training) the batch is G equal micro-batches with their own
         BatchNorm statistics; the running statistics are updated once per micro-batch, in
         order, after the forward (bit-for-bit the update sequence of G forwards)."""
         G = self.bn_groups if self.enc[0].bn1.bn.training else 0
-        if G > 1:
+        if G >= 1:
             if x.shape[0] % G:
                 raise ValueError(f"bn_groups={G} must divide the batch ({x.shape[0]})")
             self.bn_defer_prepare(1, G)
         a, s = self.features(x, defer_last=True)
         wh, bh = self._head_params()
         out = _HeadCEFn.apply(a, wh, bh, y.contiguous(), ignore_index, self, s)
-        if G > 1:
+        if G >= 1:
             self.bn_defer_apply(G)
         return out

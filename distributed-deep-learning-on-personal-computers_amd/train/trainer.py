@@ -572,7 +572,7 @@ class Trainer:
             x, y = self._cat_window(ch) if len(ch) > 1 else ch[0]
             if self.reducer is not None:
                 self.reducer.prepare(sync=ci == len(chunks) - 1)
-            eng.bn_groups = len(ch)
+            eng.bn_groups = len(ch) if len(ch) > 1 else 0
             try:
                 loss, correct = self.model.loss_and_correct(x, y)
                 (loss * float(len(ch)) if len(ch) > 1 else loss).backward()

@@ -325,24 +325,32 @@ def test_deferred_skips_match_materialised_engine():
 
 def test_bf16_hip_training_curve_tracks_fp32_reference():
     """The reference trains in fp32 with no autocast (ref.py:702-704,754-756); the HIP engine
-    computes in bf16 with fp32 master weights and fp32 Adam.  Same init, same synthetic
-    stream (same samples in the same order), 200 optimizer steps: HIP bf16 vs stock-PyTorch
-    fp32 (``impl="torch", dtype="fp32"``).  Tolerances: final train loss (mean of the last 20
-    steps) within 0.05 + 25%, held-out pixel accuracy within 0.05 and mIoU within 0.08."""
+    computes in bf16 with fp32 master weights and fp32 Adam.  Same synthetic stream (same
+    samples in the same order), 200 optimizer steps: HIP bf16 vs stock-PyTorch fp32
+    (``impl="torch", dtype="fp32"``) from the SAME init, and a second fp32 run from ANOTHER
+    init as the yardstick.  The bf16-vs-fp32 gap of the final train loss (mean of the last 20
+    steps), held-out pixel accuracy and mIoU must stay within twice the fp32 seed-to-seed
+    spread (floors 0.02 / 0.01 / 0.02 for a run where the two seeds happen to agree)."""
     import os
     os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")   # fp32 MIOpen: heuristic kernel choice
     from ddlpc.config import ModelConfig, TrainConfig
     from ddlpc.train.trainer import Trainer
     steps, B = 200, 8
     res = {}
-    for impl, dtype in (("hip", "bf16"), ("torch", "fp32")):
+    data = None
+    for name, impl, dtype, seed in (("hip", "hip", "bf16", 7), ("fp32", "torch", "fp32", 7),
+                                    ("fp32_seed8", "torch", "fp32", 8)):
         cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=B,
                           num_samples=steps * B, test_holdout=64, impl=impl, dtype=dtype,
-                          seed=7)
+                          seed=seed)
         tr = Trainer(cfg, device="cuda")
         assert tr.impl == impl and tr.autocast is False
         if impl == "hip":
             tr.model._engine.set_side_stream(False)
+        elif data is None:
+            data = (tr.train_set, tr.test_set)           # the seed-7 stream (NCHW layout)
+        else:
+            tr.train_set, tr.test_set = data             # another init, the same samples
         losses = []
         for i in range(steps):
             idx = list(range(i * B, (i + 1) * B))
@@ -351,14 +359,14 @@ def test_bf16_hip_training_curve_tracks_fp32_reference():
                 losses.append(tr.meter.reduce()["loss"])
             tr.meter.reset()
         v = tr.validate(batch=16)
-        res[impl] = (sum(losses) / len(losses), v["val_pixel_acc"], v["val_miou"])
+        res[name] = (sum(losses) / len(losses), v["val_pixel_acc"], v["val_miou"])
         tr.close()
     print("final (train loss, val acc, val mIoU):", res)
-    (lh, ah, mh), (lf, af, mf) = res["hip"], res["torch"]
-    assert lf < 1.0, res                      # the fp32 reference actually learned
-    assert abs(lh - lf) <= 0.05 + 0.25 * lf, res
-    assert abs(ah - af) <= 0.05, res
-    assert abs(mh - mf) <= 0.08, res
+    (lh, ah, mh), (lf, af, mf), (l8, a8, m8) = res["hip"], res["fp32"], res["fp32_seed8"]
+    assert lf < 1.0 and l8 < 1.0, res                # the fp32 references actually learned
+    assert abs(lh - lf) <= max(2 * abs(l8 - lf), 0.02), res
+    assert abs(ah - af) <= max(2 * abs(a8 - af), 0.01), res
+    assert abs(mh - mf) <= max(2 * abs(m8 - mf), 0.02), res
 
 
 def test_concurrent_micro_streams_match_sequential_accumulation():
@@ -444,10 +452,13 @@ def test_concurrent_micro_stream_graphs():
 @pytest.mark.parametrize("tile,accum,bpg", [(512, 50, 1), (64, 6, 2)])
 def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg):
     """The reference's regime (512^2, batch 1, 50 accumulated micro-batches, ref.py:685-687,
-    750-766) as ONE batched pass with per-micro-batch BatchNorm groups: the accumulated
-    gradient, the mean micro-batch loss, the pixel count and the in-order running statistics
-    must match the micro-batches run one by one (the batched convs sum in another order and
-    round their bf16 outputs independently, hence the tolerances: measured, see the asserts)."""
+    750-766) as ONE batched pass with per-micro-batch BatchNorm groups.  Against the same
+    micro-batches one by one through the SAME (unfused, grouped) kernels — ``bn_groups = 1``
+    per micro-batch — the gradient, mean micro-batch loss, pixel counts and in-order running
+    statistics agree to fp32 summation order (the batched convs sum in another order; bf16
+    outputs round independently).  Against the fused one-by-one path (deferred BN applied in
+    fp32 on load, prologue fusion) they agree to bf16 rounding of the intermediate
+    activations.  The measured errors are printed (GPU log)."""
     from ddlpc.config import ModelConfig, TrainConfig
     from ddlpc.data import device_random_batch
     from ddlpc.train.trainer import Trainer
@@ -455,41 +466,62 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg):
                       num_samples=1, test_holdout=0, impl="hip", micro_streams=1,
                       accum_steps=accum, bn_window=0)
     tr = Trainer(cfg, device="cuda")
+    eng = tr.model._engine
     mbs = [device_random_batch(bpg, tile, 6, tr.device, seed=300 + j) for j in range(accum)]
     bufs = {k: v for k, v in tr.model.state_dict().items() if "running" in k or "num_batches" in k}
     b0 = {k: v.clone() for k, v in bufs.items()}
-    for x, y in mbs:                                     # one by one
-        tr._micro(x, y, sync=False)
-    torch.cuda.synchronize()
-    g_seq, m_seq = tr.flat.grad_buf.clone(), tr.meter.buf.clone()
-    b_seq = {k: v.clone() for k, v in bufs.items()}
-    tr.optimizer.zero_grad()
-    tr.meter.reset()
-    for k, v in bufs.items():
-        v.copy_(b0[k])
-    tr._window_step(mbs, accum)                          # one batched pass
-    torch.cuda.synchronize()
-    g_win, m_win = tr.flat.grad_buf.clone(), tr.meter.buf.clone()
-    assert tr.model._engine.bn_groups == 0
-    scale = float(g_seq.abs().max())
-    err = float((g_win - g_seq).abs().max())
-    rel = float((g_win - g_seq).norm() / g_seq.norm())
-    print(f"window vs sequential: max err {err:.3e} (scale {scale:.3e}), rel L2 {rel:.3e}")
-    assert rel < 1e-2 and err <= 2e-2 * scale, (err, scale, rel)
-    # per parameter tensor: direction preserved
-    for p in tr.flat.order:
-        a, b = tr.flat.span(p)
-        if float(g_seq[a:b].norm()) > 0:
-            assert _cos(g_win[a:b], g_seq[a:b]) > 0.999, p.shape
-    assert m_win[2] == m_seq[2] and m_win[3] == m_seq[3] == accum, (m_win, m_seq)
-    assert abs(float(m_win[0] - m_seq[0])) <= 1e-4 * float(m_seq[0]), (m_win, m_seq)
-    assert abs(float(m_win[1] - m_seq[1])) <= 1e-4 * float(m_seq[2]), (m_win, m_seq)
-    for k in b_seq:
-        if "num_batches" in k:
-            assert torch.equal(bufs[k], b_seq[k]), k
+
+    def run(mode):
+        tr.optimizer.zero_grad()
+        tr.meter.reset()
+        for k, v in bufs.items():
+            v.copy_(b0[k])
+        if mode == "window":
+            tr._window_step(mbs, accum)                  # one batched pass
         else:
-            assert torch.allclose(bufs[k], b_seq[k], rtol=1e-4, atol=1e-5), (
-                k, float((bufs[k] - b_seq[k]).abs().max()))
+            for x, y in mbs:                             # one by one
+                eng.bn_groups = 1 if mode == "unfused" else 0
+                try:
+                    tr._micro(x, y, sync=False)
+                finally:
+                    eng.bn_groups = 0
+        torch.cuda.synchronize()
+        return (tr.flat.grad_buf.clone(), tr.meter.buf.clone(),
+                {k: v.clone() for k, v in bufs.items()})
+
+    res = {m: run(m) for m in ("fused", "unfused", "window")}
+    assert eng.bn_groups == 0
+
+    def compare(ref, got):
+        g0, g1 = res[ref][0], res[got][0]
+        rel = float((g1 - g0).norm() / g0.norm())
+        cmin, worst = 1.0, None
+        for p in tr.flat.order:
+            a, b = tr.flat.span(p)
+            if float(g0[a:b].norm()) > 1e-3 * float(g0.norm()) / len(tr.flat.order):
+                c = _cos(g1[a:b], g0[a:b])
+                if c < cmin:
+                    cmin, worst = c, tuple(p.shape)
+        print(f"{got} vs {ref}: rel L2 {rel:.3e}, min per-tensor cos {cmin:.6f} {worst}")
+        return rel, cmin
+
+    rel_u, cos_u = compare("unfused", "window")
+    rel_f, cos_f = compare("fused", "window")
+    rel_uf, cos_uf = compare("fused", "unfused")
+    assert rel_u < 3e-3 and cos_u > 0.999, (rel_u, cos_u)
+    # (the fused path's rounding points differ: same order as its gap to the unfused path)
+    assert rel_f < 1.5e-2 and cos_f > 0.99, (rel_f, cos_f, rel_uf, cos_uf)
+    for ref in ("unfused", "fused"):
+        m0, m1 = res[ref][1], res["window"][1]
+        assert m1[2] == m0[2] and m1[3] == m0[3] == accum, (m0, m1)
+        assert abs(float(m1[0] - m0[0])) <= 2e-3 * float(m0[0]), (ref, m0, m1)
+        assert abs(float(m1[1] - m0[1])) <= 2e-3 * float(m0[2]), (ref, m0, m1)
+    for k in b0:
+        bu, bw = res["unfused"][2][k], res["window"][2][k]
+        if "num_batches" in k:
+            assert torch.equal(bw, bu) and torch.equal(bw, res["fused"][2][k]), k
+        else:
+            assert torch.allclose(bw, bu, rtol=1e-4, atol=1e-5), (k, float((bw - bu).abs().max()))
     # and a full optimizer step through train_step picks the window (auto)
     tr.cfg.bn_window = -1
     assert tr._window_size(accum) == (accum if bpg * tile * tile <= tr.SMALL_MICRO_PIXELS else 0)
