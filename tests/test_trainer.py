@@ -191,3 +191,38 @@ def test_resume_rank0_state_broadcast_without_shared_fs(tmp_path):
         o = res[r]
         assert (o["step"], o["epoch_step"], o["opt_step"]) == (3, 3, 3), o
         assert abs(o["p"] - want_p) < 1e-9 and o["m"] > 0, o
+
+
+def test_window_size_policy_and_concat():
+    """bn_window policy (the batched accumulation window with per-micro-batch BatchNorm
+    groups runs on the HIP engine only) and the window batch assembly: engine-layout inputs
+    stay in that layout, labels concatenate in micro-batch order."""
+    from ddlpc.config import ModelConfig, TrainConfig
+    from ddlpc.data.datasets import engine_input
+    from ddlpc.train.trainer import Trainer
+    cfg = TrainConfig(model=ModelConfig(out_classes=2, depth=2, width_divisor=16), tile=16,
+                      num_samples=4, test_holdout=0, accum_steps=4, log_every=0)
+    tr = Trainer(cfg, device="cpu")
+    assert tr._window_size(4) == 0                      # stock-op (CPU) path: no window
+    tr.impl, tr.device = "hip", torch.device("cuda")    # policy only (nothing runs)
+    cfg.bn_window = -1
+    cfg.batch_per_gpu, cfg.tile = 1, 512
+    assert tr._window_size(50) == 50                    # the reference regime: one pass
+    assert tr._window_size(100) == 64                   # WINDOW_PIXELS caps a pass
+    assert tr._window_size(1) == 0
+    cfg.tile = 1024
+    assert tr._window_size(50) == 0                     # large micro-batches: one by one
+    cfg.bn_window = 8
+    assert tr._window_size(50) == 8
+    cfg.bn_window = 0
+    assert tr._window_size(50) == 0
+    tr.impl, tr.device = "torch", torch.device("cpu")
+    mbs = []
+    for j in range(3):
+        xp = torch.full((1, 8, 8, 8), float(j))
+        mbs.append((engine_input(xp, 3), torch.full((1, 8, 8), j, dtype=torch.int64)))
+    x, y = Trainer._cat_window(mbs)
+    assert x.shape == (3, 3, 8, 8) and x._ddlpc_nhwc.shape == (3, 8, 8, 8)
+    assert [int(v) for v in y[:, 0, 0]] == [0, 1, 2]
+    assert [float(v) for v in x._ddlpc_nhwc[:, 0, 0, 0]] == [0.0, 1.0, 2.0]
+    tr.close()
