@@ -522,13 +522,17 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg):
         assert abs(float(m1[0] - m0[0])) <= 2e-3 * float(m0[0]), (ref, m0, m1)
         assert abs(float(m1[1] - m0[1])) <= 2e-3 * float(m0[2]), (ref, m0, m1)
     for k in b0:
-        bu, bw = res["unfused"][2][k], res["window"][2][k]
+        bu, bw, bf = res["unfused"][2][k], res["window"][2][k], res["fused"][2][k]
         if "num_batches" in k:
-            assert torch.equal(bw, bu) and torch.equal(bw, res["fused"][2][k]), k
+            assert torch.equal(bw, bu) and torch.equal(bw, bf), k
         else:
-            # (per-micro-batch means of conv outputs that round to bf16 independently:
-            # measured max |diff| 2.3e-5 on running means of magnitude ~1)
-            assert torch.allclose(bw, bu, rtol=1e-3, atol=1e-4), (k, float((bw - bu).abs().max()))
+            # per-micro-batch means / variances of conv outputs that round to bf16
+            # independently: the window may differ from the one-by-one paths by no more than
+            # those two differ from each other (measured: up to 2.3e-4 on the bottleneck's
+            # means of magnitude ~1, 256 pixels per micro-batch)
+            floor = float((bf - bu).abs().max())
+            err = float((bw - bu).abs().max())
+            assert err <= 3 * floor + 1e-5, (k, err, floor)
     # and a full optimizer step through train_step picks the window (auto)
     tr.cfg.bn_window = -1
     assert tr._window_size(accum) == (accum if bpg * tile * tile <= tr.SMALL_MICRO_PIXELS else 0)
