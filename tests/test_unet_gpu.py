@@ -527,12 +527,10 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg):
             assert torch.equal(bw, bu) and torch.equal(bw, bf), k
         else:
             # per-micro-batch means / variances of conv outputs that round to bf16
-            # independently: the window may differ from the one-by-one paths by no more than
-            # those two differ from each other (measured: up to 2.3e-4 on the bottleneck's
-            # means of magnitude ~1, 256 pixels per micro-batch)
-            floor = float((bf - bu).abs().max())
+            # independently (the batched convs tile differently): measured up to 2.3e-4 on
+            # the bottleneck's running means of magnitude ~1 (256 pixels per micro-batch)
             err = float((bw - bu).abs().max())
-            assert err <= 3 * floor + 1e-5, (k, err, floor)
+            assert err <= 2e-3 * max(1.0, float(bu.abs().max())), (k, err)
     # and a full optimizer step through train_step picks the window (auto)
     tr.cfg.bn_window = -1
     assert tr._window_size(accum) == (accum if bpg * tile * tile <= tr.SMALL_MICRO_PIXELS else 0)
