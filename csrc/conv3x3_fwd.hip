@@ -213,7 +213,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     // the lane's 8-channel group is the same in every piece, so its 16 constants are read
     // once; all piece reads issue before the math, and padding is re-zeroed by a select
     // instead of a branch around each piece
-    if (C::A_ITERS <= 6 && p.rxf) {
+    if (C::A_ITERS <= 6) {
       const int c8 = cbase + sub8;
       const bool cok = c8 < climit;
       const float4* scp = reinterpret_cast<const float4*>(s_scale + (cok ? c8 : 0));
@@ -501,11 +501,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       const int tt = s / MT, mt = s % MT;
       if (s + XD - 1 < NS) xf[(s + XD - 1) % XD] = xload(s + XD - 1);
       if (mt == 0 && tt + 1 < TT) wload(tt + 1, wf[(tt + 1) & 1]);
-      if (mt == 0 && (p.prio & 2)) __builtin_amdgcn_s_setprio(1);
+      if (mt == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[tt & 1][nt], xf[s % XD], acc[mt][nt]);
       if (mt == MT - 1) {
-        if (p.prio & 2) __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(0);
         hook(tt);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -533,12 +533,12 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       if (t + 1 < 3) load_frags(t + 1, xf[(t + 1) & 1], wf[(t + 1) & 1]);
-      if (p.prio & 2) __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[t & 1][nt], xf[t & 1][mt], acc[mt][nt]);
-      if (p.prio & 2) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
       if (FRAG_DB) __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -569,12 +569,12 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 #pragma unroll
     for (int tt = 0; tt < 6; ++tt) {
       if (tt + 1 < 6) load_frags(tt + 1, xf[(tt + 1) & 1], wf[(tt + 1) & 1]);
-      if (p.prio & 2) __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[tt & 1][nt], xf[tt & 1][mt], acc[mt][nt]);
-      if (p.prio & 2) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
       hook(tt);
       if (FRAG_DB) __builtin_amdgcn_sched_barrier(0);
     }
@@ -593,8 +593,6 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   };
   // wave priorities (MI355X_MICROARCH.md, two waves per SIMD: the second-dispatched half of an
   // 8-wave workgroup loses VALU / issue arbitration; one s_setprio 1 for it, no flips)
-  if ((p.prio & 1) && C::NW == 8 && __builtin_amdgcn_readfirstlane(tid) >= C::NTH / 2)
-    __builtin_amdgcn_s_setprio(1);
   if constexpr (NBB <= 3) {
     int ops = 0, snap0 = 0, snap1 = 0;           // NBB = 3: ops issued so far; after B(s), B(s+1)
     if (S > 0) {
@@ -633,14 +631,14 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       if (rem == 0 && s > 0) { epilogue(k - 1); ops += EPI_STORES; }
       const int sn = s + NBB - 1;                     // stage whose weights are issued now
       int snapn = 0;
-      if (sn < S && !((p.diag & 1) && sn >= NBB)) {
+      if (sn < S) {
         int k1, c1, g1;
         stage_of(sn, k1, c1, g1);
         issue_B(k1, c1, g1, sn % NBB);
         ops += C::B_ITERS;
         snapn = ops;
       }
-      if (grp == 0 && more_chunks && !((p.diag & 2) && cseq + 1 >= 2)) {
+      if (grp == 0 && more_chunks) {
         const int k1 = (cseq + 1) / nchunks;
         issue_A(k1, (cseq + 1) % nchunks, (cseq + 1) & 1);
         ops += C::A_ITERS;
@@ -684,7 +682,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     // BNB with ylead 2: an item's y is loaded at its second-to-last super-stage (after that
     // stage's DMAs: the youngest MT * NT loads), so the last super-stage waits for everything
     // but y and y has two super-stages to arrive from HBM instead of one
-    const bool y2 = BNB && KS == 1 && p.ylead >= 2;
+    constexpr bool y2 = false;           // (y two super-stages ahead: 1-3% slower, profiles/r3s)
     for (int j = 0; j < J; ++j) {
       if (y2 && j > 0 && (2 * j + 2) % spi == 0) dma_wait<MT * NT>();
       else dma_wait<0>();
@@ -851,12 +849,6 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
     grid = a.persist_blocks / q * q;
   }
   a.stat_rows = grid;
-  const int diag = knob("DIAG_CONV", 0);
-  a.diag = diag;
-  a.prio = 2;       // s_setprio around every tap's MFMA cluster (profiles/conv_ab_prio_r3e.txt)
-  a.ylead = 1;      // (y two super-stages ahead: 1-3% slower per layer, profiles/r3s)
-  // batched prologue transform where a lane holds <= 6 halo pieces (the 3-D halos' 11 spill)
-  a.rxf = 1;
   // rolling fragment pipeline (pipe_taps): every configuration (the whole-tap register
   // double buffer and no buffering measured slower: profiles/r3s/conv_ab_pipe_r3s1.txt)
   launch_mode<DIMS, WM, WN, MT, NT, HALO, NBB, 2>(a, grid, st);
@@ -872,9 +864,6 @@ void launch_cfg5(ConvFwdArgs& a, hipStream_t st) {
     grid = a.persist_blocks / q * q;
   }
   a.stat_rows = grid;
-  a.diag = knob("DIAG_CONV", 0);
-  a.prio = 2;
-  a.rxf = 1;
   hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 640, 2, 2, false>), dim3(grid),
                      dim3(C::NTH), C::SMEM, st, a);
 }

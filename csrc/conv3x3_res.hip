@@ -138,15 +138,35 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   }
 
   struct Item { int n_img, h0, w0; };
-  auto item_of = [&](int k) {
+  // item geometry without integer division in the stage loop: item k of this workgroup is
+  // blockIdx.x + k * gridDim.x (gridDim.x a multiple of nTilesN: launcher), i.e. M tile
+  // m0 + k * Gs; a walker steps (tw, th, n) by Gs with carries.  One walker per consumer
+  // (halo issue, epilogue, BNB y loads), each visiting the items in order
+  struct Walk { int k, tw, th, n; };
+  const int Gs = (int)gridDim.x / p.nTilesN;
+  const int g_w = Gs % p.tilesW, g_q = Gs / p.tilesW;
+  const int g_h = g_q % p.tilesH, g_n = g_q / p.tilesH;
+  Walk w0;
+  {
+    int m = (int)blockIdx.x / p.nTilesN;
+    w0.k = 0; w0.tw = m % p.tilesW; m /= p.tilesW; w0.th = m % p.tilesH; w0.n = m / p.tilesH;
+  }
+  auto walk_item = [&](Walk& w, int k) __attribute__((always_inline)) {
+    while (w.k < k) {
+      w.tw += g_w;
+      const int c1 = w.tw >= p.tilesW ? 1 : 0;
+      w.tw -= c1 * p.tilesW;
+      w.th += g_h + c1;
+      const int c2 = w.th >= p.tilesH ? 1 : 0;
+      w.th -= c2 * p.tilesH;
+      w.n += g_n + c2;
+      ++w.k;
+    }
     Item it;
-    int m = ((int)blockIdx.x + k * (int)gridDim.x) / p.nTilesN;
-    const int tw_i = m % p.tilesW; m /= p.tilesW;
-    const int th_i = m % p.tilesH; m /= p.tilesH;
-    it.n_img = m;
-    it.h0 = th_i * p.TH; it.w0 = tw_i * p.TW;
+    it.n_img = w.n; it.h0 = w.th * p.TH; it.w0 = w.tw * p.TW;
     return it;
   };
+  Walk wA = w0, wE = w0, wY = w0;
   // ---- per-lane halo DMA geometry (no integer division in the stage loop).  Interior
   // tiles (the common case) need no bounds checks: pixel = tile base + a_rel.
   int a_dw[C::A_ITERS], a_dh[C::A_ITERS], a_sub8[C::A_ITERS], a_rel[C::A_ITERS];
@@ -173,7 +193,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   int a_item = -1, a_nimg = 0, a_base = 0;
   auto issue_A = [&](int k, int chunk, int buf) {
     if (k != a_item) {
-      const Item it = item_of(k);
+      const Item it = walk_item(wA, k);
       a_item = k;
       a_nimg = it.n_img;
       a_base = it.h0 * p.W + it.w0;
@@ -201,43 +221,12 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     const int s0 = a_base * Cs + c0;                   // scalar part of the element offset
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
-      const bool ok = ((a_valid >> i) & 1u) && (full || c0 + a_sub8[i] < Cs) && !(p.diag & 1);
+      const bool ok = ((a_valid >> i) & 1u) && (full || c0 + a_sub8[i] < Cs);
       const unsigned off = ok ? (unsigned)(a_rel[i] * Cs + a_sub8[i] + s0) * 2u : kOOB;
       dma16(r, sA(buf) + (i * NW + wave) * 1024, off);
     }
   };
-  // prologue on the pieces THIS lane DMA'd (a_valid still describes the chunk's item):
-  // packed fp32 FMA, bf16 rounding, ReLU as a packed signed-16-bit max on the bf16 bits
-  auto transform_body = [&](char* __restrict__ Ab, const float* __restrict__ scl,
-                            const float* __restrict__ shf_, int cbase, uint32_t vm, int climit) {
-#pragma unroll
-    for (int i = 0; i < C::A_ITERS; ++i) {
-      const int e = (i * NW + wave) * 64 + lane;
-      const int c8 = cbase + a_sub8[i];
-      if (((vm >> i) & 1u) && c8 < climit) {
-        uint4* q = reinterpret_cast<uint4*>(Ab + e * 16);
-        const uint4 v = *q;
-        const float4* scp = reinterpret_cast<const float4*>(scl + c8);
-        const float4* shp = reinterpret_cast<const float4*>(shf_ + c8);
-        const float4 sa = scp[0], sb = scp[1], ha = shp[0], hb = shp[1];
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        const float scf[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
-        const float shf[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
-        uint32_t o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const f32x2_t x = {lo_bf(w[j]), hi_bf(w[j])};
-          const f32x2_t sc2 = {scf[2 * j], scf[2 * j + 1]};
-          const f32x2_t sh2 = {shf[2 * j], shf[2 * j + 1]};
-          const f32x2_t y2 = __builtin_elementwise_fma(x, sc2, sh2);
-          const uint32_t pk = __builtin_bit_cast(uint32_t, __builtin_convertvector(y2, bf16x2_t));
-          const i16x2_t m = __builtin_elementwise_max(__builtin_bit_cast(i16x2_t, pk), i16x2_t{0, 0});
-          o[j] = __builtin_bit_cast(uint32_t, m);
-        }
-        *q = make_uint4(o[0], o[1], o[2], o[3]);
-      }
-    }
-  };
+  // prologue on the pieces THIS lane DMA'd (a_valid still describes the chunk's item), in a
   // batched form: a lane's 8-channel group is the same in every piece it DMAs (the XOR
   // swizzle flips bit 1 of the piece index by bit 4 of the lane only), so the chunk's 16
   // constants are read once per stage instead of once per piece, all A_ITERS piece reads
@@ -280,9 +269,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   auto transform_A = [&](int chunk, int buf) {
     const int cbase = chunk * BK;
     const bool x2ch = cbase >= p.C1;                   // X2 chunk: prologue only if deferred
-    if ((x2ch ? !has_pro2 : !has_pro) || (p.diag & 4)) return;
-    if (p.rxf) transform_batched(sA(buf), s_scale, s_shift, cbase, get_vmask(buf), x2ch ? p.Cin : p.C1);
-    else transform_body(sA(buf), s_scale, s_shift, cbase, get_vmask(buf), x2ch ? p.Cin : p.C1);
+    if (x2ch ? !has_pro2 : !has_pro) return;
+    transform_batched(sA(buf), s_scale, s_shift, cbase, get_vmask(buf), x2ch ? p.Cin : p.C1);
   };
 
   // ---- per-lane fragment geometry
@@ -335,7 +323,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   }
   struct EpiCtx { __amdgpu_buffer_rsrc_t r1, r2; int h0, w0; };
   auto epi_ctx = [&](int kk) __attribute__((always_inline)) {
-    const Item it = item_of(kk);
+    const Item it = walk_item(wE, kk);
     EpiCtx e;
     const int Co2 = p.Cout - p.Co1;
     e.r1 = make_rsrc(p.Y1 + (long long)it.n_img * img_px * p.Co1, (unsigned)(img_px * p.Co1 * 2));
@@ -347,7 +335,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     const int Co2 = p.Cout - p.Co1;
     const int gw = e.w0 + pcol[mt], gh = e.h0 + prow[mt];
     const bool pv = gw < p.W && gh < p.H;
-    const bool st_on = !(p.diag & 2);
+    constexpr bool st_on = true;
     const int lp = gh * p.W + gw;
     uint2 pkv[NT];
 #pragma unroll
@@ -409,7 +397,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   constexpr int YL = BNB ? MT * NT : 0;
   uint2 ybuf[MT][NT];
   auto issue_Y = [&](int kk) __attribute__((always_inline)) {
-    const Item it = item_of(kk);
+    const Item it = walk_item(wY, kk);
     const auto ry = make_rsrc(p.bnb_y + (long long)it.n_img * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -424,9 +412,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     }
   };
   auto epilogue_blk = [&](int k) {
-    const Item it = item_of(k);
+    const Item it = walk_item(wE, k);
     const int Co2 = p.Cout - p.Co1;
-    const bool st_on = !(p.diag & 2);
+    constexpr bool st_on = true;
     const auto r1 = make_rsrc(p.Y1 + (long long)it.n_img * img_px * p.Co1, (unsigned)(img_px * p.Co1 * 2));
     const auto r2 = SPLIT ? make_rsrc(p.Y2 + (long long)it.n_img * img_px * Co2, (unsigned)(img_px * Co2 * 2)) : r1;
     // pass 1, channel tiles outer: bias, bf16 rounding, statistics (the BNB constants of one
@@ -542,8 +530,6 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   }
   // wave priorities (DDLPC_CONV_PRIO, ConvFwdArgs::prio): bit 0 = s_setprio 1 once for the
   // second-dispatched half of an 8-wave workgroup, bit 1 = around every MFMA cluster
-  if ((p.prio & 1) && NW == 8 && __builtin_amdgcn_readfirstlane(tid) >= C::NTH / 2)
-    __builtin_amdgcn_s_setprio(1);
   int k = 0, c = 0;
   bool epi_prev = false;                              // stage s-1 ran an epilogue
   for (int s = 0; s < S; ++s) {
@@ -606,20 +592,20 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
 #pragma unroll
     for (int j = 0; j < KSTEPS; ++j) {
       if (j + 1 < KSTEPS) load_frags(j + 1, xf[(j + 1) & 1], wf[(j + 1) & 1]);
-      if (p.prio & 2) __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = mfma16x16x32(wf[j & 1][nt], xf[j & 1][mt], acc[mt][nt]);
-      if (p.prio & 2) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
       hook(j);
       __builtin_amdgcn_sched_barrier(0);
     }
     };
     const char* Wst = TAP8 ? sW : sW + c * 9 * BN * ROWB;
     auto no_hook = [](int) {};
-    if (!(p.diag & 8)) compute(sA(buf), Wst, no_hook);
+    compute(sA(buf), Wst, no_hook);
     k = k1; c = c1;
   }
   if (S > 0) {
@@ -682,11 +668,6 @@ int res_smem(const ResVariant& v, int Cin, int C1, bool pro, bool bnb) {   // C1
 
 template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF, int EPIc>
 void launch_res_i(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
-  a.prio = 2;       // s_setprio around every tap's MFMA cluster (profiles/conv_ab_prio_r3e.txt)
-  // diagnostics only (results wrong): bit 0 no halo DMA, 1 no output stores, 2 no prologue
-  // transform, 3 no MFMA stage compute
-  a.diag = knob("DIAG_RES", 0);
-  a.rxf = 1;        // batched prologue transform (profiles/r3s/res_xform_ab_b256_r3s27.txt)
   constexpr int BNc = WN * NT * 16;
   if (a.Co1 < a.Cout) {
     // split output at a 32-channel boundary: 16-byte pair stores

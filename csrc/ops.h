@@ -37,14 +37,6 @@ struct ConvFwdArgs {
   int ksplit;                     // >1: split the channel chunks, fp32 partials to `part`
   float* part;                    // [ksplit][npix][Cout] fp32 (ksplit > 1)
   long long npix;                 // N * D * H * W
-  int rxf;                        // resident kernel prologue transform: 1 = batched, branchless (DDLPC_RES_XFORM)
-  int diag;                       // diagnostics only (DDLPC_DIAG_CONV): bit 0 skip weight DMA after stage 1, bit 1 skip halo DMA after chunk 1
-  int prio;                       // wave priorities (DDLPC_CONV_PRIO): bit 0 = s_setprio 1 for the
-                                  // second half of an 8-wave workgroup (static form), bit 1 =
-                                  // s_setprio 1 / 0 around every tap's MFMA cluster
-  int ylead;                      // BN-backward epilogue, super-stage kernels: y is loaded this
-                                  // many super-stages before the item's epilogue (1 or 2;
-                                  // DDLPC_BNB_YLEAD, 0 = 1)
   // BN-backward epilogue (data gradient dA of a conv whose input went through BN + ReLU):
   // `stats` rows then hold (sum dyh, sum dyh * xhat) with dyh = [y*scale + shift > 0] * dA,
   // xhat = (y - mean) * invstd — the reduction pass of that BN's backward, fused.  2-D,

@@ -22,7 +22,13 @@ OUT=gpurun_out/${1:?usage: gpu.sh OUT STEP...}
 shift
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-python scripts/build_ext.py > "$OUT/build.log" 2>&1 || { tail -30 "$OUT/build.log"; exit 1; }
+# the library built here travels with the snapshot: rebuild only if a source is newer
+LIB=distributed-deep-learning-on-personal-computers_amd/_lib/libddlpc_hip.so
+if [ -f "$LIB" ] && [ -z "$(find csrc -newer "$LIB" -type f | head -1)" ]; then
+  echo "library up to date" > "$OUT/build.log"
+else
+  python scripts/build_ext.py > "$OUT/build.log" 2>&1 || { tail -30 "$OUT/build.log"; exit 1; }
+fi
 
 run_step() {   # name timeout cmd...
   local name=$1 t=$2; shift 2
