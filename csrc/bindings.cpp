@@ -487,6 +487,21 @@ void bn_running_apply(at::Tensor running_mean, at::Tensor running_var, const at:
                           nbp, cur_stream());
 }
 
+// every BatchNorm's deferred running-statistics updates in one launch: entries [L][4] int64
+// (running_mean*, running_var*, nbt* | 0, C | arena column << 32), arena rows 0..K-1
+void bn_running_apply_all(const at::Tensor& entries, const at::Tensor& arena, int64_t K,
+                          int64_t maxC, double momentum) {
+  TORCH_CHECK(entries.scalar_type() == at::kLong && entries.is_contiguous() && entries.dim() == 2 &&
+              entries.size(1) == 4, "entries [L][4] int64");
+  CHECK_F32(arena);
+  TORCH_CHECK(arena.dim() == 2 && arena.stride(1) == 1 && arena.size(0) >= K, "arena [rows >= K][cols]");
+  c10::DeviceGuard guard(arena.device());
+  if (K == 0 || entries.size(0) == 0) return;
+  bn_running_apply_all_launch(entries.data_ptr<int64_t>(), (int)entries.size(0), (int)maxC,
+                              arena.data_ptr<float>(), (int)K, (long long)arena.stride(0),
+                              (float)momentum, cur_stream());
+}
+
 std::vector<at::Tensor> bn_relu_apply(const at::Tensor& y, const at::Tensor& stats4, bool pool,
                                       bool full) {
   CHECK_DEV(y); CHECK_CONTIG(y); CHECK_BF16(y);
@@ -1369,6 +1384,7 @@ TORCH_LIBRARY(ddlpc, m) {
   m.def("bn_group_finalize(Tensor y, int groups, Tensor gamma, Tensor beta, float eps, "
         "Tensor(a!)? arena=None, int aoff=0) -> Tensor");
   m.def("bn_group_apply(Tensor y, Tensor stats4, int groups, bool pool) -> Tensor[]");
+  m.def("bn_running_apply_all(Tensor entries, Tensor(a!) arena, int K, int maxC, float momentum) -> ()");
   m.def("bn_group_backward(Tensor? dA, Tensor? dP, Tensor y, Tensor stats4, Tensor gamma, int groups, "
         "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None) -> Tensor[]");
   m.def("bn_backward(Tensor? dA, Tensor? dP, Tensor y, Tensor stats4, Tensor gamma, Tensor? gscale, "
@@ -1420,6 +1436,7 @@ TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
   m.impl("bn_backward", &ddlpc::bn_backward);
   m.impl("bn_group_finalize", &ddlpc::bn_group_finalize);
   m.impl("bn_group_apply", &ddlpc::bn_group_apply);
+  m.impl("bn_running_apply_all", &ddlpc::bn_running_apply_all);
   m.impl("bn_group_backward", &ddlpc::bn_group_backward);
   m.impl("convt_fwd", &ddlpc::convt_fwd);
   m.impl("convt_dgrad", &ddlpc::convt_dgrad);

@@ -549,16 +549,17 @@ __global__ __launch_bounds__(256) void bn_group_stats_kernel(const bf16_t* __res
   }
 }
 
-// one workgroup per channel; wave w finalizes groups w, w + 4, ... (fp64 sums of the group's
+// one workgroup per channel; wave w finalizes groups w, w + 16, ... (fp64 sums of the group's
 // nb partial rows): stats4 per group, and the group's (mean, unbiased var) into its arena row
 // (the running statistics are then updated in micro-batch order: bn_running_apply)
-__global__ __launch_bounds__(256) void bn_group_finalize_kernel(
+constexpr int kGW = 16;                      // waves per finalize workgroup
+__global__ __launch_bounds__(kGW * 64) void bn_group_finalize_kernel(
     const float* __restrict__ partial, int nb, int groups, int C, double count,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     float* __restrict__ out4, float* __restrict__ arena, long long astride) {
   const int c = blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int g = w; g < groups; g += 4) {
+  for (int g = w; g < groups; g += kGW) {
     const float* rows = partial + (long long)g * nb * 2 * C;
     double a = 0.0, b = 0.0;
     for (int r = lane; r < nb; r += 64) {
@@ -588,14 +589,14 @@ __global__ __launch_bounds__(256) void bn_group_finalize_kernel(
 
 // BatchNorm-backward finalize per group: coefficients [k | m1 | m2] of every group, and
 // dgamma / dbeta = the fp64 sums over groups in group order (deterministic)
-__global__ __launch_bounds__(256) void bn_group_grad_finalize_kernel(
+__global__ __launch_bounds__(kGW * 64) void bn_group_grad_finalize_kernel(
     const float* __restrict__ partial, int nb, int groups, int C, double count,
     const float* __restrict__ gamma, const float* __restrict__ stats4, float* dgamma, float* dbeta,
     float* __restrict__ coefs, int accumulate) {
   __shared__ double t1s[1024], t2s[1024];
   const int c = blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int g = w; g < groups; g += 4) {
+  for (int g = w; g < groups; g += kGW) {
     const float* rows = partial + (long long)g * nb * 2 * C;
     double a = 0.0, b = 0.0;
     for (int r = lane; r < nb; r += 64) {
@@ -641,7 +642,7 @@ void bn_group_stats_finalize_launch(const bf16_t* y, int groups, long long gpix,
                                     int nb, hipStream_t st) {
   hipLaunchKernelGGL(bn_group_stats_kernel, dim3(nb, groups), dim3(256), 0, st, y, gpix, C,
                      partial_scratch);
-  hipLaunchKernelGGL(bn_group_finalize_kernel, dim3(C), dim3(256), 0, st, partial_scratch, nb,
+  hipLaunchKernelGGL(bn_group_finalize_kernel, dim3(C), dim3(kGW * 64), 0, st, partial_scratch, nb,
                      groups, C, (double)gpix, gamma, beta, eps, out4, arena, astride);
 }
 
@@ -658,7 +659,7 @@ void bn_group_backward_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* 
   bn_bwd2_launch<0>(nb, dims, pool, dA, dP, y, s + 2 * C, s + 3 * C, s, s + C, nullptr, nullptr,
                     partial_scratch, nullptr, N, D, H, W, C, st, groups, sstride);
   const double count = (double)N * D * H * W;
-  hipLaunchKernelGGL(bn_group_grad_finalize_kernel, dim3(C), dim3(256), 0, st, partial_scratch, nb,
+  hipLaunchKernelGGL(bn_group_grad_finalize_kernel, dim3(C), dim3(kGW * 64), 0, st, partial_scratch, nb,
                      groups, C, count, gamma, stats4, dgamma, dbeta, coefs, accumulate ? 1 : 0);
   const long long items = (long long)N * (pool ? (dims == 3 ? D / 2 : 1) * (H / 2) * (W / 2)
                                                 : (long long)D * H * W);

@@ -282,6 +282,8 @@ void tile_gather_launch(const uint8_t* src, const uint8_t* lab, const int64_t* i
 
 void bn_running_apply_launch(float* rm, float* rv, const float* slots, int K, int C, long long stride,
                              float momentum, int64_t* nbt, hipStream_t st);
+void bn_running_apply_all_launch(const int64_t* entries, int L, int maxC, const float* arena, int K,
+                                 long long stride, float momentum, hipStream_t st);
 
 // ---------------------------------------------------------------- tuning knobs (bindings.cpp)
 // knob("CONV_CFG5", 1): an in-process override (torch.ops.ddlpc.set_knob, for interleaved

@@ -377,6 +377,37 @@ void scatter_sums_dscale_launch(const double* sums, long long N, float* dst, con
                      accumulate ? 1 : 0);
 }
 
+// every BatchNorm of the network in ONE launch (blockIdx.y = layer): entries [L][4] =
+// (running_mean*, running_var*, num_batches_tracked* or 0, C | column offset << 32) into an
+// arena of K rows (row stride `stride` floats); same arithmetic and order as
+// bn_running_apply_kernel
+__global__ void bn_running_apply_all_kernel(const int64_t* __restrict__ entries, const float* __restrict__ arena,
+                                            int K, long long stride, float momentum) {
+  const int64_t* e = entries + 4 * blockIdx.y;
+  float* running_mean = reinterpret_cast<float*>(e[0]);
+  float* running_var = reinterpret_cast<float*>(e[1]);
+  int64_t* nbt = reinterpret_cast<int64_t*>(e[2]);
+  const int C = (int)(e[3] & 0xffffffff);
+  const long long off = (long long)((uint64_t)e[3] >> 32);
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt != nullptr) nbt[0] += K;
+  if (c >= C) return;
+  const float* slots = arena + off;
+  float rm = running_mean[c], rv = running_var[c];
+  for (int k = 0; k < K; ++k) {
+    rm = bn_momentum_update(rm, slots[k * stride + c], momentum);
+    rv = bn_momentum_update(rv, slots[k * stride + C + c], momentum);
+  }
+  running_mean[c] = rm;
+  running_var[c] = rv;
+}
+
+void bn_running_apply_all_launch(const int64_t* entries, int L, int maxC, const float* arena, int K,
+                                 long long stride, float momentum, hipStream_t st) {
+  hipLaunchKernelGGL(bn_running_apply_all_kernel, dim3((maxC + 255) / 256, L), dim3(256), 0, st, entries,
+                     arena, K, stride, momentum);
+}
+
 void bn_running_apply_launch(float* rm, float* rv, const float* slots, int K, int C, long long stride,
                              float momentum, int64_t* nbt, hipStream_t st) {
   hipLaunchKernelGGL(bn_running_apply_kernel, dim3((C + 255) / 256), dim3(256), 0, st, rm, rv, slots, K,

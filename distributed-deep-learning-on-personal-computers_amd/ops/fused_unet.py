@@ -741,7 +741,21 @@ class UNetEngine:
 
     def bn_defer_apply(self, n: int):
         """Apply the n deferred running-statistics updates of every BatchNorm in micro-batch
-        order (one launch per BatchNorm): bit-identical to n sequential forwards."""
+        order (one launch for the whole network when the BatchNorms share a momentum, else
+        one per BatchNorm): bit-identical to n sequential forwards."""
+        moms = {(b.bn.momentum if b.bn.momentum is not None else 0.1) for b in self.bns}
+        if len(moms) == 1 and all(b.bn.track_running_stats for b in self.bns):
+            key = (self._bn_arena.data_ptr(), tuple(b.bn.running_mean.data_ptr() for b in self.bns))
+            if getattr(self, "_bn_all_key", None) != key:
+                rows = [[b.bn.running_mean.data_ptr(), b.bn.running_var.data_ptr(),
+                         b.bn.num_batches_tracked.data_ptr(),
+                         b.bn.num_features | (off << 32)] for b, off in zip(self.bns, self._bn_offs)]
+                self._bn_all = torch.tensor(rows, dtype=torch.int64).to(self._bn_arena.device)
+                self._bn_all_key = key
+                self._bn_all_maxc = max(b.bn.num_features for b in self.bns)
+            _ops().bn_running_apply_all(self._bn_all, self._bn_arena, n, self._bn_all_maxc,
+                                        float(moms.pop()))
+            return
         for b, off in zip(self.bns, self._bn_offs):
             bn = b.bn
             if not bn.track_running_stats:

@@ -147,12 +147,16 @@ def _dp_fresh_trainer_steps(rank, world, reduce, window):
         red = tr.reducer
         mbs = [device_random_batch(1, 64, 6, tr.device, seed=7 + rank + 100 * j + 1000 * rnd)
                for j in range(accum)]
-        # the local accumulated gradient, sequentially, without touching the reducer
+        # the local accumulated gradient, sequentially, without touching the reducer (window
+        # mode: through the same unfused kernels, bn_groups = 1 per micro-batch — the fused
+        # path differs from them by bf16 rounding points alone, ~3% at 64^2)
         ready = eng.grad_ready
         eng.grad_ready = None
         for x, y in mbs:
+            eng.bn_groups = 1 if window else 0
             loss, _ = tr.model.loss_and_correct(x, y)
             loss.backward()
+        eng.bn_groups = 0
         eng.grad_ready = ready
         torch.cuda.synchronize()
         g_local = tr.flat.grad_buf.clone()
