@@ -342,6 +342,10 @@ def main():
                        "train_loss_mean": round(loss["loss"], 4),
                        "recompute": int(args.recompute),
                        "micro_streams": getattr(tr, "micro_streams", 1),
+                       # accumulation micro-batches per batched pass with per-micro-batch
+                       # BatchNorm groups (0: off; the micro_streams schedule then applies)
+                       "bn_window": (tr._window_size(args.accum) if hasattr(tr, "_window_size")
+                                     else 0),
                        "micro_streams_host_ms_per_step": (round(ms_host * 1e3 / args.steps, 2)
                                                           if getattr(tr, "micro_streams", 1) > 1
                                                           else None),

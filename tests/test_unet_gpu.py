@@ -124,7 +124,7 @@ def test_trainer_hip_graph_accumulation_matches_eager(accum):
     for graph in (False, True):
         cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=1,
                           num_samples=1, test_holdout=0, impl="hip", hip_graph=graph,
-                          accum_steps=accum, micro_streams=1)
+                          accum_steps=accum, micro_streams=1, bn_window=0)
         tr = Trainer(cfg, device="cuda")
         tr.model._engine.set_side_stream(False)
         batches = [device_random_batch(1, 64, 6, tr.device, seed=s) for s in range(5)]
