@@ -117,23 +117,53 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 
   const auto rW = make_rsrc(p.Wt, (unsigned)((long long)p.Cout * p.taps * p.CinW * 2));
 
-  struct Item { int mtile, n_img, d0, h0, w0, co0, ks; };
-  auto item_of = [&](int k) {
+  struct Item { int n_img, d0, h0, w0, co0, ks; };
+  // work item k of this workgroup is blockIdx.x + k * gridDim.x with gridDim.x a multiple of
+  // KS * nTilesN (launcher), so its channel split ks and n tile are the block's own and its
+  // M tile is m0 + k * Gs: the item geometry comes from carry-walkers (one add-and-carry step
+  // per item) instead of five runtime integer divisions per call; one walker per consumer
+  // (halo issue, epilogue, BNB y loads), each visiting the items in order
+  const int ks_blk = (int)blockIdx.x % KS;
+  const int co0_item = (int)blockIdx.x / KS % p.nTilesN * BN;
+  struct Walk { int k, tw, th, td, n; };
+  const int Gs = (int)gridDim.x / (KS * p.nTilesN);
+  int g_w, g_h, g_d, g_n;
+  {
+    int q = Gs;
+    g_w = q % p.tilesW; q /= p.tilesW;
+    g_h = q % p.tilesH; q /= p.tilesH;
+    g_d = q % p.tilesD; g_n = q / p.tilesD;
+  }
+  Walk w0;
+  {
+    int m = (int)blockIdx.x / (KS * p.nTilesN);
+    w0.k = 0;
+    w0.tw = m % p.tilesW; m /= p.tilesW;
+    w0.th = m % p.tilesH; m /= p.tilesH;
+    w0.td = m % p.tilesD; w0.n = m / p.tilesD;
+  }
+  auto walk_item = [&](Walk& w, int k) __attribute__((always_inline)) {
+    while (w.k < k) {
+      w.tw += g_w;
+      const int c1 = w.tw >= p.tilesW ? 1 : 0;
+      w.tw -= c1 * p.tilesW;
+      w.th += g_h + c1;
+      const int c2 = w.th >= p.tilesH ? 1 : 0;
+      w.th -= c2 * p.tilesH;
+      w.td += g_d + c2;
+      const int c3 = w.td >= p.tilesD ? 1 : 0;
+      w.td -= c3 * p.tilesD;
+      w.n += g_n + c3;
+      ++w.k;
+    }
     Item it;
-    int w = (int)blockIdx.x + k * (int)gridDim.x;
-    it.ks = w % KS;
-    w /= KS;
-    const int ntile = w % p.nTilesN;
-    int m = w / p.nTilesN;
-    it.mtile = m;
-    const int tw_i = m % p.tilesW; m /= p.tilesW;
-    const int th_i = m % p.tilesH; m /= p.tilesH;
-    const int td_i = m % p.tilesD; m /= p.tilesD;
-    it.n_img = m;
-    it.d0 = td_i * p.TD; it.h0 = th_i * p.TH; it.w0 = tw_i * p.TW;
-    it.co0 = ntile * BN;
+    it.ks = ks_blk;
+    it.n_img = w.n;
+    it.d0 = w.td * p.TD; it.h0 = w.th * p.TH; it.w0 = w.tw * p.TW;
+    it.co0 = co0_item;
     return it;
   };
+  Walk wA = w0, wE = w0, wY = w0;
   // ---- per-lane DMA geometry.  Element e = (i*NW + wave)*64 + lane of a halo / weight
   // buffer holds row e >> 2 = (i*NW + wave)*16 + (lane >> 2), so the swizzled 8-channel
   // sub-chunk ((e & 3) ^ swz(row)) * 8 is the same for every i (swz depends on bit 2 of the
@@ -162,7 +192,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   int a_item = -1;                 // item whose pixels a_pix currently holds
   int a_nimg = 0;
   auto set_item_pixels = [&](int k) {
-    const Item it = item_of(k);
+    const Item it = walk_item(wA, k);
     a_item = k;
     a_nimg = it.n_img;
 #pragma unroll
@@ -175,7 +205,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       a_pix[i] = ok ? (gd * p.H + gh) * p.W + gw : -1;
     }
   };
-  auto chunk0_of = [&](int k) { return ((int)blockIdx.x + k * (int)gridDim.x) % KS * nchunks; };
+  auto chunk0_of = [&](int) { return ks_blk * nchunks; };     // (the block's own split)
   auto issue_A = [&](int k, int chunk, int buf) {
     if (k != a_item) set_item_pixels(k);
     const int cbase = (chunk0_of(k) + chunk) * BK;
@@ -334,7 +364,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   // stage's DMA) and consumed by its epilogue after the next stage's full wait
   uint2 ybuf[MT][NT];
   auto issue_Y = [&](int kk) __attribute__((always_inline)) {
-    const Item it = item_of(kk);
+    const Item it = walk_item(wY, kk);
     const auto ry = make_rsrc(p.bnb_y + it.n_img * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -352,7 +382,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     }
   };
   auto epilogue = [&](int k) __attribute__((always_inline)) {
-    const Item it = item_of(k);
+    const Item it = walk_item(wE, k);
     const int Co2 = p.Cout - p.Co1;
     const auto r1 = KS > 1 ? make_rsrc(p.part + ((long long)it.ks * p.npix + (long long)it.n_img * img_px) * p.Cout,
                                        (unsigned)(img_px * p.Cout * 4))
@@ -726,7 +756,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     dma_wait<0>();
     lds_sync();
     float* red = LSTAT ? s_red : reinterpret_cast<float*>(base);   // halo buffers are free now
-    const int co0 = my_items > 0 ? item_of(0).co0 : 0;
+    const int co0 = co0_item;
 #pragma unroll
     for (int nt = 0; nt < (LSTAT ? 0 : NT); ++nt)
 #pragma unroll
