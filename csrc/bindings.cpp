@@ -388,9 +388,6 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   a.ciw = 1;
   if (v3 && !img && bco == 64 && a.Cin >= 64 && g.H * g.W >= 64 * 64)
     a.ciw = 2;
-  // batched prologue transform (v3): on the 32-output-channel tiles (enc1.b / dec1.b -7%);
-  // the 64 / 128-channel tiles measured 0-2% slower with it (profiles/r3s/wgrad_xform_ab_b256_r3s36.txt)
-  a.xf = bco == 32 ? 1 : 0;
   if (img) { a.TD = 1; a.TW = 16; a.TH = conv3_wgrad_img_pt(bco) / 16; }
   else if (v3 && (bco == 128 || a.ciw == 2)) { a.TD = 1; a.TW = 16; a.TH = 6; }
   else if (v3) { a.TD = 1; a.TW = 16; a.TH = bco == 32 ? 16 : 8; }

@@ -23,6 +23,34 @@
 
 namespace ddlpc {
 
+// pixel tiles t_begin, t_begin + 1, ... of a (tilesW, tilesH, slices) grid visited in order:
+// the integer divisions once, then a carry step per tile (per-tile divisions cost ~100 scalar
+// / vector instructions per tile against 36-54 MFMAs); d = the slice's depth index (3-D)
+struct TileWalk {
+  int t, w, h, n, d;
+  DDLPC_DEVICE void init(int t0, int tilesW, int tilesH, int D) {
+    t = t0;
+    w = t0 % tilesW;
+    const int q = t0 / tilesW;
+    h = q % tilesH;
+    n = q / tilesH;
+    d = n % D;
+  }
+  DDLPC_DEVICE void to(int tile, int tilesW, int tilesH, int D) {
+    while (t < tile) {
+      ++t;
+      if (++w == tilesW) {
+        w = 0;
+        if (++h == tilesH) {
+          h = 0;
+          ++n;
+          if (++d == D) d = 0;
+        }
+      }
+    }
+  }
+};
+
 namespace {
 
 constexpr int CI = 32;          // ci per workgroup
@@ -376,14 +404,14 @@ __global__ __launch_bounds__(256, PT <= 96 ? 3 : 2) void conv3_wgrad2_kernel(Con
   // (prologue constants stay in LDS here: 16 more live VGPRs would cost the 96-pixel-tile
   // variant its third workgroup per CU — measured 55% slower on dec3.a / dec2.a)
 
+  TileWalk tw;                                     // the issue stream's tile geometry
+  tw.init(t_begin, p.tilesW, p.tilesH, p.D);
   auto issue = [&](int tile, int buf) {
-    int t = tile;
-    const int tw_i = t % p.tilesW; t /= p.tilesW;
-    const int th_i = t % p.tilesH; t /= p.tilesH;
-    const int n = t;                                 // (n, d) slice
-    const int dx = n % p.D + dshift;
+    tw.to(tile, p.tilesW, p.tilesH, p.D);
+    const int n = tw.n;                              // (n, d) slice
+    const int dx = tw.d + dshift;
     const bool dok = dx >= 0 && dx < p.D;
-    const int h0 = th_i * TH, w0 = tw_i * 16;
+    const int h0 = tw.h * TH, w0 = tw.w * 16;
     const auto ry = make_rsrc(p.dY + n * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
     const int ybase = (h0 * p.W + w0) * p.Cout;
 #pragma unroll
@@ -636,14 +664,14 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
       pro8_load(p.pscale, p.pshift, p.pscale2, p.pshift2, p.C1, c8l, second[cw] ? p.Cin : p.C1, psc[cw], psh[cw]);
   }
 
+  TileWalk tw;                                     // the issue stream's tile geometry
+  tw.init(t_begin, p.tilesW, p.tilesH, p.D);
   auto issue = [&](int tile, int buf) __attribute__((always_inline)) {
-    int t = tile;
-    const int tw_i = t % p.tilesW; t /= p.tilesW;
-    const int th_i = t % p.tilesH; t /= p.tilesH;
-    const int n = t;
-    const int dx = n % p.D + dshift;
+    tw.to(tile, p.tilesW, p.tilesH, p.D);
+    const int n = tw.n;
+    const int dx = tw.d + dshift;
     const bool dok = dx >= 0 && dx < p.D;
-    const int h0 = th_i * TH, w0 = tw_i * 16;
+    const int h0 = tw.h * TH, w0 = tw.w * 16;
     const auto ry = make_rsrc(p.dY + n * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
     const int ybase = (h0 * p.W + w0) * p.Cout;
 #pragma unroll
@@ -685,7 +713,9 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
       dok = dx >= 0 && dx < p.D;
       h0 = th_i * TH; w0 = tw_i * 16;
     }
-    if (NB == 2 && Cfg::X_ITERS <= 6 && p.xf) {
+    // (batched form on the 32-output-channel tiles: enc1.b / dec1.b -7%; the 64 / 128-channel
+    // tiles measured 0-2% slower with it, profiles/r3s/wgrad_xform_ab_b256_r3s36.txt)
+    if (NB == 2 && Cfg::X_ITERS <= 6 && BCO == 32) {
       // batched form: all piece reads issue before the math (packed fp32 FMA, bf16 rounding,
       // ReLU as a packed 16-bit max), padding re-zeroed by a select instead of a branch
       constexpr int NI = Cfg::X_ITERS <= 6 ? Cfg::X_ITERS : 1;
@@ -930,12 +960,12 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad_img_kernel(ConvWgradArgs p
     y_rel[i] = co < p.Cout ? (y_ph[i] * p.W + y_pw[i]) * p.Cout + co : -1;
     y_ok[i] = false;
   }
+  TileWalk tw;                                     // the issue stream's tile geometry
+  tw.init(t_begin, p.tilesW, p.tilesH, 1);
   auto issue = [&](int tile, int buf) {
-    int t = tile;
-    const int tw_i = t % p.tilesW; t /= p.tilesW;
-    const int th_i = t % p.tilesH; t /= p.tilesH;
-    const int n = t;
-    const int h0 = th_i * Cfg::TH, w0 = tw_i * 16;
+    tw.to(tile, p.tilesW, p.tilesH, 1);
+    const int n = tw.n;
+    const int h0 = tw.h * Cfg::TH, w0 = tw.w * 16;
     const auto ry = make_rsrc(p.dY + n * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
     const int ybase = (h0 * p.W + w0) * p.Cout;
 #pragma unroll

@@ -79,7 +79,6 @@ struct ConvWgradArgs {
   const float* dys4;
   const float* dycoef;
   int ciw;                        // v3: 32-channel input chunks per workgroup (1 or 2)
-  int xf;                         // v3 prologue transform: 1 = batched, branchless (DDLPC_WGRAD_XFORM)
 };
 void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st);
 // LDS-DMA variant (1 x TH x 16 pixel tiles of conv3_wgrad2_pt(bco) pixels; 3-D: planes = 3,
