@@ -257,6 +257,15 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
     if (a.nTilesM * a.nTilesN >= num_cus() && w5 <= 1.05) cfg = 5;
     else plan(cfg);
   }
+  // 3-D: the 8-wave configurations wherever they fill the chip with little padding (the
+  // 4-wave 3-D tiles need so much halo LDS that one workgroup = one wave per SIMD fits a CU)
+  if (g.dims == 3 && cfg <= 2) {
+    const int c8 = cfg == 0 ? 6 : cfg == 1 ? 7 : 8;
+    plan(c8);
+    const double w8 = (double)a.nTilesM * conv3_fwd_cfg_bm(c8) / ((double)g.N * g.D * g.H * g.W);
+    if (a.nTilesM * a.nTilesN >= num_cus() && w8 <= 1.15 && g.W >= 16) cfg = c8;
+    else plan(cfg);
+  }
   if (cfg == 2 && a.nTilesM * a.nTilesN < 2 * num_cus()) { cfg = 3; plan(cfg); }
   // small images: a tile larger than the image computes padding (the 8x8 bottleneck layer
   // under a 256-pixel tile is 75% padding: 48.6 -> 32.5 us with 64-pixel tiles, batch 128)
@@ -278,7 +287,7 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   at::Tensor y2;
   if (a.Co1 < a.Cout) y2 = at::empty(shape_with_c(g, a.Cout - a.Co1), opts);
   at::Tensor stats;
-  a.persist_blocks = (cfg >= 4 ? 1 : 2) * num_cus();   // cfg 4/5: one 8-wave workgroup per CU
+  a.persist_blocks = (cfg >= 4 ? 1 : 2) * num_cus();   // cfg >= 4: one 8-wave workgroup per CU
   // small layers: split the input-channel chunks across workgroups so the grid fills the
   // chip; partial sums go through an fp32 buffer and a deterministic finalize
   const int nchunks_total = (a.Cin + 31) / 32;

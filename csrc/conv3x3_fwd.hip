@@ -898,7 +898,7 @@ void launch_cfg5(ConvFwdArgs& a, hipStream_t st) {
                      dim3(C::NTH), C::SMEM, st, a);
 }
 
-int cfg_wm(int cfg) { return cfg <= 1 || cfg >= 4 ? 4 : cfg == 2 ? 2 : 1; }
+int cfg_wm(int cfg) { return cfg == 6 ? 8 : cfg == 8 ? 2 : cfg <= 1 || cfg >= 4 ? 4 : cfg == 2 ? 2 : 1; }
 
 }  // namespace
 
@@ -912,13 +912,20 @@ int cfg_wm(int cfg) { return cfg <= 1 || cfg >= 4 ? 4 : cfg == 2 ? 2 : 1; }
 //   5: BN 128, BM 512 (4x2 waves = 512 threads, 8x4 tiles: 128 px x 64 ch per wave; 2-D
 //      only) 32x16: half cfg 4's weight-stream DMA per MFMA and a quarter fewer LDS fragment
 //      reads per MFMA (each wave's weight fragments serve 8 pixel tiles)
+//   3-D with 8 waves (two per SIMD; the 4-wave 3-D configs fit one workgroup per CU in LDS,
+//   i.e. ONE wave per SIMD and no latency hiding):
+//   6: BN 32,  BM 384 (8x1 waves, 3x2 tiles) 6x4x16, halo 8x6x18
+//   7: BN 64,  BM 256 (4x2 waves, 4x2 tiles) 4x4x16
+//   8: BN 128, BM 128 (2x4 waves, 4x2 tiles) 2x4x16
 // (halo capacity = DMA instructions per wave x 64 pixels)
 int conv3_fwd_cfg_wm(int cfg) { return cfg_wm(cfg); }
-int conv3_fwd_cfg_bn(int cfg) { return cfg == 0 ? 32 : cfg == 1 ? 64 : 128; }
-int conv3_fwd_cfg_bm(int cfg) { return cfg == 5 ? 512 : cfg <= 1 || cfg == 4 ? 256 : cfg == 2 ? 128 : 64; }
+int conv3_fwd_cfg_bn(int cfg) { return cfg == 0 || cfg == 6 ? 32 : cfg == 1 || cfg == 7 ? 64 : 128; }
+int conv3_fwd_cfg_bm(int cfg) {
+  return cfg == 5 ? 512 : cfg == 6 ? 384 : cfg <= 1 || cfg == 4 || cfg == 7 ? 256 : cfg == 2 || cfg == 8 ? 128 : 64;
+}
 int conv3_fwd_cfg_halo(int dims, int cfg) {
   if (dims == 2) return cfg == 5 ? 640 : cfg <= 1 || cfg == 4 ? 384 : cfg == 2 ? 192 : 128;
-  return cfg <= 1 ? 704 : cfg == 2 ? 448 : 384;
+  return cfg == 6 ? 896 : cfg <= 1 || cfg == 7 ? 704 : cfg == 2 || cfg == 8 ? 448 : 384;
 }
 
 void conv3_splitk_finalize_launch(ConvFwdArgs& a, int grid, hipStream_t st) {
@@ -946,6 +953,9 @@ void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st) {
       case 0: launch_cfg<3, 4, 1, 4, 2, 704>(a, st); break;
       case 1: launch_cfg<3, 4, 1, 4, 4, 704>(a, st); break;
       case 2: launch_cfg<3, 2, 2, 4, 4, 448>(a, st); break;
+      case 6: launch_cfg<3, 8, 1, 3, 2, 896>(a, st); break;
+      case 7: launch_cfg<3, 4, 2, 4, 2, 704>(a, st); break;
+      case 8: launch_cfg<3, 2, 4, 4, 2, 448>(a, st); break;
       default: launch_cfg<3, 1, 4, 4, 2, 384>(a, st); break;
     }
   }
