@@ -23,29 +23,35 @@
 
 namespace ddlpc {
 
-// pixel tiles t_begin, t_begin + 1, ... of a (tilesW, tilesH, slices) grid visited in order:
-// the integer divisions once, then a carry step per tile (per-tile divisions cost ~100 scalar
-// / vector instructions per tile against 36-54 MFMAs); d = the slice's depth index (3-D)
+// pixel tiles t_begin, t_begin + 1, ... of a (slices, tilesW, tilesH, images) grid visited in
+// order: the integer divisions once, then a carry step per tile (per-tile divisions cost ~100
+// scalar / vector instructions per tile against 36-54 MFMAs).  3-D: the depth slice d is the
+// FASTEST index, so the three depth-tap-plane workgroups of a split (which run side by side
+// on one XCD) re-read the input plane a neighbour fetched one tile earlier — from L2, not
+// HBM.  n = image * D + d is the slice (2-D: D = 1, the plain w, h, image order).
 struct TileWalk {
-  int t, w, h, n, d;
+  int t, w, h, n, d, nb;
   DDLPC_DEVICE void init(int t0, int tilesW, int tilesH, int D) {
     t = t0;
-    w = t0 % tilesW;
-    const int q = t0 / tilesW;
+    d = t0 % D;
+    int q = t0 / D;
+    w = q % tilesW;
+    q /= tilesW;
     h = q % tilesH;
-    n = q / tilesH;
-    d = n % D;
+    nb = q / tilesH * D;
+    n = nb + d;
   }
   DDLPC_DEVICE void to(int tile, int tilesW, int tilesH, int D) {
     while (t < tile) {
       ++t;
-      if (++w == tilesW) {
-        w = 0;
-        if (++h == tilesH) {
-          h = 0;
-          ++n;
-          if (++d == D) d = 0;
+      ++n;
+      if (++d == D) {
+        d = 0;
+        if (++w == tilesW) {
+          w = 0;
+          if (++h == tilesH) { h = 0; nb += D; }
         }
+        n = nb;
       }
     }
   }
@@ -706,10 +712,10 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
     int h0 = 0, w0 = 0;
     bool dok = true;
     if constexpr (NB != 2) {
-      int t = tile;
+      int t = tile;                                // TileWalk's order: d, w, h, image
+      const int dx = t % p.D + dshift; t /= p.D;
       const int tw_i = t % p.tilesW; t /= p.tilesW;
-      const int th_i = t % p.tilesH; t /= p.tilesH;
-      const int dx = t % p.D + dshift;
+      const int th_i = t % p.tilesH;
       dok = dx >= 0 && dx < p.D;
       h0 = th_i * TH; w0 = tw_i * 16;
     }
