@@ -383,7 +383,8 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   }
   // the image layer: <= 4 real channels (cin_real, from the caller) of an 8-channel padded
   // input, (tap, channel)-packed kernel
-  const bool img = cin_real > 0 && cin_real <= 4 && a.C1 == 8 && !dual && g.dims == 2 && g.W >= 16 &&
+  // (3-D: per depth tap plane, as the v2 / v3 kernels)
+  const bool img = cin_real > 0 && cin_real <= 4 && a.C1 == 8 && !dual && g.W >= 16 &&
                    a.pscale == nullptr && a.pscale2 == nullptr;
   // v3 with 128 output channels per workgroup (every wave a 32-channel quarter, no k-split;
   // 96-pixel tiles): each staged input halo feeds twice the MFMAs of the 64-channel tiles

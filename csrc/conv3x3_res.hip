@@ -19,7 +19,9 @@
 //     drain under the next tile's compute instead of stalling the next vmcnt wait;
 //   * TAP8 (the image layer, Cin <= 8): K packs (tap, channel) as k = 8*tap + c, 12 taps
 //     (3 zero-weight) = 3 MFMA k-steps instead of 9 on a 4x zero-padded chunk; the halo row
-//     is one 16-B pixel.
+//     is one 16-B pixel.  TAP8 = 3: the 3-D image layer (ref.py:588 with Conv3d) as depth
+//     slices — an item is a TH x TW tile of one slice, its halo the 3 neighbouring planes,
+//     28 taps (1 zero-weight) = 7 k-steps instead of 27 on a 4x zero-padded chunk.
 // Output / statistics contracts are those of conv3_fwd_kernel (ops.h ConvFwdArgs).
 #include "common.h"
 #include "conv_lds.h"
@@ -31,7 +33,7 @@ namespace {
 
 using namespace convlds;
 
-template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF>
+template <int WM, int WN, int MT, int NT, int HALO, int TAP8, int NBUF>
 struct RCfg {
   static constexpr int NW = WM * WN;
   static constexpr int NTH = NW * 64;
@@ -49,8 +51,9 @@ template <int N>
 DDLPC_DEVICE void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
 DDLPC_HOST_DEVICE int res_ss_bytes(int C1, bool pro) { return pro ? ((8 * C1 + 15) / 16) * 16 : 0; }
-DDLPC_HOST_DEVICE int res_w_bytes(int Cin, int BN, bool tap8) {
-  return tap8 ? 3 * BN * ROWB : ((Cin + BK - 1) / BK) * 9 * BN * ROWB;
+DDLPC_HOST_DEVICE constexpr int tap8_ksteps(int tap8) { return tap8 == 3 ? 7 : 3; }
+DDLPC_HOST_DEVICE int res_w_bytes(int Cin, int BN, int tap8) {
+  return tap8 ? tap8_ksteps(tap8) * BN * ROWB : ((Cin + BK - 1) / BK) * 9 * BN * ROWB;
 }
 
 // SPLIT: 0 = one output; 1 = two outputs (concat data gradient), 8-byte stores; 2 = two
@@ -60,7 +63,7 @@ DDLPC_HOST_DEVICE int res_w_bytes(int Cin, int BN, bool tap8) {
 // 16-pixel rows of MFMA tiles with item-independent pixel geometry and packed fp32 bias /
 // statistics.  BNB keeps form 0.  (Rejected: form 1 interleaved between the next stage's
 // tap steps from a second accumulator set, 10-20% slower: profiles/r3s/res_ilv_ab_b256_r3s24.txt)
-template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF, int SPLIT, bool BNB, int EPI = 1>
+template <int WM, int WN, int MT, int NT, int HALO, int TAP8, int NBUF, int SPLIT, bool BNB, int EPI = 1>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_kernel(ConvFwdArgs p) {
   using C = RCfg<WM, WN, MT, NT, HALO, TAP8, NBUF>;
   static_assert(NBUF == 2 || NBUF == 3, "halo ring depth");
@@ -84,8 +87,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   const int wm = wave / WN;
   const int wn = wave % WN;
   const int HW2 = p.TW + 2, HH2 = p.TH + 2;
-  const int halo = HH2 * HW2;
-  const long long img_px = (long long)p.H * p.W;
+  constexpr int NPL = TAP8 == 3 ? 3 : 1;              // halo planes (3-D image layer: 3)
+  const int PL = HH2 * HW2;
+  const int halo = NPL * PL;
+  const long long img_px = (long long)p.H * p.W;      // one slice
+  const long long vol_px = NPL == 3 ? (long long)p.D * img_px : img_px;   // one image
   const int n_items = p.nTilesM * p.nTilesN;
   const int my_items = n_items > (int)blockIdx.x ? (n_items - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   const int nch = TAP8 ? 1 : (p.Cin + BK - 1) / BK;
@@ -116,7 +122,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     asm volatile("" ::"v"(bias_r[nt][0]), "v"(bias_r[nt][1]), "v"(bias_r[nt][2]), "v"(bias_r[nt][3]));
   // ---- resident weights: rows (chunk, tap, col) [TAP8: (k-step, col)], 64 B each
   {
-    const auto rW = make_rsrc(p.Wt, (unsigned)((long long)p.Cout * 9 * p.CinW * 2));
+    const auto rW = make_rsrc(p.Wt, (unsigned)((long long)p.Cout * p.taps * p.CinW * 2));
     const int pieces = res_w_bytes(p.Cin, BN, TAP8) / 16;
     for (int b = wave * 64; b < pieces; b += NW * 64) {
       const int e = b + lane;
@@ -127,7 +133,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
       unsigned off = kOOB;
       if (TAP8) {
         const int tap = (row / BN) * 4 + sub;
-        if (tap < 9 && co < p.Cout) off = (unsigned)((co * 9 + tap) * p.CinW) * 2u;
+        if (tap < p.taps && co < p.Cout) off = (unsigned)((co * p.taps + tap) * p.CinW) * 2u;
       } else {
         const int t = (row / BN) % 9, c = row / (9 * BN);
         const int ci = c * BK + sub * 8;
@@ -137,19 +143,23 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     }
   }
 
-  struct Item { int n_img, h0, w0; };
+  // n_img: the slice (image * D + d; 2-D: the image) — outputs are slice-addressed
+  struct Item { int n_img, img, d, h0, w0; };
   // item geometry without integer division in the stage loop: item k of this workgroup is
   // blockIdx.x + k * gridDim.x (gridDim.x a multiple of nTilesN: launcher), i.e. M tile
-  // m0 + k * Gs; a walker steps (tw, th, n) by Gs with carries.  One walker per consumer
-  // (halo issue, epilogue, BNB y loads), each visiting the items in order
-  struct Walk { int k, tw, th, n; };
+  // m0 + k * Gs; a walker steps (tw, th, slice) by Gs with carries, the slice as (image, d).
+  // One walker per consumer (halo issue, epilogue, BNB y loads), each visiting the items in
+  // order
+  struct Walk { int k, tw, th, img, d; };
   const int Gs = (int)gridDim.x / p.nTilesN;
   const int g_w = Gs % p.tilesW, g_q = Gs / p.tilesW;
   const int g_h = g_q % p.tilesH, g_n = g_q / p.tilesH;
+  const int g_d = NPL == 3 ? g_n % p.D : 0, g_i = NPL == 3 ? g_n / p.D : g_n;
   Walk w0;
   {
     int m = (int)blockIdx.x / p.nTilesN;
-    w0.k = 0; w0.tw = m % p.tilesW; m /= p.tilesW; w0.th = m % p.tilesH; w0.n = m / p.tilesH;
+    w0.k = 0; w0.tw = m % p.tilesW; m /= p.tilesW; w0.th = m % p.tilesH; m /= p.tilesH;
+    w0.d = NPL == 3 ? m % p.D : 0; w0.img = NPL == 3 ? m / p.D : m;
   }
   auto walk_item = [&](Walk& w, int k) __attribute__((always_inline)) {
     while (w.k < k) {
@@ -159,26 +169,36 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
       w.th += g_h + c1;
       const int c2 = w.th >= p.tilesH ? 1 : 0;
       w.th -= c2 * p.tilesH;
-      w.n += g_n + c2;
+      if constexpr (NPL == 3) {
+        w.d += g_d + c2;
+        const int c3 = w.d >= p.D ? 1 : 0;
+        w.d -= c3 * p.D;
+        w.img += g_i + c3;
+      } else {
+        w.img += g_n + c2;                              // 2-D: D = 1, d = 0
+      }
       ++w.k;
     }
     Item it;
-    it.n_img = w.n; it.h0 = w.th * p.TH; it.w0 = w.tw * p.TW;
+    it.img = w.img; it.d = NPL == 3 ? w.d : 0; it.n_img = NPL == 3 ? w.img * p.D + w.d : w.img;
+    it.h0 = w.th * p.TH; it.w0 = w.tw * p.TW;
     return it;
   };
   Walk wA = w0, wE = w0, wY = w0;
   // ---- per-lane halo DMA geometry (no integer division in the stage loop).  Interior
   // tiles (the common case) need no bounds checks: pixel = tile base + a_rel.
-  int a_dw[C::A_ITERS], a_dh[C::A_ITERS], a_sub8[C::A_ITERS], a_rel[C::A_ITERS];
+  int a_dw[C::A_ITERS], a_dh[C::A_ITERS], a_dd[C::A_ITERS], a_sub8[C::A_ITERS], a_rel[C::A_ITERS];
   uint32_t a_inhalo = 0;
 #pragma unroll
   for (int i = 0; i < C::A_ITERS; ++i) {
     const int e = (i * NW + wave) * 64 + lane;
     const int px = TAP8 ? e : e >> 2;
     a_sub8[i] = TAP8 ? 0 : ((e & 3) ^ swz(px)) << 3;
-    a_dw[i] = px % HW2 - 1;
-    a_dh[i] = px / HW2 - 1;
-    a_rel[i] = a_dh[i] * p.W + a_dw[i];
+    const int pr = NPL == 1 ? px : px % PL;
+    a_dd[i] = NPL == 1 ? 0 : px / PL - 1;
+    a_dw[i] = pr % HW2 - 1;
+    a_dh[i] = pr / HW2 - 1;
+    a_rel[i] = ((NPL == 3 ? a_dd[i] * p.H : 0) + a_dh[i]) * p.W + a_dw[i];
     if (px < halo && e < C::PIECES) a_inhalo |= 1u << i;
   }
   uint32_t a_valid = 0;            // pieces of the item last issued that are inside the image
@@ -195,17 +215,19 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     if (k != a_item) {
       const Item it = walk_item(wA, k);
       a_item = k;
-      a_nimg = it.n_img;
-      a_base = it.h0 * p.W + it.w0;
-      const bool interior = it.w0 >= 1 && it.h0 >= 1 && it.w0 + p.TW < p.W && it.h0 + p.TH < p.H;
+      a_nimg = it.img;
+      a_base = ((NPL == 3 ? it.d * p.H : 0) + it.h0) * p.W + it.w0;   // pixel within the image volume
+      const bool interior = it.w0 >= 1 && it.h0 >= 1 && it.w0 + p.TW < p.W && it.h0 + p.TH < p.H &&
+                            (NPL == 1 || (it.d >= 1 && it.d + 1 < p.D));
       if (interior) {
         a_valid = a_inhalo;
       } else {
         a_valid = 0;
 #pragma unroll
         for (int i = 0; i < C::A_ITERS; ++i) {
-          const int gw = it.w0 + a_dw[i], gh = it.h0 + a_dh[i];
-          if (gw >= 0 && gw < p.W && gh >= 0 && gh < p.H) a_valid |= 1u << i;
+          const int gw = it.w0 + a_dw[i], gh = it.h0 + a_dh[i], gd = it.d + a_dd[i];
+          if (gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && (NPL == 1 || (gd >= 0 && gd < p.D)))
+            a_valid |= 1u << i;
         }
         a_valid &= a_inhalo;
       }
@@ -217,7 +239,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     const bool full = c0 + BK <= Cs;                   // wave-uniform: no channel check
     const bf16_t* src = second ? p.X2 : p.X1;
     set_vmask(buf, a_valid);
-    const auto r = make_rsrc(src + a_nimg * img_px * Cs, (unsigned)(img_px * Cs * 2));
+    const auto r = make_rsrc(src + a_nimg * vol_px * Cs, (unsigned)(vol_px * Cs * 2));
     const int s0 = a_base * Cs + c0;                   // scalar part of the element offset
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
@@ -279,13 +301,16 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
-    hp0[mt] = (pix / p.TW) * HW2 + pix % p.TW;
+    hp0[mt] = (NPL == 3 ? PL : 0) + (pix / p.TW) * HW2 + pix % p.TW;   // (3-D: the centre plane)
   }
-  int toff8[3];                                        // TAP8: this lane group's tap offsets
+  constexpr int KS8 = tap8_ksteps(TAP8);
+  int toff8[KS8];                                      // TAP8: this lane group's tap offsets
 #pragma unroll
-  for (int ks = 0; ks < 3; ++ks) {
-    const int tap = min(ks * 4 + g, 8);
-    toff8[ks] = (tap / 3) * HW2 + tap % 3;
+  for (int ks = 0; ks < KS8; ++ks) {
+    // taps past the last are zero-weight: any in-halo address will do
+    const int tap = min(ks * 4 + g, NPL * 9 - 1);
+    const int t9 = tap % 9;
+    toff8[ks] = (NPL == 3 ? (tap / 9 - 1) * PL : 0) + (t9 / 3) * HW2 + t9 % 3;
   }
   const int wrow0 = wn * (NT * 16) + (lane & 15);
 
@@ -574,7 +599,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     // does not make them wait for the next stage's in-flight LDS-DMA: vmcnt is managed by
     // hand above)
     auto compute = [&](const char* __restrict__ A, const char* __restrict__ Wc, auto hook) {
-    constexpr int KSTEPS = TAP8 ? 3 : 9;
+    constexpr int KSTEPS = TAP8 ? KS8 : 9;
     auto load_frags = [&](int j, uint4 (&xf)[MT], uint4 (&wf)[NT]) {
       if (TAP8) {
 #pragma unroll
@@ -643,20 +668,23 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   }
 }
 
-struct ResVariant { int wm, wn, mt, nt, halo; bool tap8; int tw, th, nbuf; };
+struct ResVariant { int wm, wn, mt, nt, halo, tap8, tw, th, nbuf; };
 // BN 32 = 4x2 16x16 MFMA tiles per wave column, BN 64 = two wave columns; NBUF = halo ring
-constexpr ResVariant kRes[8] = {
-    {4, 1, 4, 2, 324, false, 16, 16, 2},   // 0: BM 256 BN 32, 4 waves, 2-deep (2 WG / CU)
-    {8, 1, 4, 2, 612, false, 32, 16, 3},   // 1: BM 512 BN 32, 8 waves, 3-deep
-    {4, 2, 4, 2, 324, false, 16, 16, 3},   // 2: BM 256 BN 64, 8 waves, 3-deep
-    {4, 1, 4, 2, 324, true, 16, 16, 2},    // 3: image layer (TAP8), 4 waves, 2-deep
-    {8, 1, 4, 2, 612, true, 32, 16, 3},    // 4: image layer (TAP8), 8 waves, 3-deep
-    {8, 1, 4, 2, 612, false, 32, 16, 2},   // 5: BM 512 BN 32, 8 waves, 2-deep (large Cin)
-    {4, 2, 4, 2, 324, false, 16, 16, 2},   // 6: BM 256 BN 64, 8 waves, 2-deep (large Cin)
+constexpr ResVariant kRes[10] = {
+    {4, 1, 4, 2, 324, 0, 16, 16, 2},       // 0: BM 256 BN 32, 4 waves, 2-deep (2 WG / CU)
+    {8, 1, 4, 2, 612, 0, 32, 16, 3},       // 1: BM 512 BN 32, 8 waves, 3-deep
+    {4, 2, 4, 2, 324, 0, 16, 16, 3},       // 2: BM 256 BN 64, 8 waves, 3-deep
+    {4, 1, 4, 2, 324, 2, 16, 16, 2},       // 3: image layer (TAP8), 4 waves, 2-deep
+    {8, 1, 4, 2, 612, 2, 32, 16, 3},       // 4: image layer (TAP8), 8 waves, 3-deep
+    {8, 1, 4, 2, 612, 0, 32, 16, 2},       // 5: BM 512 BN 32, 8 waves, 2-deep (large Cin)
+    {4, 2, 4, 2, 324, 0, 16, 16, 2},       // 6: BM 256 BN 64, 8 waves, 2-deep (large Cin)
     // 7: BM 256 BN 96, 8 waves x (2 x 6 tiles), 3-deep — the 96-channel data gradient of the
     //    first decoder conv (dY: 32 ch -> d[up | skip]: 64 + 32 ch).  One workgroup covers all
     //    96 output channels, so the dY halo is read once instead of once per 32-channel tile.
-    {8, 1, 2, 6, 324, false, 16, 16, 3}};
+    {8, 1, 2, 6, 324, 0, 16, 16, 3},
+    // 8 / 9: the 3-D image layer (TAP8 = 3): 3-plane halos of 16x16 / 32x16 slice tiles
+    {4, 1, 4, 2, 972, 3, 16, 16, 2},
+    {8, 1, 4, 2, 1836, 3, 32, 16, 3}};
 
 int res_smem(const ResVariant& v, int Cin, int C1, bool pro, bool bnb) {   // C1: channels with constants
   const int bn = v.wn * v.nt * 16;
@@ -666,7 +694,7 @@ int res_smem(const ResVariant& v, int Cin, int C1, bool pro, bool bnb) {   // C1
   return (bnb ? 16 * bn : res_ss_bytes(C1, pro)) + res_w_bytes(Cin, bn, v.tap8) + v.nbuf * a_bytes;
 }
 
-template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF, int EPIc>
+template <int WM, int WN, int MT, int NT, int HALO, int TAP8, int NBUF, int EPIc>
 void launch_res_i(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
   constexpr int BNc = WN * NT * 16;
   if (a.Co1 < a.Cout) {
@@ -696,7 +724,7 @@ void launch_res_i(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
 // non-BNB epilogue form (kernel EPI above): form 0 on the 8-wave 32-channel tiles (form 1
 // measured 1-1.5% slower there), form 1 elsewhere (image layer -19%, 64/96-channel tiles
 // -6..-11%; same-process A/B at batch 256, profiles/r3s/res_epi_ab_b256_r3s25.txt)
-template <int WM, int WN, int MT, int NT, int HALO, bool TAP8, int NBUF>
+template <int WM, int WN, int MT, int NT, int HALO, int TAP8, int NBUF>
 void launch_res(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
   constexpr bool form0 = WM == 8 && WN == 1 && NT == 2 && !TAP8;
   if (form0 || a.bnb_y != nullptr) launch_res_i<WM, WN, MT, NT, HALO, TAP8, NBUF, 0>(a, grid, smem, st);
@@ -709,9 +737,13 @@ void launch_res(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
 // belongs to the streaming kernel.  LDS budget: 160 KB per CU; two workgroups per CU when
 // a workgroup needs <= 80 KB.
 int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
-  if (a.dims != 2 || a.W < 16 || a.H < 16) return -1;
+  if (a.W < 16 || a.H < 16) return -1;
   const bool pro = a.pscale != nullptr;
   const bool tap8 = a.Cin <= 8 && a.C2 == 0 && a.CinW == 8 && !pro;
+  // 3-D: the image layer only (depth slices, a 3-plane halo addressed within one image
+  // volume through one buffer descriptor: 32-bit offsets)
+  const bool d3 = a.dims == 3;
+  if (d3 && (!tap8 || (long long)a.D * a.H * a.W * a.CinW * 2 >= (1LL << 31))) return -1;
   const int bn = a.Cout == 96 ? 96 : (a.Cout <= 32 || a.Cout % 64 != 0) ? 32 : 64;
   // halo ring depth: 2 for the 64-channel tiles (variant 6: BN-backward data gradients 9-11%
   // faster, the others 1-3.5%), 3 for the 32-channel tiles (the 2-deep 4-wave variant is
@@ -721,7 +753,8 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
   int nc = 0;
   if (tap8) {
     if (bn != 32 || a.bnb_y != nullptr) return -1;
-    if (depth == 2) { cand[nc++] = 3; } else { cand[nc++] = 4; cand[nc++] = 3; }
+    if (d3) { cand[nc++] = 9; cand[nc++] = 8; }
+    else if (depth == 2) { cand[nc++] = 3; } else { cand[nc++] = 4; cand[nc++] = 3; }
   } else if (bn == 96) {
     if (a.bnb_y != nullptr) return -1;                 // no BN-backward epilogue at BN 96
     cand[nc++] = 7;
@@ -740,10 +773,10 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
     const int bpc = nw == 4 ? (sm <= 80 * 1024 ? 2 : 0) : (sm <= 160 * 1024 ? 1 : 0);
     if (bpc == 0) continue;
     a.TD = 1; a.TW = v.tw; a.TH = v.th;
-    a.tilesD = 1;
+    a.tilesD = a.D;                                     // 3-D: one tile per slice
     a.tilesH = (a.H + a.TH - 1) / a.TH;
     a.tilesW = (a.W + a.TW - 1) / a.TW;
-    a.nTilesM = a.N * a.tilesH * a.tilesW;
+    a.nTilesM = a.N * a.D * a.tilesH * a.tilesW;
     a.nTilesN = (a.Cout + bn - 1) / bn;
     const int items = a.nTilesM * a.nTilesN;
     const int cap = bpc * num_cus;
@@ -760,14 +793,16 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
 
 void conv3_res_launch(ConvFwdArgs& a, int variant, int grid, int smem, hipStream_t st) {
   switch (variant) {
-    case 0: launch_res<4, 1, 4, 2, 324, false, 2>(a, grid, smem, st); break;
-    case 1: launch_res<8, 1, 4, 2, 612, false, 3>(a, grid, smem, st); break;
-    case 2: launch_res<4, 2, 4, 2, 324, false, 3>(a, grid, smem, st); break;
-    case 3: launch_res<4, 1, 4, 2, 324, true, 2>(a, grid, smem, st); break;
-    case 4: launch_res<8, 1, 4, 2, 612, true, 3>(a, grid, smem, st); break;
-    case 5: launch_res<8, 1, 4, 2, 612, false, 2>(a, grid, smem, st); break;
-    case 7: launch_res<8, 1, 2, 6, 324, false, 3>(a, grid, smem, st); break;
-    default: launch_res<4, 2, 4, 2, 324, false, 2>(a, grid, smem, st); break;
+    case 0: launch_res<4, 1, 4, 2, 324, 0, 2>(a, grid, smem, st); break;
+    case 1: launch_res<8, 1, 4, 2, 612, 0, 3>(a, grid, smem, st); break;
+    case 2: launch_res<4, 2, 4, 2, 324, 0, 3>(a, grid, smem, st); break;
+    case 3: launch_res<4, 1, 4, 2, 324, 2, 2>(a, grid, smem, st); break;
+    case 4: launch_res<8, 1, 4, 2, 612, 2, 3>(a, grid, smem, st); break;
+    case 5: launch_res<8, 1, 4, 2, 612, 0, 2>(a, grid, smem, st); break;
+    case 7: launch_res<8, 1, 2, 6, 324, 0, 3>(a, grid, smem, st); break;
+    case 8: launch_res<4, 1, 4, 2, 972, 3, 2>(a, grid, smem, st); break;
+    case 9: launch_res<8, 1, 4, 2, 1836, 3, 3>(a, grid, smem, st); break;
+    default: launch_res<4, 2, 4, 2, 324, 0, 2>(a, grid, smem, st); break;
   }
 }
 

@@ -899,6 +899,8 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
 // dY arrives and is optionally BN-backward-transformed exactly as in v2 (same layout, same
 // swizzle); the waves split the k-steps and their partials are summed in LDS in a fixed
 // order; the slab keeps the [co][tap][ci] contract with ci >= 4 written as zeros.
+// 3-D (Conv3d(3, 32)): one workgroup per depth tap plane as in v2 / v3 — the 2-D kernel over
+// depth slices, the input slice shifted by the plane, writing taps 9 plane + t.
 template <int BCO, int PT>
 struct WgImgCfg {
   using Y = Wg2Cfg<BCO, PT>;                       // dY staging exactly as v2
@@ -930,8 +932,10 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad_img_kernel(ConvWgradArgs p
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   int b = xcd_remap(blockIdx.x, gridDim.x);
   const int cot = b % p.coTiles; b /= p.coTiles;
+  const int plane = b % p.planes; b /= p.planes;
   const int split = b;
   const int co0 = cot * BCO;
+  const int dshift = p.planes == 3 ? plane - 1 : 0;
 
   const bool has_dyp = p.dyy != nullptr;
   if (has_dyp)
@@ -967,10 +971,12 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad_img_kernel(ConvWgradArgs p
     y_ok[i] = false;
   }
   TileWalk tw;                                     // the issue stream's tile geometry
-  tw.init(t_begin, p.tilesW, p.tilesH, 1);
+  tw.init(t_begin, p.tilesW, p.tilesH, p.D);
   auto issue = [&](int tile, int buf) {
-    tw.to(tile, p.tilesW, p.tilesH, 1);
-    const int n = tw.n;
+    tw.to(tile, p.tilesW, p.tilesH, p.D);
+    const int n = tw.n;                              // (image, d) slice
+    const int dx = tw.d + dshift;
+    const bool dok = dx >= 0 && dx < p.D;            // the plane's input slice exists
     const int h0 = tw.h * Cfg::TH, w0 = tw.w * 16;
     const auto ry = make_rsrc(p.dY + n * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
     const int ybase = (h0 * p.W + w0) * p.Cout;
@@ -986,13 +992,13 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad_img_kernel(ConvWgradArgs p
         y_ok[i] = ok;
       }
     }
-    const auto rx = make_rsrc(p.X1 + n * img_px * p.C1, (unsigned)(img_px * p.C1 * 2));
+    const auto rx = make_rsrc(p.X1 + (n + (dok ? dshift : 0)) * img_px * p.C1, (unsigned)(img_px * p.C1 * 2));
 #pragma unroll
     for (int i = 0; i < Cfg::X_ITERS; ++i) {
       if ((i * 4 + wave) >= Cfg::X_INSTR) break;
       const int px = (i * 4 + wave) * 64 + lane;          // halo pixel (one piece each)
       const int gw = w0 + px % HW2 - 1, gh = h0 + px / HW2 - 1;
-      const bool ok = px < Cfg::HALO && gw >= 0 && gw < p.W && gh >= 0 && gh < p.H;
+      const bool ok = dok && px < Cfg::HALO && gw >= 0 && gw < p.W && gh >= 0 && gh < p.H;
       dma16(rx, sX(buf) + (i * 4 + wave) * 1024, ok ? (unsigned)(gh * p.W + gw) * (unsigned)(p.C1 * 2) : kOOB);
     }
   };
@@ -1115,13 +1121,13 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad_img_kernel(ConvWgradArgs p
 #pragma unroll
           for (int w2 = 1; w2 < 4; ++w2) v += red[((((w2 - 1) * NCO + j) * 3 + n) * 4 + i) * 64 + lane];
           const int co = co0 + j * 16 + 4 * g + i;
-          if (tap < 9 && co < p.Cout && ci < p.Cin) out[((long long)co * p.taps + tap) * p.Cin + ci] = v;
+          if (tap < 9 && co < p.Cout && ci < p.Cin) out[((long long)co * p.taps + plane * 9 + tap) * p.Cin + ci] = v;
         }
       }
   }
   // padding input channels (4 .. Cin-1: zero in the image, so their gradient is exactly 0)
   for (int e = tid; e < BCO * 9 * (p.Cin - 4); e += 256) {
-    const int ci = 4 + e % (p.Cin - 4), tap = (e / (p.Cin - 4)) % 9, co = co0 + e / ((p.Cin - 4) * 9);
+    const int ci = 4 + e % (p.Cin - 4), tap = plane * 9 + (e / (p.Cin - 4)) % 9, co = co0 + e / ((p.Cin - 4) * 9);
     if (co < p.Cout) out[((long long)co * p.taps + tap) * p.Cin + ci] = 0.f;
   }
 }
@@ -1176,7 +1182,7 @@ void conv3_wgrad3_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
 }
 
 void conv3_wgrad_img_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
-  const int grid = a.coTiles * a.splits;
+  const int grid = a.coTiles * a.planes * a.splits;
   if (bco == 32)
     hipLaunchKernelGGL((conv3_wgrad_img_kernel<32, 256>), dim3(grid), dim3(256), (WgImgCfg<32, 256>::SMEM), st, a);
   else

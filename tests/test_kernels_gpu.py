@@ -593,6 +593,25 @@ def test_conv3_wgrad_image_layer(ops, N, H, W, Cout, pro):
     assert rel_err(w_img[:, :3], g) < 5e-3
 
 
+@pytest.mark.parametrize("N,D,H,W,Cout", [(2, 6, 32, 32, 32), (1, 5, 20, 18, 32), (1, 4, 24, 40, 64)])
+def test_conv3d_wgrad_image_layer(ops, N, D, H, W, Cout):
+    """3-D first-layer weight gradient: the packed image kernel per depth tap plane (depth
+    borders, partial tiles) vs fp32 autograd and vs the generic path; padding channels zero."""
+    torch.manual_seed(37)
+    x = torch.randn(N, 3, D, H, W, device=DEV).bfloat16()
+    xin = ops.to_nhwc_bf16(x, 8)
+    dy = torch.randn(N, D, H, W, Cout, device=DEV).bfloat16()
+    w_img = ops.conv3_wgrad(dy, xin, None, None, None, cin_real=3)
+    w_gen = ops.conv3_wgrad(dy, xin, None, None, None)
+    assert w_img.shape == (Cout, 8, 3, 3, 3)
+    assert torch.count_nonzero(w_img[:, 3:]) == 0
+    assert rel_err(w_img, w_gen) < 1e-5, rel_err(w_img, w_gen)
+    w = torch.zeros(Cout, 3, 3, 3, 3, device=DEV, requires_grad=True)
+    out = F.conv3d(x.float(), w, padding=1)
+    (g,) = torch.autograd.grad(out, w, dy.permute(0, 4, 1, 2, 3).float())
+    assert rel_err(w_img[:, :3], g) < 5e-3
+
+
 @pytest.mark.parametrize("N,H,W,bn", [(2, 16, 16, False), (3, 12, 20, True), (1, 40, 24, True),
                                       (4, 8, 8, True)])
 def test_convt_bwd_fused(ops, N, H, W, bn):
@@ -675,6 +694,27 @@ def test_conv3d_fwd_wgrad(ops):
     xr = torch.zeros(N, C, D, H, W, device=DEV, requires_grad=True)
     (gx,) = torch.autograd.grad(F.conv3d(xr, w.bfloat16().float(), padding=1), xr, dy.float())
     assert rel_err(nchw(dx), gx) < 1e-2
+
+
+@pytest.mark.parametrize("N,D,H,W", [(2, 32, 64, 64), (12, 5, 48, 40)])
+def test_conv3d_image_layer_resident(ops, N, D, H, W):
+    """3-D image layer (8-channel padded input -> 32): the resident kernel's (tap, channel)-
+    packed path over depth slices with 3-plane halos (conv3x3_res.hip TAP8 = 3), incl.
+    partial tiles and depth borders; output, bias and BN statistics vs fp32 torch."""
+    torch.manual_seed(19)
+    Cin, Cout = 8, 32
+    x = torch.randn(N, Cin, D, H, W, device=DEV).bfloat16()
+    x[:, 3:] = 0                                        # the engine's zero channel padding
+    w = torch.randn(Cout, Cin, 3, 3, 3, device=DEV) / math.sqrt(27 * 3)
+    b = torch.randn(Cout, device=DEV) * 0.1
+    pk = pack_conv(ops, w)
+    y, _, st = ops.conv3_fwd(nhwc(x), None, pk.fwd, b, None, None, Cout, 0, True)
+    ref = F.conv3d(x.float(), w.bfloat16().float(), b, padding=1)
+    assert rel_err(nchw(y), ref) < 1e-2
+    s = st.sum(0)
+    yf = nchw(y).float()
+    assert torch.allclose(s[0], yf.sum((0, 2, 3, 4)), rtol=1e-3, atol=1e-1)
+    assert torch.allclose(s[1], (yf * yf).sum((0, 2, 3, 4)), rtol=1e-3, atol=1.0)
 
 
 @pytest.mark.parametrize("N,D,H,W,C1,C2,Cout,pro", [
