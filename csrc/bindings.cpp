@@ -260,7 +260,7 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   // 3-D: the 8-wave configurations wherever they fill the chip with little padding (the
   // 4-wave 3-D tiles need so much halo LDS that one workgroup = one wave per SIMD fits a CU)
   if (g.dims == 3 && cfg <= 2) {
-    const int c8 = cfg == 0 ? 6 : cfg == 1 ? 7 : 8;
+    const int c8 = cfg == 0 ? 6 : cfg == 1 ? 7 : a.Cout == 96 ? 9 : 8;
     plan(c8);
     const double w8 = (double)a.nTilesM * conv3_fwd_cfg_bm(c8) / ((double)g.N * g.D * g.H * g.W);
     if (a.nTilesM * a.nTilesN >= num_cus() && w8 <= 1.15 && g.W >= 16) cfg = c8;

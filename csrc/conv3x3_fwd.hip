@@ -898,7 +898,7 @@ void launch_cfg5(ConvFwdArgs& a, hipStream_t st) {
                      dim3(C::NTH), C::SMEM, st, a);
 }
 
-int cfg_wm(int cfg) { return cfg == 6 ? 8 : cfg == 8 ? 2 : cfg <= 1 || cfg >= 4 ? 4 : cfg == 2 ? 2 : 1; }
+int cfg_wm(int cfg) { return cfg == 6 || cfg == 9 ? 8 : cfg == 8 ? 2 : cfg <= 1 || cfg >= 4 ? 4 : cfg == 2 ? 2 : 1; }
 
 }  // namespace
 
@@ -917,15 +917,18 @@ int cfg_wm(int cfg) { return cfg == 6 ? 8 : cfg == 8 ? 2 : cfg <= 1 || cfg >= 4 
 //   6: BN 32,  BM 384 (8x1 waves, 3x2 tiles) 6x4x16, halo 8x6x18
 //   7: BN 64,  BM 256 (4x2 waves, 4x2 tiles) 4x4x16
 //   8: BN 128, BM 128 (2x4 waves, 4x2 tiles) 2x4x16
+//   9: BN 96,  BM 256 (8x1 waves, 2x6 tiles) 4x4x16 — the 96-channel data gradient of the
+//      first decoder conv (d[up | skip] = 64 + 32 channels), which the 128-channel tiles
+//      would pad by a third
 // (halo capacity = DMA instructions per wave x 64 pixels)
 int conv3_fwd_cfg_wm(int cfg) { return cfg_wm(cfg); }
-int conv3_fwd_cfg_bn(int cfg) { return cfg == 0 || cfg == 6 ? 32 : cfg == 1 || cfg == 7 ? 64 : 128; }
+int conv3_fwd_cfg_bn(int cfg) { return cfg == 0 || cfg == 6 ? 32 : cfg == 1 || cfg == 7 ? 64 : cfg == 9 ? 96 : 128; }
 int conv3_fwd_cfg_bm(int cfg) {
-  return cfg == 5 ? 512 : cfg == 6 ? 384 : cfg <= 1 || cfg == 4 || cfg == 7 ? 256 : cfg == 2 || cfg == 8 ? 128 : 64;
+  return cfg == 5 ? 512 : cfg == 6 ? 384 : cfg <= 1 || cfg == 4 || cfg == 7 || cfg == 9 ? 256 : cfg == 2 || cfg == 8 ? 128 : 64;
 }
 int conv3_fwd_cfg_halo(int dims, int cfg) {
   if (dims == 2) return cfg == 5 ? 640 : cfg <= 1 || cfg == 4 ? 384 : cfg == 2 ? 192 : 128;
-  return cfg == 6 ? 896 : cfg <= 1 || cfg == 7 ? 704 : cfg == 2 || cfg == 8 ? 448 : 384;
+  return cfg == 6 ? 896 : cfg <= 1 || cfg == 7 || cfg == 9 ? 704 : cfg == 2 || cfg == 8 ? 448 : 384;
 }
 
 void conv3_splitk_finalize_launch(ConvFwdArgs& a, int grid, hipStream_t st) {
@@ -956,6 +959,7 @@ void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st) {
       case 6: launch_cfg<3, 8, 1, 3, 2, 896>(a, st); break;
       case 7: launch_cfg<3, 4, 2, 4, 2, 704>(a, st); break;
       case 8: launch_cfg<3, 2, 4, 4, 2, 448>(a, st); break;
+      case 9: launch_cfg<3, 8, 1, 2, 6, 704>(a, st); break;
       default: launch_cfg<3, 1, 4, 4, 2, 384>(a, st); break;
     }
   }

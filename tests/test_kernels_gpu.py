@@ -717,32 +717,35 @@ def test_conv3d_image_layer_resident(ops, N, D, H, W):
     assert torch.allclose(s[1], (yf * yf).sum((0, 2, 3, 4)), rtol=1e-3, atol=1.0)
 
 
-@pytest.mark.parametrize("N,D,H,W,C1,C2,Cout,pro", [
-    (2, 24, 64, 32, 32, 32, 32, True),      # 8-wave 3-D config 6: 6x4x16 tiles, BN 32
-    (2, 32, 32, 32, 64, 0, 64, False),      # config 7: 4x4x16, BN 64
-    (1, 32, 32, 32, 128, 0, 128, True),     # config 8: 2x4x16, BN 128
-    (1, 16, 32, 32, 128, 128, 256, False)])  # config 8, two channel tiles, concat
-def test_conv3d_fwd_8wave(ops, N, D, H, W, C1, C2, Cout, pro):
+@pytest.mark.parametrize("N,D,H,W,C1,C2,Cout,pro,co1", [
+    (2, 24, 64, 32, 32, 32, 32, True, 0),      # 8-wave 3-D config 6: 6x4x16 tiles, BN 32
+    (2, 32, 32, 32, 64, 0, 64, False, 0),      # config 7: 4x4x16, BN 64
+    (1, 32, 32, 32, 128, 0, 128, True, 0),     # config 8: 2x4x16, BN 128
+    (1, 16, 32, 32, 128, 128, 256, False, 0),  # config 8, two channel tiles, concat
+    (2, 32, 32, 32, 32, 0, 96, False, 64)])    # config 9: BN 96, split output (dec1.a dgrad)
+def test_conv3d_fwd_8wave(ops, N, D, H, W, C1, C2, Cout, pro, co1):
     """3-D streaming conv on the 8-wave tile configurations (bindings.cpp conv3_fwd picks them
-    when the layer fills the chip): output, bias, BN prologue, concat input and statistics."""
+    when the layer fills the chip): output, bias, BN prologue, concat input, split output and
+    statistics."""
     torch.manual_seed(17)
     x1 = torch.randn(N, C1, D, H, W, device=DEV).bfloat16()
     x2 = torch.randn(N, C2, D, H, W, device=DEV).bfloat16() if C2 else None
     w = torch.randn(Cout, C1 + C2, 3, 3, 3, device=DEV) * (1.0 / math.sqrt(27 * (C1 + C2)))
-    b = torch.randn(Cout, device=DEV) * 0.1
+    b = torch.randn(Cout, device=DEV) * 0.1 if not co1 else None
     scale = torch.rand(C1, device=DEV) + 0.5 if pro else None
     shift = torch.randn(C1, device=DEV) * 0.5 if pro else None
     pk = pack_conv(ops, w)
-    y, _, st = ops.conv3_fwd(nhwc(x1), nhwc(x2) if x2 is not None else None, pk.fwd, b, scale,
-                             shift, Cout, 0, True)
+    y, y2, st = ops.conv3_fwd(nhwc(x1), nhwc(x2) if x2 is not None else None, pk.fwd, b, scale,
+                              shift, Cout, co1, True)
     a1 = x1.float()
     if pro:
         a1 = torch.relu(a1 * scale.view(1, -1, 1, 1, 1) + shift.view(1, -1, 1, 1, 1)).bfloat16().float()
     xin = torch.cat([a1, x2.float()], 1) if x2 is not None else a1
     ref = F.conv3d(xin, w.bfloat16().float(), b, padding=1)
-    assert rel_err(nchw(y), ref) < 1e-2
+    out = torch.cat([nchw(y), nchw(y2)], 1) if co1 else nchw(y)
+    assert rel_err(out, ref) < 1e-2
     s = st.sum(0)
-    yf = nchw(y).float()
+    yf = out.float()
     assert torch.allclose(s[0], yf.sum((0, 2, 3, 4)), rtol=1e-3, atol=1e-1)
     assert torch.allclose(s[1], (yf * yf).sum((0, 2, 3, 4)), rtol=1e-3, atol=1.0)
 
