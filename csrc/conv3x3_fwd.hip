@@ -27,7 +27,7 @@
 //     torch.cat([up, skip], 1), ref.py:616) — one buffer descriptor per 32-channel chunk;
 //   * epilogue: + bias, bf16, tile staged in LDS, 16-B coalesced stores (optionally split
 //     across two outputs: the data gradient of a concat conv), and per-channel
-//     (sum, sum^2) partials of the stored values for BatchNorm statistics (K4), one partial
+//     (sum, sum^2) partials of the fp32 outputs for BatchNorm statistics (K4), one partial
 //     row per M tile (deterministic; reduced by bn_finalize).
 //
 // The data gradient (K2) is this same kernel run on dY with the flipped, transposed
@@ -437,8 +437,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         if constexpr (BNB) {
           bnb_accum(pk, ybuf[mt][nt], ok, kb, t1, t2);
         } else if (ok) {
-          // statistics of the stored (bf16-rounded) values
-          const float r0 = lo_bf(pk.x), q1 = hi_bf(pk.x), q2 = lo_bf(pk.y), q3 = hi_bf(pk.y);
+          // statistics of the fp32 outputs (before the bf16 store; ops.h ConvFwdArgs::stats)
+          const float r0 = v[0], q1 = v[1], q2 = v[2], q3 = v[3];
           if constexpr (LSTAT) {
             t1[0] += r0; t2[0] += r0 * r0;
             t1[1] += q1; t2[1] += q1 * q1;
@@ -783,7 +783,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 }
 
 // split-K finalize: sum the KS fp32 partials (fixed order), + bias, bf16 store (optionally
-// split into two outputs), per-workgroup BN statistic rows of the stored values
+// split into two outputs), per-workgroup BN statistic rows of the fp32 outputs
 __global__ void conv_splitk_finalize_kernel(const float* __restrict__ part, int KS, long long npix,
                                             int Cout, int Co1, const float* __restrict__ bias,
                                             bf16_t* __restrict__ Y1, bf16_t* __restrict__ Y2,
@@ -822,7 +822,7 @@ __global__ void conv_splitk_finalize_kernel(const float* __restrict__ part, int 
       else *reinterpret_cast<uint4*>(Y2 + px * (Cout - Co1) + (c8 - Co1)) = pk;
       if (stats != nullptr) {
         float r[8];
-        unpack8(pk, r);
+        unpack8(pk, r);                          // (BN backward: the stored dA)
         if (bnb_y != nullptr) {
           float yy[8];
           unpack8(*reinterpret_cast<const uint4*>(bnb_y + px * Cout + c8), yy);
@@ -835,7 +835,7 @@ __global__ void conv_splitk_finalize_kernel(const float* __restrict__ part, int 
           }
         } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) { s1[j] += r[j]; s2[j] += r[j] * r[j]; }
+          for (int j = 0; j < 8; ++j) { s1[j] += v[j]; s2[j] += v[j] * v[j]; }
         }
       }
     }

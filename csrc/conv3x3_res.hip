@@ -27,6 +27,8 @@
 #include "conv_lds.h"
 #include "ops.h"
 
+#include <type_traits>
+
 namespace ddlpc {
 
 namespace {
@@ -59,16 +61,18 @@ DDLPC_HOST_DEVICE int res_w_bytes(int Cin, int BN, int tap8) {
 // SPLIT: 0 = one output; 1 = two outputs (concat data gradient), 8-byte stores; 2 = two
 // outputs split at a 32-channel boundary (Co1 % 32 == 0, launcher-checked): 16-byte pair
 // stores, each pair wholly in one output (a quarter of mode 1's store instructions)
-// EPI (non-BNB epilogue form): 0 = one block, tiles channel-outer (the round-2 form); 1 = by
-// 16-pixel rows of MFMA tiles with item-independent pixel geometry and packed fp32 bias /
-// statistics.  BNB keeps form 0.  (Rejected: form 1 interleaved between the next stage's
-// tap steps from a second accumulator set, 10-20% slower: profiles/r3s/res_ilv_ab_b256_r3s24.txt)
-template <int WM, int WN, int MT, int NT, int HALO, int TAP8, int NBUF, int SPLIT, bool BNB, int EPI = 1>
+// BNB: the BN-backward epilogue (statistics of dA against y).  (Rejected: the epilogue
+// interleaved between the next stage's tap steps from a second accumulator set, 10-20%
+// slower: profiles/r3s/res_ilv_ab_b256_r3s24.txt)
+template <int WM, int WN, int MT, int NT, int HALO, int TAP8, int NBUF, int SPLIT, bool BNB>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_kernel(ConvFwdArgs p) {
   using C = RCfg<WM, WN, MT, NT, HALO, TAP8, NBUF>;
   static_assert(NBUF == 2 || NBUF == 3, "halo ring depth");
   static_assert(!BNB || (!SPLIT && !TAP8), "BN-backward epilogue: single output, no image layer");
   constexpr int NW = C::NW, BN = C::BN;
+  // the 96-channel variant serves the data gradient of the first decoder conv only: no bias,
+  // no statistics (planner / launcher), which keeps it inside 256 VGPRs
+  constexpr bool NOSTAT = BN == 96;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bool has_pro = p.pscale != nullptr;
   const bool has_pro2 = p.pscale2 != nullptr;          // deferred skip: X2 channels at C1 + c
@@ -115,7 +119,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * (lane >> 4) + i;
-      bias_r[nt][i] = (p.bias != nullptr && co < p.Cout) ? p.bias[co] : 0.0f;
+      bias_r[nt][i] = (!NOSTAT && p.bias != nullptr && co < p.Cout) ? p.bias[co] : 0.0f;
     }
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)                     // consume now: the compiler's wait
@@ -187,7 +191,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   Walk wA = w0, wE = w0, wY = w0;
   // ---- per-lane halo DMA geometry (no integer division in the stage loop).  Interior
   // tiles (the common case) need no bounds checks: pixel = tile base + a_rel.
-  int a_dw[C::A_ITERS], a_dh[C::A_ITERS], a_dd[C::A_ITERS], a_sub8[C::A_ITERS], a_rel[C::A_ITERS];
+  int a_dw[C::A_ITERS], a_dh[C::A_ITERS], a_dd[C::A_ITERS], a_sub8[C::A_ITERS];
   uint32_t a_inhalo = 0;
 #pragma unroll
   for (int i = 0; i < C::A_ITERS; ++i) {
@@ -198,9 +202,18 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     a_dd[i] = NPL == 1 ? 0 : px / PL - 1;
     a_dw[i] = pr % HW2 - 1;
     a_dh[i] = pr / HW2 - 1;
-    a_rel[i] = ((NPL == 3 ? a_dd[i] * p.H : 0) + a_dh[i]) * p.W + a_dw[i];
     if (px < halo && e < C::PIECES) a_inhalo |= 1u << i;
   }
+  // element offset of piece i relative to the item / chunk base, per input tensor (a runtime
+  // multiply per piece per stage otherwise); pieces past the halo get an offset beyond any
+  // tensor (>= 2^31 bytes: the DMA reads zeros), so an interior item's pieces need no mask
+  // (X2 chunks of the concat layers compute theirs per stage: VGPR budget of the 96-channel
+  // variant)
+  int a_relC1[C::A_ITERS];
+#pragma unroll
+  for (int i = 0; i < C::A_ITERS; ++i)
+    a_relC1[i] = (a_inhalo >> i) & 1u ? (((NPL == 3 ? a_dd[i] * p.H : 0) + a_dh[i]) * p.W + a_dw[i]) * p.C1 + a_sub8[i]
+                                      : (1 << 30);
   uint32_t a_valid = 0;            // pieces of the item last issued that are inside the image
   // a_valid of the stage held by each ring slot, 8 bits per slot in one register (a
   // runtime-indexed array would live in scratch: vm ops that break the counted waits)
@@ -210,6 +223,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     vmasks = (vmasks & ~(0xffu << (8 * buf))) | (m << (8 * buf));
   };
   auto get_vmask = [&](int buf) { return (vmasks >> (8 * buf)) & 0xffu; };
+  // wave-uniform: bit b = the item staged in ring slot b is interior (every halo piece inside
+  // the image): its prologue needs no masking
+  uint32_t ibits = 0;
+  bool a_int = false;
   int a_item = -1, a_nimg = 0, a_base = 0;
   auto issue_A = [&](int k, int chunk, int buf) {
     if (k != a_item) {
@@ -219,6 +236,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
       a_base = ((NPL == 3 ? it.d * p.H : 0) + it.h0) * p.W + it.w0;   // pixel within the image volume
       const bool interior = it.w0 >= 1 && it.h0 >= 1 && it.w0 + p.TW < p.W && it.h0 + p.TH < p.H &&
                             (NPL == 1 || (it.d >= 1 && it.d + 1 < p.D));
+      a_int = interior;
       if (interior) {
         a_valid = a_inhalo;
       } else {
@@ -239,13 +257,32 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     const bool full = c0 + BK <= Cs;                   // wave-uniform: no channel check
     const bf16_t* src = second ? p.X2 : p.X1;
     set_vmask(buf, a_valid);
+    ibits = (ibits & ~(1u << buf)) | ((a_int ? 1u : 0u) << buf);
     const auto r = make_rsrc(src + a_nimg * vol_px * Cs, (unsigned)(vol_px * Cs * 2));
     const int s0 = a_base * Cs + c0;                   // scalar part of the element offset
+    // (wave-uniform branches: interior item and full chunk = no per-piece mask at all)
+    auto pieces = [&](const int (&rel)[C::A_ITERS], auto maskc) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < C::A_ITERS; ++i) {
-      const bool ok = ((a_valid >> i) & 1u) && (full || c0 + a_sub8[i] < Cs);
-      const unsigned off = ok ? (unsigned)(a_rel[i] * Cs + a_sub8[i] + s0) * 2u : kOOB;
-      dma16(r, sA(buf) + (i * NW + wave) * 1024, off);
+      for (int i = 0; i < C::A_ITERS; ++i) {
+        unsigned off = (unsigned)(rel[i] + s0) * 2u;
+        if constexpr (decltype(maskc)::value) {
+          const bool ok = ((a_valid >> i) & 1u) && (full || c0 + a_sub8[i] < Cs);
+          off = ok ? off : kOOB;
+        }
+        dma16(r, sA(buf) + (i * NW + wave) * 1024, off);
+      }
+    };
+    if (second) {
+      int rel2[C::A_ITERS];
+#pragma unroll
+      for (int i = 0; i < C::A_ITERS; ++i)
+        rel2[i] = (a_inhalo >> i) & 1u ? (((NPL == 3 ? a_dd[i] * p.H : 0) + a_dh[i]) * p.W + a_dw[i]) * Cs + a_sub8[i]
+                                       : (1 << 30);
+      pieces(rel2, std::true_type{});
+    } else if (a_int && full) {
+      pieces(a_relC1, std::false_type{});
+    } else {
+      pieces(a_relC1, std::true_type{});
     }
   };
   // prologue on the pieces THIS lane DMA'd (a_valid still describes the chunk's item), in a
@@ -256,7 +293,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   // a branch around each piece
   const int sub8_l = TAP8 ? 0 : ((lane & 3) ^ (((lane >> 4) & 1) << 1)) << 3;
   auto transform_batched = [&](char* __restrict__ Ab, const float* __restrict__ scl,
-                               const float* __restrict__ shf_, int cbase, uint32_t vm, int climit) {
+                               const float* __restrict__ shf_, int cbase, uint32_t vm, int climit,
+                               auto maskc) {
+    constexpr bool MASK = decltype(maskc)::value;   // false: interior item, full chunk
     const int c8 = cbase + sub8_l;
     const bool cok = c8 < climit;
     const float4* scp = reinterpret_cast<const float4*>(scl + (cok ? c8 : 0));
@@ -270,7 +309,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
       v[i] = *reinterpret_cast<const uint4*>(Ab + ((i * NW + wave) * 64 + lane) * 16);
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
-      const bool ok = ((vm >> i) & 1u) && cok;
+      const bool ok = !MASK || (((vm >> i) & 1u) && cok);
       const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
       uint32_t o[4];
 #pragma unroll
@@ -292,7 +331,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     const int cbase = chunk * BK;
     const bool x2ch = cbase >= p.C1;                   // X2 chunk: prologue only if deferred
     if (x2ch ? !has_pro2 : !has_pro) return;
-    transform_batched(sA(buf), s_scale, s_shift, cbase, get_vmask(buf), x2ch ? p.Cin : p.C1);
+    const int climit = x2ch ? p.Cin : p.C1;
+    // interior item and a full chunk: no piece needs re-zeroing (pieces past the halo are
+    // never read by the fragment loads)
+    if (((ibits >> buf) & 1u) && cbase + BK <= climit)
+      transform_batched(sA(buf), s_scale, s_shift, cbase, 0u, climit, std::false_type{});
+    else
+      transform_batched(sA(buf), s_scale, s_shift, cbase, get_vmask(buf), climit, std::true_type{});
   };
 
   // ---- per-lane fragment geometry
@@ -314,11 +359,15 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   }
   const int wrow0 = wn * (NT * 16) + (lane & 15);
 
+  // accumulators start at the bias and the epilogue resets them to it (no bias add per value)
+  f32x4_t bias4[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) bias4[nt] = f32x4_t{bias_r[nt][0], bias_r[nt][1], bias_r[nt][2], bias_r[nt][3]};
   f32x4_t acc[MT][NT];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NT; ++j) acc[i][j] = bias4[j];
   float s1[NT][4], s2[NT][4];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
@@ -336,60 +385,75 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   constexpr bool PAIRS = (!SPLIT && (TAP8 || BN >= 64) && NT % 2 == 0) || SPLIT == 2;
   static_assert(SPLIT != 2 || (NT % 2 == 0 && BN % 32 == 0), "split pairs: 32-channel pairs");
   constexpr int EPI_STORES = SPLIT == 1 ? MT * NT * 2 : PAIRS ? MT * NT / 2 : MT * NT;
-  // (non-BNB) epilogue by 16-pixel rows of MFMA tiles, from accumulator set A: the per-lane
-  // pixel geometry is item-independent (no division in the loop), bias add and statistics
-  // run as packed fp32 pairs
-  int prow[MT], pcol[MT];
+  // ---- per-lane output geometry relative to an item's first pixel (item-independent): the
+  // element offset of tile (mt, nt) is item_base * Co + orel[mt] + 16 nt (pairs: + 32 np) —
+  // one add per store instead of a 64-bit multiply-add chain (the epilogue was VALU-issue
+  // bound).  q: the MFMA's 4-channel lane layout, p: the pair16 layout.
+  const int Co2 = p.Cout - p.Co1;
+  int prow[MT], pcol[MT], orel1q[MT], orel2q[MT], orel1p[MT], orel2p[MT];
+  {
+    const int coq = co0 + wn * (NT * 16) + 4 * g;
+    const int cop = co0 + wn * (NT * 16) + pair16_ch(lane);
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
-    prow[mt] = pix / p.TW;
-    pcol[mt] = pix % p.TW;
+    for (int mt = 0; mt < MT; ++mt) {
+      const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
+      prow[mt] = pix / p.TW;
+      pcol[mt] = pix % p.TW;
+      const int lr = prow[mt] * p.W + pcol[mt];
+      orel1q[mt] = lr * p.Co1 + coq;
+      orel2q[mt] = SPLIT == 1 ? lr * Co2 + coq - p.Co1 : 0;
+      orel1p[mt] = PAIRS ? lr * p.Co1 + cop : 0;
+      orel2p[mt] = SPLIT == 2 ? lr * Co2 + cop - p.Co1 : 0;
+    }
   }
-  struct EpiCtx { __amdgpu_buffer_rsrc_t r1, r2; int h0, w0; };
-  auto epi_ctx = [&](int kk) __attribute__((always_inline)) {
-    const Item it = walk_item(wE, kk);
+  // per item: output descriptors, element bases, the in-image extent, and whether the whole
+  // tile (pixels and channels) is inside the output — wave-uniform, then no masks at all
+  struct EpiCtx { __amdgpu_buffer_rsrc_t r1, r2; int b1, b2, wlim, hlim; bool full; };
+  auto epi_ctx = [&](Walk& w, int kk) __attribute__((always_inline)) {
+    const Item it = walk_item(w, kk);
     EpiCtx e;
-    const int Co2 = p.Cout - p.Co1;
     e.r1 = make_rsrc(p.Y1 + (long long)it.n_img * img_px * p.Co1, (unsigned)(img_px * p.Co1 * 2));
     e.r2 = SPLIT ? make_rsrc(p.Y2 + (long long)it.n_img * img_px * Co2, (unsigned)(img_px * Co2 * 2)) : e.r1;
-    e.h0 = it.h0; e.w0 = it.w0;
+    const int base = it.h0 * p.W + it.w0;
+    e.b1 = base * p.Co1;
+    e.b2 = SPLIT ? base * Co2 : 0;
+    e.wlim = p.W - it.w0;
+    e.hlim = p.H - it.h0;
+    e.full = it.w0 + p.TW <= p.W && it.h0 + p.TH <= p.H && co0 + BN <= p.Cout;
     return e;
   };
-  auto epi_unit = [&](const EpiCtx& e, int mt, f32x4_t (&A)[MT][NT]) __attribute__((always_inline)) {
-    const int Co2 = p.Cout - p.Co1;
-    const int gw = e.w0 + pcol[mt], gh = e.h0 + prow[mt];
-    const bool pv = gw < p.W && gh < p.H;
-    constexpr bool st_on = true;
-    const int lp = gh * p.W + gw;
+  // one 16-pixel row (mt) of tiles: bf16 stores, and the BN statistics of the tiles' fp32
+  // values as packed pairs (masked lanes add zeros); FULL: every lane is valid
+  auto epi_row = [&](const EpiCtx& e, int mt, auto fullc) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(fullc)::value;
+    const bool pv = FULL || (pcol[mt] < e.wlim && prow[mt] < e.hlim);
     uint2 pkv[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * g;
-      const bool ok = pv && co < p.Cout;
-      const f32x2_t b01 = {bias_r[nt][0], bias_r[nt][1]}, b23 = {bias_r[nt][2], bias_r[nt][3]};
-      const f32x2_t v01 = f32x2_t{A[mt][nt][0], A[mt][nt][1]} + b01;
-      const f32x2_t v23 = f32x2_t{A[mt][nt][2], A[mt][nt][3]} + b23;
+      const bool ok = FULL || (pv && co < p.Cout);
+      const f32x2_t v01 = {acc[mt][nt][0], acc[mt][nt][1]};
+      const f32x2_t v23 = {acc[mt][nt][2], acc[mt][nt][3]};
       const uint2 pk = make_uint2(pack2(v01.x, v01.y), pack2(v23.x, v23.y));
       pkv[nt] = pk;
       if constexpr (!PAIRS) {
         const u32x2_t d = u32x2_t{pk.x, pk.y};
         if constexpr (!SPLIT) {
-          unsigned o1 = ok && st_on ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
+          unsigned o1 = ok ? (unsigned)(e.b1 + orel1q[mt] + nt * 16) * 2u : kOOB;
           asm volatile("" : "+v"(o1));
           __builtin_amdgcn_raw_buffer_store_b64(d, e.r1, o1, 0, 0);
         } else {
           const bool in1 = co < p.Co1;
-          unsigned o1 = (ok && st_on && in1) ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
-          unsigned o2 = (ok && st_on && !in1) ? (unsigned)(lp * Co2 + co - p.Co1) * 2u : kOOB;
+          unsigned o1 = (ok && in1) ? (unsigned)(e.b1 + orel1q[mt] + nt * 16) * 2u : kOOB;
+          unsigned o2 = (ok && !in1) ? (unsigned)(e.b2 + orel2q[mt] + nt * 16) * 2u : kOOB;
           asm volatile("" : "+v"(o1), "+v"(o2));
           __builtin_amdgcn_raw_buffer_store_b64(d, e.r1, o1, 0, 0);
           __builtin_amdgcn_raw_buffer_store_b64(d, e.r2, o2, 0, 0);
         }
       }
-      // statistics of the stored (bf16-rounded) values; masked lanes add zeros
-      const f32x2_t r01 = {ok ? lo_bf(pk.x) : 0.f, ok ? hi_bf(pk.x) : 0.f};
-      const f32x2_t r23 = {ok ? lo_bf(pk.y) : 0.f, ok ? hi_bf(pk.y) : 0.f};
+      if constexpr (NOSTAT) continue;
+      const f32x2_t z = {0.f, 0.f};
+      const f32x2_t r01 = ok ? v01 : z, r23 = ok ? v23 : z;
       f32x2_t a01 = {s1[nt][0], s1[nt][1]}, a23 = {s1[nt][2], s1[nt][3]};
       f32x2_t q01 = {s2[nt][0], s2[nt][1]}, q23 = {s2[nt][2], s2[nt][3]};
       a01 += r01; a23 += r23;
@@ -403,14 +467,16 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
       for (int np = 0; np < NT / 2; ++np) {
         const uint4 q = pair16(pkv[2 * np], pkv[2 * np + 1]);
         const int co = co0 + wn * (NT * 16) + np * 32 + pair16_ch(lane);
+        const bool ok = FULL || (pv && co < p.Cout);
         if constexpr (SPLIT == 2) {
+          // the pair's 32 channels lie in one output (wave-uniform choice)
           const bool in1 = co0 + wn * (NT * 16) + np * 32 < p.Co1;
-          unsigned o = pv && st_on && co < p.Cout ? (unsigned)(in1 ? lp * p.Co1 + co : lp * Co2 + co - p.Co1) * 2u
-                                                 : kOOB;
+          unsigned o = ok ? (unsigned)(in1 ? e.b1 + orel1p[mt] + np * 32 : e.b2 + orel2p[mt] + np * 32) * 2u
+                          : kOOB;
           asm volatile("" : "+v"(o));
           __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, in1 ? e.r1 : e.r2, o, 0, 0);
         } else {
-          unsigned o1 = pv && st_on && co < p.Cout ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
+          unsigned o1 = ok ? (unsigned)(e.b1 + orel1p[mt] + np * 32) * 2u : kOOB;
           asm volatile("" : "+v"(o1));
           __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, e.r1, o1, 0, 0);
         }
@@ -418,123 +484,80 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     }
   };
   // BNB: y at this item's output pixels, loaded into VGPRs at the item's last stage (before
-  // that stage's halo DMA) and consumed by its epilogue one stage later
+  // that stage's halo DMA) and consumed by its epilogue one stage later (Co1 = Cout)
   constexpr int YL = BNB ? MT * NT : 0;
   uint2 ybuf[MT][NT];
   auto issue_Y = [&](int kk) __attribute__((always_inline)) {
     const Item it = walk_item(wY, kk);
     const auto ry = make_rsrc(p.bnb_y + (long long)it.n_img * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
+    const int b = (it.h0 * p.W + it.w0) * p.Cout;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const int gw = it.w0 + pcol[mt], gh = it.h0 + prow[mt];
-      const bool valid = gw < p.W && gh < p.H;
-      const int lp = gh * p.W + gw;
+      const bool valid = pcol[mt] < p.W - it.w0 && prow[mt] < p.H - it.h0;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * g;
-        ybuf[mt][nt] = buf_load8(ry, valid && co < p.Cout ? (unsigned)(lp * p.Cout + co) * 2u : kOOB);
+        ybuf[mt][nt] = buf_load8(ry, valid && co < p.Cout ? (unsigned)(b + orel1q[mt] + nt * 16) * 2u : kOOB);
       }
     }
   };
-  auto epilogue_blk = [&](int k) {
-    const Item it = walk_item(wE, k);
-    const int Co2 = p.Cout - p.Co1;
-    constexpr bool st_on = true;
-    const auto r1 = make_rsrc(p.Y1 + (long long)it.n_img * img_px * p.Co1, (unsigned)(img_px * p.Co1 * 2));
-    const auto r2 = SPLIT ? make_rsrc(p.Y2 + (long long)it.n_img * img_px * Co2, (unsigned)(img_px * Co2 * 2)) : r1;
-    // pass 1, channel tiles outer: bias, bf16 rounding, statistics (the BNB constants of one
-    // tile are read once; the scheduler barrier keeps the next tile's reads from being
-    // hoisted: VGPR pressure)
+  // BNB epilogue (a data gradient dA; no bias): channel tiles outer, so the BN-backward
+  // constants of one tile are read once; the scheduler barrier keeps the next tile's reads
+  // from being hoisted (VGPR pressure)
+  auto epilogue_bnb = [&](int kk) {
+    const EpiCtx e = epi_ctx(wE, kk);
     uint2 pkv[MT][NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int co = co0 + wn * (NT * 16) + nt * 16 + 4 * g;
-      BnbC kb;
-      if constexpr (BNB) kb = bnb_load(s_bnb, BN, wn * (NT * 16) + nt * 16 + 4 * g);
+      const BnbC kb = bnb_load(s_bnb, BN, wn * (NT * 16) + nt * 16 + 4 * g);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const int gw = it.w0 + pcol[mt], gh = it.h0 + prow[mt];
-        const bool ok = gw < p.W && gh < p.H && co < p.Cout;
-        const bool okst = ok && st_on;
-        float v[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bias_r[nt][i];
-        const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        const bool ok = pcol[mt] < e.wlim && prow[mt] < e.hlim && co < p.Cout;
+        const uint2 pk = make_uint2(pack2(acc[mt][nt][0], acc[mt][nt][1]), pack2(acc[mt][nt][2], acc[mt][nt][3]));
         pkv[mt][nt] = pk;
         if constexpr (!PAIRS) {
-          // 8-byte stores right away (split output: one of the two offsets is out of range)
-          const int lp = gh * p.W + gw;
-          const u32x2_t d = u32x2_t{pk.x, pk.y};
-          if constexpr (!SPLIT) {
-            unsigned o1 = okst ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
-            asm volatile("" : "+v"(o1));
-            __builtin_amdgcn_raw_buffer_store_b64(d, r1, o1, 0, 0);
-          } else {
-            const bool in1 = co < p.Co1;
-            unsigned o1 = (okst && in1) ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
-            unsigned o2 = (okst && !in1) ? (unsigned)(lp * Co2 + co - p.Co1) * 2u : kOOB;
-            asm volatile("" : "+v"(o1), "+v"(o2));
-            __builtin_amdgcn_raw_buffer_store_b64(d, r1, o1, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b64(d, r2, o2, 0, 0);
-          }
+          unsigned o1 = ok ? (unsigned)(e.b1 + orel1q[mt] + nt * 16) * 2u : kOOB;
+          asm volatile("" : "+v"(o1));
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk.x, pk.y}, e.r1, o1, 0, 0);
         }
-        if constexpr (BNB) {
-          bnb_accum(pk, ybuf[mt][nt], ok, kb, s1[nt], s2[nt]);
-        } else {
-          // statistics of the stored (bf16-rounded) values; masked lanes add zeros
-          const float r0 = ok ? lo_bf(pk.x) : 0.f, q1 = ok ? hi_bf(pk.x) : 0.f;
-          const float q2 = ok ? lo_bf(pk.y) : 0.f, q3 = ok ? hi_bf(pk.y) : 0.f;
-          s1[nt][0] += r0; s2[nt][0] += r0 * r0;
-          s1[nt][1] += q1; s2[nt][1] += q1 * q1;
-          s1[nt][2] += q2; s2[nt][2] += q2 * q2;
-          s1[nt][3] += q3; s2[nt][3] += q3 * q3;
-        }
-        acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        bnb_accum(pk, ybuf[mt][nt], ok, kb, s1[nt], s2[nt]);
       }
-      if constexpr (BNB) __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    // pass 2 (PAIRS): 16-byte stores.  Buffer stores with an out-of-range offset for masked
-    // lanes; the offsets go through an opaque asm so the compiler cannot turn a masked store
-    // into a branch around it (the store COUNT must not depend on the data)
     if constexpr (PAIRS) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const int gw = it.w0 + pcol[mt], gh = it.h0 + prow[mt];
-        const bool valid = gw < p.W && gh < p.H && st_on;
-        const int lp = gh * p.W + gw;                   // pixel within the image (32-bit)
+        const bool pv = pcol[mt] < e.wlim && prow[mt] < e.hlim;
 #pragma unroll
         for (int np = 0; np < NT / 2; ++np) {
           const uint4 q = pair16(pkv[mt][2 * np], pkv[mt][2 * np + 1]);
           const int co = co0 + wn * (NT * 16) + np * 32 + pair16_ch(lane);
-          if constexpr (SPLIT == 2) {
-            // the pair's 32 channels lie in one output (wave-uniform choice)
-            const bool in1 = co0 + wn * (NT * 16) + np * 32 < p.Co1;
-            unsigned o = valid && co < p.Cout ? (unsigned)(in1 ? lp * p.Co1 + co : lp * Co2 + co - p.Co1) * 2u
-                                              : kOOB;
-            asm volatile("" : "+v"(o));
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, in1 ? r1 : r2, o, 0, 0);
-          } else {
-            unsigned o1 = valid && co < p.Cout ? (unsigned)(lp * p.Co1 + co) * 2u : kOOB;
-            asm volatile("" : "+v"(o1));
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, r1, o1, 0, 0);
-          }
+          unsigned o1 = pv && co < p.Cout ? (unsigned)(e.b1 + orel1p[mt] + np * 32) * 2u : kOOB;
+          asm volatile("" : "+v"(o1));
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, e.r1, o1, 0, 0);
         }
       }
     }
   };
 
   auto epilogue = [&](int kk) __attribute__((always_inline)) {
-    if constexpr (BNB || EPI == 0) {
-      epilogue_blk(kk);
+    if constexpr (BNB) {
+      epilogue_bnb(kk);
     } else {
-      const EpiCtx e = epi_ctx(kk);
+      const EpiCtx e = epi_ctx(wE, kk);
+      if (e.full) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) epi_unit(e, mt, acc);
+        for (int mt = 0; mt < MT; ++mt) epi_row(e, mt, std::true_type{});
+      } else {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int mt = 0; mt < MT; ++mt) epi_row(e, mt, std::false_type{});
+      }
     }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = bias4[nt];
   };
 
   // ---- pipeline: the halo of stage s+NBUF-1 is issued at stage s (ring of NBUF buffers).
@@ -639,7 +662,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   }
 
   // ---- one BN-statistics partial row per workgroup (layout of conv3_fwd_kernel)
-  if (p.stats != nullptr) {
+  if (!NOSTAT && p.stats != nullptr) {
     dma_wait<0>();
     lds_sync();
     float* red = reinterpret_cast<float*>(sA0);
@@ -694,41 +717,31 @@ int res_smem(const ResVariant& v, int Cin, int C1, bool pro, bool bnb) {   // C1
   return (bnb ? 16 * bn : res_ss_bytes(C1, pro)) + res_w_bytes(Cin, bn, v.tap8) + v.nbuf * a_bytes;
 }
 
-template <int WM, int WN, int MT, int NT, int HALO, int TAP8, int NBUF, int EPIc>
-void launch_res_i(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
+template <int WM, int WN, int MT, int NT, int HALO, int TAP8, int NBUF>
+void launch_res(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
   constexpr int BNc = WN * NT * 16;
   if (a.Co1 < a.Cout) {
     // split output at a 32-channel boundary: 16-byte pair stores
     if constexpr (NT % 2 == 0 && BNc % 32 == 0 && !TAP8) {
       if (a.Co1 % 32 == 0) {
-        hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 2, false, EPIc>), dim3(grid),
+        hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 2, false>), dim3(grid),
                            dim3(WM * WN * 64), smem, st, a);
         return;
       }
     }
-    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 1, false, EPIc>), dim3(grid),
+    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 1, false>), dim3(grid),
                        dim3(WM * WN * 64), smem, st, a);
   } else if constexpr (!TAP8 && BNc != 96) {
     if (a.bnb_y != nullptr)
       hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 0, true>), dim3(grid),
                          dim3(WM * WN * 64), smem, st, a);
     else
-      hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 0, false, EPIc>), dim3(grid),
+      hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 0, false>), dim3(grid),
                          dim3(WM * WN * 64), smem, st, a);
   } else {
-    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 0, false, EPIc>), dim3(grid),
+    hipLaunchKernelGGL((conv3_res_kernel<WM, WN, MT, NT, HALO, TAP8, NBUF, 0, false>), dim3(grid),
                        dim3(WM * WN * 64), smem, st, a);
   }
-}
-
-// non-BNB epilogue form (kernel EPI above): form 0 on the 8-wave 32-channel tiles (form 1
-// measured 1-1.5% slower there), form 1 elsewhere (image layer -19%, 64/96-channel tiles
-// -6..-11%; same-process A/B at batch 256, profiles/r3s/res_epi_ab_b256_r3s25.txt)
-template <int WM, int WN, int MT, int NT, int HALO, int TAP8, int NBUF>
-void launch_res(ConvFwdArgs& a, int grid, int smem, hipStream_t st) {
-  constexpr bool form0 = WM == 8 && WN == 1 && NT == 2 && !TAP8;
-  if (form0 || a.bnb_y != nullptr) launch_res_i<WM, WN, MT, NT, HALO, TAP8, NBUF, 0>(a, grid, smem, st);
-  else launch_res_i<WM, WN, MT, NT, HALO, TAP8, NBUF, 1>(a, grid, smem, st);
 }
 
 }  // namespace
@@ -756,7 +769,8 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
     if (d3) { cand[nc++] = 9; cand[nc++] = 8; }
     else if (depth == 2) { cand[nc++] = 3; } else { cand[nc++] = 4; cand[nc++] = 3; }
   } else if (bn == 96) {
-    if (a.bnb_y != nullptr) return -1;                 // no BN-backward epilogue at BN 96
+    // no BN-backward epilogue, bias or statistics at BN 96 (bindings: no statistics wanted)
+    if (a.bnb_y != nullptr || a.bias != nullptr) return -1;
     cand[nc++] = 7;
   } else if (bn == 32) {
     if (depth == 2) { cand[nc++] = 0; cand[nc++] = 5; }

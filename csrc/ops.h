@@ -27,8 +27,10 @@ struct ConvFwdArgs {
   const float* bias;              // optional
   bf16_t* Y1;
   bf16_t* Y2;
-  float* stats;                   // optional [grid][2][Cout] per-workgroup (sum, sum^2); rows of
-                                  // channels outside a workgroup's n tile are not written
+  float* stats;                   // optional [grid][2][Cout] per-workgroup (sum, sum^2) of the fp32
+                                  // outputs (before the bf16 store: the statistics an fp32
+                                  // BatchNorm would see); rows of channels outside a
+                                  // workgroup's n tile are not written
   int TD, TH, TW;
   int tilesD, tilesH, tilesW;
   int nTilesM, nTilesN;
