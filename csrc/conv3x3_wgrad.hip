@@ -20,6 +20,7 @@
 #include "ops.h"
 
 #include <stdexcept>
+#include <type_traits>
 
 namespace ddlpc {
 
@@ -590,13 +591,12 @@ DDLPC_DEVICE int wg3_yswz(int row) {             // XOR on the 16-B piece index
   return BCO == 128 ? ((row & 3) << 2) : BCO == 64 ? (((row >> 1) & 1) << 2) : 0;
 }
 
-// NB: stages in the LDS-DMA ring (2: double buffer, one full vmcnt drain per tile; 3: the
-// DMA of tile t + 2 in flight while t computes, counted waits — with 128-pixel tiles so two
-// workgroups still fit per CU)
+// Stages: a double buffer, one full vmcnt drain per tile (rejected: a 3-deep ring with
+// counted waits, 12-18% slower per layer: profiles/wgrad_micro_b128_ring*_s2.txt)
 // CIW: 32-channel input chunks per workgroup (2: each staged dY tile feeds two X halos — the
 // concat layers' many input chunks re-read dY half as often; the waves split (co tile, chunk)
 // instead of the k-steps)
-template <int BCO, int PT, int NB = 2, int CIW = 1>
+template <int BCO, int PT, int CIW = 1>
 __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
   using namespace convlds;
   using Cfg = Wg2Cfg<BCO, PT>;                     // DMA geometry / LDS budget as v2
@@ -604,7 +604,6 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
   constexpr int NJ = BCO / 32;                     // 32-channel co tiles
   constexpr int KW = 4 / (NJ * CIW);               // waves sharing a (co tile, chunk) (k-split)
   static_assert(NJ * CIW * KW == 4, "4 waves = co tiles x input chunks x k phases");
-  static_assert(CIW == 1 || NB == 2, "two input chunks: double buffer only");
   constexpr int KS16 = PT / 16;                    // 16-pixel k-steps per tile
   static_assert(KS16 % KW == 0, "k-steps must split evenly over the waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -652,7 +651,7 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
     x_pix[i] = -1;
   }
   // per input chunk cw: source tensor, channel offset, validity, prologue constants
-  bool second[CIW], xch_ok[CIW], xpro[CIW];
+  bool second[CIW], xch_ok[CIW], xpro[CIW], xfull[CIW];
   int Cs[CIW], cs0[CIW];
   const bf16_t* xsrc[CIW];
   float psc[CIW][8] = {}, psh[CIW][8] = {};          // this lane's prologue constants
@@ -665,6 +664,7 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
     cs0[cw] = second[cw] ? c8l - p.C1 : c8l;
     xsrc[cw] = second[cw] ? p.X2 : p.X1;
     xch_ok[cw] = cs0[cw] < Cs[cw];
+    xfull[cw] = (second[cw] ? cc - p.C1 : cc) + BK <= Cs[cw];   // the whole 32-channel chunk
     xpro[cw] = second[cw] ? has_pro2 : has_pro;
     if (xpro[cw])
       pro8_load(p.pscale, p.pshift, p.pscale2, p.pshift2, p.C1, c8l, second[cw] ? p.Cin : p.C1, psc[cw], psh[cw]);
@@ -672,12 +672,14 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
 
   TileWalk tw;                                     // the issue stream's tile geometry
   tw.init(t_begin, p.tilesW, p.tilesH, p.D);
+  bool x_int = false;
   auto issue = [&](int tile, int buf) __attribute__((always_inline)) {
     tw.to(tile, p.tilesW, p.tilesH, p.D);
     const int n = tw.n;
     const int dx = tw.d + dshift;
     const bool dok = dx >= 0 && dx < p.D;
     const int h0 = tw.h * TH, w0 = tw.w * 16;
+    x_int = dok && h0 >= 1 && w0 >= 1 && h0 + TH < p.H && w0 + 16 < p.W;
     const auto ry = make_rsrc(p.dY + n * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
     const int ybase = (h0 * p.W + w0) * p.Cout;
 #pragma unroll
@@ -705,30 +707,19 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
       }
     }
   };
-  // (ring: the halo validity of `tile` is recomputed here — x_pix already holds a later tile's)
-  // (double buffer: x_pix still holds this tile's validity; the integer divisions of the
-  // recomputation measured 6-8% on the weight gradient, so only the ring pays for them)
-  auto transform = [&](int tile, char* __restrict__ X0) __attribute__((always_inline)) {
-    int h0 = 0, w0 = 0;
-    bool dok = true;
-    if constexpr (NB != 2) {
-      int t = tile;                                // TileWalk's order: d, w, h, image
-      const int dx = t % p.D + dshift; t /= p.D;
-      const int tw_i = t % p.tilesW; t /= p.tilesW;
-      const int th_i = t % p.tilesH;
-      dok = dx >= 0 && dx < p.D;
-      h0 = th_i * TH; w0 = tw_i * 16;
-    }
+  // x_pix still holds this tile's validity (the next tile's DMA is issued after the barrier
+  // that follows this transform); x_int: the tile's whole halo lies inside the image
+  auto transform = [&](char* __restrict__ X0) __attribute__((always_inline)) {
     // (batched form on the 32-output-channel tiles: enc1.b / dec1.b -7%; the 64 / 128-channel
     // tiles measured 0-2% slower with it, profiles/r3s/wgrad_xform_ab_b256_r3s36.txt)
-    if (NB == 2 && Cfg::X_ITERS <= 6 && BCO == 32) {
+    if (Cfg::X_ITERS <= 6 && BCO == 32) {
       // batched form: all piece reads issue before the math (packed fp32 FMA, bf16 rounding,
-      // ReLU as a packed 16-bit max), padding re-zeroed by a select instead of a branch
+      // ReLU as a packed 16-bit max), padding re-zeroed by a select instead of a branch —
+      // none at all on an interior tile with a full chunk (wave-uniform; pieces past the
+      // halo are never read)
       constexpr int NI = Cfg::X_ITERS <= 6 ? Cfg::X_ITERS : 1;
-#pragma unroll
-      for (int cw = 0; cw < CIW; ++cw) {
-        if (!xpro[cw]) continue;
-        char* X = X0 + cw * Cfg::X_BYTES;
+      auto run = [&](char* __restrict__ X, int cw, auto maskc) __attribute__((always_inline)) {
+        constexpr bool MASK = decltype(maskc)::value;
         uint4 v[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i)
@@ -736,7 +727,7 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
           if ((i * 4 + wave) >= Cfg::X_INSTR) break;
-          const bool ok = x_pix[i] >= 0 && xch_ok[cw];
+          const bool ok = !MASK || (x_pix[i] >= 0 && xch_ok[cw]);
           const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
           uint32_t o[4];
 #pragma unroll
@@ -751,6 +742,12 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
           }
           *reinterpret_cast<uint4*>(X + ((i * 4 + wave) * 64 + lane) * 16) = make_uint4(o[0], o[1], o[2], o[3]);
         }
+      };
+#pragma unroll
+      for (int cw = 0; cw < CIW; ++cw) {
+        if (!xpro[cw]) continue;
+        if (x_int && xfull[cw]) run(X0 + cw * Cfg::X_BYTES, cw, std::false_type{});
+        else run(X0 + cw * Cfg::X_BYTES, cw, std::true_type{});
       }
       return;
     }
@@ -761,13 +758,7 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
 #pragma unroll
       for (int i = 0; i < Cfg::X_ITERS; ++i) {
         const int e = (i * 4 + wave) * 64 + lane;
-        bool ok;
-        if constexpr (NB == 2) {
-          ok = x_pix[i] >= 0 && xch_ok[cw];
-        } else {
-          const int gw = w0 + x_dw[i], gh = h0 + x_dh[i];
-          ok = gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && xch_ok[cw] && dok;
-        }
+        const bool ok = x_pix[i] >= 0 && xch_ok[cw];
         if ((i * 4 + wave) < Cfg::X_INSTR && ok) {
           uint4* q = reinterpret_cast<uint4*>(X + e * 16);
           float f[8];
@@ -846,36 +837,14 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
     }
   };
 
-  if constexpr (NB == 2) {
-    if (t_begin < t_end) issue(t_begin, 0);
-    for (int tile = t_begin; tile < t_end; ++tile) {
-      const int buf = (tile - t_begin) & 1;
-      dma_wait<0>();
-      if (any_pro) transform(tile, sX(buf));
-      lds_sync();
-      if (tile + 1 < t_end) issue(tile + 1, buf ^ 1);
-      compute(sY(buf), sX(buf));
-    }
-  } else {
-    // this wave's DMA instructions per tile (the counted waits below)
-    int per = 0;
-#pragma unroll
-    for (int i = 0; i < Cfg::Y_ITERS; ++i) per += (i * 4 + wave) < Cfg::Y_INSTR;
-#pragma unroll
-    for (int i = 0; i < Cfg::X_ITERS; ++i) per += (i * 4 + wave) < Cfg::X_INSTR;
-#pragma unroll
-    for (int j = 0; j < NB - 1; ++j)
-      if (t_begin + j < t_end) issue(t_begin + j, j);
-    for (int tile = t_begin; tile < t_end; ++tile) {
-      const int idx = tile - t_begin, buf = idx % NB;
-      const int after = min(NB - 2, t_end - 1 - tile);   // tiles issued after this one
-      vm_wait_dyn(after * per);
-      if (any_pro) transform(tile, sX(buf));
-      lds_sync();
-      // the buffer of tile - 1 is free (every wave is past its compute): refill it
-      if (tile + NB - 1 < t_end) issue(tile + NB - 1, (idx + NB - 1) % NB);
-      compute(sY(buf), sX(buf));
-    }
+  if (t_begin < t_end) issue(t_begin, 0);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int buf = (tile - t_begin) & 1;
+    dma_wait<0>();
+    if (any_pro) transform(sX(buf));
+    lds_sync();
+    if (tile + 1 < t_end) issue(tile + 1, buf ^ 1);
+    compute(sY(buf), sX(buf));
   }
 
   // ---- k-split reduction over the KW waves of each co tile (fixed order, in LDS, one tap
@@ -1216,7 +1185,7 @@ void conv3_wgrad3_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
   if (bco == 32)
     hipLaunchKernelGGL((conv3_wgrad3_kernel<32, 256>), dim3(grid), dim3(256), (Wg2Cfg<32, 256>::SMEM), st, a);
   else if (bco == 64 && a.ciw == 2)   // two input chunks per workgroup, 96-pixel tiles
-    hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 96, 2, 2>), dim3(grid), dim3(256), SMEM64C2, st, a);
+    hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 96, 2>), dim3(grid), dim3(256), SMEM64C2, st, a);
   else if (bco == 128)   // 96-pixel tiles: two 74 KB workgroups per CU
     hipLaunchKernelGGL((conv3_wgrad3_kernel<128, 96>), dim3(grid), dim3(256), (Wg2Cfg<128, 96>::SMEM), st, a);
   else
