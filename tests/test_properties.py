@@ -135,12 +135,13 @@ def test_conv3_fwd_dgrad_wgrad_any_geometry(ops, n, h, w, ch, cout, pro):
         a1 = torch.relu(a1 * sc[None, :, None, None] + sh[None, :, None, None]).bfloat16().float()
     xin = torch.cat([a1, x2.float()], 1) if c2 else a1
     wb = wt.bfloat16().float()
-    # forward (+ BN statistics of the stored output)
+    # forward (+ BN statistics of the fp32 outputs, before the bf16 store)
     y, _, stt = ops.conv3_fwd(_nhwc(x1), _nhwc(x2) if c2 else None, pk.fwd, b, sc, sh, cout, 0,
                               True)
-    assert _rel(_nchw(y), F.conv2d(xin, wb, b, padding=1)) < 1e-2
-    yf = _nchw(y).float()
-    assert torch.allclose(stt.sum(0)[0], yf.sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+    ref_y = F.conv2d(xin, wb, b, padding=1)
+    assert _rel(_nchw(y), ref_y) < 1e-2
+    assert torch.allclose(stt.sum(0)[0], ref_y.sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+    assert torch.allclose(stt.sum(0)[1], (ref_y * ref_y).sum((0, 2, 3)), rtol=1e-3, atol=1.0)
     # data gradient, split across the concat inputs
     dy = torch.randn(n, cout, h, w, device=DEV, generator=g).bfloat16()
     dx1, dx2, _ = ops.conv3_fwd(_nhwc(dy), None, pk.dgrad, None, None, None, cin,
