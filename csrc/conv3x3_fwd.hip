@@ -435,7 +435,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
           __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk.x, pk.y}, in1 ? r1 : r2, off, 0, 0);
         }
         if constexpr (BNB) {
-          bnb_accum(pk, ybuf[mt][nt], ok, kb, t1, t2);
+          const float d[4] = {ok ? v[0] : 0.f, ok ? v[1] : 0.f, ok ? v[2] : 0.f, ok ? v[3] : 0.f};
+          bnb_accum(d, ybuf[mt][nt], kb, t1, t2);
         } else if (ok) {
           // statistics of the fp32 outputs (before the bf16 store; ops.h ConvFwdArgs::stats)
           const float r0 = v[0], q1 = v[1], q2 = v[2], q3 = v[3];
@@ -821,15 +822,13 @@ __global__ void conv_splitk_finalize_kernel(const float* __restrict__ part, int 
       if (c8 < Co1) *reinterpret_cast<uint4*>(Y1 + px * Co1 + c8) = pk;
       else *reinterpret_cast<uint4*>(Y2 + px * (Cout - Co1) + (c8 - Co1)) = pk;
       if (stats != nullptr) {
-        float r[8];
-        unpack8(pk, r);                          // (BN backward: the stored dA)
-        if (bnb_y != nullptr) {
+        if (bnb_y != nullptr) {                  // (BN backward: the fp32 dA, as the epilogues)
           float yy[8];
           unpack8(*reinterpret_cast<const uint4*>(bnb_y + px * Cout + c8), yy);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float a = fmaf(yy[j], bsc[j], bsh[j]);
-            const float dyh = a > 0.f ? r[j] : 0.f;
+            const float dyh = a > 0.f ? v[j] : 0.f;
             s1[j] += dyh;
             s2[j] = fmaf(dyh, fmaf(yy[j], bis[j], bnm[j]), s2[j]);
           }

@@ -504,8 +504,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   // BNB epilogue (a data gradient dA; no bias): channel tiles outer, so the BN-backward
   // constants of one tile are read once; the scheduler barrier keeps the next tile's reads
   // from being hoisted (VGPR pressure)
-  auto epilogue_bnb = [&](int kk) {
-    const EpiCtx e = epi_ctx(wE, kk);
+  auto epilogue_bnb_f = [&](const EpiCtx& e, auto fullc) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(fullc)::value;
     uint2 pkv[MT][NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -513,7 +513,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
       const BnbC kb = bnb_load(s_bnb, BN, wn * (NT * 16) + nt * 16 + 4 * g);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const bool ok = pcol[mt] < e.wlim && prow[mt] < e.hlim && co < p.Cout;
+        const bool ok = FULL || (pcol[mt] < e.wlim && prow[mt] < e.hlim && co < p.Cout);
         const uint2 pk = make_uint2(pack2(acc[mt][nt][0], acc[mt][nt][1]), pack2(acc[mt][nt][2], acc[mt][nt][3]));
         pkv[mt][nt] = pk;
         if constexpr (!PAIRS) {
@@ -521,24 +521,31 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
           asm volatile("" : "+v"(o1));
           __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk.x, pk.y}, e.r1, o1, 0, 0);
         }
-        bnb_accum(pk, ybuf[mt][nt], ok, kb, s1[nt], s2[nt]);
+        const float d[4] = {ok ? acc[mt][nt][0] : 0.f, ok ? acc[mt][nt][1] : 0.f,
+                            ok ? acc[mt][nt][2] : 0.f, ok ? acc[mt][nt][3] : 0.f};
+        bnb_accum(d, ybuf[mt][nt], kb, s1[nt], s2[nt]);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (PAIRS) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const bool pv = pcol[mt] < e.wlim && prow[mt] < e.hlim;
+        const bool pv = FULL || (pcol[mt] < e.wlim && prow[mt] < e.hlim);
 #pragma unroll
         for (int np = 0; np < NT / 2; ++np) {
           const uint4 q = pair16(pkv[mt][2 * np], pkv[mt][2 * np + 1]);
           const int co = co0 + wn * (NT * 16) + np * 32 + pair16_ch(lane);
-          unsigned o1 = pv && co < p.Cout ? (unsigned)(e.b1 + orel1p[mt] + np * 32) * 2u : kOOB;
+          unsigned o1 = FULL || (pv && co < p.Cout) ? (unsigned)(e.b1 + orel1p[mt] + np * 32) * 2u : kOOB;
           asm volatile("" : "+v"(o1));
           __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, e.r1, o1, 0, 0);
         }
       }
     }
+  };
+  auto epilogue_bnb = [&](int kk) __attribute__((always_inline)) {
+    const EpiCtx e = epi_ctx(wE, kk);
+    if (e.full) epilogue_bnb_f(e, std::true_type{});
+    else epilogue_bnb_f(e, std::false_type{});
   };
 
   auto epilogue = [&](int kk) __attribute__((always_inline)) {

@@ -117,22 +117,23 @@ DDLPC_DEVICE BnbC bnb_load(const float* __restrict__ tab, int nb, int col) {
   k.nm = *reinterpret_cast<const float4*>(tab + 3 * nb + col);
   return k;
 }
-// (sum dyh, sum dyh*xhat) of those 4 channels of one pixel: pk = the stored bf16 dA, yv = y;
-// the arithmetic of bn_bwd2_kernel's reduction pass
-DDLPC_DEVICE void bnb_accum(uint2 pk, uint2 yv, bool ok, const BnbC& k, float (&s1)[4], float (&s2)[4]) {
-  const float d[4] = {ok ? lo_bf(pk.x) : 0.f, ok ? hi_bf(pk.x) : 0.f, ok ? lo_bf(pk.y) : 0.f,
-                      ok ? hi_bf(pk.y) : 0.f};
-  const float y[4] = {lo_bf(yv.x), hi_bf(yv.x), lo_bf(yv.y), hi_bf(yv.y)};
-  const float scf[4] = {k.sc.x, k.sc.y, k.sc.z, k.sc.w}, shf[4] = {k.sh.x, k.sh.y, k.sh.z, k.sh.w};
-  const float isf[4] = {k.is.x, k.is.y, k.is.z, k.is.w}, nmf[4] = {k.nm.x, k.nm.y, k.nm.z, k.nm.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float a = fmaf(y[i], scf[i], shf[i]);
-    const float dyh = a > 0.f ? d[i] : 0.f;
-    const float xh = fmaf(y[i], isf[i], nmf[i]);
-    s1[i] += dyh;
-    s2[i] = fmaf(dyh, xh, s2[i]);
-  }
+// (sum dyh, sum dyh*xhat) of those 4 channels of one pixel: d = the fp32 dA (before its bf16
+// store; masked lanes pass zeros), yv = y; the arithmetic of bn_bwd2_kernel's reduction pass
+// as packed fp32 pairs
+DDLPC_DEVICE void bnb_accum(const float (&d)[4], uint2 yv, const BnbC& k, float (&s1)[4], float (&s2)[4]) {
+  const f32x2_t y01 = {lo_bf(yv.x), hi_bf(yv.x)}, y23 = {lo_bf(yv.y), hi_bf(yv.y)};
+  const f32x2_t a01 = __builtin_elementwise_fma(y01, f32x2_t{k.sc.x, k.sc.y}, f32x2_t{k.sh.x, k.sh.y});
+  const f32x2_t a23 = __builtin_elementwise_fma(y23, f32x2_t{k.sc.z, k.sc.w}, f32x2_t{k.sh.z, k.sh.w});
+  const f32x2_t x01 = __builtin_elementwise_fma(y01, f32x2_t{k.is.x, k.is.y}, f32x2_t{k.nm.x, k.nm.y});
+  const f32x2_t x23 = __builtin_elementwise_fma(y23, f32x2_t{k.is.z, k.is.w}, f32x2_t{k.nm.z, k.nm.w});
+  const f32x2_t d01 = {a01.x > 0.f ? d[0] : 0.f, a01.y > 0.f ? d[1] : 0.f};
+  const f32x2_t d23 = {a23.x > 0.f ? d[2] : 0.f, a23.y > 0.f ? d[3] : 0.f};
+  f32x2_t p01 = {s1[0], s1[1]}, p23 = {s1[2], s1[3]}, q01 = {s2[0], s2[1]}, q23 = {s2[2], s2[3]};
+  p01 += d01; p23 += d23;
+  q01 = __builtin_elementwise_fma(d01, x01, q01);
+  q23 = __builtin_elementwise_fma(d23, x23, q23);
+  s1[0] = p01.x; s1[1] = p01.y; s1[2] = p23.x; s1[3] = p23.y;
+  s2[0] = q01.x; s2[1] = q01.y; s2[2] = q23.x; s2[3] = q23.y;
 }
 
 }  // namespace convlds
