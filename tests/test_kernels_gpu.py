@@ -186,19 +186,24 @@ def test_conv3_dgrad_bn_backward_epilogue(ops, N, H, W, Cin, Cout):
     da, _, part = ops.conv3_fwd(nhwc(dy), None, pk.dgrad, None, None, None, Cin, 0, False,
                                 None, None, nhwc(y), s4)
     assert torch.equal(da, da0)                       # the epilogue only adds the partials
+    # the partials reduce the kernel's fp32 dA (before its bf16 store): reference = the fp32
+    # data gradient of the same bf16 operands (only summation order differs)
     p = part.double().sum(0)
-    yf, df = nchw(nhwc(y)).double(), nchw(da).double()
+    yf = nchw(nhwc(y)).double()
+    df = F.conv_transpose2d(dy.float(), w.bfloat16().float(), padding=1).double()
     a = yf * scale.double()[None, :, None, None] + s4[3].double()[None, :, None, None]
     dyh = torch.where(a > 0, df, torch.zeros_like(df))
     xh = (yf - mean.double()[None, :, None, None]) * invstd.double()[None, :, None, None]
     ref1, ref2 = dyh.sum((0, 2, 3)), (dyh * xh).sum((0, 2, 3))
-    assert torch.allclose(p[0], ref1, rtol=1e-4, atol=1e-2 * math.sqrt(N * H * W))
-    assert torch.allclose(p[1], ref2, rtol=1e-4, atol=1e-2 * math.sqrt(N * H * W))
-    # the BN backward from those partials == the one with its own reduction pass
+    assert torch.allclose(p[0], ref1, rtol=1e-4, atol=1e-3 * math.sqrt(N * H * W))
+    assert torch.allclose(p[1], ref2, rtol=1e-4, atol=1e-3 * math.sqrt(N * H * W))
+    # the BN backward from those partials: dgamma / dbeta are the fp32 sums above; dY matches
+    # the path with its own reduction pass over the stored dA (which differs from the fp32
+    # sums by the bf16 rounding of dA, ~2^-9 relative)
     dY0, dg0, db0 = ops.bn_backward(da, None, nhwc(y), s4, gamma, None)
     dY1, dg1, db1 = ops.bn_backward(da, None, nhwc(y), s4, gamma, None, None, None, part)
     assert rel_err(dY1, dY0) < 2e-3
-    assert rel_err(dg1, dg0) < 1e-4 and rel_err(db1, db0) < 1e-4
+    assert rel_err(dg1, ref2.float()) < 1e-4 and rel_err(db1, ref1.float()) < 1e-4
 
 
 @pytest.mark.parametrize("C1,C2,Cout", [(64, 32, 32), (0, 64, 32), (256, 256, 256)])
