@@ -776,25 +776,17 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
 
   // ---- per-lane transposed-read geometry.  16-lane group g4 = lane >> 4: columns
   // (g4 & 1) * 16 + 4 * pq, pixel rows (g4 >> 1) * 8 + 4 * h + q within the 16-pixel k-step
-  // TS (128 output channels): the waves split (co half, tap group) instead of co quarters —
-  // wave (jh, tg) owns co tiles 2 jh, 2 jh + 1 x taps 4 tg .. 4 tg + 3, plus tap 8 of co tile
-  // 2 jh + tg.  Per k-step a wave reads 2 dY and 5 X fragments for 9 MFMAs (co quarters: 1 dY
-  // and 9 X, every X fragment read by all 4 waves): 30% fewer LDS reads.
-  constexpr bool TS = BCO == 128 && CIW == 1;
-  constexpr int NA = TS ? 2 : 1;                   // dY fragments (co tiles) per wave
-  const int jh = wave & 1, tgw = wave >> 1;
+  // (Rejected: on the 128-channel tiles, waves splitting (co half, tap group) instead of co
+  // quarters — 2 dY + 5 X fragment reads per 9 MFMAs instead of 1 + 9 — measured 14-23%
+  // slower per layer: profiles/r4/wgrad_ab_tapsplit_r4r.txt)
   const int g4 = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
-  int ya[NA][2], xb[2];
+  int ya[2], xb[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int row = (g4 >> 1) * 8 + 4 * h + q;     // + 16 * ks (row bits 0..3 unchanged)
-#pragma unroll
-    for (int a = 0; a < NA; ++a) {
-      const int jt = TS ? 2 * jh + a : wj;
-      const int byte = jt * 64 + (g4 & 1) * 32 + 8 * pq;
-      const int pc = (byte >> 4) ^ wg3_yswz<BCO>(row);
-      ya[a][h] = row * Cfg::Y_ROWB + (pc << 4) + (byte & 15);
-    }
+    const int byte = wj * 64 + (g4 & 1) * 32 + 8 * pq;
+    const int pc = (byte >> 4) ^ wg3_yswz<BCO>(row);
+    ya[h] = row * Cfg::Y_ROWB + (pc << 4) + (byte & 15);
     xb[h] = row * 64 + (g4 & 1) * 32 + 8 * pq;      // halo pixel row (+ 18 * ks + tap offset)
   }
   f32x16_t acc[9];
@@ -808,31 +800,15 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
 #pragma unroll
     for (int kk = 0; kk < KS16 / KW; ++kk) {
       const int ks = kk * KW + wk;
-      uint4 af[NA];
+      const uint2 alo = lds_read_tr16(Y + ks * 16 * Cfg::Y_ROWB + ya[0]);
+      const uint2 ahi = lds_read_tr16(Y + ks * 16 * Cfg::Y_ROWB + ya[1]);
+      const uint4 af = make_uint4(alo.x, alo.y, ahi.x, ahi.y);
 #pragma unroll
-      for (int a = 0; a < NA; ++a) {
-        const uint2 alo = lds_read_tr16(Y + ks * 16 * Cfg::Y_ROWB + ya[a][0]);
-        const uint2 ahi = lds_read_tr16(Y + ks * 16 * Cfg::Y_ROWB + ya[a][1]);
-        af[a] = make_uint4(alo.x, alo.y, ahi.x, ahi.y);
-      }
-      auto xfrag = [&](int tap) __attribute__((always_inline)) {
+      for (int tap = 0; tap < 9; ++tap) {
         const int toff = (ks * HW2 + (tap / 3) * HW2 + tap % 3) * 64;
         const uint2 lo = lds_read_tr16(X + toff + xb[0]);
         const uint2 hi = lds_read_tr16(X + toff + xb[1]);
-        return make_uint4(lo.x, lo.y, hi.x, hi.y);
-      };
-      if constexpr (TS) {
-        // acc[2 tt + a] = (tap 4 tg + tt, co tile 2 jh + a); acc[8] = (tap 8, co tile 2 jh + tg)
-#pragma unroll
-        for (int tt = 0; tt < 4; ++tt) {
-          const uint4 bf = xfrag(4 * tgw + tt);
-#pragma unroll
-          for (int a = 0; a < 2; ++a) acc[2 * tt + a] = mfma32x32x16(af[a], bf, acc[2 * tt + a]);
-        }
-        acc[8] = mfma32x32x16(tgw ? af[1] : af[0], xfrag(8), acc[8]);
-      } else {
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) acc[tap] = mfma32x32x16(af[0], xfrag(tap), acc[tap]);
+        acc[tap] = mfma32x32x16(af, make_uint4(lo.x, lo.y, hi.x, hi.y), acc[tap]);
       }
     }
   };
@@ -851,21 +827,6 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
   // group at a time), then the partial slab part[split][co][tap][ci]
   dma_wait<0>();
   lds_sync();
-  if constexpr (TS) {                              // KW = 1: every (tap, co tile) has one owner
-    float* outp = p.partial + (long long)split * p.Cout * p.taps * p.Cin;
-#pragma unroll
-    for (int x = 0; x < 9; ++x) {
-      const int tap = plane * 9 + (x < 8 ? 4 * tgw + x / 2 : 8);
-      const int jt = 2 * jh + (x < 8 ? x % 2 : tgw);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int co = co0 + jt * 32 + 8 * (i >> 2) + 4 * (lane >> 5) + (i & 3);
-        const int ci = ci0 + (lane & 31);
-        if (co < p.Cout && ci < p.Cin) outp[((long long)co * p.taps + tap) * p.Cin + ci] = acc[x][i];
-      }
-    }
-    return;
-  }
   float* red = reinterpret_cast<float*>(base);     // [KW-1][NJ * CIW][3 taps][16][64] floats
   const int wjc = wc * NJ + wj;                    // (chunk, co tile) of this wave
   float* out = p.partial + (long long)split * p.Cout * p.taps * p.Cin;
