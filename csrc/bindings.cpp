@@ -214,8 +214,7 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   {
     // high-resolution few-channel layers: resident-weight kernel (conv3x3_res.hip)
     int grid = 0, smem = 0;
-    // (the 96-channel resident variant computes no statistics)
-    const int variant = want_stats && a.Cout == 96 ? -1 : conv3_res_plan(a, num_cus(), grid, smem);
+    const int variant = conv3_res_plan(a, num_cus(), grid, smem);
     if (variant >= 0) {
       at::Tensor y1 = at::empty(shape_with_c(g, a.Co1), opts);
       at::Tensor y2;

@@ -70,8 +70,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   static_assert(NBUF == 2 || NBUF == 3, "halo ring depth");
   static_assert(!BNB || (!SPLIT && !TAP8), "BN-backward epilogue: single output, no image layer");
   constexpr int NW = C::NW, BN = C::BN;
-  // the 96-channel variant serves the data gradient of the first decoder conv only: no bias,
-  // no statistics (planner / launcher), which keeps it inside 256 VGPRs
+  // the 96-channel variant serves the data gradient of the first decoder conv only (planner:
+  // single input, no prologue, no bias): its statistics rows carry the column SUMS only (the
+  // up-conv's bias gradient; the sum^2 rows are written as zeros) — 24 VGPRs fewer, which
+  // keeps it inside 256
   constexpr bool NOSTAT = BN == 96;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bool has_pro = p.pscale != nullptr;
@@ -451,16 +453,17 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
           __builtin_amdgcn_raw_buffer_store_b64(d, e.r2, o2, 0, 0);
         }
       }
-      if constexpr (NOSTAT) continue;
       const f32x2_t z = {0.f, 0.f};
       const f32x2_t r01 = ok ? v01 : z, r23 = ok ? v23 : z;
       f32x2_t a01 = {s1[nt][0], s1[nt][1]}, a23 = {s1[nt][2], s1[nt][3]};
-      f32x2_t q01 = {s2[nt][0], s2[nt][1]}, q23 = {s2[nt][2], s2[nt][3]};
       a01 += r01; a23 += r23;
-      q01 = __builtin_elementwise_fma(r01, r01, q01);
-      q23 = __builtin_elementwise_fma(r23, r23, q23);
       s1[nt][0] = a01.x; s1[nt][1] = a01.y; s1[nt][2] = a23.x; s1[nt][3] = a23.y;
-      s2[nt][0] = q01.x; s2[nt][1] = q01.y; s2[nt][2] = q23.x; s2[nt][3] = q23.y;
+      if constexpr (!NOSTAT) {
+        f32x2_t q01 = {s2[nt][0], s2[nt][1]}, q23 = {s2[nt][2], s2[nt][3]};
+        q01 = __builtin_elementwise_fma(r01, r01, q01);
+        q23 = __builtin_elementwise_fma(r23, r23, q23);
+        s2[nt][0] = q01.x; s2[nt][1] = q01.y; s2[nt][2] = q23.x; s2[nt][3] = q23.y;
+      }
     }
     if constexpr (PAIRS) {
 #pragma unroll
@@ -669,7 +672,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   }
 
   // ---- one BN-statistics partial row per workgroup (layout of conv3_fwd_kernel)
-  if (!NOSTAT && p.stats != nullptr) {
+  if (p.stats != nullptr) {
     dma_wait<0>();
     lds_sync();
     float* red = reinterpret_cast<float*>(sA0);
@@ -776,8 +779,9 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
     if (d3) { cand[nc++] = 9; cand[nc++] = 8; }
     else if (depth == 2) { cand[nc++] = 3; } else { cand[nc++] = 4; cand[nc++] = 3; }
   } else if (bn == 96) {
-    // no BN-backward epilogue, bias or statistics at BN 96 (bindings: no statistics wanted)
-    if (a.bnb_y != nullptr || a.bias != nullptr) return -1;
+    // BN 96: the concat data gradient only — no BN-backward epilogue, single input, no
+    // prologue, no bias; its statistics rows hold the column sums only (sum^2 rows zero)
+    if (a.bnb_y != nullptr || a.bias != nullptr || a.C2 != 0 || pro || a.pscale2 != nullptr) return -1;
     cand[nc++] = 7;
   } else if (bn == 32) {
     if (depth == 2) { cand[nc++] = 0; cand[nc++] = 5; }

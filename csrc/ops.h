@@ -30,7 +30,10 @@ struct ConvFwdArgs {
   float* stats;                   // optional [grid][2][Cout] per-workgroup (sum, sum^2) of the fp32
                                   // outputs (before the bf16 store: the statistics an fp32
                                   // BatchNorm would see); rows of channels outside a
-                                  // workgroup's n tile are not written
+                                  // workgroup's n tile are not written.  (The resident
+                                  // 96-channel variant — the concat data gradient: one input,
+                                  // no prologue, no bias — writes sum^2 rows of zeros: its
+                                  // sums are the up-conv's bias gradient)
   int TD, TH, TW;
   int tilesD, tilesH, tilesW;
   int nTilesM, nTilesN;
