@@ -93,6 +93,89 @@ __global__ void bn_relu_apply_kernel(const bf16_t* __restrict__ y, const float* 
   }
 }
 
+// Apply + pool, v2 (bn_bwd2_kernel's mapping): unit = 2x2 (3-D: 2x2x2) window; lanes (kw, cg)
+// cover the window's top-row pixel pair contiguously (2 x C channels), each lane also handles
+// the pixels below it (kh) and, in 3-D, in the next slice (kd); the window maximum is
+// completed with the kw partner lane (lane ^ G), whose kw = 0 lane stores the pooled value.
+// 32-bit unit geometry (no 64-bit division per element) and UNROLL units' loads in flight
+// per thread.  Requires G = C/8 a power of two <= 32 and even D, H, W.
+template <int DIMS>
+__global__ __launch_bounds__(256) void bn_relu_pool2_kernel(
+    const bf16_t* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
+    bf16_t* __restrict__ out, bf16_t* __restrict__ pooled, int N, int H, int W, int C, long long sstride) {
+  constexpr int UNROLL = 2;
+  constexpr int NK = DIMS == 3 ? 4 : 2;            // pixels per lane per unit (k = 2*kd + kh)
+  const int G = C / 8;
+  {
+    const int grp = blockIdx.y;                    // per-micro-batch BN groups (N = slices per group)
+    const long long gel = (long long)N * H * W * C;
+    y += grp * gel;
+    if (out != nullptr) out += grp * gel;
+    pooled += grp * (gel / (DIMS == 3 ? 8 : 4));
+    scale += grp * sstride;
+    shift += grp * sstride;
+  }
+  const int L = 2 * G;
+  const int tid = threadIdx.x;
+  const int cg = tid % G, c8 = cg * 8, kw = (tid / G) & 1;
+  const int upb = 256 / L;
+  const int Wo = W / 2, Ho = H / 2;
+  const int units = (DIMS == 3 ? N / 2 : N) * Ho * Wo;   // N counts (n, d) slices
+  const int stride = gridDim.x * upb;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = scale[c8 + j]; sh[j] = shift[c8 + j]; }
+  for (int u0 = blockIdx.x * upb + tid / L; u0 < units; u0 += UNROLL * stride) {
+    uint4 v[UNROLL][NK];
+    long long off[UNROLL][NK];
+    bool ok[UNROLL];
+#pragma unroll
+    for (int r = 0; r < UNROLL; ++r) {             // all loads first (memory-level parallelism)
+      const int u = u0 + r * stride;
+      ok[r] = u < units;
+      const int uu = ok[r] ? u : u0;
+      const int rr = uu / Wo, wo = uu - rr * Wo;
+      long long pix0;
+      if (DIMS == 3) {
+        const int nd = rr / Ho, ho = rr - nd * Ho;
+        pix0 = ((long long)(2 * nd) * H + 2 * ho) * W + 2 * wo + kw;
+      } else {
+        pix0 = (long long)rr * 2 * W + 2 * wo + kw;
+      }
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        off[r][k] = (pix0 + (long long)(k >> 1) * H * W + (k & 1) * W) * C + c8;
+        v[r][k] = *reinterpret_cast<const uint4*>(y + off[r][k]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < UNROLL; ++r) {
+      float mx[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mx[j] = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        float f[8];
+        unpack8(v[r][k], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
+        const uint4 q = pack8(f);
+        if (out != nullptr && ok[r]) *reinterpret_cast<uint4*>(out + off[r][k]) = q;
+        float rq[8];
+        unpack8(q, rq);                            // pool the bf16-rounded activations
+#pragma unroll
+        for (int j = 0; j < 8; ++j) mx[j] = fmaxf(mx[j], rq[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mx[j] = fmaxf(mx[j], __shfl_xor(mx[j], G, 64));
+      if (ok[r] && kw == 0) {
+        const int u = u0 + r * stride;
+        *reinterpret_cast<uint4*>(pooled + (long long)u * C + c8) = pack8(mx);
+      }
+    }
+  }
+}
+
 // --------------------------------------------------------------------- backward passes
 // Per work item: 8 channels of one pixel (no pool) or of one pooling window (pool).
 // MODE 0: reduce (write per-block partial sums), MODE 1: apply (write dY).
@@ -433,6 +516,21 @@ void bn_relu_apply_launch(const bf16_t* y, const float* scale, const float* shif
   }
   const long long items = (long long)N * (dims == 3 ? D / 2 : 1) * (H / 2) * (W / 2) * G;
   const dim3 gr(std::min(grid_for(items, 256), cap), groups);
+  const long long units = (long long)N * (dims == 3 ? D / 2 : 1) * (H / 2) * (W / 2);
+  if ((G & (G - 1)) == 0 && G <= 32 && units < (1LL << 31)) {
+    // v2: lanes (kw, cg) over the window's pixel pair, UNROLL units per thread in flight
+    const int ND = N * (dims == 3 ? D : 1);
+    const long long per = (256 / (2 * G)) * 2;       // units per block per grid-stride pass
+    const dim3 g2((unsigned)std::max<long long>(1, std::min<long long>((units + per - 1) / per,
+                                                                     std::max(1, 8192 / groups))), groups);
+    if (dims == 2)
+      hipLaunchKernelGGL((bn_relu_pool2_kernel<2>), g2, dim3(256), 0, st, y, scale, shift, out, pooled,
+                         ND, H, W, C, sstride);
+    else
+      hipLaunchKernelGGL((bn_relu_pool2_kernel<3>), g2, dim3(256), 0, st, y, scale, shift, out, pooled,
+                         ND, H, W, C, sstride);
+    return;
+  }
   if (dims == 2)
     hipLaunchKernelGGL((bn_relu_apply_kernel<2, true>), gr, dim3(256), 0, st, y, scale,
                        shift, out, pooled, N, D, H, W, C, sstride);
