@@ -458,6 +458,7 @@ __global__ __launch_bounds__(256, 3) void head_fwd_stats_mdw_kernel(
   const long long stride = (long long)gridDim.x * PPB;
   long long base = (long long)blockIdx.x * PPB;
   long long px = base + tid / G;
+  // (rejected: a second pixel of prefetch spills at three workgroups per CU)
   uint4 a_nx = make_uint4(0, 0, 0, 0);
   int64_t l_nx = ignore_index;
   if (px < P) { a_nx = *reinterpret_cast<const uint4*>(a + px * C + c8); l_nx = labels[px]; }
@@ -579,7 +580,7 @@ __global__ __launch_bounds__(256) void head_bn_apply_kernel(
     int Kreal) {
   constexpr int G = C / 8;
   constexpr int PPB = 256 / G;
-  constexpr int U = 2;
+  constexpr int U = 4;                               // pixels per lane in flight
   __shared__ __attribute__((aligned(16))) float sW[K * C];
   const int tid = threadIdx.x, lane = tid & 63;
   const int cg = lane % G, c8 = cg * 8;
