@@ -670,6 +670,20 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
       pro8_load(p.pscale, p.pshift, p.pscale2, p.pshift2, p.C1, c8l, second[cw] ? p.Cin : p.C1, psc[cw], psh[cw]);
   }
 
+  // 32-channel tiles (one input chunk): the element offset of halo piece i relative to the
+  // tile's first pixel, pieces outside the halo / past the channels pushed beyond any tensor
+  // (>= 2^31 bytes: the DMA reads zeros) — an interior tile's DMAs need no per-piece test
+  // (wave-uniform path; its prologue takes the batched unmasked form, so x_pix is not
+  // refreshed).  enc1.b / dec1.a / dec1.b -6..-9%; the 64 / 128-channel tiles measured
+  // 1-5% slower with it: profiles/r4/wgrad_ab_fastdma_r5c.txt
+  constexpr bool FASTDMA = CIW == 1 && BCO == 32 && Cfg::X_ITERS <= 6;
+  int x_relC[FASTDMA ? Cfg::X_ITERS : 1];
+  if constexpr (FASTDMA) {
+#pragma unroll
+    for (int i = 0; i < Cfg::X_ITERS; ++i)
+      x_relC[i] = x_dw[i] > -2 && xch_ok[0] ? (x_dh[i] * p.W + x_dw[i]) * Cs[0] + cs0[0] : (1 << 30);
+  }
+  const bool co_full = co0 + BCO <= p.Cout;          // every dY piece's channels exist
   TileWalk tw;                                     // the issue stream's tile geometry
   tw.init(t_begin, p.tilesW, p.tilesH, p.D);
   bool x_int = false;
@@ -682,6 +696,23 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
     x_int = dok && h0 >= 1 && w0 >= 1 && h0 + TH < p.H && w0 + 16 < p.W;
     const auto ry = make_rsrc(p.dY + n * img_px * p.Cout, (unsigned)(img_px * p.Cout * 2));
     const int ybase = (h0 * p.W + w0) * p.Cout;
+    if (FASTDMA && x_int && co_full && xfull[0]) {
+      // interior tile, full channel tiles: no per-piece tests (x_pix is not needed: the
+      // prologue of such a tile takes its unmasked path)
+#pragma unroll
+      for (int i = 0; i < Cfg::Y_ITERS; ++i) {
+        if ((i * 4 + wave) >= Cfg::Y_INSTR) break;
+        dma16(ry, sY(buf) + (i * 4 + wave) * 1024, (unsigned)(ybase + y_rel[i]) * 2u);
+      }
+      const auto rx = make_rsrc(xsrc[0] + (n + dshift) * img_px * Cs[0], (unsigned)(img_px * Cs[0] * 2));
+      const int xbase = (h0 * p.W + w0) * Cs[0];
+#pragma unroll
+      for (int i = 0; i < Cfg::X_ITERS; ++i) {
+        if ((i * 4 + wave) >= Cfg::X_INSTR) break;
+        dma16(rx, sX(buf) + (i * 4 + wave) * 1024, (unsigned)(xbase + x_relC[i]) * 2u);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < Cfg::Y_ITERS; ++i) {
       if ((i * 4 + wave) >= Cfg::Y_INSTR) break;
