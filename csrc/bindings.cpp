@@ -77,7 +77,10 @@ int pick_bn(int Cout) {
 
 }  // namespace
 
-// ---- tuning knobs: DDLPC_<NAME> environment defaults, overridable in-process
+// ---- A/B switches for experiments in progress: knob(name, def) = an in-process override
+// (torch.ops.ddlpc.set_knob) or else the environment variable DDLPC_<NAME>, or else def.
+// No shipped kernel reads one (every measured default is compiled in); the mechanism stays
+// for same-process interleaved A/B runs (bench.py --ab, scripts/conv_micro.py --ab).
 namespace {
 std::mutex g_knob_mu;
 std::unordered_map<std::string, int>& knob_map() {
@@ -416,7 +419,7 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   // split-K over pixel tiles: enough blocks to fill the chip, but every block keeps >= 8
   // tiles so the fp32 partial slab stays small next to the MFMA work
   const int base = a.coTiles * a.ciChunks * a.planes;
-  // workgroups per CU to aim for (DDLPC_WGRAD_WG_PER_CU): the weight gradient runs
+  // workgroups per CU to aim for: the weight gradient runs
   // concurrently with the data-gradient chain, and its resident workgroups' LDS decides
   // what else fits on a CU (two: 1 / 3 / 4 measured -7 / -1.5 / -1.9%, profiles/bench_s2k_*.json)
   const int wg_per_cu = 2;

@@ -239,7 +239,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     const bool x2ch = cbase >= p.C1;                // X2 channels: prologue only if deferred
     if (x2ch ? !has_pro2 : !has_pro) return;
     const int climit = x2ch ? p.Cin : p.C1;
-    // batched form (DDLPC_CONV_XFORM=1; <= 6 pieces per lane — the 3-D halos' 11 would spill):
+    // batched form (<= 6 pieces per lane — larger 3-D halos would spill):
     // the lane's 8-channel group is the same in every piece, so its 16 constants are read
     // once; all piece reads issue before the math, and padding is re-zeroed by a select
     // instead of a branch around each piece

@@ -586,8 +586,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
     next_of(kp, cp, k1, c1);
     kp = k1; cp = c1;
   }
-  // wave priorities (DDLPC_CONV_PRIO, ConvFwdArgs::prio): bit 0 = s_setprio 1 once for the
-  // second-dispatched half of an 8-wave workgroup, bit 1 = around every MFMA cluster
+  // (wave priority: s_setprio 1 around every MFMA cluster, in compute below)
   int k = 0, c = 0;
   bool epi_prev = false;                              // stage s-1 ran an epilogue
   for (int s = 0; s < S; ++s) {

@@ -400,13 +400,12 @@ __global__ __launch_bounds__(512, KS == 1 ? 2 : 1) void gemm_nt_fwd2_kernel(Gemm
   }
 }
 
-// DDLPC_CONVT_FWD2: 0 = v1 kernel, 1 = v2 with one 32-channel chunk per stage (two
-// workgroups per CU), 2 = v2 with two chunks per stage (one workgroup per CU)
+// 1 = the v2 forward (one 32-channel chunk per stage, two workgroups per CU) where its shape
+// constraints hold, 0 = the v1 kernel
 int gemm_nt_fwd2_mode(const GemmArgs& a) {
-  const int v = 1;
-  const bool ok = a.mode == GEMM_CONVT_FWD && a.K % (v == 2 ? 64 : 32) == 0 && a.K <= 512 &&
-                  a.N % 128 == 0 && a.Cout % 32 == 0;
-  return ok ? v : 0;
+  const bool ok = a.mode == GEMM_CONVT_FWD && a.K % 32 == 0 && a.K <= 512 && a.N % 128 == 0 &&
+                  a.Cout % 32 == 0;
+  return ok ? 1 : 0;
 }
 
 // ---------------------------------------------------------------- TN (weight gradient)

@@ -727,8 +727,8 @@ void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
                                          ignore_index, bn4, bnpart, K));
 }
 
-// the fused forward + statistics pass on the matrix-core dWh kernel (C = 32; DDLPC_HEAD_MDW=0:
-// the register-accumulator kernel)
+// the fused forward + statistics pass on the matrix-core dWh kernel (C = 32; other shapes: the
+// register-accumulator kernel)
 // (K <= 6: the 8- and 16-class instantiations exceed the 168-VGPR budget of three
 // workgroups per CU and spill)
 bool head_mdw(int C, int K) { return C == 32 && K <= 6; }

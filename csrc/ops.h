@@ -289,9 +289,10 @@ void bn_running_apply_launch(float* rm, float* rv, const float* slots, int K, in
 void bn_running_apply_all_launch(const int64_t* entries, int L, int maxC, const float* arena, int K,
                                  long long stride, float momentum, hipStream_t st);
 
-// ---------------------------------------------------------------- tuning knobs (bindings.cpp)
-// knob("CONV_CFG5", 1): an in-process override (torch.ops.ddlpc.set_knob, for interleaved
-// same-process A/B runs) or else the environment variable DDLPC_CONV_CFG5, or else the default
+// ---------------------------------------------------------------- A/B switches (bindings.cpp)
+// knob("NAME", def): an in-process override (torch.ops.ddlpc.set_knob, for interleaved
+// same-process A/B runs) or else the environment variable DDLPC_NAME, or else def — for
+// experiments in progress only: no shipped kernel reads one
 int knob(const char* name, int def);
 
 // ---------------------------------------------------------------- comm proxy (reduce.hip)
