@@ -117,6 +117,26 @@ def test_conv3_fwd_prologue(ops):
     assert rel_err(nchw(y), ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W", [(4, 128, 128), (4, 136, 120)])
+def test_conv3_dgrad_96_channel_split_sums(ops, N, H, W):
+    """The first decoder conv's data gradient (dY 32 ch -> d[up | skip] = 64 + 32 ch) on the
+    resident 96-channel tile: both outputs vs fp32 torch, and its statistics rows = the
+    per-channel column sums (the up-conv's bias gradient) with zero sum^2 rows (ops.h
+    ConvFwdArgs::stats)."""
+    torch.manual_seed(23)
+    Cin, Cout, co1 = 32, 96, 64                 # the dgrad: 32 -> 96 channels
+    w = torch.randn(Cin, Cout, 3, 3, device=DEV) / math.sqrt(9 * Cout)   # the fwd conv 96 -> 32
+    pk = pack_conv(ops, w)
+    dy = torch.randn(N, Cin, H, W, device=DEV).bfloat16()
+    dx1, dx2, st = ops.conv3_fwd(nhwc(dy), None, pk.dgrad, None, None, None, Cout, co1, True)
+    ref = F.conv_transpose2d(dy.float(), w.bfloat16().float(), padding=1)
+    assert rel_err(nchw(dx1), ref[:, :co1]) < 1e-2
+    assert rel_err(nchw(dx2), ref[:, co1:]) < 1e-2
+    s = st.sum(0)
+    assert torch.allclose(s[0], ref.sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+    assert torch.count_nonzero(s[1]) == 0
+
+
 # shapes that take the resident-weight kernel (conv3x3_res.hip): high resolution, few
 # channels, enough 16x16 tiles to fill the chip
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout,pro", [
