@@ -264,20 +264,28 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
 // ---------------------------------------------------------------- NT forward v2
 // The transposed-conv forward GEMM (M = input pixels, N = S*Cout, K = Cin) restructured like
 // the 3x3 conv kernels: 8 waves on a 256-pixel x 128-column tile (4 x 2 waves of 64 x 64),
-// both operands by LDS-DMA (buffer_load ... lds) into double-buffered swizzled LDS, KS
+// both operands by LDS-DMA (buffer_load ... lds) into a 3-deep swizzled LDS ring, KS
 // 32-channel sub-chunks per stage behind ONE barrier (v1: register staging, two barriers
 // per 32 channels, LDS-staged scalar epilogue), the deferred BN + ReLU of x applied in LDS
 // by the lane that DMA'd each piece.  The MFMA computes D^T (weights as the A operand), so
 // every lane holds 4 consecutive output channels of one pixel; one v_permlane16_swap per
 // dword pairs two 16-column tiles into 8 channels and the result leaves as 16-byte stores
 // at the pixel-shuffled output position (+ bias), straight from the accumulators.
-// Requires Cin % 32 == 0, (S*Cout) % 128 == 0 and Cout % 32 == 0 (launcher-checked).
+// Persistent workgroups walk their tiles with the DMA pipeline running across tile
+// boundaries: a tile's epilogue stores drain under the next tile's first stages (the
+// one-tile-per-workgroup form spent half of the 32^2 -> 64^2 x 256-channel up-sampling in
+// its store tail: 165 us without stores, 347 us with them).
+// Requires Cin % 32 == 0, (S*Cout) % 128 == 0, Cout % 32 == 0 and Cout <= 512 (launcher-checked).
 template <int KS>
 struct Nt2Cfg {
   static constexpr int BM = 256, BN = 128;
   static constexpr int A_BYTES = KS * BM * 64, B_BYTES = KS * BN * 64;
   static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int SMEM = 2 * 512 * 4 + 2 * STAGE;           // BN constants | 2 stages
+  // ring depth: 3 at KS = 1 (76 KB: still two workgroups per CU), so the DMA of stage s + 2
+  // is in flight during two stages' MFMAs instead of one
+  static constexpr int NS = KS == 1 ? 3 : 2;
+  static constexpr int SS_BYTES = 2 * 512 * 4;                   // BN scale | shift
+  static constexpr int SMEM = SS_BYTES + NS * STAGE;             // 76 KB at KS = 1
   static constexpr int A_IT = KS * BM * 4 / 512;                 // DMA pieces per thread
   static constexpr int B_IT = KS * BN * 4 / 512;
 };
@@ -288,7 +296,7 @@ __global__ __launch_bounds__(512, KS == 1 ? 2 : 1) void gemm_nt_fwd2_kernel(Gemm
   constexpr int BM = C::BM, BN = C::BN;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* s_bn = reinterpret_cast<float*>(smem);                   // scale [512] | shift [512]
-  char* base = smem + 2 * 512 * 4;
+  char* base = smem + C::SS_BYTES;
   auto sA = [&](int b) { return base + b * C::STAGE; };
   auto sB = [&](int b) { return base + b * C::STAGE + C::A_BYTES; };
   const int tid = threadIdx.x, lane = tid & 63;
@@ -297,16 +305,41 @@ __global__ __launch_bounds__(512, KS == 1 ? 2 : 1) void gemm_nt_fwd2_kernel(Gemm
   const bool bn = p.bn4 != nullptr;
   if (bn)
     for (int i = tid; i < p.K; i += 512) { s_bn[i] = p.bn4[2 * p.K + i]; s_bn[512 + i] = p.bn4[3 * p.K + i]; }
+  // persistent, XCD-aware: workgroup b sits on XCD x = b % 8 (round-robin dispatch) in slot
+  // i = b / 8 of that XCD; the slot keeps ONE column tile n = i % nTilesN for the whole launch
+  // (bias and weight rows fixed) and walks the m tiles congruent to x mod 8 with stride
+  // 8 * R (R = slots per column tile).  So all nTilesN column tiles of an m tile run at the
+  // same time on one XCD and share its A rows in L2.  (Launcher: gridDim.x = 8 * R * nTilesN.)
   const int nTilesN = p.N / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (bid / nTilesN) * BM, n0 = (bid % nTilesN) * BN;
+  const int nTilesM = (p.M + BM - 1) / BM;
+  const int xcd = (int)blockIdx.x % 8, slot = (int)blockIdx.x / 8;
+  const int R = (int)gridDim.x / (8 * nTilesN);
+  const int n0 = (slot % nTilesN) * BN;
+  const int mfirst = (slot / nTilesN) * 8 + xcd, mstep = 8 * R;
+  const int my_tiles = nTilesM > mfirst ? (nTilesM - 1 - mfirst) / mstep + 1 : 0;
+  const int nk = p.K / (32 * KS);
+  const int S = my_tiles * nk;                                    // pipeline stages
+  auto m0_of = [&](int j) __attribute__((always_inline)) { return (mfirst + j * mstep) * BM; };
+  const auto rB = convlds::make_rsrc(p.B + (long long)n0 * p.K, (unsigned)((long long)BN * p.K * 2));
+  // bias of this lane's output columns, loaded once before any DMA is in flight (a load in the
+  // epilogue would make the compiler wait vmcnt(0) on the ring's DMAs)
+  float bias_r[2][8];
+#pragma unroll
+  for (int np = 0; np < 2; ++np) {
+    const int c0 = n0 + wn * 64 + np * 32, cob = c0 % p.Cout;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bias_r[np][i] = p.bias != nullptr ? p.bias[cob + 4 * (lane >> 4) + i] : 0.f;
+      bias_r[np][4 + i] = p.bias != nullptr ? p.bias[cob + 16 + 4 * (lane >> 4) + i] : 0.f;
+    }
+  }
   // per-lane DMA geometry: piece e = i * 512 + tid -> row e >> 2, source piece swizzled
   const int sub8 = ((lane & 3) ^ (((lane >> 4) & 1) << 1)) << 3;   // same for every i
-  const auto rA = convlds::make_rsrc(p.A + (long long)m0 * p.K,
-                                     (unsigned)((long long)(p.M - m0 < BM ? p.M - m0 : BM) * p.K * 2));
-  const auto rB = convlds::make_rsrc(p.B + (long long)n0 * p.K, (unsigned)((long long)BN * p.K * 2));
-  const int nk = p.K / (32 * KS);
-  auto issue = [&](int kc, int b) __attribute__((always_inline)) {
+  // issue stage (tile j, chunk kc): A rows past M read as zeros (resource clipped to M)
+  auto issue = [&](int j, int kc, int b) __attribute__((always_inline)) {
+    const int m0 = m0_of(j);
+    const auto rA = convlds::make_rsrc(p.A + (long long)m0 * p.K,
+                                       (unsigned)((long long)(p.M - m0 < BM ? p.M - m0 : BM) * p.K * 2));
 #pragma unroll
     for (int i = 0; i < C::A_IT; ++i) {
       const int e = i * 512 + tid, row = (e >> 2) % BM, sc = (e >> 2) / BM;
@@ -321,7 +354,7 @@ __global__ __launch_bounds__(512, KS == 1 ? 2 : 1) void gemm_nt_fwd2_kernel(Gemm
     }
   };
   // deferred BN + ReLU of x on this lane's landed A pieces (rows past M stay zero)
-  auto transform = [&](int kc, char* __restrict__ A) __attribute__((always_inline)) {
+  auto transform = [&](int m0, int kc, char* __restrict__ A) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < C::A_IT; ++i) {
       const int e = i * 512 + tid, row = (e >> 2) % BM, sc = (e >> 2) / BM;
@@ -364,48 +397,98 @@ __global__ __launch_bounds__(512, KS == 1 ? 2 : 1) void gemm_nt_fwd2_kernel(Gemm
         for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16x16x32(bf[nt], af[mt], acc[mt][nt]);
     }
   };
-  if (bn) __syncthreads();                                        // s_bn visible
-  issue(0, 0);
-  for (int kc = 0; kc < nk; ++kc) {
-    const int b = kc & 1;
-    convlds::dma_wait<0>();
-    if (bn) transform(kc, sA(b));
-    convlds::lds_sync();
-    if (kc + 1 < nk) issue(kc + 1, b ^ 1);
-    compute(sA(b), sB(b));
-  }
-  // ---- epilogue: lane holds columns n0 + wn*64 + nt*16 + 4g .. +3 of pixel wm*64 + mt*16 + (lane & 15)
-  bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C);
-#pragma unroll
-  for (int np = 0; np < 2; ++np) {
-    const int c0 = n0 + wn * 64 + np * 32;                        // 32 columns in one sub-position
-    const int sub = c0 / p.Cout, cob = c0 - sub * p.Cout;
-    float b0[4] = {0.f, 0.f, 0.f, 0.f}, b1[4] = {0.f, 0.f, 0.f, 0.f};
-    if (p.bias != nullptr)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { b0[i] = p.bias[cob + 4 * g + i]; b1[i] = p.bias[cob + 16 + 4 * g + i]; }
+  // ---- epilogue of tile (m0, n0): lane holds columns n0 + wn*64 + nt*16 + 4g .. +3 of pixel
+  // wm*64 + mt*16 + (lane & 15); paired into 16-B stores at the pixel-shuffled output position
+  // (+ bias).  Exactly EPI buffer stores per wave (rows past M: out-of-range offset), so the
+  // counted waits of the next tile's stages stay exact while they drain
+  constexpr int EPI = 8;                                          // 2 column pairs x 4 m tiles
+  auto epilogue = [&](int m0) __attribute__((always_inline)) {
+    const int m_last = min(m0 + BM, p.M) - 1;
+    const long long up_lo = up_pixel(m0, 0, p.dims, p.D, p.H, p.W);
+    const long long up_hi = up_pixel(m_last, p.dims == 2 ? 3 : 7, p.dims, p.D, p.H, p.W);
+    const auto rO = convlds::make_rsrc(reinterpret_cast<bf16_t*>(p.C) + up_lo * p.Cout,
+                                       (unsigned)((up_hi - up_lo + 1) * p.Cout * 2));
+    int upr[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const int m = m0 + wm * 64 + mt * 16 + (lane & 15);
-      const f32x4_t& a0 = acc[mt][2 * np];
-      const f32x4_t& a1 = acc[mt][2 * np + 1];
-      const uint2 lo = make_uint2(pack2(a0[0] + b0[0], a0[1] + b0[1]), pack2(a0[2] + b0[2], a0[3] + b0[3]));
-      const uint2 hi = make_uint2(pack2(a1[0] + b1[0], a1[1] + b1[1]), pack2(a1[2] + b1[2], a1[3] + b1[3]));
-      const uint4 q = convlds::pair16(lo, hi);
-      if (m < p.M) {
-        const int up = up_pixel(m, sub, p.dims, p.D, p.H, p.W);
-        *reinterpret_cast<uint4*>(Cp + (long long)up * p.Cout + cob + convlds::pair16_ch(lane)) = q;
+      upr[mt] = m < p.M ? (int)(up_pixel(m, 0, p.dims, p.D, p.H, p.W) - up_lo) : -1;
+    }
+#pragma unroll
+    for (int np = 0; np < 2; ++np) {
+      const int c0 = n0 + wn * 64 + np * 32;                      // 32 columns in one sub-position
+      const int sub = c0 / p.Cout, cob = c0 - sub * p.Cout;
+      const int soff = p.dims == 2 ? (sub >> 1) * 2 * p.W + (sub & 1)
+                                   : (sub >> 2) * 4 * p.H * p.W + ((sub >> 1) & 1) * 2 * p.W + (sub & 1);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const f32x4_t& a0 = acc[mt][2 * np];
+        const f32x4_t& a1 = acc[mt][2 * np + 1];
+        const float* bb = bias_r[np];
+        const uint2 lo = make_uint2(pack2(a0[0] + bb[0], a0[1] + bb[1]), pack2(a0[2] + bb[2], a0[3] + bb[3]));
+        const uint2 hi = make_uint2(pack2(a1[0] + bb[4], a1[1] + bb[5]), pack2(a1[2] + bb[6], a1[3] + bb[7]));
+        const uint4 q = convlds::pair16(lo, hi);
+        unsigned off = upr[mt] >= 0 ? (unsigned)(((upr[mt] + soff) * p.Cout + cob + convlds::pair16_ch(lane)) * 2)
+                                    : convlds::kOOB;
+        asm volatile("" : "+v"(off));                              // store count must not depend on data
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, rO, off, 0, 0);
       }
     }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  };
+  if (bn) __syncthreads();                                        // s_bn visible
+  constexpr int NS = C::NS, PER = C::A_IT + C::B_IT;             // DMAs per thread per stage
+  static_assert(NS == 3 || NS == 2, "ring depth");
+  // stage s = (tile j, chunk kc); the issue walker (ji, ki) runs NS - 1 stages ahead
+  int ji = 0, ki = 0;
+  auto advance = [&](int& j1, int& k1) __attribute__((always_inline)) { if (++k1 == nk) { k1 = 0; ++j1; } };
+  for (int s = 0; s < NS - 1 && s < S; ++s) { issue(ji, ki, s); advance(ji, ki); }
+  int b = 0, bi = NS - 1;                                         // ring slot of stage s / s + NS - 1
+  int j = 0, kc = 0, m0 = 0;
+  unsigned epi_hist = 0;                                          // bit t: an epilogue at stage s-1-t
+  for (int s = 0; s < S; ++s) {
+    if (kc == 0) m0 = m0_of(j);
+    // stage s landed; younger than its DMA: the DMAs of stages s+1 .. s+NS-2 and the epilogue
+    // stores of stages s-NS+1 .. s-1 (issued after DMA(s) within their stage)
+    const int dmas = min(S - 1 - s, NS - 2);
+    const int epis = __builtin_popcount(epi_hist & ((1u << (NS - 1)) - 1u));
+    convlds::vm_wait_dyn(dmas * PER + epis * EPI);
+    if (bn) transform(m0, kc, sA(b));
+    convlds::lds_sync();
+    if (s + NS - 1 < S) { issue(ji, ki, bi); advance(ji, ki); }
+    compute(sA(b), sB(b));
+    const bool epi = kc == nk - 1;
+    epi_hist = (epi_hist << 1) | (epi ? 1u : 0u);
+    if (epi) epilogue(m0);
+    b = b + 1 == NS ? 0 : b + 1;
+    bi = bi + 1 == NS ? 0 : bi + 1;
+    advance(j, kc);
   }
 }
 
-// 1 = the v2 forward (one 32-channel chunk per stage, two workgroups per CU) where its shape
-// constraints hold, 0 = the v1 kernel
+// 1 = the v2 forward (one 32-channel chunk per stage, two persistent workgroups per CU) where
+// its shape constraints hold, 0 = the v1 kernel
 int gemm_nt_fwd2_mode(const GemmArgs& a) {
   const bool ok = a.mode == GEMM_CONVT_FWD && a.K % 32 == 0 && a.K <= 512 && a.N % 128 == 0 &&
-                  a.Cout % 32 == 0;
+                  a.Cout % 32 == 0 && a.Cout <= 512;
   return ok ? 1 : 0;
+}
+
+// compute units of the current device (the persistent forward's grid)
+int device_cus() {
+  static int n[64] = {};
+  int d = 0;
+  (void)hipGetDevice(&d);
+  if (d < 0 || d >= 64) d = 0;
+  if (n[d] == 0) {
+    int v = 0;
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d);
+    n[d] = v > 0 ? v : 256;
+  }
+  return n[d];
 }
 
 // ---------------------------------------------------------------- TN (weight gradient)
@@ -1025,10 +1108,15 @@ void gemm_launch(GemmArgs& a, hipStream_t st) {
   // measured (B=64 U-Net shapes): the gathered data-gradient A operand gains from wide
   // steps; the forward (contiguous A, K = Cin) runs best at one chunk per step.  The forward
   // uses 128-wide N tiles when N allows (each A tile is read from L2 half as often)
-  if (const int v2 = gemm_nt_fwd2_mode(a)) {
-    const unsigned grid2 = (unsigned)(((a.M + 255) / 256) * (long long)(a.N / 128));
-    if (v2 == 2) hipLaunchKernelGGL((gemm_nt_fwd2_kernel<2>), dim3(grid2), dim3(512), Nt2Cfg<2>::SMEM, st, a);
-    else hipLaunchKernelGGL((gemm_nt_fwd2_kernel<1>), dim3(grid2), dim3(512), Nt2Cfg<1>::SMEM, st, a);
+  if (gemm_nt_fwd2_mode(a)) {
+    // persistent: 8 XCDs x R slots per column tile x nTilesN column tiles, about two
+    // workgroups per CU (76 KB of LDS each), R no larger than the m tiles need
+    const int ntn = a.N / 128;
+    const long long mt = (a.M + 255) / 256;
+    const long long rneed = (mt + 7) / 8;
+    const int R = (int)std::max<long long>(1, std::min<long long>(rneed, 2LL * device_cus() / (8 * ntn)));
+    const unsigned grid2 = (unsigned)(8 * R * ntn);
+    hipLaunchKernelGGL((gemm_nt_fwd2_kernel<1>), dim3(grid2), dim3(512), Nt2Cfg<1>::SMEM, st, a);
     return;
   }
   const int bn = gemm_nt_bn(a);

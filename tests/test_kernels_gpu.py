@@ -396,6 +396,25 @@ def test_convt(ops, N, H, W, Cin, Cout):
     assert rel_err(db, gb) < 1e-3
 
 
+@pytest.mark.parametrize("N,H,Cin,Cout", [(9, 60, 256, 256), (4, 36, 512, 128), (3, 52, 256, 512)])
+def test_convt_fwd_persistent_gemm(ops, N, H, Cin, Cout):
+    """The persistent XCD-aware forward GEMM (gemm_nt_fwd2_kernel: shapes the resident convT
+    kernel declines, Cin 256 / 512): several m tiles per workgroup, so epilogue stores drain
+    under the next tile's DMA stages; a partial last m tile; plain and deferred-BN input."""
+    torch.manual_seed(12)
+    x = torch.randn(N, Cin, H, H, device=DEV).bfloat16()
+    w = torch.randn(Cin, Cout, 2, 2, device=DEV) / math.sqrt(Cin)
+    b = torch.randn(Cout, device=DEV) * 0.1
+    pk = pack_conv(ops, w)
+    out = ops.convt_fwd(nhwc(x), pk.fwd, b, Cout)
+    ref = F.conv_transpose2d(x.float(), w.bfloat16().float(), b, stride=2)
+    assert rel_err(nchw(out), ref) < 1e-2
+    y = nhwc(x)
+    bn4 = _bn4(Cin, 2)
+    a = ops.bn_relu_apply(y, bn4, False)[0]
+    assert torch.equal(ops.convt_fwd(y, pk.fwd, b, Cout, bn4), ops.convt_fwd(a, pk.fwd, b, Cout))
+
+
 @pytest.mark.parametrize("C,K", [(32, 6), (64, 6), (16, 3), (8, 2), (64, 11), (32, 16), (8, 1),
                                  (64, 2)])
 def test_head_ce(ops, C, K):
