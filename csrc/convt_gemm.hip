@@ -469,6 +469,173 @@ __global__ __launch_bounds__(512, KS == 1 ? 2 : 1) void gemm_nt_fwd2_kernel(Gemm
   }
 }
 
+// ---------------------------------------------------------------- NT data gradient v2
+// dx[m][ci] = sum_(sub, co) dOut[up(m, sub)][co] Wd[ci][(sub, co)] (M = input pixels, N = Cin,
+// K = S*Cout) on the forward v2 geometry: 8 waves on a 256-pixel x 128-channel tile, both
+// operands LDS-DMA'd into a 3-deep swizzled ring, one 32-deep k chunk per stage behind one
+// barrier (v1: register staging, two barriers per 4 chunks).  The A operand is a gather: a
+// chunk lies inside one sub-position (Cout % 32 == 0), so a lane's piece address is its
+// row's up-sampled base pixel (computed once) plus a per-chunk uniform offset.  Epilogue:
+// 16-B stores from the accumulators (v_permlane16_swap pairs) and, with the deferred BN of x,
+// the BN-backward partials (sum dyh, sum dyh * xhat) of the stored dx against y, one
+// full-width row per workgroup (zeros outside its channel tile).
+struct Dg2Cfg {
+  static constexpr int BM = 256, BN = 128, NS = 3;
+  static constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, STAGE = A_BYTES + B_BYTES;
+  static constexpr int SMEM = NS * STAGE;                        // 72 KB: two workgroups per CU
+};
+
+__global__ __launch_bounds__(512, 2) void gemm_nt_dgrad2_kernel(GemmArgs p) {
+  using C = Dg2Cfg;
+  constexpr int BM = C::BM, BN = C::BN, NS = C::NS;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  auto sA = [&](int b) { return smem + b * C::STAGE; };
+  auto sB = [&](int b) { return smem + b * C::STAGE + C::A_BYTES; };
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4;
+  const int nTilesN = p.N / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / nTilesN) * BM, n0 = (bid % nTilesN) * BN;
+  const int sub8 = ((lane & 3) ^ (((lane >> 4) & 1) << 1)) << 3;   // same for every piece
+  // A: pieces e = i * 512 + tid -> tile row e >> 2; its up-sampled base pixel x Cout
+  int arow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + ((i * 512 + tid) >> 2);
+    arow[i] = m < p.M ? up_pixel(m, 0, p.dims, p.D, p.H, p.W) * p.Cout + sub8 : -1;
+  }
+  const long long a_bytes = (long long)p.M * p.K * 2;            // dOut (launcher: < 2^31)
+  const auto rA = convlds::make_rsrc(p.A, (unsigned)a_bytes);
+  const auto rB = convlds::make_rsrc(p.B + (long long)n0 * p.K, (unsigned)((long long)BN * p.K * 2));
+  const int W2 = 2 * p.W, HW4 = 4 * p.H * p.W;
+  const int nk = p.K / 32;
+  auto issue = [&](int kc, int b) __attribute__((always_inline)) {
+    const int kb = kc * 32, sub = kb / p.Cout;                    // uniform
+    const int so = (p.dims == 2 ? (sub >> 1) * W2 + (sub & 1)
+                                : (sub >> 2) * HW4 + ((sub >> 1) & 1) * W2 + (sub & 1)) * p.Cout +
+                   (kb - sub * p.Cout);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      convlds::dma16(rA, sA(b) + (i * 8 + wave) * 1024, arow[i] >= 0 ? (unsigned)((arow[i] + so) * 2) : convlds::kOOB);
+    convlds::dma16(rB, sB(b) + wave * 1024, (unsigned)(((tid >> 2) * p.K + kb + sub8) * 2));
+  };
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](const char* __restrict__ A, const char* __restrict__ B) __attribute__((always_inline)) {
+    uint4 af[4], bf[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) af[mt] = *reinterpret_cast<const uint4*>(A + lds_off(wm * 64 + mt * 16 + (lane & 15), g));
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) bf[nt] = *reinterpret_cast<const uint4*>(B + lds_off(wn * 64 + nt * 16 + (lane & 15), g));
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16x16x32(bf[nt], af[mt], acc[mt][nt]);
+  };
+  constexpr int PER = 3;                                          // DMAs per thread per stage
+  for (int j = 0; j < NS - 1 && j < nk; ++j) issue(j, j);
+  int b = 0, bi = NS - 1;
+  for (int kc = 0; kc < nk; ++kc) {
+    if (kc + 1 < nk) convlds::dma_wait<PER>();                    // stage kc landed, kc + 1 in flight
+    else convlds::dma_wait<0>();
+    convlds::lds_sync();
+    if (kc + NS - 1 < nk) issue(kc + NS - 1, bi);
+    compute(sA(b), sB(b));
+    b = b + 1 == NS ? 0 : b + 1;
+    bi = bi + 1 == NS ? 0 : bi + 1;
+  }
+  // ---- epilogue: lane holds channels n0 + wn*64 + nt*16 + 4g .. +3 of pixel
+  // m0 + wm*64 + mt*16 + (lane & 15); pairs of 16-column tiles -> 8 channels per lane
+  const bool bnst = p.bnpart != nullptr;
+  float* s_bn = reinterpret_cast<float*>(smem);                   // scale|shift|mean|invstd [4][BN]
+  if (bnst) {
+    __syncthreads();                                              // every wave is done with the ring
+    for (int i = tid; i < 4 * BN; i += 512) {
+      const int q = i / BN, c = n0 + i % BN;
+      s_bn[i] = p.bn4[(q == 0 ? 2 : q == 1 ? 3 : q == 2 ? 0 : 1) * p.N + c];
+    }
+    __syncthreads();
+  }
+  bf16_t* dx = reinterpret_cast<bf16_t*>(p.C);
+  const int cl = wn * 64 + convlds::pair16_ch(lane);              // + np * 32: tile-local channel
+  float* red = s_bn + 4 * BN;                                     // [wm][2][BN] partials
+  // column halves one after the other (16 live partial sums instead of 32: two workgroups
+  // per CU need <= 128 VGPRs)
+#pragma unroll
+  for (int np = 0; np < 2; ++np) {
+    float s1[8], s2[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { s1[q] = 0.f; s2[q] = 0.f; }
+    const int c = cl + np * 32;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int m = m0 + wm * 64 + mt * 16 + (lane & 15);
+      const f32x4_t& a0 = acc[mt][2 * np];
+      const f32x4_t& a1 = acc[mt][2 * np + 1];
+      const uint2 lo = make_uint2(pack2(a0[0], a0[1]), pack2(a0[2], a0[3]));
+      const uint2 hi = make_uint2(pack2(a1[0], a1[1]), pack2(a1[2], a1[3]));
+      const uint4 q = convlds::pair16(lo, hi);
+      if (m < p.M) {
+        const long long off = (long long)m * p.N + n0 + c;
+        *reinterpret_cast<uint4*>(dx + off) = q;
+        if (bnst) {                     // dyh = dx [y*scale+shift > 0], xhat = (y-mean)*invstd
+          float d8[8], y8[8];
+          unpack8(q, d8);
+          unpack8(*reinterpret_cast<const uint4*>(p.bny + off), y8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float dyh = fmaf(y8[j], s_bn[c + j], s_bn[BN + c + j]) > 0.f ? d8[j] : 0.f;
+            s1[j] += dyh;
+            s2[j] = fmaf(dyh, (y8[j] - s_bn[2 * BN + c + j]) * s_bn[3 * BN + c + j], s2[j]);
+          }
+        }
+      }
+    }
+    if (bnst) {
+      // lanes with equal bits 4, 5 hold the same channels: butterfly over the pixel bits
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int sh = 1; sh < 16; sh <<= 1) {
+          s1[j] += __shfl_xor(s1[j], sh);
+          s2[j] += __shfl_xor(s2[j], sh);
+        }
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          red[(wm * 2 + 0) * BN + c + j] = s1[j];
+          red[(wm * 2 + 1) * BN + c + j] = s2[j];
+        }
+      }
+    }
+  }
+  if (bnst) {
+    // the 4 m waves of a column half summed in a fixed order
+    __syncthreads();
+    float* row = p.bnpart + (long long)blockIdx.x * 2 * p.N;
+    for (int e = tid; e < 2 * p.N; e += 512) {
+      const int half = e / p.N, ch = e - half * p.N;
+      float t = 0.f;
+      if (ch >= n0 && ch < n0 + BN) {
+        const int c = ch - n0;
+        for (int w = 0; w < 4; ++w) t += red[(w * 2 + half) * BN + c];
+      }
+      row[e] = t;
+    }
+  }
+}
+
+// the v2 data gradient where its shape constraints hold (else gemm_nt_kernel)
+bool gemm_nt_dgrad2_ok(const GemmArgs& a) {
+  return a.mode == GEMM_CONVT_DGRAD && a.N % 128 == 0 && a.K % 32 == 0 && a.Cout % 32 == 0 &&
+         (long long)a.M * a.K * 2 < (1LL << 31) && (long long)a.M * a.N < (1LL << 31);
+}
+
 // 1 = the v2 forward (one 32-channel chunk per stage, two persistent workgroups per CU) where
 // its shape constraints hold, 0 = the v1 kernel
 int gemm_nt_fwd2_mode(const GemmArgs& a) {
@@ -1087,6 +1254,7 @@ int gemm_nt_bn(const GemmArgs& a) {
 
 // workgroups of the NT (forward / data-gradient) launch: one BN-partial row each
 long long gemm_nt_grid(const GemmArgs& a) {
+  if (gemm_nt_dgrad2_ok(a)) return ((a.M + Dg2Cfg::BM - 1) / Dg2Cfg::BM) * (long long)(a.N / Dg2Cfg::BN);
   const int bn = gemm_nt_bn(a);
   return ((a.M + 127) / 128) * (long long)((a.N + bn - 1) / bn);
 }
@@ -1117,6 +1285,10 @@ void gemm_launch(GemmArgs& a, hipStream_t st) {
     const int R = (int)std::max<long long>(1, std::min<long long>(rneed, 2LL * device_cus() / (8 * ntn)));
     const unsigned grid2 = (unsigned)(8 * R * ntn);
     hipLaunchKernelGGL((gemm_nt_fwd2_kernel<1>), dim3(grid2), dim3(512), Nt2Cfg<1>::SMEM, st, a);
+    return;
+  }
+  if (gemm_nt_dgrad2_ok(a)) {
+    hipLaunchKernelGGL(gemm_nt_dgrad2_kernel, dim3((unsigned)gemm_nt_grid(a)), dim3(512), Dg2Cfg::SMEM, st, a);
     return;
   }
   const int bn = gemm_nt_bn(a);
