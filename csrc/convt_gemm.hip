@@ -553,12 +553,25 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_dgrad2_kernel(GemmArgs p) {
   // m0 + wm*64 + mt*16 + (lane & 15); pairs of 16-column tiles -> 8 channels per lane
   const bool bnst = p.bnpart != nullptr;
   float* s_bn = reinterpret_cast<float*>(smem);                   // scale|shift|mean|invstd [4][BN]
+  // y tile [BM][BN] bf16 (64 KB) LDS-DMA'd into the idle ring in one burst (a load per
+  // (pixel tile, column pair) in the epilogue exposed its latency 8 times per wave); 16-B
+  // slot sp of row r holds channel piece sp ^ (r & 15): conflict-free row-strided reads
+  char* ys = smem + 8192;
   if (bnst) {
     __syncthreads();                                              // every wave is done with the ring
+    const auto rY = convlds::make_rsrc(p.bny, (unsigned)((long long)p.M * p.N * 2));
+#pragma unroll
+    for (int i = 0; i < BM * BN * 2 / 16 / 512; ++i) {
+      const int e = i * 512 + tid, r = e >> 4, pc = (e & 15) ^ (r & 15);
+      const int m = m0 + r;
+      convlds::dma16(rY, ys + (i * 8 + wave) * 1024,
+                     m < p.M ? (unsigned)(((long long)m * p.N + n0 + pc * 8) * 2) : convlds::kOOB);
+    }
     for (int i = tid; i < 4 * BN; i += 512) {
       const int q = i / BN, c = n0 + i % BN;
       s_bn[i] = p.bn4[(q == 0 ? 2 : q == 1 ? 3 : q == 2 ? 0 : 1) * p.N + c];
     }
+    convlds::dma_wait<0>();
     __syncthreads();
   }
   bf16_t* dx = reinterpret_cast<bf16_t*>(p.C);
@@ -586,7 +599,8 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_dgrad2_kernel(GemmArgs p) {
         if (bnst) {                     // dyh = dx [y*scale+shift > 0], xhat = (y-mean)*invstd
           float d8[8], y8[8];
           unpack8(q, d8);
-          unpack8(*reinterpret_cast<const uint4*>(p.bny + off), y8);
+          const int r = wm * 64 + mt * 16 + (lane & 15);
+          unpack8(*reinterpret_cast<const uint4*>(ys + r * 256 + (((c >> 3) ^ (r & 15)) << 4)), y8);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float dyh = fmaf(y8[j], s_bn[c + j], s_bn[BN + c + j]) > 0.f ? d8[j] : 0.f;
@@ -633,7 +647,7 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_dgrad2_kernel(GemmArgs p) {
 // the v2 data gradient where its shape constraints hold (else gemm_nt_kernel)
 bool gemm_nt_dgrad2_ok(const GemmArgs& a) {
   return a.mode == GEMM_CONVT_DGRAD && a.N % 128 == 0 && a.K % 32 == 0 && a.Cout % 32 == 0 &&
-         (long long)a.M * a.K * 2 < (1LL << 31) && (long long)a.M * a.N < (1LL << 31);
+         (long long)a.M * a.K * 2 < (1LL << 31) && (long long)a.M * a.N * 2 < (1LL << 31);
 }
 
 // 1 = the v2 forward (one 32-channel chunk per stage, two persistent workgroups per CU) where
