@@ -893,6 +893,19 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_wgrad2_kernel(GemmArgs p) {
       b_sub[i] = n < p.N ? n / p.Cout : -1;
       b_col[i] = n < p.N ? n % p.Cout : 0;
     }
+    // 2-D: each B piece's up-sampled pixel walked by carries (the stages are issued in k
+    // order, KT pixels apart): (w, 4qW + 2w) of its input pixel plus the sub-position offset,
+    // no integer division per piece and stage
+    int b_w[Cf::NB], b_base[Cf::NB], b_so[Cf::NB];
+    const int W = p.W, dq = KT / W, dw = KT % W, dbase = 4 * W * dq + 2 * dw;
+#pragma unroll
+    for (int i = 0; i < Cf::NB; ++i) {
+      const long long px0 = k_begin + b_row[i];
+      const int qq = (int)(px0 / W);
+      b_w[i] = (int)(px0 - (long long)qq * W);
+      b_base[i] = 4 * qq * W + 2 * b_w[i];
+      b_so[i] = b_sub[i] >= 0 ? (b_sub[i] >> 1) * 2 * W + (b_sub[i] & 1) : 0;
+    }
     auto issue = [&](long long k0, int buf) {
 #pragma unroll
       for (int i = 0; i < Cf::NA; ++i) {
@@ -905,7 +918,15 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_wgrad2_kernel(GemmArgs p) {
       for (int i = 0; i < Cf::NB; ++i) {
         const long long px = k0 + b_row[i];
         const bool ok = px < k_end && b_sub[i] >= 0;
-        const long long up = ok ? up_pixel((int)px, b_sub[i], p.dims, p.D, p.H, p.W) : b_lo;
+        long long up;
+        if (p.dims == 2) {
+          up = ok ? (long long)(b_base[i] + b_so[i]) : b_lo;
+          b_w[i] += dw;
+          b_base[i] += dbase;
+          if (b_w[i] >= W) { b_w[i] -= W; b_base[i] += 2 * W; }
+        } else {
+          up = ok ? up_pixel((int)px, b_sub[i], p.dims, p.D, p.H, p.W) : b_lo;
+        }
         dma16(rb, sB(buf) + (i * 4 + wave) * 1024,
               ok ? (unsigned)(((up - b_lo) * p.Cout + b_col[i]) * 2) : kOOB);
       }
