@@ -75,10 +75,17 @@ __global__ __launch_bounds__(256, 2) void convt_res_kernel(GemmArgs p, int M, in
   const int wm = wave >> 1, wn = wave & 1;
   const int g = lane >> 4;
   const int nTilesN = p.N / TBN;
-  const int n0 = (int)blockIdx.x % nTilesN * TBN;
   const int nTilesM = (M + TBM - 1) / TBM;
+  // XCD-aware (launcher: gridDim.x = 8 R nTilesN): workgroup b sits on XCD b % 8 in slot
+  // b / 8, keeps column tile slot % nTilesN and walks the m tiles congruent to its XCD, so
+  // the nTilesN workgroups of an m tile share its pixel rows in that XCD's L2 (blocks of one
+  // m tile on different XCDs read them from HBM once per column tile: up2 forward -6..-11%;
+  // with two column tiles (up1) measured +1%, so from four on).  Other grids: b % nTilesN.
+  const bool xcd_map = nTilesN >= 4 && (int)gridDim.x % (8 * nTilesN) == 0;
+  const int slot = xcd_map ? (int)blockIdx.x / 8 : (int)blockIdx.x;
+  const int n0 = slot % nTilesN * TBN;
   const int mstride = (int)gridDim.x / nTilesN;
-  const int mfirst = (int)blockIdx.x / nTilesN;
+  const int mfirst = xcd_map ? (slot / nTilesN) * 8 + (int)blockIdx.x % 8 : (int)blockIdx.x / nTilesN;
   const int my_items = mfirst < nTilesM ? (nTilesM - 1 - mfirst) / mstride + 1 : 0;
   const int S = my_items * nch;
 
@@ -157,8 +164,14 @@ __global__ __launch_bounds__(256, 2) void convt_res_kernel(GemmArgs p, int M, in
       float f[8];
       unpack8(*q, f);
       const int c8 = c * BK + x_sp8[i] + o;
+      // (the 16 constants as four 16-B LDS reads, not 16 scalar ones)
+      const float4* vs = reinterpret_cast<const float4*>(s_bn + c8);
+      const float4* vh = reinterpret_cast<const float4*>(s_bn + K + c8);
+      const float4 s0 = vs[0], s1 = vs[1], h0 = vh[0], h1 = vh[1];
+      const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], s_bn[c8 + j], s_bn[K + c8 + j]), 0.f);
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
       *q = pack8(f);
     }
   };
@@ -376,6 +389,9 @@ int launch_grid(const ResPlan& r, const GemmArgs& a, int M, int num_cus) {
   const int nTilesN = a.N / r.tbn;
   const int nTilesM = (M + TBM - 1) / TBM;
   const int cap = std::max(1, r.per_cu * num_cus / nTilesN) * nTilesN;
+  // XCD-aware grid (the kernel's mapping): 8 XCDs x R slots x nTilesN column tiles
+  const int unit = 8 * nTilesN;
+  if (nTilesN >= 4 && cap >= unit) return std::min(cap / unit, (nTilesM + 7) / 8) * unit;
   return std::min(cap, nTilesM * nTilesN);
 }
 
