@@ -139,6 +139,13 @@ DDLPC_DEVICE int xcd_remap(int bid, int nblocks) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / kX;
 }
 
+// m / d (m >= 0) for a wave-uniform divisor: a shift when d is a power of two (the usual
+// U-Net widths), the integer division otherwise
+DDLPC_DEVICE int udiv_pow2(int m, int d) {
+  if ((d & (d - 1)) == 0) return m >> __builtin_ctz((unsigned)d);
+  return m / d;
+}
+
 // An offset the compiler cannot prove loop-invariant (an SGPR through an empty asm): LDS
 // tables indexed with it are re-read where used instead of being hoisted into live VGPRs.
 DDLPC_DEVICE int opaque_zero() {

@@ -32,12 +32,12 @@ DDLPC_DEVICE int lds_off(int row, int chunk) { return row * 64 + (swz(row, chunk
 // (pixel counts < 2^31): with q = m / W (= n*H + h for 2-D), the 2x up-sampled pixel is
 // (2q + i) * 2W + 2w + j — one integer division for 2-D, two for 3-D
 DDLPC_DEVICE int up_pixel(int m, int sub, int dims, int D, int H, int W) {
-  const int q = m / W, w = m - q * W;
+  const int q = udiv_pow2(m, W), w = m - q * W;
   if (dims == 2) {
     const int i = sub >> 1, j = sub & 1;
     return (2 * q + i) * (2 * W) + 2 * w + j;
   }
-  const int q2 = q / H, h = q - q2 * H;           // q2 = n*D + d
+  const int q2 = udiv_pow2(q, H), h = q - q2 * H; // q2 = n*D + d
   const int kd = sub >> 2, i = (sub >> 1) & 1, j = sub & 1;
   (void)D;
   return ((2 * q2 + kd) * (2 * H) + 2 * h + i) * (2 * W) + 2 * w + j;

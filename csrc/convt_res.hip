@@ -44,9 +44,9 @@ DDLPC_DEVICE void vmw() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"
 
 // up(m, 0): the up-sampled pixel of sub-position 0 of low-res pixel m (image-group relative)
 DDLPC_DEVICE int up0_of(int m, int dims, int H, int W) {
-  const int q = m / W, w = m - q * W;
+  const int q = udiv_pow2(m, W), w = m - q * W;
   if (dims == 2) return 4 * q * W + 2 * w;
-  const int q2 = q / H, h = q - q2 * H;
+  const int q2 = udiv_pow2(q, H), h = q - q2 * H;
   return (4 * q2 * H + 2 * h) * (2 * W) + 2 * w;
 }
 DDLPC_DEVICE int sub_off(int sub, int dims, int H, int W) {
