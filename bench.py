@@ -24,7 +24,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import socket
 import subprocess
 import sys
 import time
@@ -49,7 +48,11 @@ def _parse():
     ap.add_argument("--dims", type=int, default=2, help="2 = images, 3 = volumes (3-D U-Net)")
     ap.add_argument("--impl", default=os.environ.get("DDLPC_IMPL", "hip"),
                     choices=["hip", "torch"])
-    ap.add_argument("--bucket-mb", type=float, default=8.0)
+    ap.add_argument("--bucket-mb", type=float, default=8.0,
+                    help="largest gradient bucket (fp32 MB)")
+    ap.add_argument("--bucket-plan", default="readiness", choices=["readiness", "size"],
+                    help="readiness: cuts from the backward readiness model "
+                         "(parallel/bucket_plan.py); size: cut by size only")
     ap.add_argument("--bucket-sweep", default="",
                     help="comma list of bucket sizes (MB) timed after the main run (N>1), "
                          "e.g. 2,4,8,16,35; reported as config.bucket_sweep")
@@ -78,8 +81,10 @@ def _parse():
                          "latency during backward)")
     ap.add_argument("--ab", default="",
                     help="diagnostic: KNOB:v0,v1 — after the main timing, alternate a kernel "
-                         "knob (torch.ops.ddlpc.set_knob; CU_RESERVE = set_cu_reserve) over "
-                         "--ab-rounds timed blocks in this process; reported as config.ab")
+                         "knob over --ab-rounds timed blocks in this process; reported as "
+                         "config.ab.  CU_RESERVE = set_cu_reserve; any other name must be a "
+                         "knob a kernel reads (csrc/bindings.cpp kKnobs), else set_knob "
+                         "raises before anything is timed")
     ap.add_argument("--ab-rounds", type=int, default=4)
     ap.add_argument("--heartbeat", type=float, default=0.0,
                     help="seconds between 'alive' lines on stderr (long first-step autotuning)")
@@ -89,23 +94,16 @@ def _parse():
     return a
 
 
-def _free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def _launch_guard(args) -> None:
     """Enforce the one-rank-per-GPU contract BEFORE any GPU call."""
     ws = os.environ.get("WORLD_SIZE")
     if ws is None:
         if args.gpus > 1:
             # not under torchrun: become the launcher (a child process, never an exec)
+            # (c10d rendezvous on port 0: the agent's store binds its own port, no race)
             cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                   f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
-                   f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+                   f"--nproc-per-node={args.gpus}", "--rdzv-backend=c10d",
+                   "--rdzv-endpoint=127.0.0.1:0", os.path.abspath(__file__)] + sys.argv[1:]
             print(f"bench: spawning {args.gpus} ranks via torchrun", file=sys.stderr, flush=True)
             sys.exit(subprocess.call(cmd))
         return
@@ -125,9 +123,8 @@ def _baseline(args):
     if args.accum != 1 or args.classes != 6 or args.depth != 5:
         return None
     if args.dims == 3:
-        if args.tile == 128 and args.width_divisor == 2:
-            v = b.get("d3_128_images_per_sec", {}).get(str(args.batch))
-            return float(v) if v else None
+        # no meaningful 3-D anchor: the only stock run (0.59 vol/s) needed MIOpen's FAST find
+        # mode because the exhaustive search did not finish (BASELINE.json d3_128_note)
         return None
     if args.tile != 256:
         return None
@@ -167,7 +164,8 @@ def main():
                                         width_divisor=args.width_divisor, dims=args.dims),
                       tile=args.tile, batch_per_gpu=args.batch, accum_steps=args.accum,
                       num_samples=1 << 30, test_holdout=0, impl=args.impl,
-                      bucket_mb=args.bucket_mb, wire_dtype=args.wire_dtype,
+                      bucket_mb=args.bucket_mb, bucket_plan=args.bucket_plan,
+                      wire_dtype=args.wire_dtype,
                       grad_codec=args.codec, log_dir=None, hip_graph=bool(args.hip_graph),
                       recompute=int(args.recompute), reserve_cus=args.reserve_cus,
                       comm_proxy=args.comm_proxy, micro_streams=args.micro_streams)
@@ -294,6 +292,31 @@ def main():
     if tr.reducer is not None and tr.reducer.proxy:
         proxy = [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in d.items()}
                  for d in tr.reducer.proxy_times()]
+    # self-validation of a multi-rank run (after the timed steps, untimed): the backend and
+    # world the collectives really ran on, and bit-identical replicas (every rank applied the
+    # same reduced gradient); a diverged run still prints its line but exits non-zero
+    dist_rec = {"dist_backend": None, "world_size": 1, "rccl_version": None,
+                "replicas_identical": None}
+    diverged = False
+    if world > 1:
+        from ddlpc.parallel import assert_replicas_identical
+        dist_rec["dist_backend"] = str(dist.get_backend())
+        dist_rec["world_size"] = dist.get_world_size()
+        if dist_rec["dist_backend"] == "nccl":
+            try:
+                v = torch.cuda.nccl.version()
+                dist_rec["rccl_version"] = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+            except Exception as e:  # noqa: BLE001
+                dist_rec["rccl_version"] = f"unknown ({type(e).__name__})"
+        try:
+            assert_replicas_identical(tr.model)
+            dist_rec["replicas_identical"] = True
+        except RuntimeError as e:
+            dist_rec["replicas_identical"] = False
+            diverged = True
+            print(f"bench: {e}", file=sys.stderr, flush=True)
+        if dist_rec["world_size"] != args.gpus:
+            diverged = True
     base = _baseline(args)
     from ddlpc.utils.flops import PEAK_BF16_TFLOPS, unet_train_flops_per_sample
     flop_img = unet_train_flops_per_sample(cfg.model, args.tile)
@@ -327,6 +350,9 @@ def main():
             "gflop_per_sample": round(flop_img / 1e9, 2),
             "dtype": "bf16" if dev == "cuda" else "fp32",
             "data": data_desc,
+            **dist_rec,
+            "comm_wait_ms": (round(phases["comm_wait_ms"], 3) if "comm_wait_ms" in phases
+                             else None),
             "config": {"model": f"UNet depth{args.depth} width/{args.width_divisor} "
                                 f"conv_transpose ({sum(p.numel() for p in tr.model.parameters())} params)",
                        "global_batch": B * args.accum * world,
@@ -361,6 +387,12 @@ def main():
                                                         if sched else None),
                        "bucket_mb": args.bucket_mb,
                        "buckets": len(red.buckets) if red is not None else 0,
+                       "bucket_plan": cfg.bucket_plan,
+                       "bucket_sizes_mb": ([round((b.end - b.start) * 4 / 2**20, 3)
+                                            for b in red.buckets] if red is not None else None),
+                       "bucket_plan_predicted_exposed_ms": (
+                           round(tr.bucket_plan.exposed_ms, 3)
+                           if getattr(tr, "bucket_plan", None) is not None else None),
                        "wire_dtype": args.wire_dtype, "grad_codec": args.codec,
                        "phase_ms": {k: round(v, 3) for k, v in phases.items()},
                        "comm_wait_ms": (round(phases["comm_wait_ms"], 3)
@@ -377,6 +409,8 @@ def main():
     tr.close()
     if world > 1:
         dist.destroy_process_group()
+    if diverged:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

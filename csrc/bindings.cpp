@@ -79,9 +79,16 @@ int pick_bn(int Cout) {
 
 // ---- A/B switches for experiments in progress: knob(name, def) = an in-process override
 // (torch.ops.ddlpc.set_knob) or else the environment variable DDLPC_<NAME>, or else def.
-// No shipped kernel reads one (every measured default is compiled in); the mechanism stays
-// for same-process interleaved A/B runs (bench.py --ab, scripts/conv_micro.py --ab).
+// Every name a kernel reads is listed in kKnobs; set_knob rejects any other name, so an A/B
+// (bench.py --ab, scripts/conv_micro.py --ab) can never silently time two identical
+// configurations.  An empty list = no experiment in progress.
 namespace {
+const char* const kKnobs[] = {""};
+bool knob_registered(const std::string& name) {
+  for (const char* k : kKnobs)
+    if (k[0] != 0 && name == k) return true;
+  return false;
+}
 std::mutex g_knob_mu;
 std::unordered_map<std::string, int>& knob_map() {
   static std::unordered_map<std::string, int> m;
@@ -90,6 +97,7 @@ std::unordered_map<std::string, int>& knob_map() {
 }  // namespace
 
 int knob(const char* name, int def) {
+  TORCH_CHECK(knob_registered(name), "knob '", name, "' read but not listed in kKnobs");
   std::lock_guard<std::mutex> lk(g_knob_mu);
   auto& m = knob_map();
   auto it = m.find(name);
@@ -105,6 +113,8 @@ namespace {
 
 // in-process knob override -> the previous value (INT64_MIN: never read or set)
 int64_t set_knob(const std::string& name, int64_t value) {
+  TORCH_CHECK(knob_registered(name), "set_knob: no kernel reads a knob named '", name,
+              "' (registered knobs are listed in kKnobs, csrc/bindings.cpp)");
   std::lock_guard<std::mutex> lk(g_knob_mu);
   auto& m = knob_map();
   auto it = m.find(name);
@@ -708,7 +718,7 @@ std::vector<at::Tensor> bn_group_backward(const c10::optional<at::Tensor>& dA,
   TORCH_CHECK(groups >= 1 && groups <= 1024 && g.N % groups == 0 && stats4.numel() == groups * 4 * C,
               "bn_group_backward: stats4 [groups][4][C], 1 <= groups <= 1024 dividing the batch");
   TORCH_CHECK(bn_group_supported(g.dims, hasP, g.D, g.H, g.W, C),
-              "bn_group_backward: C / 8 a power of two (<= 32 with pool), even dims with pool");
+              "bn_group_backward: C / 8 a power of two <= 256, even dims with pool");
   const int Ng = g.N / (int)groups;
   const long long items = (long long)Ng * (hasP ? (g.dims == 3 ? g.D / 2 : 1) * (g.H / 2) * (g.W / 2)
                                                 : (long long)g.D * g.H * g.W);

@@ -305,8 +305,11 @@ __global__ void bn_bwd_kernel(const bf16_t* __restrict__ dA, const bf16_t* __res
 //            3-D, in the next slice (kd); the window arg-max is completed with the kw
 //            partner lane (lane ^ G) — first maximum wins in PyTorch's (kd, kh, kw) scan
 //            order.
-// Requires G = C/8 a power of two (pool: G <= 32) and even D, H, W for pool.
-template <int DIMS, bool POOL, int MODE>
+//   pool, KWIN (G > 32: the kw partner would sit in another wave): unit = window, lanes (cg)
+//            cover one pixel's channels and each lane handles both kw pixels of its rows
+//            itself (no cross-lane exchange).
+// Requires G = C/8 a power of two <= 256 and even D, H, W for pool.
+template <int DIMS, bool POOL, int MODE, bool KWIN = false>
 __global__ __launch_bounds__(256) void bn_bwd2_kernel(
     const bf16_t* __restrict__ dA, const bf16_t* __restrict__ dP, const bf16_t* __restrict__ y,
     const float* __restrict__ scale, const float* __restrict__ shift,
@@ -314,7 +317,7 @@ __global__ __launch_bounds__(256) void bn_bwd2_kernel(
     const float* __restrict__ coefs, const float* __restrict__ gscale,
     float* __restrict__ partial, bf16_t* __restrict__ dY, int N, int H, int W, int C,
     long long sstride) {
-  constexpr int UNROLL = 2;
+  constexpr int UNROLL = (POOL && KWIN && DIMS == 3) ? 1 : 2;
   const int G = C / 8;
   // per-micro-batch BatchNorm groups (bn_group_backward): blockIdx.y = group of N slices,
   // its statistics rows sstride floats apart, its coefficients [3][C] and partial rows
@@ -331,10 +334,10 @@ __global__ __launch_bounds__(256) void bn_bwd2_kernel(
     if (MODE == 1) coefs += grp * 3LL * C;
     if (MODE == 0) partial += (long long)grp * gridDim.x * 2 * C;
   }
-  const int L = POOL ? 2 * G : G;                 // lanes per unit (divides 256)
+  const int L = (POOL && !KWIN) ? 2 * G : G;     // lanes per unit (divides 256)
   const int tid = threadIdx.x;
   const int cg = tid % G, c8 = cg * 8;
-  const int kw = POOL ? (tid / G) & 1 : 0;
+  const int kw = (POOL && !KWIN) ? (tid / G) & 1 : 0;
   const int upb = 256 / L;                        // units per block per step
   const int Wo = W / 2, Ho = H / 2;
   // N counts (n, d) slices; a 3-D pooled unit row covers slices 2*nd and 2*nd + 1
@@ -349,7 +352,8 @@ __global__ __launch_bounds__(256) void bn_bwd2_kernel(
     if (MODE == 1) { k1[j] = coefs[c8 + j]; m1[j] = coefs[C + c8 + j]; m2[j] = coefs[2 * C + c8 + j]; }
     s1[j] = 0.f; s2[j] = 0.f;
   }
-  constexpr int NK = POOL ? (DIMS == 3 ? 4 : 2) : 1;  // pixels per lane per unit (k = 2*kd + kh)
+  // pixels per lane per unit: k = 2*kd + kh, KWIN: k = 2 * (2*kd + kh) + kw
+  constexpr int NK = POOL ? (DIMS == 3 ? 4 : 2) * (KWIN ? 2 : 1) : 1;
   for (int u0 = blockIdx.x * upb + tid / L; u0 < units; u0 += UNROLL * stride) {
     uint4 vy[UNROLL][NK], vd[UNROLL][NK], vp[UNROLL];
     long long off[UNROLL][NK];
@@ -369,8 +373,10 @@ __global__ __launch_bounds__(256) void bn_bwd2_kernel(
           pix0 = (long long)rr * 2 * W + 2 * wo + kw;
         }
 #pragma unroll
-        for (int k = 0; k < NK; ++k)
-          off[r][k] = (pix0 + (long long)(k >> 1) * H * W + (k & 1) * W) * C + c8;
+        for (int k = 0; k < NK; ++k) {
+          const int kk = KWIN ? k >> 1 : k;       // 2*kd + kh
+          off[r][k] = (pix0 + (long long)(kk >> 1) * H * W + (kk & 1) * W + (KWIN ? (k & 1) : 0)) * C + c8;
+        }
         vp[r] = *reinterpret_cast<const uint4*>(dP + (long long)uu * C + c8);
       } else {
         off[r][0] = (long long)uu * C + c8;
@@ -404,12 +410,18 @@ __global__ __launch_bounds__(256) void bn_bwd2_kernel(
           // window values in scan order w = 2*k + kw (k = 2*kd + kh)
           int best = 0;
           float bv = 0.f;
+          if (KWIN) {                             // my pixel k IS scan position k
 #pragma unroll
-          for (int k = 0; k < NK; ++k) {
-            const float pk = __shfl_xor(a[k][j], G, 64);
-            const float v0 = kw ? pk : a[k][j], v1 = kw ? a[k][j] : pk;
-            if (k == 0 || v0 > bv) { bv = v0; best = 2 * k; }
-            if (v1 > bv) { bv = v1; best = 2 * k + 1; }
+            for (int k = 0; k < NK; ++k)
+              if (k == 0 || a[k][j] > bv) { bv = a[k][j]; best = k; }
+          } else {
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+              const float pk = __shfl_xor(a[k][j], G, 64);
+              const float v0 = kw ? pk : a[k][j], v1 = kw ? a[k][j] : pk;
+              if (k == 0 || v0 > bv) { bv = v0; best = 2 * k; }
+              if (v1 > bv) { bv = v1; best = 2 * k + 1; }
+            }
           }
           bestk[j] = best;                        // routed to (k, kw) = (best >> 1, best & 1)
         }
@@ -422,7 +434,7 @@ __global__ __launch_bounds__(256) void bn_bwd2_kernel(
         for (int j = 0; j < 8; ++j) {
           const float a = fmaf(fy[k][j], sc[j], sh[j]);
           float dt = fd[k][j];
-          if (POOL && bestk[j] == 2 * k + kw) dt += fp[j];
+          if (POOL && bestk[j] == (KWIN ? k : 2 * k + kw)) dt += fp[j];
           const float dyh = a > 0.f ? dt * gs : 0.f;
           const float xh = fmaf(fy[k][j], is[j], nm[j]);
           if (MODE == 0) { s1[j] += dyh; s2[j] = fmaf(dyh, xh, s2[j]); }
@@ -472,7 +484,7 @@ namespace {
 bool bn_bwd2_ok(int dims, bool pool, int D, int H, int W, int C) {
   const int G = C / 8;
   if (C % 8 != 0 || (G & (G - 1)) != 0 || G > 256) return false;
-  if (pool && (G > 32 || H % 2 != 0 || W % 2 != 0 || (dims == 3 && D % 2 != 0))) return false;
+  if (pool && (H % 2 != 0 || W % 2 != 0 || (dims == 3 && D % 2 != 0))) return false;
   return true;
 }
 
@@ -485,6 +497,15 @@ void bn_bwd2_launch(int grid, int dims, bool pool, const bf16_t* dA, const bf16_
   // (groups > 1: N = images per group, the groups' tensors follow each other)
   const int ND = N * (dims == 3 ? D : 1);
   const dim3 gr(grid, groups);
+  if (pool && C / 8 > 32) {                        // window kw pair inside the lane
+    if (dims == 3)
+      hipLaunchKernelGGL((bn_bwd2_kernel<3, true, MODE, true>), gr, dim3(256), 0, st, dA, dP, y,
+                         scale, shift, mean, invstd, coefs, gscale, partial, dY, ND, H, W, C, sstride);
+    else
+      hipLaunchKernelGGL((bn_bwd2_kernel<2, true, MODE, true>), gr, dim3(256), 0, st, dA, dP, y,
+                         scale, shift, mean, invstd, coefs, gscale, partial, dY, ND, H, W, C, sstride);
+    return;
+  }
   if (dims == 3 && pool)
     hipLaunchKernelGGL((bn_bwd2_kernel<3, true, MODE>), gr, dim3(256), 0, st, dA, dP, y,
                        scale, shift, mean, invstd, coefs, gscale, partial, dY, ND, H, W, C, sstride);
@@ -584,7 +605,7 @@ void bn_bwd_apply_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y, co
                                                 : (long long)D * H * W);
   const int per = std::max(1, 256 / G);
   if (bn_bwd2_ok(dims, pool, D, H, W, C)) {
-    const int upb = 256 / (pool ? 2 * G : G);
+    const int upb = 256 / ((pool && G <= 32) ? 2 * G : G);
     const int grid2 = (int)std::max<long long>(1, std::min<long long>((items + 2 * upb - 1) / (2 * upb), 8192));
     bn_bwd2_launch<1>(grid2, dims, pool, dA, dP, y, scale, shift, mean, invstd, coefs, gscale,
                       partial, dY, N, D, H, W, C, st);
@@ -766,7 +787,7 @@ void bn_group_backward_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* 
                      groups, C, count, gamma, stats4, dgamma, dbeta, coefs, accumulate ? 1 : 0);
   const long long items = (long long)N * (pool ? (dims == 3 ? D / 2 : 1) * (H / 2) * (W / 2)
                                                 : (long long)D * H * W);
-  const int upb = 256 / (pool ? 2 * (C / 8) : C / 8);
+  const int upb = 256 / ((pool && C / 8 <= 32) ? 2 * (C / 8) : C / 8);
   const int grid2 = (int)std::max<long long>(
       1, std::min<long long>((items + 2 * upb - 1) / (2 * upb), std::max(1, 8192 / groups)));
   bn_bwd2_launch<1>(grid2, dims, pool, dA, dP, y, s + 2 * C, s + 3 * C, s, s + C, coefs, nullptr,

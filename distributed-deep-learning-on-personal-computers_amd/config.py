@@ -79,7 +79,9 @@ class TrainConfig:
     seed: int = 0
     # ---- data parallel -----------------------------------------------------------
     backend: Optional[str] = None        # None = nccl(RCCL) on GPU, gloo on CPU
-    bucket_mb: float = 8.0
+    bucket_mb: float = 8.0               # largest bucket (fp32 gradient MB)
+    bucket_plan: str = "readiness"       # readiness: cuts placed by the backward readiness
+                                         # model (parallel/bucket_plan.py) | size: size only
     reduce: str = "mean"                 # mean | sum | reference (the W=2 "sum" parity mode)
     grad_codec: str = "none"             # none | fp16_absmax | int8_absmax (ref.py:25)
     codec_scale: str = "bucket"          # global (reference parity) | bucket | tensor
@@ -138,6 +140,7 @@ class TrainConfig:
                                    ("codec_scale", self.codec_scale, CODEC_SCALES),
                                    ("reduce", self.reduce, REDUCE_OPS),
                                    ("wire_dtype", self.wire_dtype, ("fp32", "bf16")),
+                                   ("bucket_plan", self.bucket_plan, ("readiness", "size")),
                                    ("data", self.data, DATA_KINDS),
                                    ("impl", self.impl, ("auto", "hip", "torch")),
                                    ("dtype", self.dtype, ("bf16", "fp32"))):

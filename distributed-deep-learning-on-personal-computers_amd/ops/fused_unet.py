@@ -588,6 +588,20 @@ def check_supported(model: nn.Module):
                          " (use impl='torch' for this configuration)")
 
 
+def bn_groups_supported(model: nn.Module, tile: int) -> bool:
+    """Whether every BatchNorm of a ``models.UNet`` fits the per-micro-batch group kernels
+    (``csrc/bn.hip`` bn_group_supported): C a multiple of 8 with C / 8 a power of two
+    <= 256, and even spatial extents at the pooled (encoder) BatchNorms."""
+    def ok(c: int) -> bool:
+        g = c // 8
+        return c % 8 == 0 and 0 < g <= 256 and (g & (g - 1)) == 0
+    bns = [m for m in model.modules() if isinstance(m, (nn.BatchNorm2d, nn.BatchNorm3d))]
+    if not all(ok(b.num_features) for b in bns):
+        return False
+    return all((tile >> lvl) >= 2 and (tile >> lvl) % 2 == 0
+               for lvl in range(len(list(model.down_blocks()))))
+
+
 class _SideSegment:
     """``with`` body runs on the engine's side stream; on exit an event marks the segment's
     end for the lag bound (``UNetEngine.wgrad_stream``)."""
@@ -917,6 +931,9 @@ class UNetEngine:
             ok = (w >> lvl) >= 16 and c_up % 32 == 0 and c_up + c_skip <= 512
             out.append(bool(ok))
         return out
+
+    def bn_groups_supported(self, tile: int) -> bool:
+        return bn_groups_supported(self.model, tile)
 
     def _head_params(self):
         w = self.head.weight

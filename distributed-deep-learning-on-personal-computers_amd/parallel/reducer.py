@@ -62,7 +62,7 @@ class GradBucketReducer:
     def __init__(self, flat: FlatParams, group=None, bucket_mb: float = 8.0,
                  reduce: str = "mean", grad_codec: str = "none", codec_scale: str = "bucket",
                  overlap: bool = True, use_hooks: bool = True, wire_dtype: str = "fp32",
-                 proxy: int = 0):
+                 proxy: int = 0, cuts: Optional[List[int]] = None):
         if wire_dtype not in ("fp32", "bf16"):
             raise ValueError(f"wire_dtype={wire_dtype!r}")
         self.flat = flat
@@ -96,6 +96,9 @@ class GradBucketReducer:
             self.weight = C.reference_weights(self.world)[self.rank]
         else:
             raise ValueError(reduce)
+        # cuts: bucket boundaries as indices into flat.order (``parallel.bucket_plan``, the
+        # readiness-aware plan); None = cut by size only
+        self.cuts = list(cuts) if cuts is not None else None
         self.buckets = self._make_buckets(bucket_mb)
         self._bucket_of: Dict[int, _Bucket] = {}
         for b in self.buckets:
@@ -120,6 +123,16 @@ class GradBucketReducer:
 
     # ------------------------------------------------------------------ setup
     def _make_buckets(self, bucket_mb: float) -> List[_Bucket]:
+        order = self.flat.order
+        if self.cuts is not None:
+            c = self.cuts
+            if c[0] != 0 or c[-1] != len(order) or any(b <= a for a, b in zip(c[:-1], c[1:])):
+                raise ValueError(f"bucket cuts {c} do not partition {len(order)} parameters")
+            out = []
+            for a, b in zip(c[:-1], c[1:]):
+                ps = order[a:b]
+                out.append(_Bucket(len(out), self.flat.span(ps[0])[0], self.flat.span(ps[-1])[1], ps))
+            return out
         cap = max(1, int(bucket_mb * (1 << 20) // 4))
         buckets, cur, start = [], [], None
         end = 0
@@ -233,10 +246,16 @@ class GradBucketReducer:
                 continue
             ready, start, end = b.ev
             end.synchronize()
-            out.append({"bucket": b.idx, "mb": round((b.end - b.start) * 4 / 2**20, 2),
-                        "ready_to_start_ms": ready.elapsed_time(start),
-                        "ready_to_end_ms": ready.elapsed_time(end),
-                        "kernel_ms": start.elapsed_time(end)})
+            rec = {"bucket": b.idx, "mb": round((b.end - b.start) * 4 / 2**20, 2),
+                   "ready_to_start_ms": ready.elapsed_time(start),
+                   "ready_to_end_ms": ready.elapsed_time(end),
+                   "kernel_ms": start.elapsed_time(end)}
+            bwd = getattr(self, "_bwd_end", None)
+            if bwd is not None:
+                bwd.synchronize()
+                # > 0: the bucket's collective ended after backward (exposed)
+                rec["end_after_backward_ms"] = bwd.elapsed_time(end)
+            out.append(rec)
         return out
 
     def _launch_bf16(self, b: _Bucket, g: torch.Tensor):
@@ -273,6 +292,11 @@ class GradBucketReducer:
         """Complete all reductions (launch stragglers); compute stream waits, host does not."""
         if self.world == 1:
             return
+        if self.proxy:
+            # backward's end on the compute stream (proxy_times: bucket end vs backward end)
+            if getattr(self, "_bwd_end", None) is None:
+                self._bwd_end = torch.cuda.Event(enable_timing=True)
+            self._bwd_end.record(torch.cuda.current_stream(self.flat.grad_buf.device))
         if self.codec != "none" and self.codec_scale == "global":
             self._finish_global_codec()
             self._sync = False

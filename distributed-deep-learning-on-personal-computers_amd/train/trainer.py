@@ -154,11 +154,21 @@ class Trainer:
 
     def _make_reducer(self, bucket_mb: float) -> GradBucketReducer:
         c = self.cfg
+        cuts = None
+        self.bucket_plan = None
+        if c.bucket_plan == "readiness":
+            from ..parallel.bucket_plan import plan_for_model
+            world = self.world if self.world > 1 else max(2, c.comm_proxy)
+            self.bucket_plan = plan_for_model(
+                self.model, self.flat.order, c.model, c.tile, c.batch_per_gpu, world,
+                self.info.backend if self.world > 1 else "nccl", bucket_mb,
+                wire_bytes=2 if c.wire_dtype == "bf16" else 4)
+            cuts = self.bucket_plan.cuts
         return GradBucketReducer(self.flat, bucket_mb=bucket_mb, reduce=c.reduce,
                                  grad_codec=c.grad_codec, codec_scale=c.codec_scale,
                                  overlap=c.overlap_comm, use_hooks=(self.impl != "hip"),
                                  wire_dtype=c.wire_dtype,
-                                 proxy=c.comm_proxy if self.world == 1 else 0)
+                                 proxy=c.comm_proxy if self.world == 1 else 0, cuts=cuts)
 
     def set_bucket_mb(self, bucket_mb: float) -> int:
         """Re-bucket the gradient reducer between steps (bucket-size sweeps, SURVEY.md §5.8);
@@ -531,25 +541,69 @@ class Trainer:
     # ------------------------------------------------------------------ batched BN-group windows
     WINDOW_PIXELS = 64 * 512 * 512          # auto window: up to 64 512^2 images per pass
 
+    # activation bytes per sample of a grouped pass, per summed conv / BN output element:
+    # bf16 y1, a1, y2, a2 are saved (2 B per element of the yardstick) plus ~50% for the
+    # backward's transient gradients
+    WINDOW_BYTES_PER_ELEM = 3.0
+
     def _window_size(self, n_micro: int) -> int:
         """Micro-batches per batched pass (0: off).  cfg.bn_window: 0 off, k >= 2 up to k,
         -1 auto = as many as fit WINDOW_PIXELS when micro-batches are small and accumulated
-        (the reference's regime: batch 1, 50 micro-batches, ref.py:685-687)."""
+        (the reference's regime: batch 1, 50 micro-batches, ref.py:685-687).
+
+        Auto also requires: every BatchNorm shape supported by the grouped kernels
+        (``UNetEngine.bn_groups_supported``), no activation recompute (the grouped pass
+        saves y1, a1, y2 per block regardless), and a window whose activations fit in half
+        of the memory available to the allocator (measured once per window length)."""
         c = self.cfg
         if (n_micro < 2 or self.impl != "hip" or self.device.type != "cuda"
                 or c.bn_window in (0, 1)):
             return 0
-        if c.bn_window > 1:
-            return min(c.bn_window, n_micro)
-        px = c.batch_per_gpu * c.tile ** c.model.dims
-        if px > self.SMALL_MICRO_PIXELS:
+        key = (n_micro, c.bn_window, c.batch_per_gpu, c.tile, c.recompute)
+        cache = self.__dict__.setdefault("_window_cache", {})
+        if key in cache:
+            return cache[key]
+        from ..ops.fused_unet import bn_groups_supported
+        if not bn_groups_supported(self.model, c.tile):
+            if c.bn_window > 1:
+                raise ValueError("bn_window: the grouped BatchNorm kernels do not support this "
+                                 "U-Net geometry (bn_window=0 runs the micro-batches one by one)")
+            cache[key] = 0
             return 0
-        return min(n_micro, max(2, self.WINDOW_PIXELS // px))
+        if c.bn_window > 1:
+            cache[key] = min(c.bn_window, n_micro)
+            return cache[key]
+        px = c.batch_per_gpu * c.tile ** c.model.dims
+        if px > self.SMALL_MICRO_PIXELS or c.recompute > 0:
+            cache[key] = 0
+            return 0
+        from ..utils.flops import unet_activation_elems_per_sample
+        per_micro = (self.WINDOW_BYTES_PER_ELEM * c.batch_per_gpu *
+                     unet_activation_elems_per_sample(c.model, c.tile))
+        avail = self._allocator_bytes_available()
+        fit = n_micro if avail == float("inf") else int(0.5 * avail // max(per_micro, 1.0))
+        w = min(n_micro, self.WINDOW_PIXELS // px, fit)
+        cache[key] = w if w >= 2 else 0
+        return cache[key]
+
+    def _allocator_bytes_available(self) -> float:
+        """Device memory the caching allocator can still hand out (free + cached unused)."""
+        if not torch.cuda.is_available():
+            return float("inf")
+        free, _total = torch.cuda.mem_get_info(self.device)
+        return float(free + torch.cuda.memory_reserved(self.device) -
+                     torch.cuda.memory_allocated(self.device))
 
     @staticmethod
     def _cat_window(mbs: List[Tuple[torch.Tensor, torch.Tensor]]):
-        """The window's micro-batches as one batch (engine-layout inputs stay in that layout)."""
+        """The window's micro-batches as one batch (engine-layout inputs stay in that layout).
+        The micro-batches must have equal shapes: each is one BatchNorm group of batch / G
+        samples, and the window's mean loss x G is the sum of the micro-batch losses only
+        when every micro-batch has the same pixel count."""
         from ..data.datasets import engine_input
+        shapes = {(tuple(x.shape), tuple(y.shape)) for x, y in mbs}
+        if len(shapes) != 1:
+            raise ValueError(f"batched BN window: micro-batches of unequal shapes {sorted(shapes)}")
         xps = [getattr(x, "_ddlpc_nhwc", None) for x, _ in mbs]
         if all(xp is not None for xp in xps):
             x = engine_input(torch.cat(xps), mbs[0][0].shape[1])
@@ -583,6 +637,8 @@ class Trainer:
 
     def _train_step(self, micro_batches: List[Tuple[torch.Tensor, torch.Tensor]]):
         W = self._window_size(len(micro_batches))
+        if W and len({tuple(x.shape) for x, _ in micro_batches}) != 1:
+            W = 0                        # unequal micro-batches (a short last one): one by one
         if W == 0 and self._graph_ok(len(micro_batches)):
             return self._graph_step(micro_batches)
         self.model.train()

@@ -58,3 +58,39 @@ def unet_train_flops_per_sample(model_cfg, tile: int) -> float:
                                model_cfg.up_sample_mode, model_cfg.dims, probe)
     scale = (tile / probe) ** model_cfg.dims
     return 3.0 * 2.0 * macs * scale
+
+
+@functools.lru_cache(maxsize=None)
+def _activation_elems_probe(in_channels: int, out_classes: int, width_divisor: int, depth: int,
+                            up_sample_mode: str, dims: int, probe: int) -> int:
+    from ..config import ModelConfig
+    from ..models.unet import UNet
+    cfg = ModelConfig(in_channels=in_channels, out_classes=out_classes,
+                      width_divisor=width_divisor, depth=depth,
+                      up_sample_mode=up_sample_mode, dims=dims)
+    with torch.device("meta"):
+        model = UNet.from_config(cfg)
+    total = [0]
+    kinds = (nn.Conv2d, nn.Conv3d, nn.ConvTranspose2d, nn.ConvTranspose3d,
+             nn.BatchNorm2d, nn.BatchNorm3d)
+
+    def hook(mod, inp, out):
+        total[0] += out.numel()
+
+    hs = [m.register_forward_hook(hook) for m in model.modules() if isinstance(m, kinds)]
+    with torch.no_grad():
+        model(torch.empty((1, in_channels) + (probe,) * dims, device="meta"))
+    for h in hs:
+        h.remove()
+    return total[0]
+
+
+def unet_activation_elems_per_sample(model_cfg, tile: int) -> float:
+    """Summed conv / transposed-conv / BatchNorm output elements of ONE sample at edge
+    ``tile`` (every saved pre-BN and post-BN activation of a training step; SURVEY.md §2.5:
+    ~228 M at 512² for width divisor 2) — the per-sample activation-memory yardstick."""
+    probe = 2 ** model_cfg.depth * 2
+    n = _activation_elems_probe(model_cfg.in_channels, model_cfg.out_classes,
+                                model_cfg.width_divisor, model_cfg.depth,
+                                model_cfg.up_sample_mode, model_cfg.dims, probe)
+    return n * (tile / probe) ** model_cfg.dims

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import time
 from typing import Dict, List, Optional
 
 import torch
@@ -54,41 +55,48 @@ class PhaseTimer:
     ``mark(name)`` records an event; the elapsed time between consecutive marks is that
     phase.  ``end_step()`` keeps the step's events; ``read()`` (call at log points, after
     something already synchronised) returns the mean ms per phase over the kept steps.
+    On a CPU device (gloo rehearsal: every op and collective is synchronous on the host)
+    the marks are host clock readings instead.
     """
 
     def __init__(self, device: torch.device, keep: int = 64):
-        self.on = torch.device(device).type == "cuda"
+        self.cuda = torch.device(device).type == "cuda"
+        self.on = True
         self.keep = keep
         self._cur: List = []
         self._done: List[List] = []
 
     def mark(self, name: str):
-        if not self.on:
-            return
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+        else:
+            e = time.perf_counter()
         self._cur.append((name, e))
 
     def end_step(self):
-        if not self.on or not self._cur:
+        if not self._cur:
             return
         self._done.append(self._cur)
         self._cur = []
         if len(self._done) > self.keep:
             self._done.pop(0)
 
+    def _elapsed(self, a, b) -> float:
+        return a.elapsed_time(b) if self.cuda else (b - a) * 1e3
+
     def read(self, reset: bool = True) -> Dict[str, float]:
-        if not self.on or not self._done:
+        if not self._done:
             return {}
         tot: Dict[str, float] = {}
         n = 0
         for marks in self._done:
-            if not marks[-1][1].query():
+            if self.cuda and not marks[-1][1].query():
                 continue
             n += 1
             for (_, a), (name, b) in zip(marks[:-1], marks[1:]):
-                tot[name] = tot.get(name, 0.0) + a.elapsed_time(b)
-            tot["step"] = tot.get("step", 0.0) + marks[0][1].elapsed_time(marks[-1][1])
+                tot[name] = tot.get(name, 0.0) + self._elapsed(a, b)
+            tot["step"] = tot.get("step", 0.0) + self._elapsed(marks[0][1], marks[-1][1])
         if reset:
             self._done = []
         return {f"{k}_ms": v / n for k, v in tot.items()} if n else {}

@@ -1,23 +1,27 @@
 """Spawn a gloo "fake cluster" on localhost (the reference needs 6 named PCs;
 this runs the same data-parallel protocol in W processes on 127.0.0.1)."""
 import os
-import socket
 import traceback
 
 import torch.multiprocessing as mp
 
 
-def free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _agent_store(world):
+    """The rendezvous store, hosted by the test process the way torchrun's agent hosts it:
+    bound to port 0 by the store itself (no probe-then-bind race with other processes) and
+    kept open for the run; every rank connects to it as a client
+    (TORCHELASTIC_USE_AGENT_STORE)."""
+    import datetime
+
+    import torch.distributed as dist
+    return dist.TCPStore("127.0.0.1", 0, world, True, timeout=datetime.timedelta(seconds=300),
+                         wait_for_workers=False)
 
 
 def _entry(rank, world, port, fn, args, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      TORCHELASTIC_USE_AGENT_STORE="True", TORCHELASTIC_RESTART_COUNT="0")
     os.environ.setdefault("OMP_NUM_THREADS", "2")
     import torch
     torch.set_num_threads(2)
@@ -35,17 +39,8 @@ def _entry(rank, world, port, fn, args, q):
                 pass
 
 
-# rendezvous / socket failures of the local gloo mesh (a free_port() race with another
-# process, a connect that lost the race): the run is repeated once on a fresh port
-_TRANSIENT = ("Address already in use", "Connection refused", "Connection reset",
-              "Socket Timeout", "EADDRINUSE", "ECONNREFUSED", "ECONNRESET")
-
-
 def run(fn, world=2, args=(), timeout=240, allow_fail=False):
     out = _run_once(fn, world, args, timeout)
-    if not allow_fail and any(st != "ok" and any(t in str(res) for t in _TRANSIENT)
-                              for st, res in out.values()):
-        out = _run_once(fn, world, args, timeout)
     if not allow_fail:
         for r, (st, res) in sorted(out.items()):
             assert st == "ok", f"rank {r} failed: {res}"
@@ -57,7 +52,8 @@ def run(fn, world=2, args=(), timeout=240, allow_fail=False):
 def _run_once(fn, world, args, timeout):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = free_port()
+    store = _agent_store(world)          # (kept alive until every rank has finished)
+    port = store.port
     procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q)) for r in range(world)]
     for p in procs:
         p.start()
@@ -78,4 +74,5 @@ def _run_once(fn, world, args, timeout):
         if p.is_alive():
             p.kill()
             p.join()
+    del store
     return out

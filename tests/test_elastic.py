@@ -3,7 +3,6 @@ hook), ``torchrun --max-restarts`` relaunches the job, ``--resume auto`` picks u
 checkpoint — including the position inside the epoch — and the run ends with exactly the
 weights of an uninterrupted run.  CPU / gloo, 2 ranks."""
 import os
-import socket
 import subprocess
 import sys
 
@@ -16,16 +15,12 @@ ARGS = ["--impl", "torch", "--device", "cpu", "--tile", "32", "--depth", "4",
         "--log-every", "0"]
 
 
-def _port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def _torchrun(extra, restarts=0):
     env = dict(os.environ, OMP_NUM_THREADS="2")
+    # c10d rendezvous on port 0: torchrun's agent binds the store's port itself (no
+    # probe-then-bind race with other processes for a "free" port)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           "--rdzv-backend", "c10d", "--rdzv-endpoint", "127.0.0.1:0",
            "--max-restarts", str(restarts), "-m", "ddlpc", "train", *ARGS, *extra]
     return subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
 

@@ -1006,9 +1006,32 @@ def test_meter_add_single_launch(ops):
 
 
 # ------------------------------------------------------------------ per-micro-batch BN groups
+def bn_relu_pool_backward_oracle(y, dA, dP, gamma, beta, eps, s4):
+    """fp32 autograd through train-mode BatchNorm + ReLU (+ 2x2 max-pool) of ONE statistics
+    group (channel-last y [n, H, W, C]): -> (dY, dgamma, dbeta).  The ReLU mask and the
+    pool's arg-max come from the kernels' bf16-rounded activation fma(y, scale, shift) (the
+    values the forward stored), so a bf16 tie cannot route the pooled gradient elsewhere;
+    every gradient value is fp32 autograd of the BatchNorm formula."""
+    x = nchw(y).float().detach().requires_grad_(True)
+    g = gamma.detach().clone().requires_grad_(True)
+    b = beta.detach().clone().requires_grad_(True)
+    z = F.batch_norm(x, None, None, g, b, training=True, eps=eps)
+    sc, sh = s4[2].view(1, -1, 1, 1), s4[3].view(1, -1, 1, 1)
+    zk = torch.addcmul(sh, nchw(y).float(), sc).bfloat16().float().detach()
+    a = torch.where(zk > 0, z, torch.zeros_like(z))
+    loss = (a * (nchw(dA).float() if dA is not None else 0)).sum()
+    if dP is not None:
+        _, idx = F.max_pool2d(torch.relu(zk), 2, return_indices=True)
+        pooled = torch.gather(a.flatten(2), 2, idx.flatten(2)).view_as(idx)
+        loss = loss + (pooled * nchw(dP).float()).sum()
+    loss.backward()
+    return x.grad.permute(0, 2, 3, 1), g.grad, b.grad
+
+
 @pytest.mark.parametrize("G,n,H,W,C,pool", [(5, 1, 32, 32, 32, True), (3, 2, 16, 16, 256, False),
                                             (4, 1, 64, 64, 64, False), (50, 1, 16, 16, 128, True),
-                                            (2, 1, 8, 8, 256, False)])
+                                            (2, 1, 8, 8, 256, False), (2, 1, 16, 16, 512, True),
+                                            (3, 2, 8, 8, 1024, True)])
 def test_bn_group_kernels(ops, G, n, H, W, C, pool):
     """bn_group_finalize / bn_group_apply / bn_group_backward (a batched window of G
     micro-batches, each its own BatchNorm statistics group) against the fp32 per-group
@@ -1043,7 +1066,8 @@ def test_bn_group_kernels(ops, G, n, H, W, C, pool):
     if pool:
         pr = F.max_pool2d(nchw(a).float(), 2)        # max over the stored activations
         assert torch.equal(nchw(p).float(), pr)
-    # backward vs the single-group kernel per group
+    # backward vs fp32 autograd through BatchNorm + ReLU (+ pool) per group, and vs the
+    # single-group kernel run group by group
     dA = torch.randn(N, H, W, C, device=DEV).bfloat16()
     dP = torch.randn(N, H // 2, W // 2, C, device=DEV).bfloat16() if pool else None
     dg = torch.zeros(C, device=DEV)
@@ -1051,12 +1075,19 @@ def test_bn_group_kernels(ops, G, n, H, W, C, pool):
     dY, _, _ = ops.bn_group_backward(dA, dP, y, s4, gamma, G, dg, db)
     dg_ref = torch.zeros(C, device=DEV, dtype=torch.float64)
     db_ref = torch.zeros(C, device=DEV, dtype=torch.float64)
+    dg_k = torch.zeros(C, device=DEV, dtype=torch.float64)
     for g in range(G):
         sl = slice(g * n, (g + 1) * n)
-        dYg, dgg, dbg = ops.bn_backward(dA[sl].contiguous(), dP[sl].contiguous() if pool else None,
-                                        y[sl].contiguous(), s4[g].contiguous(), gamma, None)
+        dPg = dP[sl].contiguous() if pool else None
+        dYo, dgo, dbo = bn_relu_pool_backward_oracle(y[sl], dA[sl], dPg, gamma, beta, eps, s4[g])
+        assert rel_err(dY[sl], dYo) < 1e-2, (g, rel_err(dY[sl], dYo))
+        dg_ref += dgo.double()
+        db_ref += dbo.double()
+        dYg, dgg, _ = ops.bn_backward(dA[sl].contiguous(), dPg, y[sl].contiguous(),
+                                      s4[g].contiguous(), gamma, None)
         assert rel_err(dY[sl], dYg) < 2e-3, g
-        dg_ref += dgg.double()
-        db_ref += dbg.double()
-    assert torch.allclose(dg.double(), dg_ref, rtol=1e-4, atol=1e-3)
-    assert torch.allclose(db.double(), db_ref, rtol=1e-4, atol=1e-3)
+        dg_k += dgg.double()
+    assert torch.allclose(dg.double(), dg_ref, rtol=1e-3, atol=1e-2 * float(dg_ref.abs().max())), \
+        float((dg.double() - dg_ref).abs().max())
+    assert torch.allclose(db.double(), db_ref, rtol=1e-3, atol=1e-3 * float(db_ref.abs().max()) + 1e-3)
+    assert torch.allclose(dg.double(), dg_k, rtol=1e-4, atol=1e-3)

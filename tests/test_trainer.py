@@ -4,6 +4,7 @@ import os
 import subprocess
 import sys
 
+import pytest
 import torch
 
 from ddlpc.config import ModelConfig, TrainConfig
@@ -69,14 +70,24 @@ def test_profiler_trace_and_throughput_metrics(tmp_path):
     assert steps and all(l["images_per_s"] > 0 for l in steps)
 
 
-def test_phase_timer_reads_on_cpu_are_empty():
+def test_phase_timer_on_cpu_uses_the_host_clock():
+    """On a CPU device (gloo rehearsal) the phase marks are host clock readings: every op is
+    synchronous there, so the per-phase means are real (bench.py's comm_wait_ms on CPU)."""
+    import time
     from ddlpc.utils.tracing import PhaseTimer, trace_range
     pt = PhaseTimer(torch.device("cpu"))
-    pt.mark("start")
-    with trace_range("x"):
-        pt.mark("a")
-    pt.end_step()
-    assert pt.read() == {}
+    for _ in range(2):
+        pt.mark("start")
+        with trace_range("x"):
+            time.sleep(0.01)
+            pt.mark("a")
+        pt.mark("b")
+        pt.end_step()
+    r = pt.read()
+    assert set(r) == {"a_ms", "b_ms", "step_ms"}
+    assert 9.0 <= r["a_ms"] < 500 and 0 <= r["b_ms"] < r["a_ms"]
+    assert abs(r["step_ms"] - r["a_ms"] - r["b_ms"]) < 1e-6
+    assert pt.read() == {}                     # reset after a read
 
 
 def test_bench_cpu_json_contract():
@@ -94,16 +105,14 @@ def test_bench_cpu_json_contract():
 
 def test_bench_torchrun_two_ranks_gloo():
     """The driver's N>1 launch line (torch.distributed.run, 127.0.0.1) on CPU/gloo: one JSON
-    line from rank 0 with the whole-job aggregate."""
-    import socket
+    line from rank 0 with the whole-job aggregate, and the run's self-validation: the
+    backend and world size the collectives really used, bit-identical replicas after the
+    timed steps, the exposed communication wait per step."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
     env = dict(os.environ, OMP_NUM_THREADS="2")
     out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-                          "--master-port", str(port), os.path.join(root, "bench.py"),
+                          "--nproc-per-node", "2", "--rdzv-backend", "c10d",
+                          "--rdzv-endpoint", "127.0.0.1:0", os.path.join(root, "bench.py"),
                           "--gpus", "2", "--impl", "torch", "--steps", "2", "--warmup", "1",
                           "--batch", "2", "--tile", "64", "--width-divisor", "16",
                           "--wire-dtype", "bf16", "--bucket-mb", "0.5", "--bucket-sweep", "0.25,1"],
@@ -119,6 +128,33 @@ def test_bench_torchrun_two_ranks_gloo():
     assert c["wire_dtype"] == "bf16" and c["buckets"] >= 2 and "comm_wait_ms" in c
     assert set(c["bucket_sweep"]) == {"0.25", "1.0"}
     assert c["bucket_sweep"]["0.25"]["buckets"] > c["bucket_sweep"]["1.0"]["buckets"]
+    assert rec["dist_backend"] == "gloo" and rec["world_size"] == 2
+    assert rec["replicas_identical"] is True and rec["rccl_version"] is None
+    assert rec["comm_wait_ms"] is not None and rec["comm_wait_ms"] >= 0
+
+
+def test_bench_self_spawns_torchrun_for_gpus_n():
+    """``bench.py --gpus 2`` outside torchrun launches torchrun itself (a child process) and
+    the ranks report the world they really formed."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "2"
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                          "--impl", "torch", "--steps", "1", "--warmup", "1", "--batch", "2",
+                          "--tile", "64", "--width-divisor", "16"],
+                         capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["n_gpus"] == 2 and rec["world_size"] == 2 and rec["replicas_identical"] is True
+
+
+def test_bench_refuses_world_size_mismatch():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                          "--impl", "torch", "--steps", "1", "--warmup", "0"],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 2 and "refusing" in out.stderr
 
 
 def test_resume_with_max_steps_inside_an_epoch(tmp_path):
@@ -200,7 +236,8 @@ def test_window_size_policy_and_concat():
     from ddlpc.config import ModelConfig, TrainConfig
     from ddlpc.data.datasets import engine_input
     from ddlpc.train.trainer import Trainer
-    cfg = TrainConfig(model=ModelConfig(out_classes=2, depth=2, width_divisor=16), tile=16,
+    from ddlpc.utils.flops import unet_activation_elems_per_sample
+    cfg = TrainConfig(model=ModelConfig(out_classes=2, depth=2, width_divisor=8), tile=16,
                       num_samples=4, test_holdout=0, accum_steps=4, log_every=0)
     tr = Trainer(cfg, device="cpu")
     assert tr._window_size(4) == 0                      # stock-op (CPU) path: no window
@@ -216,6 +253,22 @@ def test_window_size_policy_and_concat():
     assert tr._window_size(50) == 8
     cfg.bn_window = 0
     assert tr._window_size(50) == 0
+    # activation memory bounds the auto window (half of what the allocator can hand out)
+    cfg.bn_window, cfg.tile = -1, 512
+    per = tr.WINDOW_BYTES_PER_ELEM * unet_activation_elems_per_sample(cfg.model, 512)
+    tr._allocator_bytes_available = lambda: 2 * 10.5 * per
+    tr._window_cache = {}
+    assert tr._window_size(50) == 10
+    tr._allocator_bytes_available = lambda: 2 * 1.5 * per
+    tr._window_cache = {}
+    assert tr._window_size(50) == 0                     # not even two fit: one by one
+    del tr._allocator_bytes_available
+    tr._window_cache = {}
+    cfg.recompute = 1
+    assert tr._window_size(50) == 0                     # the grouped pass ignores recompute
+    cfg.recompute = 0
+    cfg.tile = 24                                       # 24 >> 1 = 12 >> 1 = 6: ok (depth 2)
+    assert tr._window_size(50) == 50
     tr.impl, tr.device = "torch", torch.device("cpu")
     mbs = []
     for j in range(3):
@@ -225,4 +278,22 @@ def test_window_size_policy_and_concat():
     assert x.shape == (3, 3, 8, 8) and x._ddlpc_nhwc.shape == (3, 8, 8, 8)
     assert [int(v) for v in y[:, 0, 0]] == [0, 1, 2]
     assert [float(v) for v in x._ddlpc_nhwc[:, 0, 0, 0]] == [0.0, 1.0, 2.0]
+    # micro-batches of unequal size cannot form one window (their BatchNorm groups and loss
+    # weights would be wrong)
+    mbs.append((engine_input(torch.zeros(2, 8, 8, 8), 3), torch.zeros(2, 8, 8, dtype=torch.int64)))
+    with pytest.raises(ValueError):
+        Trainer._cat_window(mbs)
     tr.close()
+
+
+def test_bn_group_support_geometry():
+    """The grouped BatchNorm kernels' shape contract, checked before a window is chosen:
+    the standard U-Net widths (width divisor 1: 512 pooled channels) are supported; a BN
+    width whose C / 8 is not a power of two, or an odd pooled extent, is not."""
+    from ddlpc.models import UNet
+    from ddlpc.ops.fused_unet import bn_groups_supported
+    assert bn_groups_supported(UNet(out_classes=6, width_divisor=1), 512)
+    assert bn_groups_supported(UNet(out_classes=6, width_divisor=2), 128)
+    assert not bn_groups_supported(UNet(out_classes=6, width_divisor=2), 48)   # 48 >> 4 = 3
+    m = UNet(out_classes=6, width_divisor=2, base_widths=(24, 48, 96, 192, 192))
+    assert not bn_groups_supported(m, 256)                                    # C / 8 = 3

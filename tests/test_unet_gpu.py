@@ -449,27 +449,40 @@ def test_concurrent_micro_stream_graphs():
     assert scale > 0 and float((g0 - g1).abs().max()) <= 1e-5 * scale, float((g0 - g1).abs().max())
 
 
-@pytest.mark.parametrize("tile,accum,bpg", [(512, 50, 1), (64, 6, 2)])
-def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg):
+@pytest.mark.parametrize("tile,accum,bpg,wd", [(512, 50, 1, 2), (64, 6, 2, 2), (128, 4, 1, 1)])
+def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg, wd):
     """The reference's regime (512^2, batch 1, 50 accumulated micro-batches, ref.py:685-687,
-    750-766) as ONE batched pass with per-micro-batch BatchNorm groups.  Against the same
-    micro-batches one by one through the SAME (unfused, grouped) kernels — ``bn_groups = 1``
-    per micro-batch — the gradient, mean micro-batch loss, pixel counts and in-order running
-    statistics agree to fp32 summation order (the batched convs sum in another order; bf16
-    outputs round independently).  Against the fused one-by-one path (deferred BN applied in
-    fp32 on load, prologue fusion) they agree to bf16 rounding of the intermediate
-    activations.  The measured errors are printed (GPU log)."""
+    750-766) as ONE batched pass with per-micro-batch BatchNorm groups, and the standard
+    U-Net widths (width divisor 1, ref.py:687: 512 pooled channels at the deepest encoder
+    levels) at 128^2.  Three independent yardsticks:
+
+    * the same micro-batches one by one through the unfused grouped kernels
+      (``bn_groups = 1``): where the batched convs tile like the batch-2 ones (64^2) the
+      window must agree to fp32 summation order (rel L2 <= 1e-5; measured 6.7e-8) with
+      bit-identical running statistics; elsewhere to a FIXED bound (rel L2 <= 2e-2,
+      per-tensor cosine >= 0.95; measured at 512^2 x 50: 4.2e-3);
+    * the fused one-by-one path (deferred BN, prologue fusion): the same fixed bound;
+    * (small cases) the stock fp32 PyTorch model run micro-batch by micro-batch with its own
+      train-mode BatchNorm: every gradient tensor as close to it as stock bf16 autocast is
+      (cosine >= min(0.98, autocast - 0.08)) — no dependence on the new kernels."""
     from ddlpc.config import ModelConfig, TrainConfig
     from ddlpc.data import device_random_batch
+    from ddlpc.models import UNet
     from ddlpc.train.trainer import Trainer
-    cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=tile, batch_per_gpu=bpg,
-                      num_samples=1, test_holdout=0, impl="hip", micro_streams=1,
-                      accum_steps=accum, bn_window=0)
+    cfg = TrainConfig(model=ModelConfig(out_classes=6, width_divisor=wd), tile=tile,
+                      batch_per_gpu=bpg, num_samples=1, test_holdout=0, impl="hip",
+                      micro_streams=1, accum_steps=accum, bn_window=0)
     tr = Trainer(cfg, device="cuda")
     eng = tr.model._engine
+    assert eng.bn_groups_supported(tile)
     mbs = [device_random_batch(bpg, tile, 6, tr.device, seed=300 + j) for j in range(accum)]
     bufs = {k: v for k, v in tr.model.state_dict().items() if "running" in k or "num_batches" in k}
     b0 = {k: v.clone() for k, v in bufs.items()}
+    oracle = tile <= 128
+    if oracle:
+        ref = UNet(out_classes=6, width_divisor=wd).cuda()
+        ref.load_state_dict(tr.model.state_dict())
+        amp = copy.deepcopy(ref)
 
     def run(mode):
         tr.optimizer.zero_grad()
@@ -492,8 +505,8 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg):
     res = {m: run(m) for m in ("fused", "unfused", "window")}
     assert eng.bn_groups == 0
 
-    def compare(ref, got):
-        g0, g1 = res[ref][0], res[got][0]
+    def compare(ref_mode, got):
+        g0, g1 = res[ref_mode][0], res[got][0]
         rel = float((g1 - g0).norm() / g0.norm())
         cmin, worst = 1.0, None
         for p in tr.flat.order:
@@ -502,37 +515,53 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg):
                 c = _cos(g1[a:b], g0[a:b])
                 if c < cmin:
                     cmin, worst = c, tuple(p.shape)
-        print(f"{got} vs {ref}: rel L2 {rel:.3e}, min per-tensor cos {cmin:.6f} {worst}")
+        print(f"{got} vs {ref_mode}: rel L2 {rel:.3e}, min per-tensor cos {cmin:.6f} {worst}")
         return rel, cmin
 
     rel_u, cos_u = compare("unfused", "window")
     rel_f, cos_f = compare("fused", "window")
-    # the noise floor: two mathematically equivalent one-by-one paths (fused vs unfused
-    # kernels) differ by their bf16 rounding points alone — measured: rel L2 3.7e-3, min
-    # per-tensor cosine 0.970 at 512^2 x 50 (a 256-channel BatchNorm gradient, a sum of many
-    # cancelling terms); 2.8e-2 / 0.972 at 64^2 (2x2-pixel bottleneck statistics).  The
-    # window may differ from either by no more than twice that.  (Where the batched convs
-    # tile like the batch-1 ones — the 64^2 case — window and unfused agree to fp32
-    # summation order: measured rel L2 6.7e-8.)
-    rel_uf, cos_uf = compare("fused", "unfused")
-    for rel, cmin in ((rel_u, cos_u), (rel_f, cos_f)):
-        assert rel <= 2 * rel_uf + 1e-4, (rel, rel_uf)
-        assert 1 - cmin <= 2 * (1 - cos_uf) + 1e-4, (cmin, cos_uf)
-    for ref in ("unfused", "fused"):
-        m0, m1 = res[ref][1], res["window"][1]
+    compare("fused", "unfused")                          # (the two one-by-one paths, printed)
+    if tile == 64:
+        assert rel_u <= 1e-5, rel_u
+    else:
+        assert rel_u <= 2e-2 and cos_u >= 0.95, (rel_u, cos_u)
+    assert rel_f <= 2e-2 and cos_f >= 0.95, (rel_f, cos_f)
+    for ref_mode in ("unfused", "fused"):
+        m0, m1 = res[ref_mode][1], res["window"][1]
         assert m1[2] == m0[2] and m1[3] == m0[3] == accum, (m0, m1)
-        assert abs(float(m1[0] - m0[0])) <= 2e-3 * float(m0[0]), (ref, m0, m1)
-        assert abs(float(m1[1] - m0[1])) <= 2e-3 * float(m0[2]), (ref, m0, m1)
+        assert abs(float(m1[0] - m0[0])) <= 2e-3 * float(m0[0]), (ref_mode, m0, m1)
+        assert abs(float(m1[1] - m0[1])) <= 2e-3 * float(m0[2]), (ref_mode, m0, m1)
     for k in b0:
         bu, bw, bf = res["unfused"][2][k], res["window"][2][k], res["fused"][2][k]
+        if "num_batches" in k or tile == 64:
+            assert torch.equal(bw, bu), (k, float((bw.float() - bu.float()).abs().max()))
         if "num_batches" in k:
-            assert torch.equal(bw, bu) and torch.equal(bw, bf), k
+            assert torch.equal(bw, bf), k
         else:
             # per-micro-batch means / variances of conv outputs that round to bf16
             # independently (the batched convs tile differently): measured up to 2.3e-4 on
             # the bottleneck's running means of magnitude ~1 (256 pixels per micro-batch)
             err = float((bw - bu).abs().max())
             assert err <= 2e-3 * max(1.0, float(bu.abs().max())), (k, err)
+    if oracle:
+        # fp32 stock model (and bf16 autocast), micro-batch by micro-batch, own BatchNorm each
+        for x, y in mbs:
+            F.cross_entropy(ref(x.float().contiguous()), y).backward()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                F.cross_entropy(amp(x.float().contiguous()).float(), y).backward()
+        gw = res["window"][0]
+        bad, worst = [], []
+        for (n, pr), (_, pa), ph in zip(ref.named_parameters(), amp.named_parameters(),
+                                        tr.model.parameters()):
+            if n.endswith((".0.bias", ".3.bias")) and "double_conv.double_conv" in n:
+                continue
+            a, b = tr.flat.span(ph)
+            ch, ca = _cos(pr.grad, gw[a:b]), _cos(pr.grad, pa.grad)
+            worst.append((ch - ca, n, ch, ca))
+            if ch < min(0.98, ca - 0.08):
+                bad.append((n, ch, ca))
+        print("window vs fp32, worst cosine deltas to autocast:", sorted(worst)[:3])
+        assert not bad, bad
     # and a full optimizer step through train_step picks the window (auto)
     tr.cfg.bn_window = -1
     assert tr._window_size(accum) == (accum if bpg * tile * tile <= tr.SMALL_MICRO_PIXELS else 0)
