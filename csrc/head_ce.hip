@@ -631,6 +631,401 @@ __global__ __launch_bounds__(256) void head_bn_apply_kernel(
   }
 }
 
+// ===================================================================== the C = 32 head on MFMA
+// The flagship head (32 input channels, up to 16 classes) with the per-pixel arithmetic on the
+// matrix cores.  A wave works on 16 pixels at a time; lane l holds pixel n = l & 15 and
+// channel group g = l >> 4 (channels 8g..8g+7: one 16-B load, the same bytes the channel-split
+// kernels read), which is exactly the B operand of v_mfma_f32_16x16x32_bf16:
+//   logits^T [16 classes][16 px] = Wh [16][32] . act^T        (Wh as bf16 hi + lo: 2 MFMAs)
+// and its output layout (lane: classes 4g..4g+3 of pixel n) is exactly the B operand of
+// v_mfma_f32_16x16x16_bf16 for the head's input gradient:
+//   dA^T [channels][16 px] = Wh^T . dlogits^T                  (hi/lo products: 3 MFMAs per
+//                                                                 16-channel tile, 2 tiles)
+// with the A rows permuted so the output lane again holds channels 8g..8g+7 of pixel n (the
+// lane's own y for the BatchNorm-backward arithmetic and a 16-B store).  The softmax runs on
+// the 4 class values per lane; its max / sum over a pixel's 4 lanes (rows of the wave) are
+// two v_permlane{16,32}_swap steps.  The channel-split kernels (one lane per 8 channels of a
+// pixel, 48 FMAs for the logits and 48 for dA per lane, the softmax repeated on the 4 lanes
+// of a pixel) were VALU-issue bound at ~1.5-2.6 TB/s (profiles/r4/pmc_head_r6e.txt); here the
+// VALU work per pixel is the BatchNorm transform, 4 exponentials and the stats.  Products are
+// exact bf16 x bf16 (hi + lo splits of the fp32 weights and dlogits: ~2^-16 relative), sums fp32.
+// dWh^T [class][ch] += dlogits^T . act uses the LDS-transposed operands of the former MDW kernel.
+
+// sum / max of a value over the 4 rows of the wave (the 4 channel / class groups of a pixel):
+// permlane16_swap pairs rows (0,1), (2,3); permlane32_swap pairs halves — every lane gets the
+// same result, summed in the same order
+DDLPC_DEVICE float rows4_sum(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                            false, false);
+  const float s = __builtin_bit_cast(float, (unsigned)a[0]) + __builtin_bit_cast(float, (unsigned)a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, s), __builtin_bit_cast(unsigned, s),
+                                            false, false);
+  return __builtin_bit_cast(float, (unsigned)b[0]) + __builtin_bit_cast(float, (unsigned)b[1]);
+}
+DDLPC_DEVICE float rows4_max(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                            false, false);
+  const float s = fmaxf(__builtin_bit_cast(float, (unsigned)a[0]), __builtin_bit_cast(float, (unsigned)a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, s), __builtin_bit_cast(unsigned, s),
+                                            false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)b[0]), __builtin_bit_cast(float, (unsigned)b[1]));
+}
+DDLPC_DEVICE int rows4_min_i(int v) {
+  auto a = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+  const int s = min((int)a[0], (int)a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap((unsigned)s, (unsigned)s, false, false);
+  return min((int)b[0], (int)b[1]);
+}
+
+// the lane's constant MFMA operands: logits A = Wh[class n][8g..8g+7] (hi, lo), dA tiles
+// A = Wh[4g..4g+3][ch(n, t)] with ch(m, t) = 8 (m >> 2) + 4 t + (m & 3) (hi, lo), and the
+// logit bias of classes 4g..4g+3 (padded classes: zero weights, bias -inf)
+struct Head32W { uint4 zh, zl; uint2 th[2], tl[2]; f32x4_t b4; };
+DDLPC_DEVICE Head32W head32_weights(const float* __restrict__ Wh, const float* __restrict__ bh, int Kreal,
+                                    int lane) {
+  const int n = lane & 15, g = lane >> 4;
+  Head32W w;
+  float hi[8], lo[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float v = n < Kreal ? Wh[n * 32 + 8 * g + j] : 0.f;
+    hi[j] = lo_bf(pack2(v, 0.f));
+    lo[j] = v - hi[j];
+  }
+  w.zh = pack8(hi);
+  w.zl = pack8(lo);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int ch = 8 * (n >> 2) + 4 * t + (n & 3);
+    float h4[4], l4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = 4 * g + i;
+      const float v = k < Kreal ? Wh[k * 32 + ch] : 0.f;
+      h4[i] = lo_bf(pack2(v, 0.f));
+      l4[i] = v - h4[i];
+    }
+    w.th[t] = make_uint2(pack2(h4[0], h4[1]), pack2(h4[2], h4[3]));
+    w.tl[t] = make_uint2(pack2(l4[0], l4[1]), pack2(l4[2], l4[3]));
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w.b4[i] = 4 * g + i < Kreal ? bh[4 * g + i] : -INFINITY;
+  return w;
+}
+
+// one 16-pixel step of a wave: from the lane's 8 raw channels yv (pixel n, channels 8g..),
+// its label and validity -> the activation f (BN + ReLU when DEFER, bf16-rounded), the 4
+// dlogits d (classes 4g..4g+3, scaled by gs; zero for ignored / tail pixels), dA before
+// rounding (o8, the lane's 8 channels) and rounded (pk); LOSS extras: lse, the label's
+// logit, the arg-max class (valid on every lane of the pixel)
+template <bool DEFER, bool LOSS>
+DDLPC_DEVICE void head32_step(const uint4 yv, const int64_t lab, const bool valid, const Head32W& w,
+                              const float (&sc)[8], const float (&sh)[8], float gs, int ignore_index,
+                              int g, float (&y8)[8], float (&f)[8], float (&d)[4], float (&o8)[8],
+                              uint4& pk, float& lse, float& zy, int& am) {
+  unpack8(yv, y8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = DEFER ? fmaxf(fmaf(y8[j], sc[j], sh[j]), 0.f) : y8[j];
+  const uint4 fb = pack8(f);
+  unpack8(fb, f);                                   // the activation as materialised (bf16)
+  const uint4 fz = valid ? fb : make_uint4(0, 0, 0, 0);
+  f32x4_t z = mfma16x16x32(w.zh, fz, w.b4);
+  z = mfma16x16x32(w.zl, fz, z);
+  float m = fmaxf(fmaxf(z[0], z[1]), fmaxf(z[2], z[3]));
+  m = rows4_max(m);
+  float e[4], se = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { e[i] = __expf(z[i] - m); se += e[i]; }
+  se = rows4_sum(se);
+  const float inv = __builtin_amdgcn_rcpf(se);     // (se >= 1: the max term is exp(0))
+  const bool live = valid && lab != ignore_index;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) d[i] = live ? (e[i] * inv - (4 * g + i == lab ? 1.f : 0.f)) * gs : 0.f;
+  if (LOSS) {
+    lse = m + __logf(se);
+    float t = 0.f;
+    int c = 16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      t = (4 * g + i == lab) ? z[i] : t;
+      c = (z[i] == m && c == 16) ? 4 * g + i : c;   // first maximum
+    }
+    zy = rows4_sum(t);
+    am = rows4_min_i(c);
+  }
+  // dA: hi / lo splits of the dlogits as the B operand (classes 4g..4g+3 of pixel n)
+  float dh[4], dl[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { dh[i] = lo_bf(pack2(d[i], 0.f)); dl[i] = d[i] - dh[i]; }
+  const uint2 bh2 = make_uint2(pack2(dh[0], dh[1]), pack2(dh[2], dh[3]));
+  const uint2 bl2 = make_uint2(pack2(dl[0], dl[1]), pack2(dl[2], dl[3]));
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    f32x4_t o = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    o = mfma16x16x16(w.th[t], bh2, o);
+    o = mfma16x16x16(w.th[t], bl2, o);
+    o = mfma16x16x16(w.tl[t], bh2, o);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o8[4 * t + i] = o[i];
+  }
+  pk = pack8(o8);
+}
+
+// Loads run HEAD32_D steps ahead (a wave's 1 KB activation tile + its 16 labels per step): the
+// channel-split kernels and a first one-step-prefetch form of these were latency-bound at
+// 1.9 TB/s (12 waves x 1.1 KB in flight per CU); the per-lane channel constants live in LDS
+// (re-read per step; an opaque offset keeps the compiler from hoisting them into VGPRs) to pay
+// for the deeper register pipeline.
+constexpr int HEAD32_D = 3;             // head32_kernel (4 spills at three waves per SIMD)
+constexpr int HEAD32_DA = 4;            // head32_apply_kernel
+
+template <int D>
+struct Head32Ld {
+  uint4 y[D];
+  int64_t l[D];
+};
+
+// The C = 32 counterpart of head_ce_bwd_kernel<32, K, DEFER, STORE, LOSS> (same outputs, same
+// row layouts): stats of the backward (dWh, dbh; with DEFER the deferred BatchNorm's backward
+// partials), the dA store (STORE), and with LOSS the training forward's loss / hits / count at
+// a unit gradient scale.
+template <bool DEFER, bool STORE, bool LOSS>
+__global__ __launch_bounds__(256, 3) void head32_kernel(
+    const bf16_t* __restrict__ a, const float* __restrict__ Wh, const float* __restrict__ bh,
+    const int64_t* __restrict__ labels, const float* __restrict__ gscale,
+    const float* __restrict__ stats3, bf16_t* __restrict__ dA, float* __restrict__ dWp,
+    long long P, int ignore_index, const float* __restrict__ bn4, float* __restrict__ bnpart,
+    int Kreal, float* __restrict__ lossp) {
+  static_assert(!LOSS || (DEFER && !STORE), "the fused forward is the deferred stats pass");
+  constexpr int C = 32;
+  // per wave: act [16][32] bf16 (1 KB) | dlogits hi [16][16] | lo [16][16]; reused at the end
+  // as the wave's dWh^T [16][32] fp32 (2 KB)
+  __shared__ __attribute__((aligned(16))) char sT[4][2048];
+  __shared__ float sred[4][4][24];                 // [wave][row g][db 4 | bn 16 | loss 3]
+  __shared__ __attribute__((aligned(16))) float sK[4][C];   // scale | shift | invstd | -mean*invstd
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const Head32W w = head32_weights(Wh, bh, Kreal, lane);
+  if (DEFER && tid < C) {
+    sK[0][tid] = bn4[2 * C + tid];
+    sK[1][tid] = bn4[3 * C + tid];
+    sK[2][tid] = bn4[C + tid];
+    sK[3][tid] = -bn4[tid] * bn4[C + tid];
+  }
+  __syncthreads();
+  const float cnt = LOSS ? 1.f : stats3[2];
+  const float gs = LOSS ? 1.f : (gscale != nullptr ? gscale[0] : 1.0f) / (cnt > 0.f ? cnt : 1.f);
+  char* tA = sT[wave];
+  char* tDh = tA + 1024;
+  char* tDl = tA + 1536;
+  const int q = (lane & 15) >> 2, pq = lane & 3;
+  const int rA = (4 * g + q) * 64 + pq * 8;          // transposed reads (see the MDW notes)
+  const int rD = (4 * g + q) * 32 + pq * 8;
+  f32x4_t dw[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+  float db[4] = {0.f, 0.f, 0.f, 0.f}, b1[8], b2[8], ls[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { b1[j] = 0.f; b2[j] = 0.f; }
+  const long long steps = (P + 15) / 16;
+  const long long wstride = (long long)gridDim.x * 4;
+  const long long s0 = (long long)blockIdx.x * 4 + wave;
+  auto load = [&](long long st, uint4& yv, int64_t& lb) __attribute__((always_inline)) {
+    const long long px = st * 16 + n;
+    const long long pc = px < P ? px : 0;
+    yv = *reinterpret_cast<const uint4*>(a + pc * C + 8 * g);
+    lb = labels[pc];
+  };
+  Head32Ld<HEAD32_D> q4;
+#pragma unroll
+  for (int j = 0; j < HEAD32_D; ++j) load(s0 + j * wstride < steps ? s0 + j * wstride : s0, q4.y[j], q4.l[j]);
+#pragma unroll 1
+  for (long long sb = s0; sb < steps; sb += HEAD32_D * wstride) {   // wave-uniform trip count
+#pragma unroll
+    for (int j = 0; j < HEAD32_D; ++j) {
+      const long long s = sb + j * wstride;
+      const uint4 yv = q4.y[j];
+      const int64_t lab = q4.l[j];
+      if (s + HEAD32_D * wstride < steps) load(s + HEAD32_D * wstride, q4.y[j], q4.l[j]);
+      if (s >= steps) break;                           // wave-uniform
+      const long long px = s * 16 + n;
+      const bool valid = px < P;
+      float sc[8], sh[8];
+      if (DEFER) {
+        const float4* kp = reinterpret_cast<const float4*>(&sK[0][0] + opaque_zero() + 8 * g);
+        const float4 a0 = kp[0], a1 = kp[1], c0 = kp[8], c1 = kp[9];
+        sc[0] = a0.x; sc[1] = a0.y; sc[2] = a0.z; sc[3] = a0.w; sc[4] = a1.x; sc[5] = a1.y; sc[6] = a1.z; sc[7] = a1.w;
+        sh[0] = c0.x; sh[1] = c0.y; sh[2] = c0.z; sh[3] = c0.w; sh[4] = c1.x; sh[5] = c1.y; sh[6] = c1.z; sh[7] = c1.w;
+      } else {
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) { sc[jj] = 0.f; sh[jj] = 0.f; }
+      }
+      float y8[8], f[8], d[4], o8[8], lse = 0.f, zy = 0.f;
+      int am = 0;
+      uint4 pk;
+      head32_step<DEFER, LOSS>(yv, lab, valid, w, sc, sh, gs, ignore_index, g, y8, f, d, o8, pk, lse, zy, am);
+      if (STORE && valid) *reinterpret_cast<uint4*>(dA + px * C + 8 * g) = pk;
+      // dWh via the LDS transpose: act row (the lane's 8 channels; zero for tail pixels),
+      // dlogits hi / lo (the lane's 4 classes)
+      *reinterpret_cast<uint4*>(tA + n * 64 + g * 16) = valid ? pack8(f) : make_uint4(0, 0, 0, 0);
+      {
+        float dh[4], dl[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { dh[i] = lo_bf(pack2(d[i], 0.f)); dl[i] = d[i] - dh[i]; }
+        *reinterpret_cast<uint2*>(tDh + n * 32 + g * 8) = make_uint2(pack2(dh[0], dh[1]), pack2(dh[2], dh[3]));
+        *reinterpret_cast<uint2*>(tDl + n * 32 + g * 8) = make_uint2(pack2(dl[0], dl[1]), pack2(dl[2], dl[3]));
+      }
+      const uint2 ah = lds_read_tr16(tDh + rD);
+      const uint2 al = lds_read_tr16(tDl + rD);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const uint2 b = lds_read_tr16(tA + rA + nt * 32);
+        dw[nt] = mfma16x16x16(ah, b, dw[nt]);
+        dw[nt] = mfma16x16x16(al, b, dw[nt]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) db[i] += d[i];
+      if (LOSS && g == 0 && valid) {
+        if (lab != ignore_index) { ls[0] += lse - zy; ls[2] += 1.f; }
+        ls[1] += am == lab ? 1.f : 0.f;
+      }
+      if (DEFER) {
+        float r[8];
+        if (LOSS) {                                  // unit scale: the unrounded dA
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) r[jj] = o8[jj];
+        } else {
+          unpack8(pk, r);                            // BN backward sees the stored dA
+        }
+        const float4* kp = reinterpret_cast<const float4*>(&sK[2][0] + opaque_zero() + 8 * g);
+        const float4 a0 = kp[0], a1 = kp[1], c0 = kp[8], c1 = kp[9];
+        const float xi[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float xm[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const float dyh = (valid && fmaf(y8[jj], sc[jj], sh[jj]) > 0.f) ? r[jj] : 0.f;
+          b1[jj] += dyh;
+          b2[jj] = fmaf(dyh, fmaf(y8[jj], xi[jj], xm[jj]), b2[jj]);
+        }
+      }
+    }
+  }
+  // ---- workgroup reduction (fixed order): dWh^T of each wave to its LDS tile (lane: class
+  // 4g + i, channel 16 nt + n), db / BN partials / loss summed over the 16 pixel lanes of
+  // each row, then the 4 waves
+  float* wd = reinterpret_cast<float*>(tA);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wd[(4 * g + i) * 32 + nt * 16 + n] = dw[nt][i];
+  float red[23];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[i] = row16_sum(db[i]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[4 + j] = DEFER ? row16_sum(b1[j]) : 0.f; red[12 + j] = DEFER ? row16_sum(b2[j]) : 0.f; }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) red[20 + i] = LOSS ? row16_sum(ls[i]) : 0.f;
+  if (n == 0)
+#pragma unroll
+    for (int i = 0; i < 23; ++i) sred[wave][g][i] = red[i];
+  __syncthreads();
+  const int nout = Kreal * C + Kreal;
+  for (int o = tid; o < nout; o += 256) {            // [dW (k, c) | db (k)]
+    float t = 0.f;
+    if (o < Kreal * C) {
+      const int k = o / C, c = o % C;
+      for (int wv = 0; wv < 4; ++wv) t += reinterpret_cast<const float*>(sT[wv])[k * 32 + c];
+    } else {
+      const int k = o - Kreal * C;
+      for (int wv = 0; wv < 4; ++wv) t += sred[wv][k >> 2][k & 3];
+    }
+    dWp[(long long)blockIdx.x * nout + o] = t;
+  }
+  if (DEFER)
+    for (int o = tid; o < 2 * C; o += 256) {         // [sum dyh (c) | sum dyh * xhat (c)]
+      const int half = o / C, c = o % C;
+      float t = 0.f;
+      for (int wv = 0; wv < 4; ++wv) t += sred[wv][c >> 3][4 + 8 * half + (c & 7)];
+      bnpart[(long long)blockIdx.x * 2 * C + o] = t;
+    }
+  if (LOSS && tid < 3) {                             // row g = 0 holds them
+    float t = 0.f;
+    for (int wv = 0; wv < 4; ++wv) t += sred[wv][0][20 + tid];
+    lossp[(long long)blockIdx.x * 3 + tid] = t;
+  }
+}
+
+// The C = 32 counterpart of head_bn_apply_kernel: dA recomputed exactly as head32_kernel
+// stores it, the deferred BatchNorm's backward applied in registers (bn_bwd2_kernel's apply
+// arithmetic), dY stored.  A HEAD32_DA-deep load pipeline.
+__global__ __launch_bounds__(256, 3) void head32_apply_kernel(
+    const bf16_t* __restrict__ a, const float* __restrict__ Wh, const float* __restrict__ bh,
+    const int64_t* __restrict__ labels, const float* __restrict__ gscale,
+    const float* __restrict__ stats3, const float* __restrict__ bn4,
+    const float* __restrict__ coefs, bf16_t* __restrict__ dY, long long P, int ignore_index,
+    int Kreal) {
+  constexpr int C = 32;
+  // scale | shift | invstd | -mean*invstd | k | m1 | m2 (the BN backward coefficients)
+  __shared__ __attribute__((aligned(16))) float sK[7][C];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const Head32W w = head32_weights(Wh, bh, Kreal, lane);
+  if (tid < C) {
+    sK[0][tid] = bn4[2 * C + tid]; sK[1][tid] = bn4[3 * C + tid];
+    sK[2][tid] = bn4[C + tid]; sK[3][tid] = -bn4[tid] * bn4[C + tid];
+    sK[4][tid] = coefs[tid]; sK[5][tid] = coefs[C + tid]; sK[6][tid] = coefs[2 * C + tid];
+  }
+  __syncthreads();
+  const float cnt = stats3[2];
+  const float gs = (gscale != nullptr ? gscale[0] : 1.0f) / (cnt > 0.f ? cnt : 1.f);
+  const long long steps = (P + 15) / 16;
+  const long long wstride = (long long)gridDim.x * 4;
+  const long long s0 = (long long)blockIdx.x * 4 + wave;
+  auto load = [&](long long st, uint4& yv, int64_t& lb) __attribute__((always_inline)) {
+    const long long px = st * 16 + n;
+    const long long pc = px < P ? px : 0;
+    yv = *reinterpret_cast<const uint4*>(a + pc * C + 8 * g);
+    lb = labels[pc];
+  };
+  auto k8 = [&](int r, float (&v)[8]) __attribute__((always_inline)) {
+    const float4* kp = reinterpret_cast<const float4*>(&sK[r][0] + opaque_zero() + 8 * g);
+    const float4 a0 = kp[0], a1 = kp[1];
+    v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+  };
+  Head32Ld<HEAD32_DA> q4;
+#pragma unroll
+  for (int j = 0; j < HEAD32_DA; ++j) load(s0 + j * wstride < steps ? s0 + j * wstride : s0, q4.y[j], q4.l[j]);
+#pragma unroll 1
+  for (long long sb = s0; sb < steps; sb += HEAD32_DA * wstride) {
+#pragma unroll
+    for (int j = 0; j < HEAD32_DA; ++j) {
+      const long long s = sb + j * wstride;
+      const uint4 yv = q4.y[j];
+      const int64_t lab = q4.l[j];
+      if (s + HEAD32_DA * wstride < steps) load(s + HEAD32_DA * wstride, q4.y[j], q4.l[j]);
+      if (s >= steps) break;
+      const long long px = s * 16 + n;
+      const bool valid = px < P;
+      float sc[8], sh[8];
+      k8(0, sc);
+      k8(1, sh);
+      float y8[8], f[8], d[4], o8[8], lse, zy;
+      int am;
+      uint4 pk;
+      head32_step<true, false>(yv, lab, valid, w, sc, sh, gs, ignore_index, g, y8, f, d, o8, pk, lse, zy, am);
+      float rr[8], o[8], is[8], nm[8], k1[8], m1[8], m2[8];
+      unpack8(pk, rr);
+      k8(2, is); k8(3, nm); k8(4, k1); k8(5, m1); k8(6, m2);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const float av2 = fmaf(y8[jj], sc[jj], sh[jj]);
+        const float dyh = av2 > 0.f ? rr[jj] : 0.f;
+        const float xh = fmaf(y8[jj], is[jj], nm[jj]);
+        o[jj] = k1[jj] * (dyh - m1[jj] - xh * m2[jj]);
+      }
+      if (valid) *reinterpret_cast<uint4*>(dY + px * C + 8 * g) = pack8(o);
+    }
+  }
+}
+
 template <int C, int K, bool DEFER>
 __global__ __launch_bounds__(256) void head_logits_kernel(const bf16_t* __restrict__ a, const float* __restrict__ Wh,
                                    const float* __restrict__ bh, float* __restrict__ out,
@@ -693,7 +1088,28 @@ void head_ce_fwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
 // occupancy of the instantiation, from the HIP occupancy API), capped by the pixel count
 // (the SAME grid with and without the deferred BatchNorm — the smaller occupancy of the two
 // — so both paths reduce dWh in the same order: bit-identical weight gradients)
+namespace {
+// resident workgroups per CU of a head32 kernel (occupancy API)
+int head32_per_cu(const void* fn) {
+  int n = 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 256, 0) == hipSuccess && n > 0 ? n : 1;
+}
+int head32_grid(long long P, int per_cu, int num_cus) {
+  const long long steps4 = ((P + 15) / 16 + 3) / 4;        // 4 waves x 16 pixels per workgroup step
+  return (int)std::max<long long>(1, std::min<long long>(steps4, (long long)per_cu * num_cus));
+}
+int head32_bwd_per_cu() {
+  static int n = std::min({head32_per_cu(reinterpret_cast<const void*>(&head32_kernel<true, true, false>)),
+                           head32_per_cu(reinterpret_cast<const void*>(&head32_kernel<true, false, false>)),
+                           head32_per_cu(reinterpret_cast<const void*>(&head32_kernel<false, true, false>))});
+  return n;
+}
+}  // namespace
+
 int head_ce_bwd_blocks(int C, int K, bool /*defer*/, long long P, int num_cus) {
+  // C = 32: the MFMA kernels — the same grid for every variant, so the deferred / plain /
+  // stats-only paths reduce dWh in the same order (bit-identical weight gradients)
+  if (C == 32) return head32_grid(P, head32_bwd_per_cu(), num_cus);
   int per_cu = 8;
   auto occ = [&](const void* fn) {
     int n = 0;
@@ -713,6 +1129,18 @@ void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
                         const float* gscale, const float* stats3, int /*unused*/, bf16_t* dA,
                         float* dW_partial, int nblocks, long long P, int C, int K,
                         int ignore_index, const float* bn4, float* bnpart, hipStream_t st) {
+  if (C == 32 && K <= MAXK) {
+    if (bn4 != nullptr && dA == nullptr)
+      hipLaunchKernelGGL((head32_kernel<true, false, false>), dim3(nblocks), dim3(256), 0, st, a, Wh, bh,
+                         labels, gscale, stats3, dA, dW_partial, P, ignore_index, bn4, bnpart, K, nullptr);
+    else if (bn4 != nullptr)
+      hipLaunchKernelGGL((head32_kernel<true, true, false>), dim3(nblocks), dim3(256), 0, st, a, Wh, bh,
+                         labels, gscale, stats3, dA, dW_partial, P, ignore_index, bn4, bnpart, K, nullptr);
+    else
+      hipLaunchKernelGGL((head32_kernel<false, true, false>), dim3(nblocks), dim3(256), 0, st, a, Wh, bh,
+                         labels, gscale, stats3, dA, dW_partial, P, ignore_index, bn4, bnpart, K, nullptr);
+    return;
+  }
   if (bn4 != nullptr && dA == nullptr)               // stats pass of the two-pass backward
     HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_ce_bwd_kernel<CC, KK, true, false>), dim3(nblocks), dim3(256), 0,
                                          st, a, Wh, bh, labels, gscale, stats3, dA, dW_partial, P,
@@ -734,6 +1162,10 @@ void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
 bool head_mdw(int C, int K) { return C == 32 && K <= 6; }
 
 int head_fwd_stats_blocks(int C, int K, long long P, int num_cus) {
+  if (C == 32 && K <= MAXK) {
+    static const int n = head32_per_cu(reinterpret_cast<const void*>(&head32_kernel<true, false, true>));
+    return head32_grid(P, n, num_cus);
+  }
   if (!head_mdw(C, K)) return head_ce_bwd_blocks(C, K, true, P, num_cus);
   int per_cu = 8;
   HEAD_SWITCH(C, K, if constexpr (KK <= 6) {
@@ -752,7 +1184,10 @@ void head_ce_fwd_stats_launch(const bf16_t* a, const float* Wh, const float* bh,
                               const int64_t* labels, const float* bn4, float* dW_partial,
                               float* bnpart, float* loss_partial, float* out3, int nblocks,
                               long long P, int C, int K, int ignore_index, hipStream_t st) {
-  if (head_mdw(C, K))
+  if (C == 32 && K <= MAXK)
+    hipLaunchKernelGGL((head32_kernel<true, false, true>), dim3(nblocks), dim3(256), 0, st, a, Wh, bh, labels,
+                       nullptr, nullptr, nullptr, dW_partial, P, ignore_index, bn4, bnpart, K, loss_partial);
+  else if (head_mdw(C, K))
     HEAD_SWITCH(C, K, if constexpr (KK <= 6) {
       hipLaunchKernelGGL((head_fwd_stats_mdw_kernel<KK>), dim3(nblocks), dim3(256), 0, st, a, Wh, bh, labels,
                          dW_partial, P, ignore_index, bn4, bnpart, K, loss_partial);
@@ -774,6 +1209,18 @@ void head_bn_apply_launch(const bf16_t* a, const float* Wh, const float* bh, con
                           const float* gscale, const float* stats3, const float* bn4,
                           const float* coefs, bf16_t* dY, long long P, int C, int K,
                           int ignore_index, hipStream_t st) {
+  if (C == 32 && K <= MAXK) {
+    static const int per_cu = head32_per_cu(reinterpret_cast<const void*>(&head32_apply_kernel));
+    static const int cus = [] {
+      hipDeviceProp_t prop;
+      int dev = 0;
+      hipGetDevice(&dev);
+      return hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
+    }();
+    hipLaunchKernelGGL(head32_apply_kernel, dim3(head32_grid(P, per_cu, cus)), dim3(256), 0, st, a, Wh, bh,
+                       labels, gscale, stats3, bn4, coefs, dY, P, ignore_index, K);
+    return;
+  }
   const int nb = head_bn_apply_blocks(P, C);
   HEAD_SWITCH(C, K, hipLaunchKernelGGL((head_bn_apply_kernel<CC, KK>), dim3(nb), dim3(256), 0, st,
                                        a, Wh, bh, labels, gscale, stats3, bn4, coefs, dY, P,

@@ -256,7 +256,10 @@ def test_conv3_dgrad_split(ops, C1, C2, Cout):
     # layers, ref.py:579,582 at C_out >= 128), with and without the prologue / a concat input
     (4, 32, 32, 256, 0, 256, True), (2, 64, 64, 128, 0, 128, False),
     (2, 32, 32, 256, 256, 256, False), (1, 64, 64, 256, 256, 256, True),
-    (2, 64, 64, 128, 128, 128, True), (2, 40, 56, 128, 0, 128, True)])
+    (2, 64, 64, 128, 128, 128, True), (2, 40, 56, 128, 0, 128, True),
+    # the first decoder conv's shape (32 output channels over a 64 + 32 concat input):
+    # partial tiles, full size
+    (3, 80, 72, 64, 32, 32, False), (1, 256, 256, 64, 32, 32, False)])
 def test_conv3_wgrad(ops, N, H, W, C1, C2, Cout, pro):
     torch.manual_seed(3)
     x1 = torch.randn(N, C1, H, W, device=DEV).bfloat16()
