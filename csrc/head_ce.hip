@@ -719,15 +719,28 @@ DDLPC_DEVICE Head32W head32_weights(const float* __restrict__ Wh, const float* _
 // rounding (o8, the lane's 8 channels) and rounded (pk); LOSS extras: lse, the label's
 // logit, the arg-max class (valid on every lane of the pixel)
 template <bool DEFER, bool LOSS>
-DDLPC_DEVICE void head32_step(const uint4 yv, const int64_t lab, const bool valid, const Head32W& w,
+DDLPC_DEVICE void head32_step(const uint4 yv, const int lab, const bool valid, const Head32W& w,
                               const float (&sc)[8], const float (&sh)[8], float gs, int ignore_index,
-                              int g, float (&y8)[8], float (&f)[8], float (&d)[4], float (&o8)[8],
-                              uint4& pk, float& lse, float& zy, int& am) {
+                              int g, float (&y8)[8], uint4& fb, float (&d)[4], uint2& bh2, uint2& bl2,
+                              float (&o8)[8], uint4& pk, float& lse, float& zy, int& am) {
   unpack8(yv, y8);
+  if (DEFER) {
+    // the activation as materialised (bf16 of relu(y * scale + shift)), packed: two channels
+    // per v_pk_fma_f32, one v_cvt_pk_bf16_f32, ReLU as a packed 16-bit max on the bf16 bits
+    uint32_t o[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = DEFER ? fmaxf(fmaf(y8[j], sc[j], sh[j]), 0.f) : y8[j];
-  const uint4 fb = pack8(f);
-  unpack8(fb, f);                                   // the activation as materialised (bf16)
+    for (int j = 0; j < 4; ++j) {
+      const f32x2_t r2 = __builtin_elementwise_fma(f32x2_t{y8[2 * j], y8[2 * j + 1]},
+                                                   f32x2_t{sc[2 * j], sc[2 * j + 1]},
+                                                   f32x2_t{sh[2 * j], sh[2 * j + 1]});
+      const uint32_t pb = __builtin_bit_cast(uint32_t, __builtin_convertvector(r2, bf16x2_t));
+      o[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2_t, pb),
+                                                                    i16x2_t{0, 0}));
+    }
+    fb = make_uint4(o[0], o[1], o[2], o[3]);
+  } else {
+    fb = yv;
+  }
   const uint4 fz = valid ? fb : make_uint4(0, 0, 0, 0);
   f32x4_t z = mfma16x16x32(w.zh, fz, w.b4);
   z = mfma16x16x32(w.zl, fz, z);
@@ -753,12 +766,15 @@ DDLPC_DEVICE void head32_step(const uint4 yv, const int64_t lab, const bool vali
     zy = rows4_sum(t);
     am = rows4_min_i(c);
   }
-  // dA: hi / lo splits of the dlogits as the B operand (classes 4g..4g+3 of pixel n)
-  float dh[4], dl[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) { dh[i] = lo_bf(pack2(d[i], 0.f)); dl[i] = d[i] - dh[i]; }
-  const uint2 bh2 = make_uint2(pack2(dh[0], dh[1]), pack2(dh[2], dh[3]));
-  const uint2 bl2 = make_uint2(pack2(dl[0], dl[1]), pack2(dl[2], dl[3]));
+  // dA: hi / lo splits of the dlogits as the B operand (classes 4g..4g+3 of pixel n; also the
+  // caller's dWh staging)
+  {
+    const uint32_t h01 = pack2(d[0], d[1]), h23 = pack2(d[2], d[3]);
+    const float dl0 = d[0] - lo_bf(h01), dl1 = d[1] - hi_bf(h01);
+    const float dl2 = d[2] - lo_bf(h23), dl3 = d[3] - hi_bf(h23);
+    bh2 = make_uint2(h01, h23);
+    bl2 = make_uint2(pack2(dl0, dl1), pack2(dl2, dl3));
+  }
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     f32x4_t o = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -843,7 +859,7 @@ __global__ __launch_bounds__(256, 3) void head32_kernel(
     for (int j = 0; j < HEAD32_D; ++j) {
       const long long s = sb + j * wstride;
       const uint4 yv = q4.y[j];
-      const int64_t lab = q4.l[j];
+      const int lab = (int)q4.l[j];
       if (s + HEAD32_D * wstride < steps) load(s + HEAD32_D * wstride, q4.y[j], q4.l[j]);
       if (s >= steps) break;                           // wave-uniform
       const long long px = s * 16 + n;
@@ -858,21 +874,18 @@ __global__ __launch_bounds__(256, 3) void head32_kernel(
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) { sc[jj] = 0.f; sh[jj] = 0.f; }
       }
-      float y8[8], f[8], d[4], o8[8], lse = 0.f, zy = 0.f;
+      float y8[8], d[4], o8[8], lse = 0.f, zy = 0.f;
       int am = 0;
-      uint4 pk;
-      head32_step<DEFER, LOSS>(yv, lab, valid, w, sc, sh, gs, ignore_index, g, y8, f, d, o8, pk, lse, zy, am);
+      uint4 pk, fb;
+      uint2 bh2, bl2;
+      head32_step<DEFER, LOSS>(yv, lab, valid, w, sc, sh, gs, ignore_index, g, y8, fb, d, bh2, bl2, o8, pk,
+                               lse, zy, am);
       if (STORE && valid) *reinterpret_cast<uint4*>(dA + px * C + 8 * g) = pk;
       // dWh via the LDS transpose: act row (the lane's 8 channels; zero for tail pixels),
-      // dlogits hi / lo (the lane's 4 classes)
-      *reinterpret_cast<uint4*>(tA + n * 64 + g * 16) = valid ? pack8(f) : make_uint4(0, 0, 0, 0);
-      {
-        float dh[4], dl[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { dh[i] = lo_bf(pack2(d[i], 0.f)); dl[i] = d[i] - dh[i]; }
-        *reinterpret_cast<uint2*>(tDh + n * 32 + g * 8) = make_uint2(pack2(dh[0], dh[1]), pack2(dh[2], dh[3]));
-        *reinterpret_cast<uint2*>(tDl + n * 32 + g * 8) = make_uint2(pack2(dl[0], dl[1]), pack2(dl[2], dl[3]));
-      }
+      // dlogits hi / lo (the lane's 4 classes; zero for tail pixels already)
+      *reinterpret_cast<uint4*>(tA + n * 64 + g * 16) = valid ? fb : make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint2*>(tDh + n * 32 + g * 8) = bh2;
+      *reinterpret_cast<uint2*>(tDl + n * 32 + g * 8) = bl2;
       const uint2 ah = lds_read_tr16(tDh + rD);
       const uint2 al = lds_read_tr16(tDl + rD);
 #pragma unroll
@@ -883,9 +896,12 @@ __global__ __launch_bounds__(256, 3) void head32_kernel(
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) db[i] += d[i];
-      if (LOSS && g == 0 && valid) {
-        if (lab != ignore_index) { ls[0] += lse - zy; ls[2] += 1.f; }
-        ls[1] += am == lab ? 1.f : 0.f;
+      if (LOSS) {                                    // (branch-free: row g = 0 counts a pixel)
+        const bool cnt_px = g == 0 && valid;
+        const bool lv = cnt_px && lab != ignore_index;
+        ls[0] += lv ? lse - zy : 0.f;
+        ls[2] += lv ? 1.f : 0.f;
+        ls[1] += (cnt_px && am == lab) ? 1.f : 0.f;
       }
       if (DEFER) {
         float r[8];
@@ -899,11 +915,20 @@ __global__ __launch_bounds__(256, 3) void head32_kernel(
         const float4 a0 = kp[0], a1 = kp[1], c0 = kp[8], c1 = kp[9];
         const float xi[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
         const float xm[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        // (packed: two channels per v_pk_fma / v_pk_add; the ReLU mask compares the fp32
+        // y * scale + shift like bn_bwd2_kernel)
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          const float dyh = (valid && fmaf(y8[jj], sc[jj], sh[jj]) > 0.f) ? r[jj] : 0.f;
-          b1[jj] += dyh;
-          b2[jj] = fmaf(dyh, fmaf(y8[jj], xi[jj], xm[jj]), b2[jj]);
+        for (int jj = 0; jj < 8; jj += 2) {
+          const f32x2_t y2 = {y8[jj], y8[jj + 1]};
+          const f32x2_t a2 = __builtin_elementwise_fma(y2, f32x2_t{sc[jj], sc[jj + 1]},
+                                                       f32x2_t{sh[jj], sh[jj + 1]});
+          const f32x2_t x2 = __builtin_elementwise_fma(y2, f32x2_t{xi[jj], xi[jj + 1]},
+                                                       f32x2_t{xm[jj], xm[jj + 1]});
+          const f32x2_t d2 = {(valid && a2.x > 0.f) ? r[jj] : 0.f, (valid && a2.y > 0.f) ? r[jj + 1] : 0.f};
+          f32x2_t s1 = {b1[jj], b1[jj + 1]}, s2 = {b2[jj], b2[jj + 1]};
+          s1 += d2;
+          s2 = __builtin_elementwise_fma(d2, x2, s2);
+          b1[jj] = s1.x; b1[jj + 1] = s1.y; b2[jj] = s2.x; b2[jj + 1] = s2.y;
         }
       }
     }
@@ -999,7 +1024,7 @@ __global__ __launch_bounds__(256, 3) void head32_apply_kernel(
     for (int j = 0; j < HEAD32_DA; ++j) {
       const long long s = sb + j * wstride;
       const uint4 yv = q4.y[j];
-      const int64_t lab = q4.l[j];
+      const int lab = (int)q4.l[j];
       if (s + HEAD32_DA * wstride < steps) load(s + HEAD32_DA * wstride, q4.y[j], q4.l[j]);
       if (s >= steps) break;
       const long long px = s * 16 + n;
@@ -1007,10 +1032,12 @@ __global__ __launch_bounds__(256, 3) void head32_apply_kernel(
       float sc[8], sh[8];
       k8(0, sc);
       k8(1, sh);
-      float y8[8], f[8], d[4], o8[8], lse, zy;
+      float y8[8], d[4], o8[8], lse, zy;
       int am;
-      uint4 pk;
-      head32_step<true, false>(yv, lab, valid, w, sc, sh, gs, ignore_index, g, y8, f, d, o8, pk, lse, zy, am);
+      uint4 pk, fb;
+      uint2 bh2, bl2;
+      head32_step<true, false>(yv, lab, valid, w, sc, sh, gs, ignore_index, g, y8, fb, d, bh2, bl2, o8, pk,
+                               lse, zy, am);
       float rr[8], o[8], is[8], nm[8], k1[8], m1[8], m2[8];
       unpack8(pk, rr);
       k8(2, is); k8(3, nm); k8(4, k1); k8(5, m1); k8(6, m2);

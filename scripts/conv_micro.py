@@ -147,6 +147,22 @@ def main():
                "tbwds": lambda: (F.convt_dgrad(dout, pk.dgrad, C, x, bn4), F.convt_wgrad(x, dout, None, None, None, bn4))}
         for ps in tpasses:
             fn = fns[ps]
+            if a.ab:
+                knob, vals = a.ab.split(":")
+                vals = [int(v) for v in vals.split(",")]
+                samples = {v: [] for v in vals}
+                for v in vals:                       # warm every variant once
+                    F.set_knob(knob, v)
+                    fn()
+                for _ in range(a.rounds):
+                    for v in vals:
+                        F.set_knob(knob, v)
+                        samples[v].append(_time(fn, a.iters))
+                med = {v: sorted(x)[len(x) // 2] for v, x in samples.items()}
+                print(f"{name:8s} {ps:6s} " + "  ".join(
+                    f"{knob}={v}: {med[v]:8.1f} us {flops / med[v] / 1e6:7.1f} TF/s" for v in vals),
+                    flush=True)
+                continue
             fn()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
