@@ -166,7 +166,7 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
                                   const c10::optional<at::Tensor>& pscale2,
                                   const c10::optional<at::Tensor>& pshift2,
                                   const c10::optional<at::Tensor>& bnb_y,
-                                  const c10::optional<at::Tensor>& bnb_s4) {
+                                  const c10::optional<at::Tensor>& bnb_s4, int64_t groups) {
   CHECK_DEV(x1); CHECK_CONTIG(x1); CHECK_BF16(x1); CHECK_BF16(w); CHECK_CONTIG(w);
   c10::DeviceGuard guard(x1.device());
   const Geo g = geo_of(x1);
@@ -193,6 +193,24 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   a.Co1 = co1 > 0 ? (int)co1 : (int)cout;
   TORCH_CHECK(a.Cout % 8 == 0 && a.Co1 % 8 == 0, "Cout and Co1 must be multiples of 8");
   if (pscale.has_value() && pscale->defined()) TORCH_CHECK(a.C1 <= 512, "prologue supports C1 <= 512");
+  // BN groups (ConvFwdArgs::groups): group-major statistics rows; pscale / pshift (and the
+  // BNB table) per group — pscale / pshift are [groups][C1] views with a common row stride
+  // (the scale / shift rows of group statistics [groups][4][C1])
+  const bool grouped = groups > 1;
+  if (grouped) {
+    TORCH_CHECK(groups <= 1024 && g.N % groups == 0, "conv3_fwd: groups must divide the batch");
+    TORCH_CHECK(!(pscale2.has_value() && pscale2->defined()), "conv3_fwd groups: no X2 prologue");
+    a.groups = (int)groups;
+    if (pscale.has_value() && pscale->defined()) {
+      TORCH_CHECK(pshift.has_value() && pshift->defined(), "conv3_fwd groups: pscale needs pshift");
+      CHECK_F32(*pscale); CHECK_F32(*pshift);
+      TORCH_CHECK(pscale->dim() == 2 && pscale->size(0) == groups && pscale->size(1) == g.C &&
+                  pscale->stride(1) == 1 && pshift->sizes() == pscale->sizes() &&
+                  pshift->strides() == pscale->strides(),
+                  "conv3_fwd groups: pscale / pshift must be [groups][C1] views with one row stride");
+      a.gstride = pscale->stride(0);
+    }
+  }
   a.X1 = bptr(x1);
   a.X2 = dual ? bptr(*x2) : nullptr;
   a.pscale = fptr_opt(pscale);
@@ -207,8 +225,10 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   if (bnb_y.has_value() && bnb_y->defined()) {
     // BN-backward epilogue: the stats rows become that BN's (sum dyh, sum dyh*xhat) partials
     CHECK_CONTIG(*bnb_y); CHECK_BF16(*bnb_y);
-    TORCH_CHECK(bnb_s4.has_value() && bnb_s4->defined() && bnb_s4->numel() == 4 * cout,
-                "bnb: stats4 [4][Cout] required");
+    const int64_t ng = grouped ? groups : 1;
+    TORCH_CHECK(bnb_s4.has_value() && bnb_s4->defined() && bnb_s4->numel() == ng * 4 * cout,
+                "bnb: stats4 [4][Cout] ([groups][4][Cout] with groups) required");
+    if (grouped) a.gstride = 4LL * cout;
     CHECK_F32(*bnb_s4); CHECK_CONTIG(*bnb_s4);
     const Geo gy = geo_of(*bnb_y);
     TORCH_CHECK(g.dims == 2 && gy.N == g.N && gy.H == g.H && gy.W == g.W && gy.C == cout,
@@ -308,7 +328,7 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   {
     const int items = a.nTilesM * a.nTilesN;
     int best = 1;
-    if (items < num_cus())
+    if (items < num_cus() && !grouped)      // (BN groups: group-major rows, no split-K)
       for (int ks = 2; ks <= 8; ++ks)
         if (nchunks_total % ks == 0 && nchunks_total / ks >= 2 && items * ks <= 2 * num_cus())
           best = ks;
@@ -325,10 +345,7 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   const int fin_grid = (int)std::min<long long>(
       std::max<long long>(1, (a.npix + fin_px_per_block - 1) / fin_px_per_block), 2048);
   if (want_stats) {
-    const int items = a.nTilesM * a.nTilesN * a.ksplit;
-    const int q = a.nTilesN * a.ksplit;
-    const int grid = a.ksplit > 1 ? fin_grid
-                                  : (items > a.persist_blocks ? a.persist_blocks / q * q : items);
+    const int grid = a.ksplit > 1 ? fin_grid : conv3_fwd_grid(a);
     stats = at::empty({(int64_t)grid, 2, a.Cout}, opts.dtype(at::kFloat));
   }
   a.Y1 = bptr_mut(y1);
@@ -349,7 +366,8 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
                        const c10::optional<at::Tensor>& pshift2,
                        const c10::optional<at::Tensor>& dy_y,
                        const c10::optional<at::Tensor>& dy_s4,
-                       const c10::optional<at::Tensor>& dy_coefs, int64_t cin_real) {
+                       const c10::optional<at::Tensor>& dy_coefs, int64_t cin_real,
+                       int64_t groups) {
   CHECK_DEV(dy); CHECK_CONTIG(dy); CHECK_BF16(dy); CHECK_CONTIG(x1); CHECK_BF16(x1);
   c10::DeviceGuard guard(dy.device());
   const Geo g = geo_of(x1);
@@ -372,6 +390,19 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   a.pscale2 = fptr_opt(pscale2);
   a.pshift2 = fptr_opt(pshift2);
   if (a.pscale) TORCH_CHECK(a.C1 <= 512, "prologue supports C1 <= 512");
+  // BN groups: the X1 prologue constants per group of images (pscale / pshift: [groups][C1]
+  // views with one row stride, as conv3_fwd's); v3 kernel only (checked below)
+  if (groups > 1 && a.pscale != nullptr) {
+    TORCH_CHECK(groups <= 1024 && g.N % groups == 0, "conv3_wgrad: groups must divide the batch");
+    TORCH_CHECK(a.pscale2 == nullptr && !dual, "conv3_wgrad groups: single input, no X2 prologue");
+    TORCH_CHECK(pscale->dim() == 2 && pscale->size(0) == groups && pscale->size(1) == a.C1 &&
+                pscale->stride(1) == 1 && pshift->sizes() == pscale->sizes() &&
+                pshift->strides() == pscale->strides(),
+                "conv3_wgrad groups: pscale / pshift must be [groups][C1] views with one row stride");
+    a.groups = (int)groups;
+    a.gimg = g.N / (int)groups;
+    a.gstride = pscale->stride(0);
+  }
   if (a.pscale2) TORCH_CHECK(dual && a.pshift2 && a.C1 + a.C2 <= 512, "X2 prologue: x2, pscale2/pshift2, C1 + C2 <= 512");
   int bco = a.Cout <= 32 ? 32 : 64;
   // v2 / v3 (LDS-DMA pixel tiles 16 wide; narrower images run with masked columns: the 8x8
@@ -441,6 +472,7 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   a.partial = part.data_ptr<float>();
   TORCH_CHECK(a.pscale2 == nullptr || v2, "X2 prologue needs the v2/v3 weight-gradient kernels "
               "(2-D or 3-D, W >= 16, C1 % 32 == 0)");
+  TORCH_CHECK(a.groups <= 1 || (v3 && !img), "conv3_wgrad groups: the v3 kernel only (W >= 8, C1 % 32 == 0)");
   if (img) conv3_wgrad_img_launch(a, bco, cur_stream());
   else if (v3) conv3_wgrad3_launch(a, bco, cur_stream());
   else if (v2) conv3_wgrad2_launch(a, bco, cur_stream());
@@ -676,6 +708,33 @@ at::Tensor bn_group_finalize(const at::Tensor& y, int64_t groups, const at::Tens
   return st;
 }
 
+// the same statistics from partial rows a conv epilogue wrote group-major (conv3_fwd with
+// groups): partial [groups * nb][2][C], count = pixels per group
+at::Tensor bn_group_finalize_rows(const at::Tensor& partial, int64_t groups, double count,
+                                  const at::Tensor& gamma, const at::Tensor& beta, double eps,
+                                  const c10::optional<at::Tensor>& arena, int64_t aoff) {
+  CHECK_DEV(partial); CHECK_F32(partial); CHECK_CONTIG(partial); CHECK_F32(gamma); CHECK_F32(beta);
+  c10::DeviceGuard guard(partial.device());
+  const int64_t C = gamma.numel();
+  TORCH_CHECK(groups >= 1 && groups <= 1024 && partial.numel() % (groups * 2 * C) == 0,
+              "bn_group_finalize_rows: partial [groups * nb][2][C]");
+  const int nb = (int)(partial.numel() / (groups * 2 * C));
+  at::Tensor st = at::empty({groups, 4, C}, partial.options());
+  float* ap = nullptr;
+  long long astride = 0;
+  if (arena.has_value() && arena->defined()) {
+    CHECK_F32(*arena);
+    TORCH_CHECK(arena->dim() == 2 && arena->size(0) >= groups && arena->stride(1) == 1 &&
+                aoff + 2 * C <= arena->size(1), "arena [rows >= groups][>= aoff + 2C]");
+    ap = arena->data_ptr<float>() + aoff;
+    astride = arena->stride(0);
+  }
+  bn_group_finalize_rows_launch(partial.data_ptr<float>(), nb, (int)groups, (long long)count, (int)C,
+                                gamma.data_ptr<float>(), beta.data_ptr<float>(), (float)eps,
+                                st.data_ptr<float>(), ap, astride, cur_stream());
+  return st;
+}
+
 std::vector<at::Tensor> bn_group_apply(const at::Tensor& y, const at::Tensor& stats4,
                                        int64_t groups, bool pool) {
   CHECK_DEV(y); CHECK_CONTIG(y); CHECK_BF16(y); CHECK_F32(stats4); CHECK_CONTIG(stats4);
@@ -705,7 +764,8 @@ std::vector<at::Tensor> bn_group_backward(const c10::optional<at::Tensor>& dA,
                                           const at::Tensor& stats4, const at::Tensor& gamma,
                                           int64_t groups,
                                           const c10::optional<at::Tensor>& dgamma_out,
-                                          const c10::optional<at::Tensor>& dbeta_out) {
+                                          const c10::optional<at::Tensor>& dbeta_out,
+                                          const c10::optional<at::Tensor>& partial) {
   CHECK_DEV(y); CHECK_CONTIG(y); CHECK_BF16(y); CHECK_F32(stats4); CHECK_CONTIG(stats4);
   c10::DeviceGuard guard(y.device());
   const Geo g = geo_of(y);
@@ -722,9 +782,17 @@ std::vector<at::Tensor> bn_group_backward(const c10::optional<at::Tensor>& dA,
   const int Ng = g.N / (int)groups;
   const long long items = (long long)Ng * (hasP ? (g.dims == 3 ? g.D / 2 : 1) * (g.H / 2) * (g.W / 2)
                                                 : (long long)g.D * g.H * g.W);
-  const int nb = bn_group_bwd_rows(items, (int)groups);
+  // partial: group-major rows [groups * nb][2][C] of (sum dyh, sum dyh * xhat) from the
+  // data-gradient conv's BN-backward epilogue (conv3_fwd with bnb_y and groups)
+  const bool have_part = partial.has_value() && partial->defined();
+  if (have_part) {
+    CHECK_F32(*partial); CHECK_CONTIG(*partial);
+    TORCH_CHECK(!hasP && partial->numel() % (groups * 2 * C) == 0,
+                "bn_group_backward: partial [groups * nb][2][C], no pooled gradient");
+  }
+  const int nb = have_part ? (int)(partial->numel() / (groups * 2 * C)) : bn_group_bwd_rows(items, (int)groups);
   auto fopts = y.options().dtype(at::kFloat);
-  at::Tensor part = at::empty({groups, nb, 2, C}, fopts);
+  at::Tensor part = have_part ? *partial : at::empty({groups, nb, 2, C}, fopts);
   at::Tensor coefs = at::empty({groups, 3, C}, fopts);
   const bool into = dgamma_out.has_value() && dgamma_out->defined();
   at::Tensor dgamma = into ? *dgamma_out : at::empty({C}, fopts);
@@ -734,7 +802,7 @@ std::vector<at::Tensor> bn_group_backward(const c10::optional<at::Tensor>& dA,
                            stats4.data_ptr<float>(), gamma.data_ptr<float>(), dgamma.data_ptr<float>(),
                            dbeta.data_ptr<float>(), into, coefs.data_ptr<float>(),
                            part.data_ptr<float>(), nb, bptr_mut(dY), g.dims, (int)groups, Ng, g.D,
-                           g.H, g.W, C, cur_stream());
+                           g.H, g.W, C, cur_stream(), have_part);
   return {dY, dgamma, dbeta};
 }
 
@@ -1389,10 +1457,10 @@ TORCH_LIBRARY(ddlpc, m) {
   m.def("comm_proxy(Tensor(a!) g, int blocks, int passes) -> ()");
   m.def("conv3_fwd(Tensor x1, Tensor? x2, Tensor w, Tensor? bias, Tensor? pscale, Tensor? pshift, "
         "int cout, int co1, bool stats, Tensor? pscale2=None, Tensor? pshift2=None, Tensor? bnb_y=None, "
-        "Tensor? bnb_s4=None) -> Tensor[]");
+        "Tensor? bnb_s4=None, int groups=0) -> Tensor[]");
   m.def("conv3_wgrad(Tensor dy, Tensor x1, Tensor? x2, Tensor? pscale, Tensor? pshift, Tensor(a!)? out=None, "
         "Tensor? pscale2=None, Tensor? pshift2=None, Tensor? dy_y=None, Tensor? dy_s4=None, "
-        "Tensor? dy_coefs=None, int cin_real=0) -> Tensor");
+        "Tensor? dy_coefs=None, int cin_real=0, int groups=0) -> Tensor");
   m.def("reduce_rows(Tensor partial, int R, int N) -> Tensor");
   m.def("bn_finalize(Tensor partial, float count, Tensor gamma, Tensor beta, Tensor(a!) running_mean, "
         "Tensor(b!) running_var, float momentum, float eps, bool update_running, Tensor(c!)? nbt) -> Tensor");
@@ -1406,7 +1474,9 @@ TORCH_LIBRARY(ddlpc, m) {
   m.def("bn_group_apply(Tensor y, Tensor stats4, int groups, bool pool) -> Tensor[]");
   m.def("bn_running_apply_all(Tensor entries, Tensor(a!) arena, int K, int maxC, float momentum) -> ()");
   m.def("bn_group_backward(Tensor? dA, Tensor? dP, Tensor y, Tensor stats4, Tensor gamma, int groups, "
-        "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None) -> Tensor[]");
+        "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None, Tensor? partial=None) -> Tensor[]");
+  m.def("bn_group_finalize_rows(Tensor partial, int groups, float count, Tensor gamma, Tensor beta, "
+        "float eps, Tensor(a!)? arena=None, int aoff=0) -> Tensor");
   m.def("bn_backward(Tensor? dA, Tensor? dP, Tensor y, Tensor stats4, Tensor gamma, Tensor? gscale, "
         "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None, Tensor? partial=None) -> Tensor[]");
   m.def("convt_fwd(Tensor x, Tensor wt, Tensor? bias, int cout, Tensor? bn4=None) -> Tensor");
@@ -1458,6 +1528,7 @@ TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
   m.impl("bn_group_apply", &ddlpc::bn_group_apply);
   m.impl("bn_running_apply_all", &ddlpc::bn_running_apply_all);
   m.impl("bn_group_backward", &ddlpc::bn_group_backward);
+  m.impl("bn_group_finalize_rows", &ddlpc::bn_group_finalize_rows);
   m.impl("convt_fwd", &ddlpc::convt_fwd);
   m.impl("convt_dgrad", &ddlpc::convt_dgrad);
   m.impl("convt_wgrad", &ddlpc::convt_wgrad);

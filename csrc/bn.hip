@@ -772,16 +772,28 @@ void bn_group_stats_finalize_launch(const bf16_t* y, int groups, long long gpix,
 
 int bn_group_stats_rows(long long gpix, int C, int groups) { return bn_group_rows(gpix, C, groups); }
 
+// statistics from partial rows a producer already wrote group-major ([groups][nb][2][C]: the
+// conv epilogues' rows in BN-group mode, ConvFwdArgs::groups)
+void bn_group_finalize_rows_launch(const float* partial, int nb, int groups, long long gpix, int C,
+                                   const float* gamma, const float* beta, float eps, float* out4,
+                                   float* arena, long long astride, hipStream_t st) {
+  hipLaunchKernelGGL(bn_group_finalize_kernel, dim3(C), dim3(kGW * 64), 0, st, partial, nb, groups, C,
+                     (double)gpix, gamma, beta, eps, out4, arena, astride);
+}
+
 void bn_group_backward_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y,
                               const float* stats4, const float* gamma, float* dgamma, float* dbeta,
                               bool accumulate, float* coefs, float* partial_scratch, int nb,
                               bf16_t* dY, int dims, int groups, int N, int D, int H, int W, int C,
-                              hipStream_t st) {
+                              hipStream_t st, bool have_partial) {
   const bool pool = dP != nullptr;
   const long long sstride = 4LL * C;
   const float* s = stats4;
-  bn_bwd2_launch<0>(nb, dims, pool, dA, dP, y, s + 2 * C, s + 3 * C, s, s + C, nullptr, nullptr,
-                    partial_scratch, nullptr, N, D, H, W, C, st, groups, sstride);
+  // have_partial: the rows [groups][nb][2][C] came from the data-gradient conv's BN-backward
+  // epilogue (ConvFwdArgs::bnb_y in group mode) — no reduction pass
+  if (!have_partial)
+    bn_bwd2_launch<0>(nb, dims, pool, dA, dP, y, s + 2 * C, s + 3 * C, s, s + C, nullptr, nullptr,
+                      partial_scratch, nullptr, N, D, H, W, C, st, groups, sstride);
   const double count = (double)N * D * H * W;
   hipLaunchKernelGGL(bn_group_grad_finalize_kernel, dim3(C), dim3(kGW * 64), 0, st, partial_scratch, nb,
                      groups, C, count, gamma, stats4, dgamma, dbeta, coefs, accumulate ? 1 : 0);

@@ -102,31 +102,41 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   const int halo = (DIMS == 3 ? p.TD + 2 : 1) * HH2 * HW2;
   const long long img_px = (long long)p.D * p.H * p.W;
   const int KS = p.ksplit;                        // channel-chunk split (small layers)
-  const int n_items = p.nTilesM * p.nTilesN * KS;
-  const int my_items = n_items > (int)blockIdx.x ? (n_items - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  // M-tile walk: workgroup b = blockIdx.x / (KS * nTilesN) serves M tiles m0 + k * Gs.  One
+  // group: m0 = b, Gs = the workgroups per n tile.  BN groups (ConvFwdArgs::groups): group-
+  // major — b = grp * Gs + r serves tiles grp * Mg + r + k * Gs of its own group only
+  const int Q = KS * p.nTilesN;
+  const int NG_ = p.groups > 1 ? p.groups : 1;
+  const int Gs = (int)gridDim.x / (Q * NG_);
+  const int Mg = p.nTilesM / NG_;                  // M tiles per group
+  const int grp = (int)blockIdx.x / Q / Gs;
+  const int r_blk = (int)blockIdx.x / Q % Gs;
+  const int my_items = r_blk < Mg ? (Mg - 1 - r_blk) / Gs + 1 : 0;
   const int nchunks = ((p.Cin + BK - 1) / BK) / KS;  // chunks per item (KS divides the total)
   const int spi = nchunks * NG;                   // stages per item
   const int S = my_items * spi;
 
   const bool has_pro = p.pscale != nullptr;
   const bool has_pro2 = p.pscale2 != nullptr;         // deferred skip: X2 channels at C1 + c
-  if (has_pro)
-    for (int c = tid; c < p.C1; c += C::NTH) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
+  if (has_pro) {
+    const float* psc = p.pscale + grp * p.gstride;    // (BN groups: this workgroup's group)
+    const float* psh = p.pshift + grp * p.gstride;
+    for (int c = tid; c < p.C1; c += C::NTH) { s_scale[c] = psc[c]; s_shift[c] = psh[c]; }
+  }
   if (has_pro2)
     for (int c = tid; c < p.C2; c += C::NTH) { s_scale[p.C1 + c] = p.pscale2[c]; s_shift[p.C1 + c] = p.pshift2[c]; }
 
   const auto rW = make_rsrc(p.Wt, (unsigned)((long long)p.Cout * p.taps * p.CinW * 2));
 
   struct Item { int n_img, d0, h0, w0, co0, ks; };
-  // work item k of this workgroup is blockIdx.x + k * gridDim.x with gridDim.x a multiple of
-  // KS * nTilesN (launcher), so its channel split ks and n tile are the block's own and its
-  // M tile is m0 + k * Gs: the item geometry comes from carry-walkers (one add-and-carry step
-  // per item) instead of five runtime integer divisions per call; one walker per consumer
-  // (halo issue, epilogue, BNB y loads), each visiting the items in order
+  // work item k of this workgroup: gridDim.x is a multiple of KS * nTilesN (launcher), so its
+  // channel split ks and n tile are the block's own and its M tile is m0 + k * Gs: the item
+  // geometry comes from carry-walkers (one add-and-carry step per item) instead of five
+  // runtime integer divisions per call; one walker per consumer (halo issue, epilogue, BNB y
+  // loads), each visiting the items in order
   const int ks_blk = (int)blockIdx.x % KS;
   const int co0_item = (int)blockIdx.x / KS % p.nTilesN * BN;
   struct Walk { int k, tw, th, td, n; };
-  const int Gs = (int)gridDim.x / (KS * p.nTilesN);
   int g_w, g_h, g_d, g_n;
   {
     int q = Gs;
@@ -136,7 +146,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   }
   Walk w0;
   {
-    int m = (int)blockIdx.x / (KS * p.nTilesN);
+    int m = grp * Mg + r_blk;
     w0.k = 0;
     w0.tw = m % p.tilesW; m /= p.tilesW;
     w0.th = m % p.tilesH; m /= p.tilesH;
@@ -180,7 +190,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   const int co0_blk = (int)blockIdx.x / KS % p.nTilesN * BN;
   // BNB (a data gradient: no prologue, so the prologue constants' LDS holds the BN-backward
   // table [4][BN]; published by the first stage barrier)
-  if constexpr (BNB) bnb_fill(s_scale, BN, co0_blk, p.Cout, p.bnb_s4, tid, C::NTH);
+  if constexpr (BNB) bnb_fill(s_scale, BN, co0_blk, p.Cout, p.bnb_s4 + grp * p.gstride, tid, C::NTH);
   int b_off[C::B_ITERS];
 #pragma unroll
   for (int i = 0; i < C::B_ITERS; ++i) {
@@ -854,6 +864,27 @@ __global__ void conv_splitk_finalize_kernel(const float* __restrict__ part, int 
     }
 }
 
+}  // namespace
+
+// persistent grid of the streaming kernel: one workgroup per item up to persist_blocks, a
+// multiple of KS * nTilesN (every block stays on one n tile and channel split); BN groups:
+// groups x R x (KS * nTilesN) with R workgroups per (group, n tile) — as many as fit the
+// persistent grid, at least one, at most the group's M tiles
+int conv3_fwd_grid(const ConvFwdArgs& a) {
+  const int q = a.nTilesN * a.ksplit;
+  if (a.groups > 1) {
+    const int Mg = a.nTilesM / a.groups;
+    const int cap = a.persist_blocks > 0 ? a.persist_blocks : a.nTilesM * q;
+    const int R = std::max(1, std::min(Mg, cap / (a.groups * q)));
+    return a.groups * R * q;
+  }
+  int grid = a.nTilesM * q;
+  if (a.persist_blocks > 0 && grid > a.persist_blocks) grid = a.persist_blocks / q * q;
+  return grid;
+}
+
+namespace {
+
 template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, int FDB>
 void launch_mode(ConvFwdArgs& a, int grid, hipStream_t st) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
@@ -871,12 +902,7 @@ void launch_mode(ConvFwdArgs& a, int grid, hipStream_t st) {
 template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB = 2>
 void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
-  const int items = a.nTilesM * a.nTilesN * a.ksplit;
-  int grid = items;
-  if (a.persist_blocks > 0 && grid > a.persist_blocks) {
-    const int q = a.nTilesN * a.ksplit;          // keeps each block on one n tile
-    grid = a.persist_blocks / q * q;
-  }
+  const int grid = conv3_fwd_grid(a);
   a.stat_rows = grid;
   // rolling fragment pipeline (pipe_taps): every configuration (the whole-tap register
   // double buffer and no buffering measured slower: profiles/r3s/conv_ab_pipe_r3s1.txt)
@@ -886,12 +912,7 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
 // cfg 5 (BM-512, LEAN tiles: never with the BN-backward epilogue) on the rolling pipeline
 void launch_cfg5(ConvFwdArgs& a, hipStream_t st) {
   using C = Cfg<2, 4, 2, 8, 4, 640, 2>;
-  const int items = a.nTilesM * a.nTilesN * a.ksplit;
-  int grid = items;
-  if (a.persist_blocks > 0 && grid > a.persist_blocks) {
-    const int q = a.nTilesN * a.ksplit;
-    grid = a.persist_blocks / q * q;
-  }
+  const int grid = conv3_fwd_grid(a);
   a.stat_rows = grid;
   hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 640, 2, 2, false>), dim3(grid),
                      dim3(C::NTH), C::SMEM, st, a);

@@ -98,19 +98,28 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   const int halo = NPL * PL;
   const long long img_px = (long long)p.H * p.W;      // one slice
   const long long vol_px = NPL == 3 ? (long long)p.D * img_px : img_px;   // one image
-  const int n_items = p.nTilesM * p.nTilesN;
-  const int my_items = n_items > (int)blockIdx.x ? (n_items - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  // M-tile walk (conv3_fwd_kernel's): workgroup b = blockIdx.x / nTilesN serves M tiles
+  // grp * Mg + r + k * Gs — one group: grp = 0, r = b; BN groups: group-major blocks
+  const int NG_ = p.groups > 1 ? p.groups : 1;
+  const int Gs = (int)gridDim.x / (p.nTilesN * NG_);
+  const int Mg = p.nTilesM / NG_;
+  const int grp = (int)blockIdx.x / p.nTilesN / Gs;
+  const int r_blk = (int)blockIdx.x / p.nTilesN % Gs;
+  const int my_items = r_blk < Mg ? (Mg - 1 - r_blk) / Gs + 1 : 0;
   const int nch = TAP8 ? 1 : (p.Cin + BK - 1) / BK;
   const int S = my_items * nch;
   // every item of a block has the same n tile (launcher: grid % nTilesN == 0)
   const int co0 = (int)blockIdx.x % p.nTilesN * BN;
 
-  if (has_pro)
-    for (int c = tid; c < p.C1; c += C::NTH) { s_scale[c] = p.pscale[c]; s_shift[c] = p.pshift[c]; }
+  if (has_pro) {
+    const float* psc = p.pscale + grp * p.gstride;      // (BN groups: this workgroup's group)
+    const float* psh = p.pshift + grp * p.gstride;
+    for (int c = tid; c < p.C1; c += C::NTH) { s_scale[c] = psc[c]; s_shift[c] = psh[c]; }
+  }
   if (has_pro2)
     for (int c = tid; c < p.C2; c += C::NTH) { s_scale[p.C1 + c] = p.pscale2[c]; s_shift[p.C1 + c] = p.pshift2[c]; }
   float* s_bnb = reinterpret_cast<float*>(smem);       // BNB: [4][BN] (published by the first barrier)
-  if constexpr (BNB) bnb_fill(s_bnb, BN, co0, p.Cout, p.bnb_s4, tid, C::NTH);
+  if constexpr (BNB) bnb_fill(s_bnb, BN, co0, p.Cout, p.bnb_s4 + grp * p.gstride, tid, C::NTH);
 
   // bias of this block's channel tile, loaded once (a global load inside the epilogue would
   // make the compiler wait vmcnt(0) — on this tile's stores — before every use); loaded
@@ -152,18 +161,16 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_res_
   // n_img: the slice (image * D + d; 2-D: the image) — outputs are slice-addressed
   struct Item { int n_img, img, d, h0, w0; };
   // item geometry without integer division in the stage loop: item k of this workgroup is
-  // blockIdx.x + k * gridDim.x (gridDim.x a multiple of nTilesN: launcher), i.e. M tile
-  // m0 + k * Gs; a walker steps (tw, th, slice) by Gs with carries, the slice as (image, d).
-  // One walker per consumer (halo issue, epilogue, BNB y loads), each visiting the items in
-  // order
+  // M tile m0 + k * Gs (gridDim.x a multiple of nTilesN: launcher); a walker steps (tw, th,
+  // slice) by Gs with carries, the slice as (image, d).  One walker per consumer (halo issue,
+  // epilogue, BNB y loads), each visiting the items in order
   struct Walk { int k, tw, th, img, d; };
-  const int Gs = (int)gridDim.x / p.nTilesN;
   const int g_w = Gs % p.tilesW, g_q = Gs / p.tilesW;
   const int g_h = g_q % p.tilesH, g_n = g_q / p.tilesH;
   const int g_d = NPL == 3 ? g_n % p.D : 0, g_i = NPL == 3 ? g_n / p.D : g_n;
   Walk w0;
   {
-    int m = (int)blockIdx.x / p.nTilesN;
+    int m = grp * Mg + r_blk;
     w0.k = 0; w0.tw = m % p.tilesW; m /= p.tilesW; w0.th = m % p.tilesH; m /= p.tilesH;
     w0.d = NPL == 3 ? m % p.D : 0; w0.img = NPL == 3 ? m / p.D : m;
   }
@@ -806,6 +813,11 @@ int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
     const int cap = bpc * num_cus;
     if (items < cap) return -1;                         // too small: streaming kernel
     grid = cap / a.nTilesN * a.nTilesN;
+    if (a.groups > 1) {
+      // BN groups: group-major blocks, R per (group, n tile) (conv3_res_kernel's walk)
+      const int R = std::max(1, std::min(a.nTilesM / a.groups, cap / (a.groups * a.nTilesN)));
+      grid = a.groups * R * a.nTilesN;
+    }
     smem = sm;
     a.ksplit = 1;
     a.persist_blocks = cap;

@@ -844,10 +844,24 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
     }
   };
 
+  // BN groups (ConvWgradArgs::groups, X1 prologue only): the tile's image decides its group;
+  // a workgroup's tiles are contiguous, so the constants reload only at a group boundary —
+  // after the full drain below, with no DMA in flight
+  int cur_grp = 0;
   if (t_begin < t_end) issue(t_begin, 0);
   for (int tile = t_begin; tile < t_end; ++tile) {
     const int buf = (tile - t_begin) & 1;
     dma_wait<0>();
+    if (p.groups > 1 && any_pro) {
+      const int gg = tw.n / p.gimg;                 // (tw: this tile, the last one issued)
+      if (gg != cur_grp) {
+        cur_grp = gg;
+#pragma unroll
+        for (int cw = 0; cw < CIW; ++cw)
+          pro8_load(p.pscale + gg * p.gstride, p.pshift + gg * p.gstride, nullptr, nullptr, p.C1,
+                    ci0 + cw * BK + (lane & 3) * 8, p.C1, psc[cw], psh[cw]);
+      }
+    }
     if (any_pro) transform(sX(buf));
     lds_sync();
     if (tile + 1 < t_end) issue(tile + 1, buf ^ 1);

@@ -48,9 +48,19 @@ struct ConvFwdArgs {
   // single output, no prologue.
   const bf16_t* bnb_y;            // y [N][H][W][Cout] (pre-BN activations of that layer)
   const float* bnb_s4;            // [4][Cout]: mean, invstd, scale, shift
+  // per-micro-batch BatchNorm groups (a batched accumulation window, UNetEngine.bn_groups):
+  // groups > 1 splits the batch into `groups` equal runs of images and walks the M tiles
+  // GROUP-MAJOR — workgroup b serves group b / (R * nTilesN * ksplit) only (R = workgroups per
+  // (group, n tile), launcher-chosen) — so every statistics row (forward (sum, sum^2) or the
+  // BN-backward partials) belongs to one group: rows [groups][R * nTilesN][2][Cout], and the
+  // prologue constants (pscale / pshift) and the BNB table (bnb_s4) of group g sit at
+  // + g * gstride floats.  ksplit must be 1.
+  int groups;
+  long long gstride;
 };
 void conv3_splitk_finalize_launch(ConvFwdArgs& a, int grid, hipStream_t st);
 void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st);
+int conv3_fwd_grid(const ConvFwdArgs& a);       // the streaming kernel's grid (= statistics rows)
 int conv3_fwd_cfg_wm(int cfg);
 // resident-weight kernel for high-resolution few-channel layers (conv3x3_res.hip)
 int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem);
@@ -84,6 +94,11 @@ struct ConvWgradArgs {
   const float* dys4;
   const float* dycoef;
   int ciw;                        // v3: 32-channel input chunks per workgroup (1 or 2)
+  // per-micro-batch BatchNorm groups (v3 only): images [g * gimg, (g+1) * gimg) use the
+  // prologue constants pscale / pshift + g * gstride (the X1 prologue; no X2 prologue)
+  int groups;
+  int gimg;
+  long long gstride;
 };
 void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st);
 // LDS-DMA variant (1 x TH x 16 pixel tiles of conv3_wgrad2_pt(bco) pixels; 3-D: planes = 3,
@@ -177,7 +192,10 @@ void bn_group_backward_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* 
                               const float* stats4, const float* gamma, float* dgamma, float* dbeta,
                               bool accumulate, float* coefs, float* partial_scratch, int nb,
                               bf16_t* dY, int dims, int groups, int N, int D, int H, int W, int C,
-                              hipStream_t st);
+                              hipStream_t st, bool have_partial = false);
+void bn_group_finalize_rows_launch(const float* partial, int nb, int groups, long long gpix, int C,
+                                   const float* gamma, const float* beta, float eps, float* out4,
+                                   float* arena, long long astride, hipStream_t st);
 
 // ---------------------------------------------------------------- head + cross-entropy
 bool head_supported(int C, int K);

@@ -126,6 +126,16 @@ class _BNState:
         off = eng._bn_offs[self.index] if arena is not None else 0
         return _ops().bn_group_finalize(y, groups, bn.weight, bn.bias, float(bn.eps), arena, off)
 
+    def finalize_group_rows(self, rows: torch.Tensor, groups: int, count: float) -> torch.Tensor:
+        """``finalize_groups`` from group-major partial rows a conv epilogue wrote
+        (``conv3_fwd`` with ``groups``): no statistics pass over y."""
+        bn = self.bn
+        eng = self.engine
+        arena = eng._bn_arena if (bn.track_running_stats and eng._bn_arena is not None) else None
+        off = eng._bn_offs[self.index] if arena is not None else 0
+        return _ops().bn_group_finalize_rows(rows, groups, float(count), bn.weight, bn.bias,
+                                             float(bn.eps), arena, off)
+
     def eval_stats(self) -> torch.Tensor:
         bn = self.bn
         inv = torch.rsqrt(bn.running_var.float() + bn.eps)
@@ -210,15 +220,33 @@ class _DoubleConvFn(torch.autograd.Function):
     def _group_forward(ctx, x1, x2, b1, b2, g1, g2, blk, pool: bool, G: int):
         """A batched window of G micro-batches (``UNetEngine.bn_groups``): the convolutions
         run over the whole batch, every BatchNorm normalises each micro-batch with its own
-        statistics (ref.py:580,583 at batch_size 1).  BN + ReLU is materialised per group
-        (a1, a2) and the convs read it without a prologue; y1 / y2 stay for the backward."""
+        statistics (ref.py:580,583 at batch_size 1).
+
+        Fused (``UNetEngine.group_fused``, the large levels): the convs walk their tiles
+        group-major, so each conv's epilogue writes per-group BN statistic rows (no
+        statistics pass), the second conv applies the per-group BN1 + ReLU in its prologue
+        (a1 is never materialised) and its weight gradient re-applies it on load.
+        Otherwise BN + ReLU is materialised per group (a1) and the convs read it plainly.
+        a2 (+ pool) is materialised in both; y1 / y2 stay for the backward."""
         F = _ops()
         p1, p2 = blk.pack1, blk.pack2
-        y1 = F.conv3_fwd(x1, x2, p1.fwd, b1, None, None, p1.cout, 0, False)[0]
-        s1 = blk.bn1.finalize_groups(y1, G)
-        a1 = F.bn_group_apply(y1, s1, G, False)[0]
-        y2 = F.conv3_fwd(a1, None, p2.fwd, b2, None, None, p2.cout, 0, False)[0]
-        s2 = blk.bn2.finalize_groups(y2, G)
+        fused = blk.engine.group_fused(x1, G, p1.cout)
+        ctx.fused = fused
+        if fused:
+            count = float(x1.shape[0] // G * x1.shape[1] * x1.shape[2])   # pixels per group
+            y1, _, r1 = F.conv3_fwd(x1, x2, p1.fwd, b1, None, None, p1.cout, 0, True,
+                                    None, None, None, None, G)
+            s1 = blk.bn1.finalize_group_rows(r1, G, count)
+            y2, _, r2 = F.conv3_fwd(y1, None, p2.fwd, b2, s1[:, 2], s1[:, 3], p2.cout, 0, True,
+                                    None, None, None, None, G)
+            s2 = blk.bn2.finalize_group_rows(r2, G, count)
+            a1 = torch.empty(0, device=y1.device, dtype=y1.dtype)
+        else:
+            y1 = F.conv3_fwd(x1, x2, p1.fwd, b1, None, None, p1.cout, 0, False)[0]
+            s1 = blk.bn1.finalize_groups(y1, G)
+            a1 = F.bn_group_apply(y1, s1, G, False)[0]
+            y2 = F.conv3_fwd(a1, None, p2.fwd, b2, None, None, p2.cout, 0, False)[0]
+            s2 = blk.bn2.finalize_groups(y2, G)
         a2, pooled = F.bn_group_apply(y2, s2, G, pool)
         ctx.groups = G
         ctx.blk, ctx.pool, ctx.defer = blk, pool, False
@@ -244,21 +272,31 @@ class _DoubleConvFn(torch.autograd.Function):
         p1, p2 = blk.pack1, blk.pack2
         w1 = blk.conv1.weight
         direct = eng.direct_grads
+        fused = ctx.fused
+        # (fused: conv2's input is relu(bn1(y1)) per group, formed on load from y1)
+        xw2, psc, psh = (y1, s1[:, 2], s1[:, 3]) if fused else (a1, None, None)
         # ---- second conv: per-group BN2 + ReLU (+ unpool + skip sum) backward, its gradients
         if direct:
             dy2 = F.bn_group_backward(da2, dpool, y2, s2, g2, G, bn2.weight.grad, bn2.bias.grad)[0]
-            with eng.wgrad_stream(dy2, a1):
-                F.conv3_wgrad(dy2, a1, None, None, None, blk.conv2.weight.grad)
+            with eng.wgrad_stream(dy2, xw2, s1):
+                F.conv3_wgrad(dy2, xw2, None, psc, psh, blk.conv2.weight.grad, groups=G)
                 eng.ready(bn2.weight, bn2.bias, blk.conv2.weight, blk.conv2.bias)
             dg2 = dbe2 = dw2 = None
         else:
             dy2, dg2, dbe2 = F.bn_group_backward(da2, dpool, y2, s2, g2, G, None, None)
-            dw2 = F.conv3_wgrad(dy2, a1, None, None, None).view_as(blk.conv2.weight)
-        da1 = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False)[0]
+            dw2 = F.conv3_wgrad(dy2, xw2, None, psc, psh, groups=G).view_as(blk.conv2.weight)
+        # fused: BN1 backward's reduction in the data gradient's epilogue (group-major rows)
+        part1 = None
+        if fused:
+            da1, _, part1 = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False,
+                                        None, None, y1, s1, G)
+        else:
+            da1 = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False)[0]
         # ---- first conv
         padded_in = x2 is None and x1.shape[-1] != w1.shape[1]     # first layer: 3 -> 8 ch
         if direct:
-            dy1 = F.bn_group_backward(da1, None, y1, s1, g1, G, bn1.weight.grad, bn1.bias.grad)[0]
+            dy1 = F.bn_group_backward(da1, None, y1, s1, g1, G, bn1.weight.grad, bn1.bias.grad,
+                                      part1)[0]
             with eng.wgrad_stream(dy1, x1, x2):
                 if padded_in:
                     w1.grad.add_(F.conv3_wgrad(dy1, x1, None, None, None,
@@ -268,7 +306,7 @@ class _DoubleConvFn(torch.autograd.Function):
                 eng.ready(bn1.weight, bn1.bias, w1, blk.conv1.bias)
             dg1 = dbe1 = dw1 = None
         else:
-            dy1, dg1, dbe1 = F.bn_group_backward(da1, None, y1, s1, g1, G, None, None)
+            dy1, dg1, dbe1 = F.bn_group_backward(da1, None, y1, s1, g1, G, None, None, part1)
             dw1 = F.conv3_wgrad(dy1, x1, x2, None, None, None,
                                 cin_real=w1.shape[1] if padded_in else 0)
             dw1 = (dw1[:, :w1.shape[1]] if padded_in else dw1).reshape(w1.shape)
@@ -666,6 +704,12 @@ class UNetEngine:
         # its own statistics (no deferred BN / prologue fusion in this mode; G = 1 runs one
         # micro-batch through the same unfused kernels); 0 = the fused path
         self.bn_groups = 0
+        # BN groups: fuse the statistics / BN1 prologue / BN1-backward reduction into the
+        # convs (group-major tiles, ``_DoubleConvFn._group_forward``) on levels with at least
+        # this many pixels per group: smaller levels have too few tiles per group to keep
+        # every CU busy (and their unfused passes are cheap); None disables
+        fmin = os.environ.get("DDLPC_GROUP_FUSE_MIN_PX", "16384")
+        self.group_fuse_min_px: Optional[int] = None if fmin == "off" else int(fmin)
         # encoder skips handed out pre-BN (see ``defer_skip_levels``): saves ~1 GB at
         # 256^2 x 128 but measured ~1.2% slower end to end (docs/PERF.md), so opt-in
         self.defer_skip = False
@@ -931,6 +975,16 @@ class UNetEngine:
             ok = (w >> lvl) >= 16 and c_up % 32 == 0 and c_up + c_skip <= 512
             out.append(bool(ok))
         return out
+
+    def group_fused(self, x: torch.Tensor, G: int, cmid: int) -> bool:
+        """Whether a DoubleConv on input ``x`` runs the fused BN-group path: 2-D (the
+        BN-backward epilogue), a middle width the v3 weight gradient's per-group prologue
+        takes (a multiple of 32, images >= 8 wide) and enough pixels per group."""
+        if self.group_fuse_min_px is None or x.dim() != 4 or G < 2:
+            return False
+        n, h, w = x.shape[0], x.shape[1], x.shape[2]
+        return (cmid % 32 == 0 and w >= 8 and n % G == 0 and
+                (n // G) * h * w >= self.group_fuse_min_px)
 
     def bn_groups_supported(self, tile: int) -> bool:
         return bn_groups_supported(self.model, tile)

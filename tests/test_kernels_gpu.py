@@ -1094,3 +1094,71 @@ def test_bn_group_kernels(ops, G, n, H, W, C, pool):
         float((dg.double() - dg_ref).abs().max())
     assert torch.allclose(db.double(), db_ref, rtol=1e-3, atol=1e-3 * float(db_ref.abs().max()) + 1e-3)
     assert torch.allclose(dg.double(), dg_k, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("G,n,H,W,Cin,Cmid", [(2, 1, 256, 256, 32, 32), (3, 2, 64, 64, 64, 64),
+                                              (4, 1, 128, 128, 8, 32), (50, 1, 16, 16, 64, 128),
+                                              (2, 2, 96, 80, 32, 64)])
+def test_conv_bn_group_fusion(ops, G, n, H, W, Cin, Cmid):
+    """The fused BN-group path of a batched window (``UNetEngine.group_fused``): convs walking
+    their tiles group-major write per-group statistic rows (forward (sum, sum^2), and the
+    BN-backward partials of the data gradient), the second conv and its weight gradient apply
+    each group's BN + ReLU on load.  Against fp32 torch per group and the unfused kernels."""
+    torch.manual_seed(G * 13 + Cmid)
+    N = G * n
+    x = torch.randn(N, H, W, Cin, device=DEV).bfloat16()
+    w1 = torch.randn(Cmid, Cin, 3, 3, device=DEV) / math.sqrt(9 * Cin)
+    w2 = torch.randn(Cmid, Cmid, 3, 3, device=DEV) / math.sqrt(9 * Cmid)
+    b1 = torch.randn(Cmid, device=DEV) * 0.1
+    gamma = torch.rand(Cmid, device=DEV) + 0.5
+    beta = torch.randn(Cmid, device=DEV) * 0.3
+    eps = 1e-5
+    pk1, pk2 = pack_conv(ops, w1), pack_conv(ops, w2)
+    count = float(n * H * W)
+    # conv1: group-major statistic rows
+    y1, _, r1 = ops.conv3_fwd(x, None, pk1.fwd, b1, None, None, Cmid, 0, True, None, None, None, None, G)
+    assert r1.shape[0] % G == 0 and r1.shape[1:] == (2, Cmid)
+    ref1 = F.conv2d(nchw(x).float(), w1.bfloat16().float(), b1, padding=1)
+    assert rel_err(nchw(y1), ref1) < 1e-2
+    rows = r1.view(G, -1, 2, Cmid).sum(1)
+    for g in range(G):
+        rg = ref1[g * n:(g + 1) * n]
+        assert torch.allclose(rows[g, 0], rg.sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+        assert torch.allclose(rows[g, 1], (rg * rg).sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+    s1 = ops.bn_group_finalize_rows(r1, G, count, gamma, beta, eps)
+    s1y = ops.bn_group_finalize(y1, G, gamma, beta, eps)       # (statistics of the bf16 y)
+    assert torch.allclose(s1[:, 0], s1y[:, 0], rtol=1e-2, atol=1e-3)
+    assert torch.allclose(s1[:, 1], s1y[:, 1], rtol=1e-2)
+    # conv2 with the per-group BN1 + ReLU prologue
+    y2, _, r2 = ops.conv3_fwd(y1, None, pk2.fwd, None, s1[:, 2], s1[:, 3], Cmid, 0, True,
+                              None, None, None, None, G)
+    a1 = torch.relu(y1.float().view(G, -1, Cmid) * s1[:, 2][:, None] + s1[:, 3][:, None])
+    a1 = a1.bfloat16().float().view(N, H, W, Cmid)
+    ref2 = F.conv2d(nchw(a1), w2.bfloat16().float(), None, padding=1)
+    assert rel_err(nchw(y2), ref2) < 1e-2, rel_err(nchw(y2), ref2)
+    rows2 = r2.view(G, -1, 2, Cmid).sum(1)
+    assert torch.allclose(rows2[:, 0], ref2.view(G, n, Cmid, H, W).sum((1, 3, 4)), rtol=2e-3, atol=0.5)
+    # weight gradient of conv2 with the per-group prologue
+    dy = (torch.randn(N, H, W, Cmid, device=DEV) * 0.1).bfloat16()
+    dW = ops.conv3_wgrad(dy, y1, None, s1[:, 2], s1[:, 3], groups=G)
+    dW_ref = torch.nn.grad.conv2d_weight(nchw(a1), w2.shape, nchw(dy).float(), padding=1)
+    assert rel_err(dW.view_as(dW_ref), dW_ref) < 1e-2, rel_err(dW.view_as(dW_ref), dW_ref)
+    # data gradient with the per-group BN-backward epilogue vs the unfused kernels group by group
+    da, _, part = ops.conv3_fwd(dy, None, pk2.dgrad, None, None, None, Cmid, 0, False,
+                                None, None, y1, s1, G)
+    assert part.shape[0] % G == 0
+    prow = part.view(G, -1, 2, Cmid).sum(1)
+    for g in range(G):
+        sl = slice(g * n, (g + 1) * n)
+        da_g, _, part_g = ops.conv3_fwd(dy[sl].contiguous(), None, pk2.dgrad, None, None, None, Cmid,
+                                        0, False, None, None, y1[sl].contiguous(), s1[g].contiguous())
+        assert rel_err(da[sl], da_g) < 1e-2
+        pg = part_g.sum(0)
+        assert torch.allclose(prow[g], pg, rtol=1e-3, atol=1e-3 * float(pg.abs().max()) + 1e-4), g
+    dg0, db0 = torch.zeros(Cmid, device=DEV), torch.zeros(Cmid, device=DEV)
+    dg1, db1 = torch.zeros(Cmid, device=DEV), torch.zeros(Cmid, device=DEV)
+    dY0, _, _ = ops.bn_group_backward(da, None, y1, s1, gamma, G, dg0, db0)
+    dY1, _, _ = ops.bn_group_backward(da, None, y1, s1, gamma, G, dg1, db1, part)
+    assert rel_err(dY1, dY0) < 2e-3, rel_err(dY1, dY0)
+    assert torch.allclose(dg1, dg0, rtol=2e-3, atol=2e-3 * float(dg0.abs().max()))
+    assert torch.allclose(db1, db0, rtol=2e-3, atol=2e-3 * float(db0.abs().max()))

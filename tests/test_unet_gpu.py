@@ -553,10 +553,13 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg, wd):
             assert torch.equal(bw, bf), k
         else:
             # per-micro-batch means / variances of conv outputs that round to bf16
-            # independently (the batched convs tile differently): measured up to 2.3e-4 on
-            # the bottleneck's running means of magnitude ~1 (256 pixels per micro-batch)
+            # independently (the batched convs tile differently; on the fused levels the
+            # window's statistics come from the fp32 conv outputs before the bf16 store, the
+            # unfused path's from the stored bf16 y): measured up to 2.3e-4 on the
+            # bottleneck's running means of magnitude ~1 (256 pixels per micro-batch), 2.1e-3
+            # on a 64-pixel bottleneck running variance at 128^2 width divisor 1
             err = float((bw - bu).abs().max())
-            assert err <= 2e-3 * max(1.0, float(bu.abs().max())), (k, err)
+            assert err <= 5e-3 * max(1.0, float(bu.abs().max())), (k, err)
     if oracle:
         # fp32 stock model (and bf16 autocast), micro-batch by micro-batch, own BatchNorm each
         for x, y in mbs:
