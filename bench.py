@@ -197,11 +197,22 @@ def main():
             return tr.train_set.get(idx)
         return pool[k % len(pool)]
 
-    fixed = [batch(j) for j in range(args.accum)] if args.fixed_batch else None
+    def window(i):
+        # on-device data: the step's accum micro-batches rendered in ONE pass (one index
+        # vector, one synth launch) and handed out as zero-copy views (data.split_batch; the
+        # batched BN window joins them back without a copy); each micro-batch holds the same
+        # distinct samples as micro-batch-by-micro-batch rendering would
+        if on_device_data and args.accum > 1:
+            from ddlpc.data import split_batch
+            ks = torch.arange(i * args.accum, (i + 1) * args.accum, device=device, dtype=torch.int64)
+            idx = ((ks * world + rank) * B)[:, None] + torch.arange(B, device=device, dtype=torch.int64)
+            return split_batch(*tr.train_set.get(idx.reshape(-1)), args.accum)
+        return [batch(i * args.accum + j) for j in range(args.accum)]
+
+    fixed = window(0) if args.fixed_batch else None
 
     def step(i):
-        tr.train_step(fixed if fixed is not None else
-                      [batch(i * args.accum + j) for j in range(args.accum)])
+        tr.train_step(fixed if fixed is not None else window(i))
 
     def sync():
         if dev == "cuda":
@@ -229,7 +240,7 @@ def main():
     # schedule calibration (untimed): overlapped weight-gradient stream vs serial
     sched = {}
     if args.schedule == "auto":
-        sched = tr.choose_schedule([batch(10_000 + j) for j in range(args.accum)])
+        sched = tr.choose_schedule(window(10_000))
         if rank == 0 and sched:
             print(f"schedule: {sched}", file=sys.stderr, flush=True)
     elif args.schedule == "serial" and tr.impl == "hip":

@@ -847,19 +847,25 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
   // BN groups (ConvWgradArgs::groups, X1 prologue only): the tile's image decides its group;
   // a workgroup's tiles are contiguous, so the constants reload only at a group boundary —
   // after the full drain below, with no DMA in flight
-  int cur_grp = 0;
+  // (v3 chunks are whole 32-channel chunks of X1: the lane's 8 constants are two float4s)
+  int grp_end = p.groups > 1 ? p.gimg : (1 << 30);  // first image past the current group
+  long long goff = 0;
   if (t_begin < t_end) issue(t_begin, 0);
   for (int tile = t_begin; tile < t_end; ++tile) {
     const int buf = (tile - t_begin) & 1;
     dma_wait<0>();
-    if (p.groups > 1 && any_pro) {
-      const int gg = tw.n / p.gimg;                 // (tw: this tile, the last one issued)
-      if (gg != cur_grp) {
-        cur_grp = gg;
+    if (tw.n >= grp_end) {                           // (tw: this tile, the last one issued)
+      while (tw.n >= grp_end) { grp_end += p.gimg; goff += p.gstride; }
+      const float4* bs = reinterpret_cast<const float4*>(p.pscale + goff + ci0 + (lane & 3) * 8);
+      const float4* bh = reinterpret_cast<const float4*>(p.pshift + goff + ci0 + (lane & 3) * 8);
 #pragma unroll
-        for (int cw = 0; cw < CIW; ++cw)
-          pro8_load(p.pscale + gg * p.gstride, p.pshift + gg * p.gstride, nullptr, nullptr, p.C1,
-                    ci0 + cw * BK + (lane & 3) * 8, p.C1, psc[cw], psh[cw]);
+      for (int cw = 0; cw < CIW; ++cw) {
+        const float4 s0 = bs[cw * BK / 4], s1 = bs[cw * BK / 4 + 1];
+        const float4 h0 = bh[cw * BK / 4], h1 = bh[cw * BK / 4 + 1];
+        psc[cw][0] = s0.x; psc[cw][1] = s0.y; psc[cw][2] = s0.z; psc[cw][3] = s0.w;
+        psc[cw][4] = s1.x; psc[cw][5] = s1.y; psc[cw][6] = s1.z; psc[cw][7] = s1.w;
+        psh[cw][0] = h0.x; psh[cw][1] = h0.y; psh[cw][2] = h0.z; psh[cw][3] = h0.w;
+        psh[cw][4] = h1.x; psh[cw][5] = h1.y; psh[cw][6] = h1.z; psh[cw][7] = h1.w;
       }
     }
     if (any_pro) transform(sX(buf));

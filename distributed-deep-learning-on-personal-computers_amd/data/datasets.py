@@ -94,6 +94,38 @@ def engine_input(x_nhwc: torch.Tensor, in_channels: int) -> torch.Tensor:
     return v
 
 
+def split_batch(x: torch.Tensor, y: torch.Tensor, n: int) -> List[Tuple[torch.Tensor, torch.Tensor]]:
+    """A batch rendered in one pass (e.g. a whole accumulation window) as ``n`` equal
+    micro-batches that are zero-copy views of it (engine-layout inputs keep their layout),
+    so the trainer's batched window (``Trainer._cat_window``) can take the batch back
+    without a copy."""
+    if x.shape[0] % n:
+        raise ValueError(f"batch of {x.shape[0]} does not split into {n} equal micro-batches")
+    b = x.shape[0] // n
+    xp = getattr(x, "_ddlpc_nhwc", None)
+    out = []
+    for i in range(n):
+        xi = engine_input(xp[i * b:(i + 1) * b], x.shape[1]) if xp is not None else x[i * b:(i + 1) * b]
+        out.append((xi, y[i * b:(i + 1) * b]))
+    return out
+
+
+def cat_adjacent(ts: List[torch.Tensor]) -> torch.Tensor:
+    """torch.cat along dim 0 — without a copy when the tensors are contiguous, equal-shaped
+    and lie back to back in one storage (the views ``split_batch`` hands out)."""
+    t0 = ts[0]
+    step = t0.numel()
+    ok = all(t.is_contiguous() and t.shape == t0.shape and t.dtype == t0.dtype and
+             t.untyped_storage().data_ptr() == t0.untyped_storage().data_ptr() and
+             t.storage_offset() == t0.storage_offset() + i * step for i, t in enumerate(ts))
+    if not ok or t0.dim() == 0:
+        return torch.cat(ts)
+    out = t0.new_empty(0)
+    out.set_(t0.untyped_storage(), t0.storage_offset(), (t0.shape[0] * len(ts),) + tuple(t0.shape[1:]),
+             t0.stride())
+    return out
+
+
 # ---------------------------------------------------------------------- synthetic tiles
 def device_indices(idx, device) -> torch.Tensor:
     """Sample indices as an int64 tensor on ``device`` without a blocking host round trip:

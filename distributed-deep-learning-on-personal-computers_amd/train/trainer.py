@@ -600,16 +600,18 @@ class Trainer:
         The micro-batches must have equal shapes: each is one BatchNorm group of batch / G
         samples, and the window's mean loss x G is the sum of the micro-batch losses only
         when every micro-batch has the same pixel count."""
-        from ..data.datasets import engine_input
+        from ..data.datasets import cat_adjacent, engine_input
         shapes = {(tuple(x.shape), tuple(y.shape)) for x, y in mbs}
         if len(shapes) != 1:
             raise ValueError(f"batched BN window: micro-batches of unequal shapes {sorted(shapes)}")
+        # (micro-batches that are back-to-back views of one rendered window — data.split_batch
+        # — are joined without a copy)
         xps = [getattr(x, "_ddlpc_nhwc", None) for x, _ in mbs]
         if all(xp is not None for xp in xps):
-            x = engine_input(torch.cat(xps), mbs[0][0].shape[1])
+            x = engine_input(cat_adjacent(xps), mbs[0][0].shape[1])
         else:
-            x = torch.cat([x for x, _ in mbs])
-        return x, torch.cat([y for _, y in mbs])
+            x = cat_adjacent([x for x, _ in mbs])
+        return x, cat_adjacent([y for _, y in mbs])
 
     def _window_step(self, micro_batches: List[Tuple[torch.Tensor, torch.Tensor]], W: int):
         """The accumulation window as batched passes of up to W micro-batches, each micro-batch

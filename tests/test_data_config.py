@@ -125,3 +125,31 @@ def test_device_dataset_rejects_out_of_range_host_indices():
     ds.base = base
     with pytest.raises(IndexError):
         DeviceTileDataset.get(ds, [0, 3])
+
+
+def test_split_batch_views_rejoin_without_copy():
+    """A whole accumulation window rendered at once (bench.py) is handed to the trainer as
+    zero-copy micro-batch views; ``Trainer._cat_window`` joins them back without a copy, and
+    anything else (separately allocated micro-batches) still concatenates by copy."""
+    import torch
+    from ddlpc.data import cat_adjacent, split_batch
+    from ddlpc.data.datasets import engine_input
+    from ddlpc.train.trainer import Trainer
+    xp = torch.randn(6, 4, 4, 8)
+    x, y = engine_input(xp, 3), torch.randint(0, 5, (6, 4, 4))
+    mbs = split_batch(x, y, 3)
+    assert [tuple(m[0].shape) for m in mbs] == [(2, 3, 4, 4)] * 3
+    assert all(m[0]._ddlpc_nhwc.shape == (2, 4, 4, 8) for m in mbs)
+    xw, yw = Trainer._cat_window(mbs)
+    assert xw._ddlpc_nhwc.data_ptr() == xp.data_ptr() and torch.equal(xw._ddlpc_nhwc, xp)
+    assert yw.data_ptr() == y.data_ptr() and torch.equal(yw, y)
+    parts = [y[:2].clone(), y[2:4].clone()]
+    joined = cat_adjacent(parts)
+    assert joined.data_ptr() != parts[0].data_ptr() and torch.equal(joined, y[:4])
+    # out of order views are copied in the given order
+    assert torch.equal(cat_adjacent([y[2:4], y[:2]]), torch.cat([y[2:4], y[:2]]))
+    try:
+        split_batch(x, y, 4)
+        raise AssertionError("uneven split accepted")
+    except ValueError:
+        pass
