@@ -798,11 +798,12 @@ std::vector<at::Tensor> bn_group_backward(const c10::optional<at::Tensor>& dA,
   at::Tensor dgamma = into ? *dgamma_out : at::empty({C}, fopts);
   at::Tensor dbeta = into ? *dbeta_out : at::empty({C}, fopts);
   at::Tensor dY = at::empty_like(y);
+  at::Tensor gsum = at::empty({groups, 2, C}, y.options().dtype(at::kDouble));
   bn_group_backward_launch(hasA ? bptr(*dA) : nullptr, hasP ? bptr(*dP) : nullptr, bptr(y),
                            stats4.data_ptr<float>(), gamma.data_ptr<float>(), dgamma.data_ptr<float>(),
                            dbeta.data_ptr<float>(), into, coefs.data_ptr<float>(),
                            part.data_ptr<float>(), nb, bptr_mut(dY), g.dims, (int)groups, Ng, g.D,
-                           g.H, g.W, C, cur_stream(), have_part);
+                           g.H, g.W, C, cur_stream(), have_part, gsum.data_ptr<double>());
   return {dY, dgamma, dbeta};
 }
 
@@ -1115,12 +1116,39 @@ std::vector<at::Tensor> head_ce_bn_bwd(const at::Tensor& a, const at::Tensor& Wh
                                        const at::Tensor& gamma,
                                        const c10::optional<at::Tensor>& dgamma_out,
                                        const c10::optional<at::Tensor>& dbeta_out,
-                                       const c10::optional<at::Tensor>& pscale) {
+                                       const c10::optional<at::Tensor>& pscale, int64_t groups) {
   CHECK_DEV(a); CHECK_CONTIG(a); CHECK_BF16(a);
   // pscale: device factor on the partial rows (rows from the fused forward at unit scale)
   const float* ps = fptr_opt(pscale);
   c10::DeviceGuard guard(a.device());
   const int C = (int)a.size(-1), K = (int)Wh.size(0);
+  if (groups > 1) {
+    // BN groups (a batched window): bn4 [groups][4][C], partial rows group-major (the fused
+    // forward's head_ce_fwd_stats with groups), per-group coefficients
+    const long long P = a.numel() / C;
+    TORCH_CHECK(C == 32 && K <= 16 && P % (groups * 16) == 0,
+                "head_ce_bn_bwd groups: C = 32 head, pixels per group a multiple of 16");
+    CHECK_F32(bn4); CHECK_CONTIG(bn4); CHECK_F32(partial); CHECK_CONTIG(partial); CHECK_F32(gamma);
+    TORCH_CHECK(bn4.numel() == groups * 4 * C && partial.numel() % (groups * 2 * C) == 0,
+                "head_ce_bn_bwd groups: bn4 [groups][4][C], partial [groups * R][2][C]");
+    auto fopts = a.options().dtype(at::kFloat);
+    const bool into = dgamma_out.has_value() && dgamma_out->defined();
+    at::Tensor dgamma = into ? *dgamma_out : at::empty({C}, fopts);
+    at::Tensor dbeta = into ? *dbeta_out : at::empty({C}, fopts);
+    at::Tensor coefs = at::empty({groups, 3, C}, fopts);
+    at::Tensor gsum = at::empty({groups, 2, C}, a.options().dtype(at::kDouble));
+    const int nb = (int)(partial.numel() / (groups * 2 * C));
+    bn_group_grad_rows_launch(partial.data_ptr<float>(), nb, (int)groups, C, (double)(P / groups),
+                              gamma.data_ptr<float>(), bn4.data_ptr<float>(), dgamma.data_ptr<float>(),
+                              dbeta.data_ptr<float>(), into, coefs.data_ptr<float>(),
+                              gsum.data_ptr<double>(), ps, cur_stream());
+    at::Tensor dY = at::empty_like(a);
+    head_bn_apply_launch(bptr(a), Wh.data_ptr<float>(), bh.data_ptr<float>(), labels.data_ptr<int64_t>(),
+                         fptr_opt(gscale), out3.data_ptr<float>(), bn4.data_ptr<float>(),
+                         coefs.data_ptr<float>(), bptr_mut(dY), P, C, K, (int)ignore_index, cur_stream(),
+                         (int)groups);
+    return {dY, dgamma, dbeta};
+  }
   const float* pbn = bn4_ptr(bn4, C);
   TORCH_CHECK(head_supported(C, K), "head kernel: unsupported (C, K)");
   CHECK_F32(partial); CHECK_CONTIG(partial); CHECK_F32(gamma);
@@ -1156,16 +1184,27 @@ std::vector<at::Tensor> head_ce_bn_bwd(const at::Tensor& a, const at::Tensor& Wh
 // dL/count on the device (head_wgrad_from_rows, head_ce_bn_bwd pscale).
 std::vector<at::Tensor> head_ce_fwd_stats(const at::Tensor& a, const at::Tensor& Wh,
                                           const at::Tensor& bh, const at::Tensor& labels,
-                                          int64_t ignore_index, const at::Tensor& bn4) {
+                                          int64_t ignore_index, const at::Tensor& bn4,
+                                          int64_t groups) {
   CHECK_DEV(a); CHECK_CONTIG(a); CHECK_BF16(a); CHECK_CONTIG(labels);
   TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
   c10::DeviceGuard guard(a.device());
   const int C = (int)a.size(-1), K = (int)Wh.size(0);
-  const float* pbn = bn4_ptr(bn4, C);
-  TORCH_CHECK(head_supported(C, K), "head kernel: unsupported (C, K)");
   const long long P = a.numel() / C;
+  const float* pbn = nullptr;
+  if (groups > 1) {
+    // BN groups: per-group statistics bn4 [groups][4][C], group-major rows (C = 32 kernel)
+    CHECK_F32(bn4); CHECK_CONTIG(bn4);
+    TORCH_CHECK(C == 32 && K <= 16 && P % (groups * 16) == 0 && bn4.numel() == groups * 4 * C,
+                "head_ce_fwd_stats groups: C = 32 head, bn4 [groups][4][C], pixels per group a "
+                "multiple of 16");
+    pbn = bn4.data_ptr<float>();
+  } else {
+    pbn = bn4_ptr(bn4, C);
+  }
+  TORCH_CHECK(head_supported(C, K), "head kernel: unsupported (C, K)");
   TORCH_CHECK(labels.numel() == P, "labels / activation pixel count mismatch");
-  const int nb = head_fwd_stats_blocks(C, K, P, num_cus());
+  const int nb = head_fwd_stats_blocks(C, K, P, num_cus(), groups > 1 ? (int)groups : 1);
   auto fopts = a.options().dtype(at::kFloat);
   at::Tensor wrows = at::empty({nb, K * C + K}, fopts);
   at::Tensor brows = at::empty({nb, 2, C}, fopts);
@@ -1173,7 +1212,8 @@ std::vector<at::Tensor> head_ce_fwd_stats(const at::Tensor& a, const at::Tensor&
   at::Tensor out3 = at::empty({3}, fopts);
   head_ce_fwd_stats_launch(bptr(a), Wh.data_ptr<float>(), bh.data_ptr<float>(), labels.data_ptr<int64_t>(),
                            pbn, wrows.data_ptr<float>(), brows.data_ptr<float>(), lrows.data_ptr<float>(),
-                           out3.data_ptr<float>(), nb, P, C, K, (int)ignore_index, cur_stream());
+                           out3.data_ptr<float>(), nb, P, C, K, (int)ignore_index, cur_stream(),
+                           groups > 1 ? (int)groups : 1);
   return {out3, wrows, brows};
 }
 
@@ -1491,9 +1531,9 @@ TORCH_LIBRARY(ddlpc, m) {
         "bool store_da=True) -> Tensor[]");
   m.def("head_ce_bn_bwd(Tensor a, Tensor Wh, Tensor bh, Tensor labels, Tensor out3, Tensor? gscale, "
         "int ignore_index, Tensor bn4, Tensor partial, Tensor gamma, Tensor(a!)? dgamma_out=None, "
-        "Tensor(b!)? dbeta_out=None, Tensor? pscale=None) -> Tensor[]");
+        "Tensor(b!)? dbeta_out=None, Tensor? pscale=None, int groups=0) -> Tensor[]");
   m.def("head_ce_fwd_stats(Tensor a, Tensor Wh, Tensor bh, Tensor labels, int ignore_index, "
-        "Tensor bn4) -> Tensor[]");
+        "Tensor bn4, int groups=0) -> Tensor[]");
   m.def("head_wgrad_from_rows(Tensor rows, Tensor scale, int K, int C, Tensor(a!)? dw_out=None, "
         "Tensor(b!)? db_out=None) -> Tensor[]");
   m.def("meter_add(Tensor(a!) buf, Tensor loss, Tensor correct, float pixels, float count=1.) -> ()");

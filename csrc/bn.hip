@@ -673,74 +673,103 @@ __global__ __launch_bounds__(256) void bn_group_stats_kernel(const bf16_t* __res
   }
 }
 
-// one workgroup per channel; wave w finalizes groups w, w + 16, ... (fp64 sums of the group's
-// nb partial rows): stats4 per group, and the group's (mean, unbiased var) into its arena row
-// (the running statistics are then updated in micro-batch order: bn_running_apply)
-constexpr int kGW = 16;                      // waves per finalize workgroup
-__global__ __launch_bounds__(kGW * 64) void bn_group_finalize_kernel(
-    const float* __restrict__ partial, int nb, int groups, int C, double count,
-    const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-    float* __restrict__ out4, float* __restrict__ arena, long long astride) {
-  const int c = blockIdx.x;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int g = w; g < groups; g += kGW) {
-    const float* rows = partial + (long long)g * nb * 2 * C;
-    double a = 0.0, b = 0.0;
-    for (int r = lane; r < nb; r += 64) {
-      a += rows[(long long)r * 2 * C + c];
-      b += rows[(long long)r * 2 * C + C + c];
-    }
-    a = wave_sum_d(a);
-    b = wave_sum_d(b);
-    if (lane != 0) continue;
-    const double mean = a / count;
-    double var = b / count - mean * mean;
-    if (var < 0) var = 0;
-    const float inv = (float)(1.0 / sqrt(var + (double)eps));
-    const float sc = gamma[c] * inv;
-    float* o = out4 + (long long)g * 4 * C;
-    o[c] = (float)mean;
-    o[C + c] = inv;
-    o[2 * C + c] = sc;
-    o[3 * C + c] = beta[c] - (float)mean * sc;
-    if (arena != nullptr) {
-      const double unb = count > 1 ? var * count / (count - 1) : var;
-      arena[g * astride + c] = (float)mean;
-      arena[g * astride + C + c] = (float)unb;
-    }
+// Finalize kernels: grid (channel chunks of 64, groups), 256 threads = 64 channels x 4 row
+// lanes.  A thread sums rows r = lane4, lane4 + 4, ... of its (group, channel) in fp64 —
+// loads coalesced across the 64 channels (the partial rows are [groups][nb][2][C]) — and the
+// 4 row lanes combine in LDS in a fixed order (deterministic).
+constexpr int kFR = 4;                       // row lanes per finalize workgroup
+DDLPC_DEVICE void group_rows_sum(const float* __restrict__ rows, int nb, int C, int c, int rl,
+                                 double& a, double& b) {
+  a = 0.0; b = 0.0;
+  int r = rl;
+  for (; r + 3 * kFR < nb; r += 4 * kFR) {   // four rows' loads in flight
+    const float a0 = rows[(long long)r * 2 * C + c], b0 = rows[(long long)r * 2 * C + C + c];
+    const float a1 = rows[(long long)(r + kFR) * 2 * C + c], b1 = rows[(long long)(r + kFR) * 2 * C + C + c];
+    const float a2 = rows[(long long)(r + 2 * kFR) * 2 * C + c], b2 = rows[(long long)(r + 2 * kFR) * 2 * C + C + c];
+    const float a3 = rows[(long long)(r + 3 * kFR) * 2 * C + c], b3 = rows[(long long)(r + 3 * kFR) * 2 * C + C + c];
+    a += (double)a0 + (double)a1 + (double)a2 + (double)a3;
+    b += (double)b0 + (double)b1 + (double)b2 + (double)b3;
+  }
+  for (; r < nb; r += kFR) {
+    a += (double)rows[(long long)r * 2 * C + c];
+    b += (double)rows[(long long)r * 2 * C + C + c];
   }
 }
 
-// BatchNorm-backward finalize per group: coefficients [k | m1 | m2] of every group, and
-// dgamma / dbeta = the fp64 sums over groups in group order (deterministic)
-__global__ __launch_bounds__(kGW * 64) void bn_group_grad_finalize_kernel(
+// stats4 per group (mean | invstd | scale | shift), and the group's (mean, unbiased var) into
+// its arena row (the running statistics are then updated in micro-batch order:
+// bn_running_apply)
+__global__ __launch_bounds__(64 * kFR) void bn_group_finalize_kernel(
     const float* __restrict__ partial, int nb, int groups, int C, double count,
-    const float* __restrict__ gamma, const float* __restrict__ stats4, float* dgamma, float* dbeta,
-    float* __restrict__ coefs, int accumulate) {
-  __shared__ double t1s[1024], t2s[1024];
-  const int c = blockIdx.x;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int g = w; g < groups; g += kGW) {
-    const float* rows = partial + (long long)g * nb * 2 * C;
-    double a = 0.0, b = 0.0;
-    for (int r = lane; r < nb; r += 64) {
-      a += rows[(long long)r * 2 * C + c];
-      b += rows[(long long)r * 2 * C + C + c];
-    }
-    a = wave_sum_d(a);
-    b = wave_sum_d(b);
-    if (lane != 0) continue;
-    t1s[g] = a;
-    t2s[g] = b;
-    float* k = coefs + (long long)g * 3 * C;
-    k[c] = gamma[c] * stats4[(long long)g * 4 * C + C + c];
-    k[C + c] = (float)(a / count);
-    k[2 * C + c] = (float)(b / count);
-  }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+    float* __restrict__ out4, float* __restrict__ arena, long long astride) {
+  __shared__ double red[2][kFR][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl, g = blockIdx.y;
   double a = 0.0, b = 0.0;
-  for (int g = 0; g < groups; ++g) { a += t1s[g]; b += t2s[g]; }
+  if (c < C) group_rows_sum(partial + (long long)g * nb * 2 * C, nb, C, c, rl, a, b);
+  red[0][rl][cl] = a;
+  red[1][rl][cl] = b;
+  __syncthreads();
+  if (rl != 0 || c >= C) return;
+  a = 0.0; b = 0.0;
+#pragma unroll
+  for (int k = 0; k < kFR; ++k) { a += red[0][k][cl]; b += red[1][k][cl]; }
+  const double mean = a / count;
+  double var = b / count - mean * mean;
+  if (var < 0) var = 0;
+  const float inv = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * inv;
+  float* o = out4 + (long long)g * 4 * C;
+  o[c] = (float)mean;
+  o[C + c] = inv;
+  o[2 * C + c] = sc;
+  o[3 * C + c] = beta[c] - (float)mean * sc;
+  if (arena != nullptr) {
+    const double unb = count > 1 ? var * count / (count - 1) : var;
+    arena[g * astride + c] = (float)mean;
+    arena[g * astride + C + c] = (float)unb;
+  }
+}
+
+// BatchNorm-backward finalize per group: coefficients [k | m1 | m2] of every group and the
+// group's fp64 sums into gsum [groups][2][C] (dbeta / dgamma terms) ...
+__global__ __launch_bounds__(64 * kFR) void bn_group_grad_finalize_kernel(
+    const float* __restrict__ partial, int nb, int groups, int C, double count,
+    const float* __restrict__ gamma, const float* __restrict__ stats4, double* __restrict__ gsum,
+    float* __restrict__ coefs, const float* __restrict__ dscale) {
+  __shared__ double red[2][kFR][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl, g = blockIdx.y;
+  double a = 0.0, b = 0.0;
+  if (c < C) group_rows_sum(partial + (long long)g * nb * 2 * C, nb, C, c, rl, a, b);
+  red[0][rl][cl] = a;
+  red[1][rl][cl] = b;
+  __syncthreads();
+  if (rl != 0 || c >= C) return;
+  a = 0.0; b = 0.0;
+#pragma unroll
+  for (int k = 0; k < kFR; ++k) { a += red[0][k][cl]; b += red[1][k][cl]; }
+  if (dscale != nullptr) { a *= (double)dscale[0]; b *= (double)dscale[0]; }
+  gsum[((long long)g * 2) * C + c] = a;
+  gsum[((long long)g * 2 + 1) * C + c] = b;
+  float* k = coefs + (long long)g * 3 * C;
+  k[c] = gamma[c] * stats4[(long long)g * 4 * C + C + c];
+  k[C + c] = (float)(a / count);
+  k[2 * C + c] = (float)(b / count);
+}
+
+// ... then dbeta / dgamma = those sums over the groups in group order (deterministic)
+__global__ __launch_bounds__(256) void bn_group_grad_sum_kernel(const double* __restrict__ gsum, int groups,
+                                                                int C, float* dgamma, float* dbeta,
+                                                                int accumulate) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0, b = 0.0;
+  for (int g = 0; g < groups; ++g) {
+    a += gsum[((long long)g * 2) * C + c];
+    b += gsum[((long long)g * 2 + 1) * C + c];
+  }
   dbeta[c] = accumulate ? dbeta[c] + (float)a : (float)a;
   dgamma[c] = accumulate ? dgamma[c] + (float)b : (float)b;
 }
@@ -766,8 +795,8 @@ void bn_group_stats_finalize_launch(const bf16_t* y, int groups, long long gpix,
                                     int nb, hipStream_t st) {
   hipLaunchKernelGGL(bn_group_stats_kernel, dim3(nb, groups), dim3(256), 0, st, y, gpix, C,
                      partial_scratch);
-  hipLaunchKernelGGL(bn_group_finalize_kernel, dim3(C), dim3(kGW * 64), 0, st, partial_scratch, nb,
-                     groups, C, (double)gpix, gamma, beta, eps, out4, arena, astride);
+  hipLaunchKernelGGL(bn_group_finalize_kernel, dim3((C + 63) / 64, groups), dim3(64 * kFR), 0, st,
+                     partial_scratch, nb, groups, C, (double)gpix, gamma, beta, eps, out4, arena, astride);
 }
 
 int bn_group_stats_rows(long long gpix, int C, int groups) { return bn_group_rows(gpix, C, groups); }
@@ -777,15 +806,15 @@ int bn_group_stats_rows(long long gpix, int C, int groups) { return bn_group_row
 void bn_group_finalize_rows_launch(const float* partial, int nb, int groups, long long gpix, int C,
                                    const float* gamma, const float* beta, float eps, float* out4,
                                    float* arena, long long astride, hipStream_t st) {
-  hipLaunchKernelGGL(bn_group_finalize_kernel, dim3(C), dim3(kGW * 64), 0, st, partial, nb, groups, C,
-                     (double)gpix, gamma, beta, eps, out4, arena, astride);
+  hipLaunchKernelGGL(bn_group_finalize_kernel, dim3((C + 63) / 64, groups), dim3(64 * kFR), 0, st,
+                     partial, nb, groups, C, (double)gpix, gamma, beta, eps, out4, arena, astride);
 }
 
 void bn_group_backward_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* y,
                               const float* stats4, const float* gamma, float* dgamma, float* dbeta,
                               bool accumulate, float* coefs, float* partial_scratch, int nb,
                               bf16_t* dY, int dims, int groups, int N, int D, int H, int W, int C,
-                              hipStream_t st, bool have_partial) {
+                              hipStream_t st, bool have_partial, double* gsum_scratch) {
   const bool pool = dP != nullptr;
   const long long sstride = 4LL * C;
   const float* s = stats4;
@@ -795,8 +824,10 @@ void bn_group_backward_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* 
     bn_bwd2_launch<0>(nb, dims, pool, dA, dP, y, s + 2 * C, s + 3 * C, s, s + C, nullptr, nullptr,
                       partial_scratch, nullptr, N, D, H, W, C, st, groups, sstride);
   const double count = (double)N * D * H * W;
-  hipLaunchKernelGGL(bn_group_grad_finalize_kernel, dim3(C), dim3(kGW * 64), 0, st, partial_scratch, nb,
-                     groups, C, count, gamma, stats4, dgamma, dbeta, coefs, accumulate ? 1 : 0);
+  hipLaunchKernelGGL(bn_group_grad_finalize_kernel, dim3((C + 63) / 64, groups), dim3(64 * kFR), 0, st,
+                     partial_scratch, nb, groups, C, count, gamma, stats4, gsum_scratch, coefs, nullptr);
+  hipLaunchKernelGGL(bn_group_grad_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, st, gsum_scratch,
+                     groups, C, dgamma, dbeta, accumulate ? 1 : 0);
   const long long items = (long long)N * (pool ? (dims == 3 ? D / 2 : 1) * (H / 2) * (W / 2)
                                                 : (long long)D * H * W);
   const int upb = 256 / ((pool && C / 8 <= 32) ? 2 * (C / 8) : C / 8);
@@ -804,6 +835,16 @@ void bn_group_backward_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* 
       1, std::min<long long>((items + 2 * upb - 1) / (2 * upb), std::max(1, 8192 / groups)));
   bn_bwd2_launch<1>(grid2, dims, pool, dA, dP, y, s + 2 * C, s + 3 * C, s, s + C, coefs, nullptr,
                     nullptr, dY, N, D, H, W, C, st, groups, sstride);
+}
+
+void bn_group_grad_rows_launch(const float* partial, int nb, int groups, int C, double count,
+                               const float* gamma, const float* stats4, float* dgamma, float* dbeta,
+                               bool accumulate, float* coefs, double* gsum_scratch,
+                               const float* dscale, hipStream_t st) {
+  hipLaunchKernelGGL(bn_group_grad_finalize_kernel, dim3((C + 63) / 64, groups), dim3(64 * kFR), 0, st,
+                     partial, nb, groups, C, count, gamma, stats4, gsum_scratch, coefs, dscale);
+  hipLaunchKernelGGL(bn_group_grad_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, st, gsum_scratch,
+                     groups, C, dgamma, dbeta, accumulate ? 1 : 0);
 }
 
 int bn_group_bwd_rows(long long items, int groups) {

@@ -811,9 +811,16 @@ __global__ __launch_bounds__(256, 3) void head32_kernel(
     const int64_t* __restrict__ labels, const float* __restrict__ gscale,
     const float* __restrict__ stats3, bf16_t* __restrict__ dA, float* __restrict__ dWp,
     long long P, int ignore_index, const float* __restrict__ bn4, float* __restrict__ bnpart,
-    int Kreal, float* __restrict__ lossp) {
+    int Kreal, float* __restrict__ lossp, int groups, long long gsteps) {
   static_assert(!LOSS || (DEFER && !STORE), "the fused forward is the deferred stats pass");
   constexpr int C = 32;
+  // BN groups (a batched window, groups > 1): the deferred BatchNorm has per-group statistics
+  // bn4 [groups][4][C]; the grid is groups x Rb workgroups and workgroup b walks only the
+  // 16-pixel steps of group b / Rb (gsteps per group: a step never straddles two groups), so
+  // its BN partial row belongs to that group (rows [groups][Rb][2][C])
+  const int Rb = groups > 1 ? (int)gridDim.x / groups : (int)gridDim.x;
+  const int grp = groups > 1 ? (int)blockIdx.x / Rb : 0;
+  if (DEFER) bn4 += (long long)grp * 4 * C;
   // per wave: act [16][32] bf16 (1 KB) | dlogits hi [16][16] | lo [16][16]; reused at the end
   // as the wave's dWh^T [16][32] fp32 (2 KB)
   __shared__ __attribute__((aligned(16))) char sT[4][2048];
@@ -841,9 +848,9 @@ __global__ __launch_bounds__(256, 3) void head32_kernel(
   float db[4] = {0.f, 0.f, 0.f, 0.f}, b1[8], b2[8], ls[3] = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < 8; ++j) { b1[j] = 0.f; b2[j] = 0.f; }
-  const long long steps = (P + 15) / 16;
-  const long long wstride = (long long)gridDim.x * 4;
-  const long long s0 = (long long)blockIdx.x * 4 + wave;
+  const long long steps = groups > 1 ? (long long)(grp + 1) * gsteps : (P + 15) / 16;   // (end step)
+  const long long wstride = (long long)Rb * 4;
+  const long long s0 = (long long)grp * gsteps + (long long)((int)blockIdx.x - grp * Rb) * 4 + wave;
   auto load = [&](long long st, uint4& yv, int64_t& lb) __attribute__((always_inline)) {
     const long long px = st * 16 + n;
     const long long pc = px < P ? px : 0;
@@ -986,12 +993,17 @@ __global__ __launch_bounds__(256, 3) void head32_apply_kernel(
     const int64_t* __restrict__ labels, const float* __restrict__ gscale,
     const float* __restrict__ stats3, const float* __restrict__ bn4,
     const float* __restrict__ coefs, bf16_t* __restrict__ dY, long long P, int ignore_index,
-    int Kreal) {
+    int Kreal, int groups, long long gsteps) {
   constexpr int C = 32;
   // scale | shift | invstd | -mean*invstd | k | m1 | m2 (the BN backward coefficients)
   __shared__ __attribute__((aligned(16))) float sK[7][C];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, g = lane >> 4;
+  // BN groups: group-major workgroups as head32_kernel (bn4 [groups][4][C], coefs [groups][3][C])
+  const int Rb = groups > 1 ? (int)gridDim.x / groups : (int)gridDim.x;
+  const int grp = groups > 1 ? (int)blockIdx.x / Rb : 0;
+  bn4 += (long long)grp * 4 * C;
+  coefs += (long long)grp * 3 * C;
   const Head32W w = head32_weights(Wh, bh, Kreal, lane);
   if (tid < C) {
     sK[0][tid] = bn4[2 * C + tid]; sK[1][tid] = bn4[3 * C + tid];
@@ -1001,9 +1013,9 @@ __global__ __launch_bounds__(256, 3) void head32_apply_kernel(
   __syncthreads();
   const float cnt = stats3[2];
   const float gs = (gscale != nullptr ? gscale[0] : 1.0f) / (cnt > 0.f ? cnt : 1.f);
-  const long long steps = (P + 15) / 16;
-  const long long wstride = (long long)gridDim.x * 4;
-  const long long s0 = (long long)blockIdx.x * 4 + wave;
+  const long long steps = groups > 1 ? (long long)(grp + 1) * gsteps : (P + 15) / 16;   // (end step)
+  const long long wstride = (long long)Rb * 4;
+  const long long s0 = (long long)grp * gsteps + (long long)((int)blockIdx.x - grp * Rb) * 4 + wave;
   auto load = [&](long long st, uint4& yv, int64_t& lb) __attribute__((always_inline)) {
     const long long px = st * 16 + n;
     const long long pc = px < P ? px : 0;
@@ -1159,13 +1171,13 @@ void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
   if (C == 32 && K <= MAXK) {
     if (bn4 != nullptr && dA == nullptr)
       hipLaunchKernelGGL((head32_kernel<true, false, false>), dim3(nblocks), dim3(256), 0, st, a, Wh, bh,
-                         labels, gscale, stats3, dA, dW_partial, P, ignore_index, bn4, bnpart, K, nullptr);
+                         labels, gscale, stats3, dA, dW_partial, P, ignore_index, bn4, bnpart, K, nullptr, 1, 0LL);
     else if (bn4 != nullptr)
       hipLaunchKernelGGL((head32_kernel<true, true, false>), dim3(nblocks), dim3(256), 0, st, a, Wh, bh,
-                         labels, gscale, stats3, dA, dW_partial, P, ignore_index, bn4, bnpart, K, nullptr);
+                         labels, gscale, stats3, dA, dW_partial, P, ignore_index, bn4, bnpart, K, nullptr, 1, 0LL);
     else
       hipLaunchKernelGGL((head32_kernel<false, true, false>), dim3(nblocks), dim3(256), 0, st, a, Wh, bh,
-                         labels, gscale, stats3, dA, dW_partial, P, ignore_index, bn4, bnpart, K, nullptr);
+                         labels, gscale, stats3, dA, dW_partial, P, ignore_index, bn4, bnpart, K, nullptr, 1, 0LL);
     return;
   }
   if (bn4 != nullptr && dA == nullptr)               // stats pass of the two-pass backward
@@ -1188,10 +1200,11 @@ void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
 // workgroups per CU and spill)
 bool head_mdw(int C, int K) { return C == 32 && K <= 6; }
 
-int head_fwd_stats_blocks(int C, int K, long long P, int num_cus) {
+int head_fwd_stats_blocks(int C, int K, long long P, int num_cus, int groups) {
   if (C == 32 && K <= MAXK) {
     static const int n = head32_per_cu(reinterpret_cast<const void*>(&head32_kernel<true, false, true>));
-    return head32_grid(P, n, num_cus);
+    const int nb = head32_grid(P, n, num_cus);
+    return groups > 1 ? groups * std::max(1, nb / groups) : nb;   // (groups x Rb, group-major)
   }
   if (!head_mdw(C, K)) return head_ce_bwd_blocks(C, K, true, P, num_cus);
   int per_cu = 8;
@@ -1210,10 +1223,11 @@ int head_fwd_stats_blocks(int C, int K, long long P, int num_cus) {
 void head_ce_fwd_stats_launch(const bf16_t* a, const float* Wh, const float* bh,
                               const int64_t* labels, const float* bn4, float* dW_partial,
                               float* bnpart, float* loss_partial, float* out3, int nblocks,
-                              long long P, int C, int K, int ignore_index, hipStream_t st) {
+                              long long P, int C, int K, int ignore_index, hipStream_t st, int groups) {
   if (C == 32 && K <= MAXK)
     hipLaunchKernelGGL((head32_kernel<true, false, true>), dim3(nblocks), dim3(256), 0, st, a, Wh, bh, labels,
-                       nullptr, nullptr, nullptr, dW_partial, P, ignore_index, bn4, bnpart, K, loss_partial);
+                       nullptr, nullptr, nullptr, dW_partial, P, ignore_index, bn4, bnpart, K, loss_partial,
+                       groups, groups > 1 ? P / groups / 16 : 0LL);
   else if (head_mdw(C, K))
     HEAD_SWITCH(C, K, if constexpr (KK <= 6) {
       hipLaunchKernelGGL((head_fwd_stats_mdw_kernel<KK>), dim3(nblocks), dim3(256), 0, st, a, Wh, bh, labels,
@@ -1235,7 +1249,7 @@ int head_bn_apply_blocks(long long P, int C) {
 void head_bn_apply_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
                           const float* gscale, const float* stats3, const float* bn4,
                           const float* coefs, bf16_t* dY, long long P, int C, int K,
-                          int ignore_index, hipStream_t st) {
+                          int ignore_index, hipStream_t st, int groups) {
   if (C == 32 && K <= MAXK) {
     static const int per_cu = head32_per_cu(reinterpret_cast<const void*>(&head32_apply_kernel));
     static const int cus = [] {
@@ -1244,8 +1258,11 @@ void head_bn_apply_launch(const bf16_t* a, const float* Wh, const float* bh, con
       hipGetDevice(&dev);
       return hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
     }();
-    hipLaunchKernelGGL(head32_apply_kernel, dim3(head32_grid(P, per_cu, cus)), dim3(256), 0, st, a, Wh, bh,
-                       labels, gscale, stats3, bn4, coefs, dY, P, ignore_index, K);
+    const int nb = head32_grid(P, per_cu, cus);
+    const int grid = groups > 1 ? groups * std::max(1, nb / groups) : nb;
+    hipLaunchKernelGGL(head32_apply_kernel, dim3(grid), dim3(256), 0, st, a, Wh, bh,
+                       labels, gscale, stats3, bn4, coefs, dY, P, ignore_index, K, groups,
+                       groups > 1 ? P / groups / 16 : 0LL);
     return;
   }
   const int nb = head_bn_apply_blocks(P, C);

@@ -192,7 +192,14 @@ void bn_group_backward_launch(const bf16_t* dA, const bf16_t* dP, const bf16_t* 
                               const float* stats4, const float* gamma, float* dgamma, float* dbeta,
                               bool accumulate, float* coefs, float* partial_scratch, int nb,
                               bf16_t* dY, int dims, int groups, int N, int D, int H, int W, int C,
-                              hipStream_t st, bool have_partial = false);
+                              hipStream_t st, bool have_partial, double* gsum_scratch);
+// per-group BatchNorm-backward coefficients [groups][3][C] and dgamma / dbeta (summed over the
+// groups in order) from group-major partial rows [groups][nb][2][C]; dscale: optional device
+// factor on the rows (rows reduced at a unit gradient scale)
+void bn_group_grad_rows_launch(const float* partial, int nb, int groups, int C, double count,
+                               const float* gamma, const float* stats4, float* dgamma, float* dbeta,
+                               bool accumulate, float* coefs, double* gsum_scratch,
+                               const float* dscale, hipStream_t st);
 void bn_group_finalize_rows_launch(const float* partial, int nb, int groups, long long gpix, int C,
                                    const float* gamma, const float* beta, float eps, float* out4,
                                    float* arena, long long astride, hipStream_t st);
@@ -207,7 +214,10 @@ void head_ce_fwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
 // bnpart (with bn4): [nblocks][2][C] BatchNorm-backward partial rows of the stored dA;
 // nblocks from head_ce_bwd_blocks (one persistent wave of workgroups)
 int head_ce_bwd_blocks(int C, int K, bool defer, long long P, int num_cus);
-int head_fwd_stats_blocks(int C, int K, long long P, int num_cus);
+// groups > 1 (C = 32 head only): a batched window whose deferred BatchNorm has per-group
+// statistics — group-major workgroups (grid = groups x Rb, BN partial rows [groups][Rb][2][C]),
+// bn4 [groups][4][C], coefs [groups][3][C]; pixels per group a multiple of 16
+int head_fwd_stats_blocks(int C, int K, long long P, int num_cus, int groups = 1);
 void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
                         const float* gscale, const float* stats3, int unused, bf16_t* dA,
                         float* dW_partial, int nblocks, long long P, int C, int K,
@@ -220,11 +230,12 @@ void head_ce_bwd_launch(const bf16_t* a, const float* Wh, const float* bh, const
 void head_ce_fwd_stats_launch(const bf16_t* a, const float* Wh, const float* bh,
                               const int64_t* labels, const float* bn4, float* dW_partial,
                               float* bnpart, float* loss_partial, float* out3, int nblocks,
-                              long long P, int C, int K, int ignore_index, hipStream_t st);
+                              long long P, int C, int K, int ignore_index, hipStream_t st,
+                              int groups = 1);
 void head_bn_apply_launch(const bf16_t* a, const float* Wh, const float* bh, const int64_t* labels,
                           const float* gscale, const float* stats3, const float* bn4,
                           const float* coefs, bf16_t* dY, long long P, int C, int K,
-                          int ignore_index, hipStream_t st);
+                          int ignore_index, hipStream_t st, int groups = 1);
 void head_logits_launch(const bf16_t* a, const float* Wh, const float* bh, float* logits_nchw,
                         long long P, long long HW, int C, int K, const float* bn4, hipStream_t st);
 

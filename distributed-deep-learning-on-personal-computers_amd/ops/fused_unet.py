@@ -157,8 +157,8 @@ class _DoubleConvFn(torch.autograd.Function):
         training = blk.bn1.bn.training
         G = blk.engine.bn_groups if training else 0
         if G >= 1:
-            assert not defer and not defer_skip and x2_bn is None, "BN groups: no deferred BN"
-            return _DoubleConvFn._group_forward(ctx, x1, x2, b1, b2, g1, g2, blk, pool, G)
+            assert not defer_skip and x2_bn is None, "BN groups: no deferred skips"
+            return _DoubleConvFn._group_forward(ctx, x1, x2, b1, b2, g1, g2, blk, pool, G, defer)
         ctx.groups = 0
         c1 = p1.cout
         sc2 = x2_bn[2] if x2_bn is not None else None
@@ -217,7 +217,7 @@ class _DoubleConvFn(torch.autograd.Function):
         return a2, None, None
 
     @staticmethod
-    def _group_forward(ctx, x1, x2, b1, b2, g1, g2, blk, pool: bool, G: int):
+    def _group_forward(ctx, x1, x2, b1, b2, g1, g2, blk, pool: bool, G: int, defer: bool = False):
         """A batched window of G micro-batches (``UNetEngine.bn_groups``): the convolutions
         run over the whole batch, every BatchNorm normalises each micro-batch with its own
         statistics (ref.py:580,583 at batch_size 1).
@@ -227,7 +227,11 @@ class _DoubleConvFn(torch.autograd.Function):
         statistics pass), the second conv applies the per-group BN1 + ReLU in its prologue
         (a1 is never materialised) and its weight gradient re-applies it on load.
         Otherwise BN + ReLU is materialised per group (a1) and the convs read it plainly.
-        a2 (+ pool) is materialised in both; y1 / y2 stay for the backward."""
+        a2 (+ pool) is materialised in both — except for the last decoder block with
+        ``defer`` (``UNetEngine.group_head_defer``): it hands out the pre-BN y2 and the group
+        statistics to the C = 32 head kernels, which apply each group's BN + ReLU on load and
+        return the two-pass head gradient with group-major BN-backward partial rows.  y1 / y2
+        stay for the backward."""
         F = _ops()
         p1, p2 = blk.pack1, blk.pack2
         fused = blk.engine.group_fused(x1, G, p1.cout)
@@ -247,10 +251,17 @@ class _DoubleConvFn(torch.autograd.Function):
             a1 = F.bn_group_apply(y1, s1, G, False)[0]
             y2 = F.conv3_fwd(a1, None, p2.fwd, b2, None, None, p2.cout, 0, False)[0]
             s2 = blk.bn2.finalize_groups(y2, G)
-        a2, pooled = F.bn_group_apply(y2, s2, G, pool)
         ctx.groups = G
-        ctx.blk, ctx.pool, ctx.defer = blk, pool, False
+        ctx.blk, ctx.pool, ctx.defer = blk, pool, defer
         ctx.has_x2 = x2 is not None
+        if defer:
+            assert not pool, "BN groups: only the head's input is deferred"
+            ctx.save_for_backward(x1, x2 if x2 is not None else torch.empty(0), y1, y2, s1, s2, g1,
+                                  g2, a1)
+            ctx.set_materialize_grads(False)
+            ctx.mark_non_differentiable(s2)
+            return y2, None, s2
+        a2, pooled = F.bn_group_apply(y2, s2, G, pool)
         ctx.save_for_backward(x1, x2 if x2 is not None else torch.empty(0), y1, y2, s1, s2, g1,
                               g2, a1)
         ctx.set_materialize_grads(False)
@@ -266,7 +277,8 @@ class _DoubleConvFn(torch.autograd.Function):
         x2 = x2 if ctx.has_x2 else None
         if da2 is None and dpool is None:
             return (None,) * 15
-        da2 = da2.contiguous() if da2 is not None else None
+        if da2 is not None and not ctx.defer:
+            da2 = da2.contiguous()
         dpool = dpool.contiguous() if dpool is not None else None
         bn1, bn2 = blk.bn1.bn, blk.bn2.bn
         p1, p2 = blk.pack1, blk.pack2
@@ -275,8 +287,24 @@ class _DoubleConvFn(torch.autograd.Function):
         fused = ctx.fused
         # (fused: conv2's input is relu(bn1(y1)) per group, formed on load from y1)
         xw2, psc, psh = (y1, s1[:, 2], s1[:, 3]) if fused else (a1, None, None)
+        # deferred into the head: its second pass recomputes dA and applies each group's BN2
+        # backward (group-major partial rows from the fused forward, at unit scale)
+        head = getattr(da2, "_ddlpc_head", None) if (ctx.defer and da2 is not None) else None
+        if ctx.defer and head is None:
+            raise RuntimeError("BN groups: the deferred head input has a second autograd consumer")
+        hargs = ((*head, s2, da2._ddlpc_bn_partial, g2) if head is not None else None)
+        hps = getattr(da2, "_ddlpc_bn_pscale", None) if head is not None else None
         # ---- second conv: per-group BN2 + ReLU (+ unpool + skip sum) backward, its gradients
-        if direct:
+        if direct and head is not None:
+            dy2 = F.head_ce_bn_bwd(*hargs, bn2.weight.grad, bn2.bias.grad, hps, G)[0]
+            with eng.wgrad_stream(dy2, xw2, s1):
+                F.conv3_wgrad(dy2, xw2, None, psc, psh, blk.conv2.weight.grad, groups=G)
+                eng.ready(bn2.weight, bn2.bias, blk.conv2.weight, blk.conv2.bias)
+            dg2 = dbe2 = dw2 = None
+        elif head is not None:
+            dy2, dg2, dbe2 = F.head_ce_bn_bwd(*hargs, None, None, hps, G)
+            dw2 = F.conv3_wgrad(dy2, xw2, None, psc, psh, groups=G).view_as(blk.conv2.weight)
+        elif direct:
             dy2 = F.bn_group_backward(da2, dpool, y2, s2, g2, G, bn2.weight.grad, bn2.bias.grad)[0]
             with eng.wgrad_stream(dy2, xw2, s1):
                 F.conv3_wgrad(dy2, xw2, None, psc, psh, blk.conv2.weight.grad, groups=G)
@@ -520,11 +548,15 @@ class _HeadCEFn(torch.autograd.Function):
         ctx.rows = None
         # (Function.forward runs with grad mode off: needs_input_grad says whether a
         # backward will follow)
+        # (BN groups: bn = [groups][4][C] per-group statistics, fused forward only —
+        # UNetEngine.group_head_defer)
+        groups = bn.shape[0] if (bn is not None and bn.dim() == 3) else 0
         if (bn is not None and engine.head_apply and engine.head_fused_fwd
                 and any(ctx.needs_input_grad[:3])):
-            out3, wrows, brows = _ops().head_ce_fwd_stats(a, wh, bh, labels, ignore_index, bn)
+            out3, wrows, brows = _ops().head_ce_fwd_stats(a, wh, bh, labels, ignore_index, bn, groups)
             ctx.rows = (wrows, brows)
         else:
+            assert groups == 0, "grouped head statistics need the fused training forward"
             out3 = _ops().head_ce_fwd(a, wh, bh, labels, ignore_index, bn)
         ctx.save_for_backward(a, wh, bh, labels, out3, bn if bn is not None else torch.empty(0))
         ctx.has_bn = bn is not None
@@ -948,7 +980,7 @@ class UNetEngine:
         n = len(self.dec)
         mode = self.defer_mode if not grouped else "none"    # "all" | "convt" | "none"
         feeds_convt = [pack is not None and mode != "none" for _, pack, _ in self.dec]
-        defer_last = defer_last and mode == "all"
+        defer_last = defer_last and (self.group_head_defer(x) if grouped else mode == "all")
         h, _, s = self.mid(h, None, False, defer=n > 0 and feeds_convt[0])
         for i, ((ub, pack, blk), (skip, s_skip)) in enumerate(zip(self.dec, reversed(skips))):
             if pack is not None:
@@ -985,6 +1017,19 @@ class UNetEngine:
         n, h, w = x.shape[0], x.shape[1], x.shape[2]
         return (cmid % 32 == 0 and w >= 8 and n % G == 0 and
                 (n // G) * h * w >= self.group_fuse_min_px)
+
+    def group_head_defer(self, x: torch.Tensor) -> bool:
+        """BN groups: whether the last decoder block's BatchNorm is deferred into the head
+        (the C = 32 matrix-core head kernels, group-major; the fused training forward and the
+        two-pass backward; pixels per group a multiple of 16)."""
+        G = self.bn_groups
+        wh = self.head.weight
+        if not (self.head_apply and self.head_fused_fwd and G >= 2 and self.group_fuse_min_px is not None):
+            return False
+        pix = x.shape[0] // G
+        for d in x.shape[2:]:
+            pix *= d
+        return wh.shape[1] == 32 and wh.shape[0] <= 16 and x.shape[0] % G == 0 and pix % 16 == 0
 
     def bn_groups_supported(self, tile: int) -> bool:
         return bn_groups_supported(self.model, tile)

@@ -1162,3 +1162,55 @@ def test_conv_bn_group_fusion(ops, G, n, H, W, Cin, Cmid):
     assert rel_err(dY1, dY0) < 2e-3, rel_err(dY1, dY0)
     assert torch.allclose(dg1, dg0, rtol=2e-3, atol=2e-3 * float(dg0.abs().max()))
     assert torch.allclose(db1, db0, rtol=2e-3, atol=2e-3 * float(db0.abs().max()))
+
+
+@pytest.mark.parametrize("G,n,H,W,K", [(4, 1, 32, 32, 6), (3, 2, 16, 24, 6), (50, 1, 16, 16, 6),
+                                       (2, 1, 64, 48, 16)])
+def test_head_bn_groups(ops, G, n, H, W, K):
+    """The C = 32 head with the last decoder block's BatchNorm deferred in a batched window
+    of G micro-batches (per-group statistics, group-major workgroups): the fused training
+    forward (loss, hits, dWh rows, BN partial rows) and the two-pass backward's per-group BN
+    apply against fp32 autograd through each group's BatchNorm + ReLU, the 1x1 head and the
+    cross-entropy over the whole window."""
+    torch.manual_seed(G * 3 + K)
+    C, N = 32, G * n
+    eps = 1e-5
+    y = (torch.randn(N, H, W, C, device=DEV) * 1.5 + 0.3).bfloat16()
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.3
+    s4 = ops.bn_group_finalize(y, G, gamma, beta, eps)
+    wh = torch.randn(K, C, device=DEV) * 0.3
+    bh = torch.randn(K, device=DEV) * 0.1
+    lab = torch.randint(0, K, (N, H, W), device=DEV)
+    lab[0, 0, :3] = -100
+    out3, wrows, brows = ops.head_ce_fwd_stats(y, wh, bh, lab, -100, s4, G)
+    assert brows.shape[0] % G == 0
+    # fp32 reference: per-group BN + ReLU as the kernel forms it (fma, bf16, max 0)
+    sc = s4[:, 2].repeat_interleave(n, 0)[:, None, None, :]
+    sh = s4[:, 3].repeat_interleave(n, 0)[:, None, None, :]
+    a = torch.relu(torch.addcmul(sh, y.float(), sc).bfloat16().float()).requires_grad_(True)
+    w_ = wh.clone().requires_grad_(True)
+    b_ = bh.clone().requires_grad_(True)
+    logits = a @ w_.t() + b_
+    loss = F.cross_entropy(logits.reshape(-1, K), lab.reshape(-1), ignore_index=-100)
+    loss.backward()
+    valid = lab != -100
+    hits = ((logits.argmax(-1) == lab) & valid).sum()
+    assert abs(float(out3[0]) - float(loss)) <= 2e-3 * float(loss), (float(out3[0]), float(loss))
+    assert float(out3[2]) == float(valid.sum())
+    assert abs(float(out3[1]) - float(hits)) <= 0.002 * float(valid.sum()) + 2
+    scale = ops.head_grad_scale(out3, None)
+    dw, db = ops.head_wgrad_from_rows(wrows, scale, K, C)
+    assert rel_err(dw, w_.grad) < 1e-2 and rel_err(db, b_.grad) < 1e-2
+    dY, dg, dbeta = ops.head_ce_bn_bwd(y, wh, bh, lab, out3, None, -100, s4, brows, gamma, None,
+                                       None, scale, G)
+    dg_ref = torch.zeros(C, device=DEV, dtype=torch.float64)
+    db_ref = torch.zeros(C, device=DEV, dtype=torch.float64)
+    for g in range(G):
+        sl = slice(g * n, (g + 1) * n)
+        dYo, dgo, dbo = bn_relu_pool_backward_oracle(y[sl], a.grad[sl], None, gamma, beta, eps, s4[g])
+        assert rel_err(dY[sl], dYo) < 2e-2, (g, rel_err(dY[sl], dYo))
+        dg_ref += dgo.double()
+        db_ref += dbo.double()
+    assert torch.allclose(dg.double(), dg_ref, rtol=1e-2, atol=2e-2 * float(dg_ref.abs().max()))
+    assert torch.allclose(dbeta.double(), db_ref, rtol=1e-2, atol=2e-2 * float(db_ref.abs().max()))

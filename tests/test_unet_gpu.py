@@ -458,9 +458,11 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg, wd):
 
     * the same micro-batches one by one through the unfused grouped kernels
       (``bn_groups = 1``): where the batched convs tile like the batch-2 ones (64^2) the
-      window must agree to fp32 summation order (rel L2 <= 1e-5; measured 6.7e-8) with
-      bit-identical running statistics; elsewhere to FIXED bounds (rel L2 <= 3e-2,
-      conv-weight cosine >= 0.9; measured at 512^2 x 50: 4.6e-3 / 0.959);
+      plain grouped window (no group fusions) must agree to fp32 summation order (rel L2
+      <= 1e-5; measured 6.7e-8) with bit-identical running statistics, and the fused window
+      (group-major conv statistics / prologues, the per-group deferred head) must stay
+      within rel L2 5e-3 / cosine 0.999 of it; elsewhere FIXED bounds (rel L2 <= 3e-2,
+      conv-weight cosine >= 0.9; measured at 512^2 x 50: 7.0e-3 / 0.909);
     * the fused one-by-one path (deferred BN, prologue fusion): rel L2 <= 8e-2, conv-weight
       cosine >= 0.85 (the same distance as fused vs unfused one by one, see below);
     * (small cases) the stock fp32 PyTorch model run micro-batch by micro-batch with its own
@@ -490,8 +492,15 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg, wd):
         tr.meter.reset()
         for k, v in bufs.items():
             v.copy_(b0[k])
-        if mode == "window":
-            tr._window_step(mbs, accum)                  # one batched pass
+        if mode in ("window", "window_plain"):
+            # window_plain: the round-4 grouped path (no conv / head fusion of the groups)
+            keep = eng.group_fuse_min_px
+            if mode == "window_plain":
+                eng.group_fuse_min_px = None
+            try:
+                tr._window_step(mbs, accum)              # one batched pass
+            finally:
+                eng.group_fuse_min_px = keep
         else:
             for x, y in mbs:                             # one by one
                 eng.bn_groups = 1 if mode == "unfused" else 0
@@ -503,7 +512,7 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg, wd):
         return (tr.flat.grad_buf.clone(), tr.meter.buf.clone(),
                 {k: v.clone() for k, v in bufs.items()})
 
-    res = {m: run(m) for m in ("fused", "unfused", "window")}
+    res = {m: run(m) for m in ("fused", "unfused", "window_plain", "window")}
     assert eng.bn_groups == 0
 
     def compare(ref_mode, got):
@@ -528,6 +537,8 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg, wd):
 
     rel_u, cos_u = compare("unfused", "window")
     rel_f, cos_f = compare("fused", "window")
+    rel_p, cos_p = compare("unfused", "window_plain")
+    rel_w, cos_w = compare("window_plain", "window")     # the group fusions (conv tiles, head)
     compare("fused", "unfused")                          # (the two one-by-one paths, printed)
     # fixed bounds.  Measured (rel L2 / min conv-weight cosine): window vs unfused 4.6e-3 /
     # 0.959 at 512^2 x 50, 1.9e-2 / 0.944 at 128^2 width-divisor 1; window vs fused 7.0e-3 /
@@ -535,10 +546,15 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg, wd):
     # differ from each other by exactly as much: the deepest weight gradients of a small-
     # batch U-Net, whose bottleneck BatchNorms normalise 2x2 .. 16x16 pixels, amplify bf16
     # rounding differences.  (The fp32 yardstick below is the kernel-independent check.)
+    # (64^2: the plain grouped window runs the same arithmetic as the one-by-one unfused
+    # path; the fused window moves the head's BN (deferred, per-group) and, from 16384 pixels
+    # per group, the conv statistics to other rounding points: measured 1.5e-3 / 0.99994)
     if tile == 64:
-        assert rel_u <= 1e-5, rel_u
+        assert rel_p <= 1e-5, rel_p
+        assert rel_w <= 5e-3 and cos_w >= 0.999, (rel_w, cos_w)
     else:
         assert rel_u <= 3e-2 and cos_u >= 0.9, (rel_u, cos_u)
+        assert rel_p <= 3e-2 and cos_p >= 0.9, (rel_p, cos_p)
     assert rel_f <= 8e-2 and cos_f >= 0.85, (rel_f, cos_f)
     for ref_mode in ("unfused", "fused"):
         m0, m1 = res[ref_mode][1], res["window"][1]
@@ -548,7 +564,8 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg, wd):
     for k in b0:
         bu, bw, bf = res["unfused"][2][k], res["window"][2][k], res["fused"][2][k]
         if "num_batches" in k or tile == 64:
-            assert torch.equal(bw, bu), (k, float((bw.float() - bu.float()).abs().max()))
+            bp = res["window_plain"][2][k]
+            assert torch.equal(bp, bu), (k, float((bp.float() - bu.float()).abs().max()))
         if "num_batches" in k:
             assert torch.equal(bw, bf), k
         else:
