@@ -494,6 +494,48 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   return into ? at::empty({0}, dy.options().dtype(at::kFloat)) : dW;
 }
 
+// ------------------------------------------------------------------------ fused 32-channel backward
+// The second conv of a 32-channel DoubleConv (input relu(bn1(y))): data gradient dA with the
+// BN1-backward partial rows [grid][2][32] and the weight gradient (OIHW [32][32][3][3],
+// accumulated into dw_out when given) from one pass over dY and y (conv3x3_bwd32.hip)
+std::vector<at::Tensor> conv3_bwd32(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& s4,
+                                    const at::Tensor& wd, const c10::optional<at::Tensor>& dw_out) {
+  CHECK_DEV(dy); CHECK_CONTIG(dy); CHECK_BF16(dy); CHECK_CONTIG(y); CHECK_BF16(y);
+  CHECK_BF16(wd); CHECK_CONTIG(wd); CHECK_F32(s4); CHECK_CONTIG(s4);
+  c10::DeviceGuard guard(dy.device());
+  const Geo g = geo_of(dy);
+  const Geo gy = geo_of(y);
+  TORCH_CHECK(g.dims == 2 && g.C == 32 && gy.dims == 2 && gy.C == 32 && gy.N == g.N && gy.H == g.H &&
+              gy.W == g.W, "conv3_bwd32: 2-D dY and y of one shape with 32 channels");
+  TORCH_CHECK(wd.numel() == 32 * 9 * 32 && s4.numel() == 4 * 32,
+              "conv3_bwd32: data-gradient pack [32][9][32] and stats4 [4][32]");
+  TORCH_CHECK((long long)g.H * g.W * 64 < (1LL << 31), "conv3_bwd32: image too large for 32-bit offsets");
+  Bwd32Args a{};
+  a.N = g.N; a.H = g.H; a.W = g.W;
+  a.dY = bptr(dy); a.Y = bptr(y); a.s4 = s4.data_ptr<float>(); a.Wd = bptr(wd);
+  a.tilesH = (g.H + 15) / 16; a.tilesW = (g.W + 15) / 16;
+  a.nTiles = g.N * a.tilesH * a.tilesW;
+  const int grid = conv3_bwd32_grid(a.nTiles, num_cus());
+  auto fopts = dy.options().dtype(at::kFloat);
+  at::Tensor dA = at::empty_like(dy);
+  at::Tensor bnpart = at::empty({grid, 2, 32}, fopts);
+  at::Tensor wpart = at::empty({(int64_t)grid * 32 * 9 * 32}, fopts);
+  a.dA = bptr_mut(dA); a.bnpart = bnpart.data_ptr<float>(); a.wpart = wpart.data_ptr<float>();
+  conv3_bwd32_launch(a, grid, cur_stream());
+  const bool into = dw_out.has_value() && dw_out->defined();
+  if (into) {
+    CHECK_F32(*dw_out); CHECK_CONTIG(*dw_out);
+    TORCH_CHECK(dw_out->numel() == 32 * 32 * 9, "dW out size mismatch");
+  }
+  at::Tensor dW = into ? *dw_out : at::empty({32, 32, 3, 3}, fopts);
+  const long long NW = 32LL * 9 * 32;
+  at::Tensor tmp = grid > 64 ? at::empty({(int64_t)((grid + 63) / 64) * NW}, dy.options().dtype(at::kDouble))
+                             : at::empty({0}, dy.options().dtype(at::kDouble));
+  reduce_rows_scatter_launch(wpart.data_ptr<float>(), grid, NW, tmp.data_ptr<double>(), dW.data_ptr<float>(),
+                             0, 32, 9, 32, into, cur_stream());
+  return {dA, bnpart, into ? at::empty({0}, fopts) : dW};
+}
+
 // ------------------------------------------------------------------------ BatchNorm
 // returns stats4 [4][C] = (mean, invstd, scale, shift)
 at::Tensor bn_finalize(const at::Tensor& partial, double count, const at::Tensor& gamma,
@@ -1501,6 +1543,7 @@ TORCH_LIBRARY(ddlpc, m) {
   m.def("conv3_wgrad(Tensor dy, Tensor x1, Tensor? x2, Tensor? pscale, Tensor? pshift, Tensor(a!)? out=None, "
         "Tensor? pscale2=None, Tensor? pshift2=None, Tensor? dy_y=None, Tensor? dy_s4=None, "
         "Tensor? dy_coefs=None, int cin_real=0, int groups=0) -> Tensor");
+  m.def("conv3_bwd32(Tensor dy, Tensor y, Tensor s4, Tensor wd, Tensor(a!)? dw_out=None) -> Tensor[]");
   m.def("reduce_rows(Tensor partial, int R, int N) -> Tensor");
   m.def("bn_finalize(Tensor partial, float count, Tensor gamma, Tensor beta, Tensor(a!) running_mean, "
         "Tensor(b!) running_var, float momentum, float eps, bool update_running, Tensor(c!)? nbt) -> Tensor");
@@ -1563,6 +1606,7 @@ TORCH_LIBRARY_IMPL(ddlpc, CUDA, m) {
   m.impl("bn_relu_apply", &ddlpc::bn_relu_apply);
   m.impl("bn_running_apply", &ddlpc::bn_running_apply);
   m.impl("bn_grad_coefs", &ddlpc::bn_grad_coefs);
+  m.impl("conv3_bwd32", &ddlpc::conv3_bwd32);
   m.impl("bn_backward", &ddlpc::bn_backward);
   m.impl("bn_group_finalize", &ddlpc::bn_group_finalize);
   m.impl("bn_group_apply", &ddlpc::bn_group_apply);

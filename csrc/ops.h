@@ -69,6 +69,24 @@ int conv3_fwd_cfg_bn(int cfg);
 int conv3_fwd_cfg_bm(int cfg);
 int conv3_fwd_cfg_halo(int dims, int cfg);
 
+// ---------------------------------------------------------------- fused 32-channel backward
+// data + weight gradient of a 32 -> 32-channel 3x3 conv whose input is relu(bn1(Y)), from one
+// read of dY and Y (conv3x3_bwd32.hip): dA [N][H][W][32] bf16, BN1-backward partial rows
+// bnpart [grid][2][32] (sum dyh, sum dyh * xhat), weight-gradient slabs wpart [grid][32][9][32]
+struct Bwd32Args {
+  int N, H, W;
+  const bf16_t* dY;
+  const bf16_t* Y;
+  const float* s4;                // [4][32] BN1 (mean, invstd, scale, shift)
+  const bf16_t* Wd;               // data-gradient pack [32 ci][9][32 co] (flipped taps)
+  bf16_t* dA;
+  float* bnpart;
+  float* wpart;
+  int tilesH, tilesW, nTiles;     // 16 x 16 pixel tiles
+};
+int conv3_bwd32_grid(int nTiles, int num_cus);
+void conv3_bwd32_launch(const Bwd32Args& a, int grid, hipStream_t st);
+
 // ---------------------------------------------------------------- conv 3x3 wgrad
 struct ConvWgradArgs {
   int dims;

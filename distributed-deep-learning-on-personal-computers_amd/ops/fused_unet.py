@@ -389,6 +389,11 @@ class _DoubleConvFn(torch.autograd.Function):
         part2 = getattr(da2, "_ddlpc_bn_partial", None) if ctx.defer else None
         bn1, bn2 = blk.bn1.bn, blk.bn2.bn
         direct = eng.direct_grads
+        p1, p2 = blk.pack1, blk.pack2
+        # the 32-channel level: conv2's data and weight gradients in ONE kernel that reads dY2
+        # and y1 once (conv3x3_bwd32.hip; BN1-backward partials in its epilogue)
+        bwd32 = (eng.bwd32 and eng.bnb_epilogue and y1.dim() == 4 and p2.cin == 32 and
+                 p2.cout == 32)
         # ---- second conv: BN2 + ReLU (+ unpool + skip sum) backward, then its gradients
         if direct:
             if head is not None:
@@ -397,9 +402,14 @@ class _DoubleConvFn(torch.autograd.Function):
             else:
                 dy2, _, _ = F.bn_backward(da2, dpool, y2, s2, g2, None, bn2.weight.grad,
                                           bn2.bias.grad, part2)
-            with eng.wgrad_stream(dy2, y1, s1):
-                F.conv3_wgrad(dy2, y1, None, s1[2], s1[3], blk.conv2.weight.grad)
-                eng.ready(bn2.weight, bn2.bias, blk.conv2.weight, blk.conv2.bias)
+            if bwd32:
+                da1, part1, _ = F.conv3_bwd32(dy2, y1, s1, p2.dgrad, blk.conv2.weight.grad)
+                with eng.wgrad_stream():
+                    eng.ready(bn2.weight, bn2.bias, blk.conv2.weight, blk.conv2.bias)
+            else:
+                with eng.wgrad_stream(dy2, y1, s1):
+                    F.conv3_wgrad(dy2, y1, None, s1[2], s1[3], blk.conv2.weight.grad)
+                    eng.ready(bn2.weight, bn2.bias, blk.conv2.weight, blk.conv2.bias)
             dg2 = dbe2 = dw2 = None
         else:
             if head is not None:
@@ -407,14 +417,17 @@ class _DoubleConvFn(torch.autograd.Function):
                                                   getattr(da2, "_ddlpc_bn_pscale", None))
             else:
                 dy2, dg2, dbe2 = F.bn_backward(da2, dpool, y2, s2, g2, None, None, None, part2)
-            dw2 = F.conv3_wgrad(dy2, y1, None, s1[2], s1[3]).view_as(blk.conv2.weight)
-        p1, p2 = blk.pack1, blk.pack2
-        part1 = None
-        if eng.bnb_epilogue and y1.dim() == 4:
+            if bwd32:
+                da1, part1, dw2 = F.conv3_bwd32(dy2, y1, s1, p2.dgrad)
+                dw2 = dw2.view_as(blk.conv2.weight)
+            else:
+                dw2 = F.conv3_wgrad(dy2, y1, None, s1[2], s1[3]).view_as(blk.conv2.weight)
+        if not bwd32 and eng.bnb_epilogue and y1.dim() == 4:
             # the epilogue also reduces BN1 backward's (sum dyh, sum dyh*xhat) against y1
             da1, _, part1 = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False,
                                         None, None, y1, s1)
-        else:
+        elif not bwd32:
+            part1 = None
             da1, _, _ = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False)
         # ---- first conv
         w1 = blk.conv1.weight
@@ -760,6 +773,9 @@ class UNetEngine:
         # first block: BN1 backward applied on load by its weight gradient (no apply pass;
         # False: separate bn_backward)
         self.wgrad_dy_prologue = True
+        # 32 -> 32-channel second convs: data + weight gradient in one kernel (conv3x3_bwd32;
+        # False: the resident data gradient + the v3 weight gradient on the side stream)
+        self.bwd32 = os.environ.get("DDLPC_BWD32", "1") != "0"
         self.enc = [_Block(b.double_conv, first=(i == 0), engine=self)
                     for i, b in enumerate(model.down_blocks())]
         self.mid = _Block(model.double_conv, first=False, engine=self)

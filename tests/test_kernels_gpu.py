@@ -1214,3 +1214,37 @@ def test_head_bn_groups(ops, G, n, H, W, K):
         db_ref += dbo.double()
     assert torch.allclose(dg.double(), dg_ref, rtol=1e-2, atol=2e-2 * float(dg_ref.abs().max()))
     assert torch.allclose(dbeta.double(), db_ref, rtol=1e-2, atol=2e-2 * float(db_ref.abs().max()))
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 32, 32), (3, 24, 40), (1, 50, 18), (300, 16, 16)])
+def test_conv3_bwd32(ops, N, H, W):
+    """The fused backward of a 32 -> 32-channel conv on relu(bn1(y)) (data gradient + BN1
+    partials + weight gradient from one pass over dY and y) against fp32 torch and against
+    the separate kernels it replaces (resident data gradient with the BN-backward epilogue,
+    v3 weight gradient with the BN prologue).  Partial 16x16 tiles and more tiles than CUs
+    (persistent workgroups) included."""
+    torch.manual_seed(N + H)
+    C = 32
+    y = (torch.randn(N, H, W, C, device=DEV) * 1.3 + 0.2).bfloat16()
+    dy = (torch.randn(N, H, W, C, device=DEV) * 0.1).bfloat16()
+    w = torch.randn(C, C, 3, 3, device=DEV) / math.sqrt(9 * C)
+    s4 = _bn4(C, 7)
+    pk = pack_conv(ops, w)
+    dA, part, dW = ops.conv3_bwd32(dy, y, s4, pk.dgrad)
+    # fp32 references on the bf16-rounded a1 = relu(bf16(y * scale + shift))
+    a1 = torch.relu(torch.addcmul(s4[3], y.float(), s4[2]).bfloat16().float())
+    dW_ref = torch.nn.grad.conv2d_weight(nchw(a1), w.shape, nchw(dy).float(), padding=1)
+    dA_ref = torch.nn.grad.conv2d_input(nchw(a1).shape, w.bfloat16().float(), nchw(dy).float(), padding=1)
+    assert rel_err(dW, dW_ref) < 5e-3, rel_err(dW, dW_ref)
+    assert rel_err(nchw(dA), dA_ref) < 1e-2, rel_err(nchw(dA), dA_ref)
+    # against the kernels it replaces
+    dA0, _, part0 = ops.conv3_fwd(dy, None, pk.dgrad, None, None, None, C, 0, False, None, None, y, s4)
+    dW0 = ops.conv3_wgrad(dy, y, None, s4[2], s4[3])
+    assert rel_err(dA, dA0) < 2e-3 and rel_err(dW, dW0) < 1e-3, (rel_err(dA, dA0), rel_err(dW, dW0))
+    ps, ps0 = part.sum(0), part0.sum(0)
+    assert torch.allclose(ps, ps0, rtol=2e-3, atol=2e-3 * float(ps0.abs().max())), \
+        float((ps - ps0).abs().max())
+    # accumulate into a caller buffer (direct-grad mode)
+    acc = torch.ones_like(w)
+    _, _, none = ops.conv3_bwd32(dy, y, s4, pk.dgrad, acc)
+    assert none.numel() == 0 and torch.allclose(acc, dW + 1, rtol=1e-5, atol=1e-5)
