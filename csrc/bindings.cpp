@@ -157,6 +157,15 @@ at::Tensor reduce_rows(const at::Tensor& partial, int64_t R, int64_t N) {
   return sums;
 }
 
+// 3-D depth-streaming kernel on (DDLPC_CONV3D_DS=0: the streaming kernel, for A/B runs)
+static bool conv3d_ds_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DDLPC_CONV3D_DS");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  return on;
+}
+
 // ------------------------------------------------------------------------ conv3 forward
 std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::Tensor>& x2,
                                   const at::Tensor& w, const c10::optional<at::Tensor>& bias,
@@ -244,6 +253,21 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
               "(the engine pads the 3-channel image to 8)");
   auto opts = x1.options();
   a.npix = (long long)g.N * g.D * g.H * g.W;
+  if (g.dims == 3 && conv3d_ds_enabled()) {
+    // the 3-D 32 -> 32-channel level: depth-streaming resident kernel (conv3x3x3_ds.hip)
+    int grid = 0, smem = 0;
+    if (conv3d_ds_plan(a, num_cus(), grid, smem) >= 0) {
+      at::Tensor y1 = at::empty(shape_with_c(g, a.Co1), opts);
+      at::Tensor stats;
+      if (want_stats) stats = at::empty({(int64_t)grid, 2, a.Cout}, opts.dtype(at::kFloat));
+      a.Y1 = bptr_mut(y1);
+      a.Y2 = nullptr;
+      a.stats = want_stats ? stats.data_ptr<float>() : nullptr;
+      conv3d_ds_launch(a, grid, smem, cur_stream());
+      at::Tensor none = at::empty({0}, opts);
+      return {y1, none, stats.defined() ? stats : none};
+    }
+  }
   {
     // high-resolution few-channel layers: resident-weight kernel (conv3x3_res.hip)
     int grid = 0, smem = 0;
@@ -499,7 +523,8 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
 // BN1-backward partial rows [grid][2][32] and the weight gradient (OIHW [32][32][3][3],
 // accumulated into dw_out when given) from one pass over dY and y (conv3x3_bwd32.hip)
 std::vector<at::Tensor> conv3_bwd32(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& s4,
-                                    const at::Tensor& wd, const c10::optional<at::Tensor>& dw_out) {
+                                    const at::Tensor& wd, const c10::optional<at::Tensor>& dw_out,
+                                    int64_t groups) {
   CHECK_DEV(dy); CHECK_CONTIG(dy); CHECK_BF16(dy); CHECK_CONTIG(y); CHECK_BF16(y);
   CHECK_BF16(wd); CHECK_CONTIG(wd); CHECK_F32(s4); CHECK_CONTIG(s4);
   c10::DeviceGuard guard(dy.device());
@@ -507,15 +532,18 @@ std::vector<at::Tensor> conv3_bwd32(const at::Tensor& dy, const at::Tensor& y, c
   const Geo gy = geo_of(y);
   TORCH_CHECK(g.dims == 2 && g.C == 32 && gy.dims == 2 && gy.C == 32 && gy.N == g.N && gy.H == g.H &&
               gy.W == g.W, "conv3_bwd32: 2-D dY and y of one shape with 32 channels");
-  TORCH_CHECK(wd.numel() == 32 * 9 * 32 && s4.numel() == 4 * 32,
-              "conv3_bwd32: data-gradient pack [32][9][32] and stats4 [4][32]");
+  const int G = groups > 1 ? (int)groups : 1;
+  TORCH_CHECK(G <= 1024 && g.N % G == 0, "conv3_bwd32: groups must divide the batch");
+  TORCH_CHECK(wd.numel() == 32 * 9 * 32 && s4.numel() == (int64_t)G * 4 * 32,
+              "conv3_bwd32: data-gradient pack [32][9][32] and stats4 [4][32] ([groups][4][32])");
   TORCH_CHECK((long long)g.H * g.W * 64 < (1LL << 31), "conv3_bwd32: image too large for 32-bit offsets");
   Bwd32Args a{};
   a.N = g.N; a.H = g.H; a.W = g.W;
   a.dY = bptr(dy); a.Y = bptr(y); a.s4 = s4.data_ptr<float>(); a.Wd = bptr(wd);
   a.tilesH = (g.H + 15) / 16; a.tilesW = (g.W + 15) / 16;
   a.nTiles = g.N * a.tilesH * a.tilesW;
-  const int grid = conv3_bwd32_grid(a.nTiles, num_cus());
+  a.groups = G;
+  const int grid = conv3_bwd32_grid(a.nTiles, num_cus(), G);
   auto fopts = dy.options().dtype(at::kFloat);
   at::Tensor dA = at::empty_like(dy);
   at::Tensor bnpart = at::empty({grid, 2, 32}, fopts);
@@ -1543,7 +1571,7 @@ TORCH_LIBRARY(ddlpc, m) {
   m.def("conv3_wgrad(Tensor dy, Tensor x1, Tensor? x2, Tensor? pscale, Tensor? pshift, Tensor(a!)? out=None, "
         "Tensor? pscale2=None, Tensor? pshift2=None, Tensor? dy_y=None, Tensor? dy_s4=None, "
         "Tensor? dy_coefs=None, int cin_real=0, int groups=0) -> Tensor");
-  m.def("conv3_bwd32(Tensor dy, Tensor y, Tensor s4, Tensor wd, Tensor(a!)? dw_out=None) -> Tensor[]");
+  m.def("conv3_bwd32(Tensor dy, Tensor y, Tensor s4, Tensor wd, Tensor(a!)? dw_out=None, int groups=0) -> Tensor[]");
   m.def("reduce_rows(Tensor partial, int R, int N) -> Tensor");
   m.def("bn_finalize(Tensor partial, float count, Tensor gamma, Tensor beta, Tensor(a!) running_mean, "
         "Tensor(b!) running_var, float momentum, float eps, bool update_running, Tensor(c!)? nbt) -> Tensor");

@@ -36,29 +36,39 @@ using namespace convlds;
 
 constexpr int B32_TH = 16, B32_TW = 16, B32_HW2 = 18;
 constexpr int B32_HALO = 18 * 18;                     // halo pixels of a 16x16 tile
-constexpr int B32_ITERS = 3;                          // DMA instructions per wave per halo
-constexpr int B32_HBYTES = B32_ITERS * 8 * 1024;      // 1536 pieces (>= 4 x 324) per halo
+constexpr int B32_INSTR = (B32_HALO * 4 + 63) / 64;  // 21 DMA wave-instructions per halo
+constexpr int B32_ITERS = (B32_INSTR + 7) / 8;        // per wave: 3 (waves 0-4) or 2 (5-7)
+constexpr int B32_HBYTES = B32_INSTR * 1024;          // 1344 pieces (>= 4 x 324) per halo
 constexpr int B32_WBYTES = 9 * 32 * ROWB;             // resident dgrad weights (9 taps x 32 rows)
-constexpr int B32_YBYTES = 256 * ROWB;               // raw y of the tile's 256 output pixels
-constexpr int B32_SMEM = 4 * 32 * 4 + B32_WBYTES + 2 * (2 * B32_HBYTES + B32_YBYTES);
+constexpr int B32_NBUF = 3;                           // halo ring depth
+constexpr int B32_SMEM = 4 * 32 * 4 + B32_WBYTES + B32_NBUF * 2 * B32_HBYTES;
 
 __global__ __launch_bounds__(512, 1) void conv3_bwd32_kernel(Bwd32Args p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* s_bnb = reinterpret_cast<float*>(smem);               // BN1 table [4][32]
   char* sW = smem + 4 * 32 * 4;
   char* sH = sW + B32_WBYTES;
-  constexpr int STG = 2 * B32_HBYTES + B32_YBYTES;
+  constexpr int STG = 2 * B32_HBYTES;
   auto sDY = [&](int b) { return sH + b * STG; };                      // dY halo (swizzled rows)
   auto sX = [&](int b) { return sH + b * STG + B32_HBYTES; };          // y -> a1 halo
-  auto sYi = [&](int b) { return sH + b * STG + 2 * B32_HBYTES; };     // raw y, tile interior
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool dgrad = wave < 4;                                 // wave-uniform role
-  const int my_tiles = p.nTiles > (int)blockIdx.x ? (p.nTiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  // tiles t0 + k * tstride.  One group: t0 = blockIdx.x, tstride = gridDim.x.  BN groups
+  // (Bwd32Args::groups, a batched window): group-major — workgroup b serves only the tiles of
+  // group b / R (R = gridDim.x / groups), so its BN-partial row belongs to that group and the
+  // BN1 constants are that group's
+  const int NG_ = p.groups > 1 ? p.groups : 1;
+  const int R = (int)gridDim.x / NG_;
+  const int grp = (int)blockIdx.x / R;
+  const int Tg = p.nTiles / NG_;                     // tiles per group
+  const int r_blk = (int)blockIdx.x - grp * R;
+  const int t0 = grp * Tg + r_blk, tstride = R;
+  const int my_tiles = r_blk < Tg ? (Tg - 1 - r_blk) / R + 1 : 0;
   const long long img_px = (long long)p.H * p.W;
 
-  bnb_fill(s_bnb, 32, 0, 32, p.s4, tid, 512);
+  bnb_fill(s_bnb, 32, 0, 32, p.s4 + grp * 4 * 32, tid, 512);
   // resident data-gradient weights: rows (tap, ci) of 32 co (64 B), swizzled pieces
   {
     const auto rW = make_rsrc(p.Wd, 32u * 9u * 32u * 2u);
@@ -74,7 +84,11 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd32_kernel(Bwd32Args p) {
   // ---- per-lane halo DMA geometry: piece e = (i * 8 + wave) * 64 + lane, pixel e >> 2 (its
   // halo row / column recomputed per issue: registers are the wgrad role's budget)
   const int sub_dy = lane & 3;                       // (the swizzle flips it by the row below)
-  uint32_t xvalid = 0;                               // in-image y pieces of the tile last issued
+  // in-image y pieces of the tile staged in each ring slot, 8 bits per slot (a runtime-indexed
+  // array would live in scratch)
+  uint32_t vmasks = 0;
+  // DMA wave-instructions per halo for this wave (21 over 8 waves: 3 for waves 0-4, 2 after)
+  const int nins = (B32_INSTR - wave + 7) / 8;
   auto tile_geo = [&](int t, int& n, int& h0, int& w0) {
     n = t / (p.tilesH * p.tilesW);
     const int r = t - n * p.tilesH * p.tilesW;
@@ -86,42 +100,45 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd32_kernel(Bwd32Args p) {
     tile_geo(t, n, h0, w0);
     const auto rdy = make_rsrc(p.dY + n * img_px * 32, (unsigned)(img_px * 64));
     const auto ry = make_rsrc(p.Y + n * img_px * 32, (unsigned)(img_px * 64));
-    xvalid = 0;
+    uint32_t xvalid = 0;
 #pragma unroll
     for (int i = 0; i < B32_ITERS; ++i) {
+      if (i * 8 + wave >= B32_INSTR) break;          // (wave-uniform)
       const int px = ((i * 8 + wave) * 64 + lane) >> 2;
       const int gh = h0 + px / B32_HW2 - 1, gw = w0 + px % B32_HW2 - 1;
       const bool ok = px < B32_HALO && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W;
       const unsigned pix = (unsigned)(gh * p.W + gw);
-      // dY: LDS piece (e & 3) of row px holds source piece (e & 3) ^ swz(px)
-      dma16(rdy, sDY(buf) + (i * 8 + wave) * 1024, ok ? (pix * 32 + ((sub_dy ^ swz(px)) << 3)) * 2u : kOOB);
+      // dY: LDS piece (e & 3) of row px holds source piece (e & 3) ^ swz(halo column) — the
+      // swizzle follows the column (bit 2 still flips between lanes 4 pixels apart: conflict-
+      // free 16-pixel reads), so a read's XOR depends on the tap's column offset only and the
+      // row / tap-row terms of every fragment address are immediates
+      dma16(rdy, sDY(buf) + (i * 8 + wave) * 1024,
+            ok ? (pix * 32 + ((sub_dy ^ swz(px % B32_HW2)) << 3)) * 2u : kOOB);
       // y: unswizzled (the weight gradient's transposed reads are conflict-free on 64-B rows)
       dma16(ry, sX(buf) + (i * 8 + wave) * 1024, ok ? (pix * 32 + (sub_dy << 3)) * 2u : kOOB);
       xvalid |= (ok ? 1u : 0u) << i;
     }
+    vmasks = (vmasks & ~(0xffu << (8 * buf))) | (xvalid << (8 * buf));
   };
   // a1 = relu(bf16(y * scale + shift)) on this lane's own landed y pieces; padding stays 0.  The
   // raw y of interior pixels is kept (the data gradient's BN-backward epilogue needs y itself)
   // (the lane's 8 channels, 8 (lane & 3) .. + 7 — an unswizzled y piece a lane DMAs — read
   // from the BN table per tile rather than held in 16 VGPRs across the loop)
-  auto transform = [&](int buf) {
-    char* X = sX(buf);
+  // (the buffer comes in restrict-qualified so its LDS accesses carry alias scopes: the
+  // compiler would otherwise drain the other ring slots' in-flight DMA before them)
+  auto transform_body = [&](char* __restrict__ X, int buf) __attribute__((always_inline)) {
+    const uint32_t xvalid = (vmasks >> (8 * buf)) & 0xffu;
     const float4* kp = reinterpret_cast<const float4*>(s_bnb + opaque_zero() + (lane & 3) * 8);
     const float4 sa = kp[0], sb = kp[1], ha = kp[8], hb = kp[9];
     const float psc[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
     const float psh[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
     uint4 v[B32_ITERS];
 #pragma unroll
-    for (int i = 0; i < B32_ITERS; ++i) v[i] = *reinterpret_cast<const uint4*>(X + ((i * 8 + wave) * 64 + lane) * 16);
+    for (int i = 0; i < B32_ITERS; ++i)
+      if (i * 8 + wave < B32_INSTR) v[i] = *reinterpret_cast<const uint4*>(X + ((i * 8 + wave) * 64 + lane) * 16);
 #pragma unroll
     for (int i = 0; i < B32_ITERS; ++i) {
-      const int px = ((i * 8 + wave) * 64 + lane) >> 2;
-      const int hr = px / B32_HW2, hc = px % B32_HW2;
-      if (px < B32_HALO && hr >= 1 && hr <= B32_TH && hc >= 1 && hc <= B32_TW)
-        *reinterpret_cast<uint4*>(sYi(buf) + ((hr - 1) * B32_TW + hc - 1) * ROWB + (lane & 3) * 16) = v[i];
-    }
-#pragma unroll
-    for (int i = 0; i < B32_ITERS; ++i) {
+      if (i * 8 + wave >= B32_INSTR) break;
       const bool ok = (xvalid >> i) & 1u;
       const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
       uint32_t o[4];
@@ -137,6 +154,38 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd32_kernel(Bwd32Args p) {
       *reinterpret_cast<uint4*>(X + ((i * 8 + wave) * 64 + lane) * 16) = make_uint4(o[0], o[1], o[2], o[3]);
     }
   };
+  auto transform = [&](int buf) __attribute__((always_inline)) { transform_body(sX(buf), buf); };
+
+  // ---- the tile loop (each role passes its own work; both run the same DMA / transform /
+  // barrier sequence per tile).  Ring of B32_NBUF slots: tile k's halos are issued two tiles
+  // ahead; before transforming tile k a wave waits, with a COUNTED vmcnt, only for its own
+  // DMAs of tile k — `issued` counts this wave's vector-memory ops in issue order (the DMAs,
+  // the data-gradient role's y loads and dA stores), m0 / m1 its count right after the DMAs
+  // of tiles k and k+1.  after_sync / work return how many vector-memory ops they issued.
+  auto pipeline = [&](auto after_sync, auto work) __attribute__((always_inline)) {
+    const int nd = 2 * nins;
+    int issued = 0, m0 = 0, m1 = 0;
+    if (my_tiles > 0) { issue(t0, 0); issued += nd; m0 = issued; }
+    if (my_tiles > 1) { issue(t0 + tstride, 1); issued += nd; m1 = issued; }
+    int buf = 0;
+    for (int k = 0; k < my_tiles; ++k) {
+      const int t = t0 + k * tstride;
+      vm_wait_dyn(issued - m0);                      // this wave's halo DMAs of tile k landed
+      transform(buf);
+      lds_sync();                                    // every halo piece visible; tile k-1 done by all
+      issued += after_sync(k, t, buf);
+      int m2 = m1;
+      if (k + 2 < my_tiles) {                        // into the slot tile k-1 used
+        issue(t + 2 * tstride, buf == 0 ? 2 : buf - 1);
+        issued += nd;
+        m2 = issued;
+      }
+      issued += work(t, buf);
+      m0 = m1;
+      m1 = m2;
+      buf = buf == 2 ? 0 : buf + 1;
+    }
+  };
 
   // The two roles run separate tile loops (same DMA / transform / barrier sequence per
   // tile) so their accumulators are never live together: one kernel, each wave's registers
@@ -145,16 +194,38 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd32_kernel(Bwd32Args p) {
     // ---- data-gradient waves: wave w owns tile pixels 64 w .. 64 w + 63 (MT = 4 rows of 16)
     // x 32 ci (NT = 2); A = weights (rows ci), B = dY halo pixels (K = 32 co)
     const int g = lane >> 4;
-    int hp0[4];
+    // per-lane byte offsets: dY halo pixel (wave*4 rows down, column c + dw) with its column
+    // swizzle, for the three tap columns dw; the weight row c of a 16-row block (rows j*32 +
+    // nt*16 + c keep c's bit 2)
+    const int c16 = lane & 15;
+    int xo[3];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) hp0[mt] = (wave * 4 + mt) * B32_HW2 + (lane & 15);
+    for (int dw = 0; dw < 3; ++dw)
+      xo[dw] = (wave * 4 * B32_HW2 + c16 + dw) * ROWB + ((g ^ swz(c16 + dw)) << 4);
+    const int wo = c16 * ROWB + ((g ^ swz(c16)) << 4);
     float s1[2][4], s2[2][4];
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) { s1[nt][i] = 0.f; s2[nt][i] = 0.f; }
-    auto compute = [&](int t, const char* __restrict__ A, const char* __restrict__ Wc,
-                       const char* __restrict__ Yi) {
+    // y at this wave's output pixels for the BN-backward partials: loaded right after the
+    // tile's barrier, before the next halo DMA is issued (L2 hits: the halo just landed), so
+    // the epilogue's wait for them leaves that DMA in flight
+    uint2 ybuf[4][2];
+    auto load_y = [&](int t) {
+      int n, h0, w0;
+      tile_geo(t, n, h0, w0);
+      const auto ry = make_rsrc(p.Y + n * img_px * 32, (unsigned)(img_px * 64));
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int gh = h0 + wave * 4 + mt, gw = w0 + (lane & 15);
+        const bool ok = gh < p.H && gw < p.W;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          ybuf[mt][nt] = buf_load8(ry, ok ? (unsigned)((gh * p.W + gw) * 32 + nt * 16 + 4 * g) * 2u : kOOB);
+      }
+    };
+    auto compute = [&](int t, const char* __restrict__ A, const char* __restrict__ Wc) {
       int n, h0, w0;
       tile_geo(t, n, h0, w0);
       f32x4_t acc[4][2];
@@ -166,11 +237,11 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd32_kernel(Bwd32Args p) {
       // (the 36 swizzled (row, tap) addresses are recomputed per read — an opaque offset keeps
       // them from being hoisted out of the tile loop into 36 live VGPRs, which spilled)
       auto load = [&](int j, uint4 (&x)[4], uint4 (&w)[2]) __attribute__((always_inline)) {
-        const int toff = (j / 3) * B32_HW2 + j % 3 + opaque_zero();
+        const int dh = j / 3, dw = j % 3;
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) x[mt] = lds128(A + lds_off(hp0[mt] + toff, g));
+        for (int mt = 0; mt < 4; ++mt) x[mt] = lds128(A + xo[dw] + (mt + dh) * B32_HW2 * ROWB);
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) w[nt] = lds128(Wc + lds_off(j * 32 + nt * 16 + (lane & 15), g));
+        for (int nt = 0; nt < 2; ++nt) w[nt] = lds128(Wc + wo + (j * 32 + nt * 16) * ROWB);
       };
       load(0, xf[0], wf[0]);
 #pragma unroll
@@ -196,9 +267,7 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd32_kernel(Bwd32Args p) {
           const BnbC kb = bnb_load(s_bnb, 32, nt * 16 + 4 * g);
           const float d[4] = {ok ? acc[mt][nt][0] : 0.f, ok ? acc[mt][nt][1] : 0.f,
                               ok ? acc[mt][nt][2] : 0.f, ok ? acc[mt][nt][3] : 0.f};
-          const uint2 yv = *reinterpret_cast<const uint2*>(Yi + ((wave * 4 + mt) * B32_TW + (lane & 15)) * ROWB +
-                                                           (nt * 16 + 4 * g) * 2);
-          bnb_accum(d, yv, kb, s1[nt], s2[nt]);
+          bnb_accum(d, ybuf[mt][nt], kb, s1[nt], s2[nt]);
         }
         const uint4 qv = pair16(pk[0], pk[1]);
         unsigned off = ok ? (unsigned)((gh * p.W + gw) * 32 + pair16_ch(lane)) * 2u : kOOB;
@@ -207,16 +276,8 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd32_kernel(Bwd32Args p) {
         __builtin_amdgcn_sched_barrier(0);           // (one row's table / y reads at a time)
       }
     };
-    if (my_tiles > 0) issue(blockIdx.x, 0);
-    for (int k = 0; k < my_tiles; ++k) {
-      const int t = (int)blockIdx.x + k * (int)gridDim.x;
-      const int buf = k & 1;
-      dma_wait<0>();                                 // this wave's halo DMAs of tile k
-      transform(buf);
-      lds_sync();                                    // every halo piece visible; tile k-1 done by all
-      if (k + 1 < my_tiles) issue(t + (int)gridDim.x, buf ^ 1);
-      compute(t, sDY(buf), sW, sYi(buf));
-    }
+    pipeline([&](int k, int t, int buf) { load_y(t); (void)k; return 8; },
+             [&](int t, int buf) { compute(t, sDY(buf), sW); return 4; });
     dma_wait<0>();
     lds_sync();
     // BN-backward partial row: 16 pixel lanes, then the 4 waves in a fixed order
@@ -251,19 +312,22 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd32_kernel(Bwd32Args p) {
     for (int t = 0; t < 9; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) wacc[t][i] = 0.f;
+    // per-lane byte offsets of the transposed A reads: halo column 1 + px of the tile row, the
+    // chunk XOR of that column (the k-step row term is an immediate)
+    int ao[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int px = (g4 >> 1) * 8 + 4 * h + q;      // pixel within the tile row
+      ao[h] = (1 + px) * ROWB + ((((g4 & 1) * 2 + (pq >> 1)) ^ swz(1 + px)) << 4) + (pq & 1) * 8;
+    }
     auto compute = [&](const char* __restrict__ DY, const char* __restrict__ X) {
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         const int ks = kk * 4 + kw;                  // tile row = 16-pixel k-step
         uint2 av[2];
-        // A = dY^T (rows co, k = the row's 16 pixels) from the swizzled halo interior
+        // A = dY^T (rows co, k = the row's 16 pixels) from the halo interior (column swizzle)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int px = (g4 >> 1) * 8 + 4 * h + q;  // pixel within the tile row
-          const int hr = (ks + 1) * B32_HW2 + 1 + px;
-          const int piece = ((g4 & 1) * 2 + (pq >> 1)) ^ swz(hr);
-          av[h] = lds_read_tr16(DY + hr * ROWB + piece * 16 + (pq & 1) * 8);
-        }
+        for (int h = 0; h < 2; ++h) av[h] = lds_read_tr16(DY + ao[h] + (ks + 1) * B32_HW2 * ROWB);
         const uint4 af = make_uint4(av[0].x, av[0].y, av[1].x, av[1].y);
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
@@ -275,16 +339,8 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd32_kernel(Bwd32Args p) {
         __builtin_amdgcn_sched_barrier(0);           // (operand reads one k-step ahead at most)
       }
     };
-    if (my_tiles > 0) issue(blockIdx.x, 0);
-    for (int k = 0; k < my_tiles; ++k) {
-      const int t = (int)blockIdx.x + k * (int)gridDim.x;
-      const int buf = k & 1;
-      dma_wait<0>();
-      transform(buf);
-      lds_sync();
-      if (k + 1 < my_tiles) issue(t + (int)gridDim.x, buf ^ 1);
-      compute(sDY(buf), sX(buf));
-    }
+    pipeline([&](int, int, int) { return 0; },
+             [&](int, int buf) { compute(sDY(buf), sX(buf)); return 0; });
     dma_wait<0>();
     lds_sync();
     lds_sync();                                      // (the data-gradient waves' partial row)
@@ -322,7 +378,10 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd32_kernel(Bwd32Args p) {
 
 }  // namespace
 
-int conv3_bwd32_grid(int nTiles, int num_cus) { return std::max(1, std::min(nTiles, num_cus)); }
+int conv3_bwd32_grid(int nTiles, int num_cus, int groups) {
+  if (groups > 1) return groups * std::max(1, std::min(nTiles / groups, num_cus / groups));
+  return std::max(1, std::min(nTiles, num_cus));
+}
 
 void conv3_bwd32_launch(const Bwd32Args& a, int grid, hipStream_t st) {
   hipLaunchKernelGGL(conv3_bwd32_kernel, dim3(grid), dim3(512), B32_SMEM, st, a);

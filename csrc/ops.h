@@ -64,6 +64,10 @@ int conv3_fwd_grid(const ConvFwdArgs& a);       // the streaming kernel's grid (
 int conv3_fwd_cfg_wm(int cfg);
 // resident-weight kernel for high-resolution few-channel layers (conv3x3_res.hip)
 int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem);
+// 3-D 32 -> 32-channel layers: depth-streaming resident kernel (conv3x3x3_ds.hip); -1 = not
+// eligible (grid = one workgroup per CU, statistics rows [grid][2][32])
+int conv3d_ds_plan(const ConvFwdArgs& a, int num_cus, int& grid, int& smem);
+void conv3d_ds_launch(ConvFwdArgs& a, int grid, int smem, hipStream_t st);
 void conv3_res_launch(ConvFwdArgs& a, int variant, int grid, int smem, hipStream_t st);
 int conv3_fwd_cfg_bn(int cfg);
 int conv3_fwd_cfg_bm(int cfg);
@@ -83,8 +87,11 @@ struct Bwd32Args {
   float* bnpart;
   float* wpart;
   int tilesH, tilesW, nTiles;     // 16 x 16 pixel tiles
+  // BN groups (a batched window): `groups` equal runs of images with their own BN1 statistics
+  // s4 [groups][4][32]; group-major workgroups, BN-partial rows [groups][R][2][32]
+  int groups;
 };
-int conv3_bwd32_grid(int nTiles, int num_cus);
+int conv3_bwd32_grid(int nTiles, int num_cus, int groups);
 void conv3_bwd32_launch(const Bwd32Args& a, int grid, hipStream_t st);
 
 // ---------------------------------------------------------------- conv 3x3 wgrad

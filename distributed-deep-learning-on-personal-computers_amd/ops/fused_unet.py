@@ -294,32 +294,42 @@ class _DoubleConvFn(torch.autograd.Function):
             raise RuntimeError("BN groups: the deferred head input has a second autograd consumer")
         hargs = ((*head, s2, da2._ddlpc_bn_partial, g2) if head is not None else None)
         hps = getattr(da2, "_ddlpc_bn_pscale", None) if head is not None else None
-        # ---- second conv: per-group BN2 + ReLU (+ unpool + skip sum) backward, its gradients
-        if direct and head is not None:
-            dy2 = F.head_ce_bn_bwd(*hargs, bn2.weight.grad, bn2.bias.grad, hps, G)[0]
-            with eng.wgrad_stream(dy2, xw2, s1):
-                F.conv3_wgrad(dy2, xw2, None, psc, psh, blk.conv2.weight.grad, groups=G)
-                eng.ready(bn2.weight, bn2.bias, blk.conv2.weight, blk.conv2.bias)
-            dg2 = dbe2 = dw2 = None
-        elif head is not None:
-            dy2, dg2, dbe2 = F.head_ce_bn_bwd(*hargs, None, None, hps, G)
-            dw2 = F.conv3_wgrad(dy2, xw2, None, psc, psh, groups=G).view_as(blk.conv2.weight)
-        elif direct:
-            dy2 = F.bn_group_backward(da2, dpool, y2, s2, g2, G, bn2.weight.grad, bn2.bias.grad)[0]
-            with eng.wgrad_stream(dy2, xw2, s1):
-                F.conv3_wgrad(dy2, xw2, None, psc, psh, blk.conv2.weight.grad, groups=G)
-                eng.ready(bn2.weight, bn2.bias, blk.conv2.weight, blk.conv2.bias)
-            dg2 = dbe2 = dw2 = None
+        # ---- second conv: per-group BN2 + ReLU (+ unpool + skip sum) backward
+        if head is not None:
+            dy2, dg2, dbe2 = F.head_ce_bn_bwd(*hargs, bn2.weight.grad if direct else None,
+                                              bn2.bias.grad if direct else None, hps, G)
         else:
-            dy2, dg2, dbe2 = F.bn_group_backward(da2, dpool, y2, s2, g2, G, None, None)
-            dw2 = F.conv3_wgrad(dy2, xw2, None, psc, psh, groups=G).view_as(blk.conv2.weight)
-        # fused: BN1 backward's reduction in the data gradient's epilogue (group-major rows)
+            dy2, dg2, dbe2 = F.bn_group_backward(da2, dpool, y2, s2, g2, G,
+                                                 bn2.weight.grad if direct else None,
+                                                 bn2.bias.grad if direct else None)
+        if direct:
+            dg2 = dbe2 = None
+        # its gradients: at 32 -> 32 channels on the fused levels one kernel (conv3x3_bwd32,
+        # group-major) for both; otherwise the weight gradient (per-group prologue when fused)
+        # and the data gradient (per-group BN1-backward partials in its epilogue when fused)
+        g32 = fused and eng.bwd32 and p2.cin == 32 and p2.cout == 32
         part1 = None
-        if fused:
-            da1, _, part1 = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False,
-                                        None, None, y1, s1, G)
+        dw2 = None
+        if g32:
+            if direct:
+                da1, part1, _ = F.conv3_bwd32(dy2, y1, s1, p2.dgrad, blk.conv2.weight.grad, G)
+                with eng.wgrad_stream():
+                    eng.ready(bn2.weight, bn2.bias, blk.conv2.weight, blk.conv2.bias)
+            else:
+                da1, part1, dw2 = F.conv3_bwd32(dy2, y1, s1, p2.dgrad, None, G)
+                dw2 = dw2.view_as(blk.conv2.weight)
         else:
-            da1 = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False)[0]
+            if direct:
+                with eng.wgrad_stream(dy2, xw2, s1):
+                    F.conv3_wgrad(dy2, xw2, None, psc, psh, blk.conv2.weight.grad, groups=G)
+                    eng.ready(bn2.weight, bn2.bias, blk.conv2.weight, blk.conv2.bias)
+            else:
+                dw2 = F.conv3_wgrad(dy2, xw2, None, psc, psh, groups=G).view_as(blk.conv2.weight)
+            if fused:
+                da1, _, part1 = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False,
+                                            None, None, y1, s1, G)
+            else:
+                da1 = F.conv3_fwd(dy2, None, p2.dgrad, None, None, None, p2.cin, 0, False)[0]
         # ---- first conv
         padded_in = x2 is None and x1.shape[-1] != w1.shape[1]     # first layer: 3 -> 8 ch
         if direct:

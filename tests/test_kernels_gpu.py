@@ -1248,3 +1248,59 @@ def test_conv3_bwd32(ops, N, H, W):
     acc = torch.ones_like(w)
     _, _, none = ops.conv3_bwd32(dy, y, s4, pk.dgrad, acc)
     assert none.numel() == 0 and torch.allclose(acc, dW + 1, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("G,n,H,W", [(4, 1, 32, 32), (3, 2, 24, 40), (50, 1, 16, 16)])
+def test_conv3_bwd32_groups(ops, G, n, H, W):
+    """The fused 32-channel backward in a batched window (per-group BN1 statistics, group-
+    major workgroups): each group's partial rows and data gradient equal the single-group
+    kernel run on that group; the weight gradient is the sum over groups."""
+    torch.manual_seed(G * 5 + H)
+    C, N = 32, G * n
+    y = (torch.randn(N, H, W, C, device=DEV) * 1.3 + 0.2).bfloat16()
+    dy = (torch.randn(N, H, W, C, device=DEV) * 0.1).bfloat16()
+    w = torch.randn(C, C, 3, 3, device=DEV) / math.sqrt(9 * C)
+    s4 = torch.stack([_bn4(C, 11 + g) for g in range(G)]).contiguous()
+    pk = pack_conv(ops, w)
+    dA, part, dW = ops.conv3_bwd32(dy, y, s4, pk.dgrad, None, G)
+    assert part.shape[0] % G == 0
+    rows = part.view(G, -1, 2, C).sum(1)
+    dW_sum = torch.zeros_like(dW)
+    for g in range(G):
+        sl = slice(g * n, (g + 1) * n)
+        dA_g, part_g, dW_g = ops.conv3_bwd32(dy[sl].contiguous(), y[sl].contiguous(), s4[g].contiguous(),
+                                             pk.dgrad)
+        assert rel_err(dA[sl], dA_g) < 1e-3, g
+        pg = part_g.sum(0)
+        assert torch.allclose(rows[g], pg, rtol=1e-3, atol=1e-3 * float(pg.abs().max()) + 1e-5), g
+        dW_sum += dW_g
+    assert rel_err(dW, dW_sum) < 1e-4
+
+
+@pytest.mark.parametrize("N,D,H,W,pro,bias", [(4, 6, 128, 128, True, True), (4, 5, 120, 120, False, True),
+                                              (2, 3, 256, 136, True, False), (300, 2, 16, 16, False, False)])
+def test_conv3d_depth_streaming(ops, N, D, H, W, pro, bias):
+    """The 3-D 32 -> 32-channel depth-streaming resident kernel (conv3x3x3_ds.hip; chosen by
+    conv3_fwd when the layer has at least one 16x16 tile column per CU) against F.conv3d:
+    output, bias, BN prologue, statistics rows; partial (h, w) tiles, shallow volumes (the
+    first / last planes skip the missing depth taps) and more columns than CUs."""
+    torch.manual_seed(D * 7 + H)
+    C = 32
+    x = torch.randn(N, C, D, H, W, device=DEV).bfloat16()
+    w = torch.randn(C, C, 3, 3, 3, device=DEV) / math.sqrt(27 * C)
+    b = torch.randn(C, device=DEV) * 0.1 if bias else None
+    scale = torch.rand(C, device=DEV) + 0.5 if pro else None
+    shift = torch.randn(C, device=DEV) * 0.5 if pro else None
+    pk = pack_conv(ops, w)
+    y, _, st = ops.conv3_fwd(nhwc(x), None, pk.fwd, b, scale, shift, C, 0, True)
+    a1 = x.float()
+    if pro:
+        a1 = torch.relu(a1 * scale.view(1, -1, 1, 1, 1) + shift.view(1, -1, 1, 1, 1)).bfloat16().float()
+    ref = F.conv3d(a1, w.bfloat16().float(), b, padding=1)
+    assert rel_err(nchw(y), ref) < 1e-2, rel_err(nchw(y), ref)
+    assert_stats(st, ref, 1.0, 10.0)
+    # data-gradient use (flipped, transposed pack; no prologue)
+    dy = torch.randn(N, D, H, W, C, device=DEV).bfloat16()
+    dx, _, _ = ops.conv3_fwd(dy, None, pk.dgrad, None, None, None, C, 0, False)
+    dref = torch.nn.grad.conv3d_input(a1.shape, w.bfloat16().float(), nchw(dy).float(), padding=1)
+    assert rel_err(nchw(dx), dref) < 1e-2, rel_err(nchw(dx), dref)
