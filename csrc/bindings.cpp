@@ -165,6 +165,14 @@ static bool conv3d_ds_enabled() {
   }();
   return on;
 }
+// (DDLPC_CONV3D_WGRAD_DS=0: the per-depth-tap-plane v3 weight gradient instead)
+static bool conv3d_wgrad_ds_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DDLPC_CONV3D_WGRAD_DS");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  return on;
+}
 
 // ------------------------------------------------------------------------ conv3 forward
 std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::Tensor>& x2,
@@ -492,12 +500,20 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   int splits = std::max(1, (target + base - 1) / base);
   splits = std::min(splits, std::max(1, a.nTiles / 8));
   a.splits = splits;
+  // 3-D, 32 output channels: the depth-streaming kernel (one pass over dY and X for all 27
+  // taps) when eligible
+  int ds_grid = -1;
+  if (g.dims == 3 && !img && a.groups <= 1 && conv3d_wgrad_ds_enabled()) {
+    ds_grid = conv3d_wgrad_ds_plan(a, num_cus());
+    if (ds_grid >= 0) splits = a.splits;
+  }
   auto part = at::empty({(int64_t)splits * a.Cout * a.taps * a.Cin}, dy.options().dtype(at::kFloat));
   a.partial = part.data_ptr<float>();
   TORCH_CHECK(a.pscale2 == nullptr || v2, "X2 prologue needs the v2/v3 weight-gradient kernels "
               "(2-D or 3-D, W >= 16, C1 % 32 == 0)");
   TORCH_CHECK(a.groups <= 1 || (v3 && !img), "conv3_wgrad groups: the v3 kernel only (W >= 8, C1 % 32 == 0)");
-  if (img) conv3_wgrad_img_launch(a, bco, cur_stream());
+  if (ds_grid >= 0) conv3d_wgrad_ds_launch(a, ds_grid, cur_stream());
+  else if (img) conv3_wgrad_img_launch(a, bco, cur_stream());
   else if (v3) conv3_wgrad3_launch(a, bco, cur_stream());
   else if (v2) conv3_wgrad2_launch(a, bco, cur_stream());
   else conv3_wgrad_launch(a, bco, cur_stream());

@@ -126,6 +126,11 @@ struct ConvWgradArgs {
   long long gstride;
 };
 void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st);
+// 3-D weight gradient of the 32-output-channel layers, depth-streaming
+// (conv3x3x3_wgrad_ds.hip): -1 = not eligible, else the grid (sets ciChunks, splits; partial
+// slab [splits][32][27][Cin])
+int conv3d_wgrad_ds_plan(ConvWgradArgs& a, int num_cus);
+void conv3d_wgrad_ds_launch(ConvWgradArgs& a, int grid, hipStream_t st);
 // LDS-DMA variant (1 x TH x 16 pixel tiles of conv3_wgrad2_pt(bco) pixels; 3-D: planes = 3,
 // one depth tap plane per workgroup)
 void conv3_wgrad2_launch(ConvWgradArgs& a, int bco, hipStream_t st);

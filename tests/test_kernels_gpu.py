@@ -1304,3 +1304,39 @@ def test_conv3d_depth_streaming(ops, N, D, H, W, pro, bias):
     dx, _, _ = ops.conv3_fwd(dy, None, pk.dgrad, None, None, None, C, 0, False)
     dref = torch.nn.grad.conv3d_input(a1.shape, w.bfloat16().float(), nchw(dy).float(), padding=1)
     assert rel_err(nchw(dx), dref) < 1e-2, rel_err(nchw(dx), dref)
+
+
+@pytest.mark.parametrize("N,D,H,W,C1,C2,pro,pro2", [
+    (4, 6, 128, 128, 32, 0, True, False), (2, 5, 120, 120, 32, 64, True, True),
+    (300, 2, 16, 16, 32, 0, False, False), (1, 4, 256, 136, 64, 32, False, True)])
+def test_conv3d_wgrad_depth_streaming(ops, N, D, H, W, C1, C2, pro, pro2):
+    """The depth-streaming 3-D weight gradient of the 32-output-channel layers
+    (conv3x3x3_wgrad_ds.hip; chosen by conv3_wgrad when (input chunk, tile column) pairs fill
+    the chip) against the fp32 autograd weight gradient: BN prologues on either input of a
+    concat, partial (h, w) tiles, shallow volumes (missing depth taps), uneven column splits."""
+    torch.manual_seed(D * 11 + H + C2)
+    Cout = 32
+    x1 = torch.randn(N, C1, D, H, W, device=DEV).bfloat16()
+    x2 = torch.randn(N, C2, D, H, W, device=DEV).bfloat16() if C2 else None
+    dy = torch.randn(N, Cout, D, H, W, device=DEV).bfloat16()
+    bc = (None, slice(None), None, None, None)
+
+    def pro_of(x, C, on):
+        if not on:
+            return x.float(), None, None
+        sc = torch.rand(C, device=DEV) + 0.5
+        sh = torch.randn(C, device=DEV) * 0.5
+        return torch.relu(x.float() * sc[bc] + sh[bc]).bfloat16().float(), sc, sh
+
+    a1, s1, h1 = pro_of(x1, C1, pro)
+    xin = a1
+    s2 = h2 = None
+    if x2 is not None:
+        a2, s2, h2 = pro_of(x2, C2, pro2)
+        xin = torch.cat([a1, a2], 1)
+    dw = ops.conv3_wgrad(nhwc(dy), nhwc(x1), nhwc(x2) if x2 is not None else None, s1, h1,
+                         None, s2, h2)
+    w = torch.zeros(Cout, C1 + C2, 3, 3, 3, device=DEV, requires_grad=True)
+    (g,) = torch.autograd.grad(F.conv3d(xin, w, padding=1), w, dy.float())
+    assert dw.shape == g.shape
+    assert rel_err(dw, g) < 5e-3, rel_err(dw, g)
