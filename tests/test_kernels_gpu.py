@@ -1308,12 +1308,14 @@ def test_conv3d_depth_streaming(ops, N, D, H, W, pro, bias):
 
 @pytest.mark.parametrize("N,D,H,W,C1,C2,pro,pro2", [
     (4, 6, 128, 128, 32, 0, True, False), (2, 5, 120, 120, 32, 64, True, True),
-    (300, 2, 16, 16, 32, 0, False, False), (1, 4, 256, 136, 64, 32, False, True)])
+    (300, 4, 16, 16, 32, 0, False, False), (1, 4, 256, 136, 64, 32, False, True),
+    (2, 24, 64, 64, 32, 32, True, False)])
 def test_conv3d_wgrad_depth_streaming(ops, N, D, H, W, C1, C2, pro, pro2):
     """The depth-streaming 3-D weight gradient of the 32-output-channel layers
     (conv3x3x3_wgrad_ds.hip; chosen by conv3_wgrad when (input chunk, tile column) pairs fill
     the chip) against the fp32 autograd weight gradient: BN prologues on either input of a
-    concat, partial (h, w) tiles, shallow volumes (missing depth taps), uneven column splits."""
+    concat, partial (h, w) tiles, shallow volumes (missing depth taps), uneven item ranges
+    crossing chunk boundaries, depth segments (the last shape: 4 segments of 6 planes)."""
     torch.manual_seed(D * 11 + H + C2)
     Cout = 32
     x1 = torch.randn(N, C1, D, H, W, device=DEV).bfloat16()
