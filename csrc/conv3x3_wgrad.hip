@@ -19,6 +19,8 @@
 #include "conv_lds.h"
 #include "ops.h"
 
+#include <cstdlib>
+
 #include <stdexcept>
 #include <type_traits>
 
@@ -596,7 +598,7 @@ DDLPC_DEVICE int wg3_yswz(int row) {             // XOR on the 16-B piece index
 // CIW: 32-channel input chunks per workgroup (2: each staged dY tile feeds two X halos — the
 // concat layers' many input chunks re-read dY half as often; the waves split (co tile, chunk)
 // instead of the k-steps)
-template <int BCO, int PT, int CIW = 1>
+template <int BCO, int PT, int CIW = 1, bool PIPE = true>
 __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
   using namespace convlds;
   using Cfg = Wg2Cfg<BCO, PT>;                     // DMA geometry / LDS budget as v2
@@ -828,6 +830,41 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
 
   auto compute = [&](const char* __restrict__ Y, const char* __restrict__ X0) __attribute__((always_inline)) {
     const char* X = X0 + wc * Cfg::X_BYTES;          // this wave's input chunk
+    if constexpr (PIPE) {
+      // software-pipelined: the (k-step, tap) sequence flattened, the X fragment of step i + LA
+      // (and the dY fragment of the next k-step) read before the MFMA of step i — LA MFMAs
+      // of LDS latency cover instead of none (the plain loop waits lgkmcnt(0) before every
+      // MFMA: the compiler keeps one fragment in flight at 222-240 VGPRs)
+      constexpr int NI = KS16 / KW * 9, LA = 3;      // LA: X-fragment lookahead (steps)
+      uint4 af[2], bq[LA + 1];
+      auto ldA = [&](int kk, uint4& a) __attribute__((always_inline)) {
+        const int ks = kk * KW + wk;
+        const uint2 lo = lds_read_tr16(Y + ks * 16 * Cfg::Y_ROWB + ya[0]);
+        const uint2 hi = lds_read_tr16(Y + ks * 16 * Cfg::Y_ROWB + ya[1]);
+        a = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      };
+      auto ldB = [&](int i, uint4& b) __attribute__((always_inline)) {
+        const int ks = (i / 9) * KW + wk, tap = i % 9;
+        const int toff = (ks * HW2 + (tap / 3) * HW2 + tap % 3) * 64;
+        const uint2 lo = lds_read_tr16(X + toff + xb[0]);
+        const uint2 hi = lds_read_tr16(X + toff + xb[1]);
+        b = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      };
+      ldA(0, af[0]);
+#pragma unroll
+      for (int i = 0; i < LA; ++i) ldB(i, bq[i]);
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int j = i + LA;
+        if (j < NI) {
+          if (j % 9 == 0) ldA(j / 9, af[(j / 9) & 1]);
+          ldB(j, bq[j % (LA + 1)]);
+        }
+        acc[i % 9] = mfma32x32x16(af[(i / 9) & 1], bq[i % (LA + 1)], acc[i % 9]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < KS16 / KW; ++kk) {
       const int ks = kk * KW + wk;
@@ -1187,7 +1224,9 @@ void conv3_wgrad2_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
 // input chunks per workgroup on 96-pixel tiles (ciw 2); 128 on 96-pixel tiles.  (Rejected:
 // 128-pixel 32-channel tiles with a 3-deep ring, 12-18% slower per layer:
 // profiles/wgrad_micro_b128_ring*_s2.txt.)
-void conv3_wgrad3_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
+// (DDLPC_WGRAD3_PIPE=0: the plain compute loop — A/B)
+template <bool PIPE>
+static void conv3_wgrad3_launch_t(ConvWgradArgs& a, int bco, hipStream_t st) {
   const int grid = a.coTiles * a.ciChunks * a.planes * a.splits;
   // (64 output channels x two input chunks, 96-pixel tiles: dY + two halos per stage)
   constexpr int SMEM64C2 = Wg2Cfg<64, 96>::SS_BYTES + 2 * (Wg2Cfg<64, 96>::Y_BYTES + 2 * Wg2Cfg<64, 96>::X_BYTES);
@@ -1195,13 +1234,22 @@ void conv3_wgrad3_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
   if (a.TH * 16 != (bco == 32 ? 256 : (bco == 128 || a.ciw == 2) ? 96 : 128))
     throw std::runtime_error("conv3_wgrad3_launch: pixel tile does not match the v3 variant");
   if (bco == 32)
-    hipLaunchKernelGGL((conv3_wgrad3_kernel<32, 256>), dim3(grid), dim3(256), (Wg2Cfg<32, 256>::SMEM), st, a);
+    hipLaunchKernelGGL((conv3_wgrad3_kernel<32, 256, 1, PIPE>), dim3(grid), dim3(256), (Wg2Cfg<32, 256>::SMEM), st, a);
   else if (bco == 64 && a.ciw == 2)   // two input chunks per workgroup, 96-pixel tiles
-    hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 96, 2>), dim3(grid), dim3(256), SMEM64C2, st, a);
+    hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 96, 2, PIPE>), dim3(grid), dim3(256), SMEM64C2, st, a);
   else if (bco == 128)   // 96-pixel tiles: two 74 KB workgroups per CU
-    hipLaunchKernelGGL((conv3_wgrad3_kernel<128, 96>), dim3(grid), dim3(256), (Wg2Cfg<128, 96>::SMEM), st, a);
+    hipLaunchKernelGGL((conv3_wgrad3_kernel<128, 96, 1, PIPE>), dim3(grid), dim3(256), (Wg2Cfg<128, 96>::SMEM), st, a);
   else
-    hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 128>), dim3(grid), dim3(256), (Wg2Cfg<64, 128>::SMEM), st, a);
+    hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 128, 1, PIPE>), dim3(grid), dim3(256), (Wg2Cfg<64, 128>::SMEM), st, a);
+}
+
+void conv3_wgrad3_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
+  static const bool pipe = [] {
+    const char* e = std::getenv("DDLPC_WGRAD3_PIPE");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  if (pipe) conv3_wgrad3_launch_t<true>(a, bco, st);
+  else conv3_wgrad3_launch_t<false>(a, bco, st);
 }
 
 void conv3_wgrad_img_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
