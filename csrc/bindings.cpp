@@ -157,13 +157,14 @@ at::Tensor reduce_rows(const at::Tensor& partial, int64_t R, int64_t N) {
   return sums;
 }
 
-// 3-D depth-streaming kernel on (DDLPC_CONV3D_DS=0: the streaming kernel, for A/B runs)
-static bool conv3d_ds_enabled() {
-  static const bool on = [] {
+// 3-D depth-streaming kernel on (DDLPC_CONV3D_DS=0: the streaming kernel; =1: 32 -> 32
+// layers only, without the 32-channel output chunks — for A/B runs)
+static int conv3d_ds_level() {
+  static const int lvl = [] {
     const char* e = std::getenv("DDLPC_CONV3D_DS");
-    return !(e != nullptr && e[0] == '0');
+    return e != nullptr && e[0] == '0' ? 0 : e != nullptr && e[0] == '1' ? 1 : 2;
   }();
-  return on;
+  return lvl;
 }
 // (DDLPC_CONV3D_WGRAD_DS=0: the per-depth-tap-plane v3 weight gradient instead)
 static bool conv3d_wgrad_ds_enabled() {
@@ -261,19 +262,22 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
               "(the engine pads the 3-channel image to 8)");
   auto opts = x1.options();
   a.npix = (long long)g.N * g.D * g.H * g.W;
-  if (g.dims == 3 && conv3d_ds_enabled()) {
-    // the 3-D 32 -> 32-channel level: depth-streaming resident kernel (conv3x3x3_ds.hip)
+  if (g.dims == 3 && conv3d_ds_level() > (a.Cout == 32 ? 0 : 1)) {
+    // the 3-D 32-input-channel layers: depth-streaming resident kernel (conv3x3x3_ds.hip;
+    // 32-channel output chunks, outputs split at Co1 for a concat conv's data gradient)
     int grid = 0, smem = 0;
     if (conv3d_ds_plan(a, num_cus(), grid, smem) >= 0) {
       at::Tensor y1 = at::empty(shape_with_c(g, a.Co1), opts);
+      at::Tensor y2;
+      if (a.Co1 < a.Cout) y2 = at::empty(shape_with_c(g, a.Cout - a.Co1), opts);
       at::Tensor stats;
       if (want_stats) stats = at::empty({(int64_t)grid, 2, a.Cout}, opts.dtype(at::kFloat));
       a.Y1 = bptr_mut(y1);
-      a.Y2 = nullptr;
+      a.Y2 = y2.defined() ? bptr_mut(y2) : nullptr;
       a.stats = want_stats ? stats.data_ptr<float>() : nullptr;
       conv3d_ds_launch(a, grid, smem, cur_stream());
       at::Tensor none = at::empty({0}, opts);
-      return {y1, none, stats.defined() ? stats : none};
+      return {y1, y2.defined() ? y2 : none, stats.defined() ? stats : none};
     }
   }
   {

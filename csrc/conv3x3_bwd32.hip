@@ -320,23 +320,43 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd32_kernel(Bwd32Args p) {
       const int px = (g4 >> 1) * 8 + 4 * h + q;      // pixel within the tile row
       ao[h] = (1 + px) * ROWB + ((((g4 & 1) * 2 + (pq >> 1)) ^ swz(1 + px)) << 4) + (pq & 1) * 8;
     }
-    auto compute = [&](const char* __restrict__ DY, const char* __restrict__ X) {
+    // X fragment rows of the lane (+ the tap's halo row: an immediate / SGPR term)
+    int xb[2];
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
+    for (int h = 0; h < 2; ++h) xb[h] = ((g4 >> 1) * 8 + 4 * h + q) * ROWB + (g4 & 1) * 32 + 8 * pq;
+    // the (k-step, tap) sequence flattened and software-pipelined: the X fragment of step
+    // i + LA (and the dY fragment of the next k-step) is read before the MFMA of step i (the
+    // per-k-step form waited lgkmcnt(0) at every k-step boundary)
+    auto compute = [&](const char* __restrict__ DY, const char* __restrict__ X) {
+      constexpr int NI = 4 * 9, LA = 3;
+      uint4 af[2], bq[LA + 1];
+      auto ldA = [&](int kk, uint4& a) __attribute__((always_inline)) {
         const int ks = kk * 4 + kw;                  // tile row = 16-pixel k-step
         uint2 av[2];
         // A = dY^T (rows co, k = the row's 16 pixels) from the halo interior (column swizzle)
 #pragma unroll
         for (int h = 0; h < 2; ++h) av[h] = lds_read_tr16(DY + ao[h] + (ks + 1) * B32_HW2 * ROWB);
-        const uint4 af = make_uint4(av[0].x, av[0].y, av[1].x, av[1].y);
+        a = make_uint4(av[0].x, av[0].y, av[1].x, av[1].y);
+      };
+      auto ldB = [&](int i, uint4& b) __attribute__((always_inline)) {
+        const int ks = (i / 9) * 4 + kw, tap = i % 9;
+        const int base = (ks + tap / 3) * B32_HW2 + tap % 3;   // halo row of pixel 0 at this tap
+        const uint2 lo = lds_read_tr16(X + base * ROWB + xb[0]);
+        const uint2 hi = lds_read_tr16(X + base * ROWB + xb[1]);
+        b = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      };
+      ldA(0, af[0]);
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-          const int base = (ks + tap / 3) * B32_HW2 + tap % 3;   // halo row of pixel 0 at this tap
-          const uint2 lo = lds_read_tr16(X + (base + (g4 >> 1) * 8 + q) * ROWB + (g4 & 1) * 32 + 8 * pq);
-          const uint2 hi = lds_read_tr16(X + (base + (g4 >> 1) * 8 + 4 + q) * ROWB + (g4 & 1) * 32 + 8 * pq);
-          wacc[tap] = mfma32x32x16(af, make_uint4(lo.x, lo.y, hi.x, hi.y), wacc[tap]);
+      for (int i = 0; i < LA; ++i) ldB(i, bq[i]);
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int j = i + LA;
+        if (j < NI) {
+          if (j % 9 == 0) ldA(j / 9, af[(j / 9) & 1]);
+          ldB(j, bq[j % (LA + 1)]);
         }
-        __builtin_amdgcn_sched_barrier(0);           // (operand reads one k-step ahead at most)
+        wacc[i % 9] = mfma32x32x16(af[(i / 9) & 1], bq[i % (LA + 1)], wacc[i % 9]);
+        __builtin_amdgcn_sched_barrier(0);
       }
     };
     pipeline([&](int, int, int) { return 0; },

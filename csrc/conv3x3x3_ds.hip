@@ -18,6 +18,13 @@
 // previous layer's BatchNorm + ReLU (prologue) is applied in place by the lanes that DMA'd each
 // piece, padding left zero; the epilogue stores bf16 and accumulates the BN (sum, sum^2) of the
 // fp32 outputs, one statistics row per workgroup (conv3_fwd_kernel's contract).
+//
+// More than 32 output channels (enc2.a's 32 -> 64 forward at 64^3, dec1.a's 32 -> 96 data
+// gradient at 128^3 — its outputs split at Co1 into the two concat inputs' gradients): work
+// items are (32-channel output chunk, column) pairs dealt to the workgroups as even contiguous
+// ranges of the chunk-major order; at a chunk change the workgroup re-loads that chunk's
+// 27 x 32 x 32 weight slice and bias and flushes the finished chunk's statistics into its row
+// ([grid][2][Cout]; chunks it never met stay zero).
 #include "common.h"
 #include "conv_lds.h"
 #include "ops.h"
@@ -47,21 +54,24 @@ __global__ __launch_bounds__(512, 1) void conv3d_ds_kernel(ConvFwdArgs p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tilesH = (p.H + DS_T - 1) / DS_T, tilesW = (p.W + DS_T - 1) / DS_T;
   const int ncol = p.N * tilesH * tilesW;
+  const int nco = p.Cout / 32;                       // output chunks
+  const int it_begin = (int)((long long)nco * ncol * blockIdx.x / gridDim.x);
+  const int it_end = (int)((long long)nco * ncol * (blockIdx.x + 1) / gridDim.x);
   const long long plane_px = (long long)p.H * p.W;
   const long long vol_px = (long long)p.D * plane_px;
   const bool has_pro = p.pscale != nullptr;
   if (has_pro && tid < 32) { s_pro[tid] = p.pscale[tid]; s_pro[32 + tid] = p.pshift[tid]; }
-  // ---- resident weights: row (tap, co) of 32 ci, piece q at q ^ swz(co)
-  {
-    const auto rW = make_rsrc(p.Wt, (unsigned)(32 * 27 * p.CinW * 2));
+  // ---- resident weights of output chunk cc: row (tap, co) of 32 ci, piece q at q ^ swz(co)
+  auto load_weights = [&](int cc) {
+    const auto rW = make_rsrc(p.Wt, (unsigned)(p.Cout * 27 * p.CinW * 2));
     for (int b = wave * 64; b < DS_WBYTES / 16; b += 512) {
       const int e = b + lane;
       const int row = e >> 2;
       const int t = row >> 5, co = row & 31;
       const int sub = (e & 3) ^ swz(co);
-      dma16(rW, sW + b * 16, (unsigned)((co * 27 + t) * p.CinW + sub * 8) * 2u);
+      dma16(rW, sW + b * 16, (unsigned)(((cc * 32 + co) * 27 + t) * p.CinW + sub * 8) * 2u);
     }
-  }
+  };
 
   // ---- plane DMA: piece e = (i * 8 + wave) * 64 + lane -> halo pixel e >> 2, its channel
   // piece (e & 3) ^ swz(column) (the column swizzle: see the header)
@@ -131,16 +141,22 @@ __global__ __launch_bounds__(512, 1) void conv3d_ds_kernel(ConvFwdArgs p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) { st1[nt][i] = 0.f; st2[nt][i] = 0.f; }
   const bool want_stats = p.stats != nullptr;
-  // bias of the lane's output channels, loaded before any DMA (a global load in the epilogue
-  // would make the compiler drain the in-flight plane DMA first)
+  // bias of the lane's output channels of chunk cc, loaded before any DMA of the chunk (a
+  // global load in the epilogue would make the compiler drain the in-flight plane DMA first)
   float bias_r[2][4];
+  auto load_bias = [&](int cc) {
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
+    for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bias_r[nt][i] = p.bias != nullptr ? p.bias[nt * 16 + 4 * g + i] : 0.f;
+      for (int i = 0; i < 4; ++i) bias_r[nt][i] = p.bias != nullptr ? p.bias[cc * 32 + nt * 16 + 4 * g + i] : 0.f;
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
-    asm volatile("" ::"v"(bias_r[nt][0]), "v"(bias_r[nt][1]), "v"(bias_r[nt][2]), "v"(bias_r[nt][3]));
+    for (int nt = 0; nt < 2; ++nt)
+      asm volatile("" ::"v"(bias_r[nt][0]), "v"(bias_r[nt][1]), "v"(bias_r[nt][2]), "v"(bias_r[nt][3]));
+  };
+  // the current chunk's output tensor (Y1: channels < Co1, else Y2), its channel count and
+  // the chunk's channel offset in it
+  bf16_t* ybase = p.Y1;
+  int ych = p.Co1, yoff = 0;
 
   auto compute = [&](int d, const char* __restrict__ Pm, const char* __restrict__ P0,
                      const char* __restrict__ Pp, const char* __restrict__ Wc) __attribute__((always_inline)) {
@@ -176,7 +192,7 @@ __global__ __launch_bounds__(512, 1) void conv3d_ds_kernel(ConvFwdArgs p) {
     }
     // epilogue: + bias, bf16 16-byte channel-pair stores, BN statistics of the fp32 values
     // (lane: channels nt*16 + 4g .. + 3 of pixel c16 of tile row 2w + mt)
-    const auto ry = make_rsrc(p.Y1 + (long long)col_n * vol_px * 32, (unsigned)(vol_px * 64));
+    const auto ry = make_rsrc(ybase + (long long)col_n * vol_px * ych, (unsigned)(vol_px * ych * 2));
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       const int gh = col_h0 + 2 * wave + mt, gw = col_w0 + c16;
@@ -195,18 +211,64 @@ __global__ __launch_bounds__(512, 1) void conv3d_ds_kernel(ConvFwdArgs p) {
         pk[nt] = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
       }
       const uint4 q = pair16(pk[0], pk[1]);
-      unsigned off = ok ? (unsigned)((d * plane_px + gh * p.W + gw) * 32 + pair16_ch(lane)) * 2u : kOOB;
+      unsigned off = ok ? (unsigned)((d * plane_px + gh * p.W + gw) * ych + yoff + pair16_ch(lane)) * 2u : kOOB;
       asm volatile("" : "+v"(off));
       __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, ry, off, 0, 0);
     }
   };
 
-  // ---- columns c = blockIdx.x + k * gridDim.x, each marched through d = 0 .. D-1.  Counted
-  // waits from a per-wave ledger of issued vector-memory ops (a plane: nins DMAs; a step's
-  // epilogue: 2 stores)
+  // ---- one BN-statistics row per workgroup and output chunk: 16 pixel lanes, then the 8
+  // waves (fixed order) — after every DMA landed and every wave is done with the planes (the
+  // reduction reuses the plane ring)
+  auto flush_stats = [&](int cc) {
+    dma_wait<0>();
+    lds_sync();
+    float* red = reinterpret_cast<float*>(sP);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float a1 = row16_sum(st1[nt][i]), a2 = row16_sum(st2[nt][i]);
+        st1[nt][i] = 0.f;
+        st2[nt][i] = 0.f;
+        if (c16 == 0) {
+          const int co = nt * 16 + 4 * g + i;
+          red[(wave * 2) * 32 + co] = a1;
+          red[(wave * 2 + 1) * 32 + co] = a2;
+        }
+      }
+    lds_sync();
+    if (tid < 64) {
+      const int half = tid >> 5, co = tid & 31;
+      float v = 0.f;
+      for (int w = 0; w < 8; ++w) v += red[(w * 2 + half) * 32 + co];
+      p.stats[((long long)blockIdx.x * 2 + half) * p.Cout + cc * 32 + co] = v;
+    }
+    lds_sync();
+  };
+
+  // ---- items (output chunk, column) it_begin .. it_end, each column marched through
+  // d = 0 .. D-1.  Counted waits from a per-wave ledger of issued vector-memory ops (a plane:
+  // nins DMAs; a step's epilogue: 2 stores)
   __syncthreads();                                   // prologue constants visible
   int issued = 0;
-  for (int c = (int)blockIdx.x; c < ncol; c += (int)gridDim.x) {
+  int cc = -1;
+  uint32_t met = 0;                                  // output chunks of this workgroup
+  for (int it = it_begin; it < it_end; ++it) {
+    const int ck = it / ncol, c = it - ck * ncol;
+    if (ck != cc) {                                  // (the previous item ended with a barrier)
+      if (cc >= 0 && want_stats) flush_stats(cc);
+      cc = ck;
+      met |= 1u << ck;
+      load_bias(ck);
+      load_weights(ck);
+      const bool second = ck * 32 >= p.Co1;
+      ybase = second ? p.Y2 : p.Y1;
+      ych = second ? p.Cout - p.Co1 : p.Co1;
+      yoff = second ? ck * 32 - p.Co1 : ck * 32;
+      dma_wait<0>();
+      lds_sync();                                    // weights visible
+    }
     col_n = c / (tilesH * tilesW);
     const int rr = c - col_n * tilesH * tilesW;
     col_h0 = (rr / tilesW) * DS_T;
@@ -238,43 +300,26 @@ __global__ __launch_bounds__(512, 1) void conv3d_ds_kernel(ConvFwdArgs p) {
     }
     lds_sync();                                      // the column's last planes read by all
   }
-  // ---- one BN-statistics row per workgroup: 16 pixel lanes, then the 8 waves (fixed order)
   if (want_stats) {
-    dma_wait<0>();
-    lds_sync();
-    float* red = reinterpret_cast<float*>(sP);
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float a1 = row16_sum(st1[nt][i]), a2 = row16_sum(st2[nt][i]);
-        if (c16 == 0) {
-          const int co = nt * 16 + 4 * g + i;
-          red[(wave * 2) * 32 + co] = a1;
-          red[(wave * 2 + 1) * 32 + co] = a2;
-        }
-      }
-    lds_sync();
-    if (tid < 64) {
-      const int half = tid >> 5, co = tid & 31;
-      float v = 0.f;
-      for (int w = 0; w < 8; ++w) v += red[(w * 2 + half) * 32 + co];
-      p.stats[(long long)blockIdx.x * 64 + half * 32 + co] = v;
-    }
+    if (cc >= 0) flush_stats(cc);
+    if (tid < 64)                                    // chunks this workgroup never met
+      for (int k = 0; k < nco; ++k)
+        if (!((met >> k) & 1u)) p.stats[((long long)blockIdx.x * 2 + (tid >> 5)) * p.Cout + k * 32 + (tid & 31)] = 0.f;
   }
 }
 
 }  // namespace
 
-// planner: the 3-D 32 -> 32-channel layers with enough (h, w) tile columns to fill the chip
-// (one per CU at least); -1 = the streaming kernel
+// planner: the 3-D layers with 32 input channels and 32-channel output chunks (outputs split
+// at Co1 on a chunk boundary) with enough (chunk, column) items to fill the chip (one per CU
+// at least); -1 = the streaming kernel
 int conv3d_ds_plan(const ConvFwdArgs& a, int num_cus, int& grid, int& smem) {
-  if (a.dims != 3 || a.C1 != 32 || a.C2 != 0 || a.Cin != 32 || a.Cout != 32 || a.Co1 != 32 ||
-      a.CinW != 32 || a.pscale2 != nullptr || a.bnb_y != nullptr || a.groups > 1)
+  if (a.dims != 3 || a.C1 != 32 || a.C2 != 0 || a.Cin != 32 || a.Cout % 32 != 0 || a.Cout > 32 * 32 ||
+      a.Co1 % 32 != 0 || a.CinW != 32 || a.pscale2 != nullptr || a.bnb_y != nullptr || a.groups > 1)
     return -1;
-  if ((long long)a.D * a.H * a.W * 64 >= (1LL << 31)) return -1;
-  const int ncol = a.N * ((a.H + DS_T - 1) / DS_T) * ((a.W + DS_T - 1) / DS_T);
-  if (ncol < num_cus) return -1;
+  if ((long long)a.D * a.H * a.W * a.Cout * 2 >= (1LL << 31)) return -1;
+  const long long items = (long long)(a.Cout / 32) * a.N * ((a.H + DS_T - 1) / DS_T) * ((a.W + DS_T - 1) / DS_T);
+  if (items < num_cus || items >= (1LL << 31)) return -1;
   grid = num_cus;
   smem = DS_SMEM;
   return 0;

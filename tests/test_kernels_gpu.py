@@ -1306,6 +1306,36 @@ def test_conv3d_depth_streaming(ops, N, D, H, W, pro, bias):
     assert rel_err(nchw(dx), dref) < 1e-2, rel_err(nchw(dx), dref)
 
 
+@pytest.mark.parametrize("N,D,H,W,Cout,co1,pro,bias", [
+    (2, 5, 128, 120, 64, 0, True, True), (2, 4, 96, 136, 96, 32, False, False),
+    (1, 3, 256, 256, 96, 64, False, True)])
+def test_conv3d_depth_streaming_chunks(ops, N, D, H, W, Cout, co1, pro, bias):
+    """The depth-streaming 3-D conv with several 32-channel output chunks (conv3x3x3_ds.hip:
+    enc2.a's 32 -> 64 forward, dec1.a's 32 -> 96 data gradient split into the two concat
+    inputs' gradients): outputs, bias, prologue and the per-workgroup statistics rows (chunks a
+    workgroup never met are zero) against F.conv3d; item ranges cross chunk boundaries."""
+    torch.manual_seed(D * 5 + W)
+    C = 32
+    x = torch.randn(N, C, D, H, W, device=DEV).bfloat16()
+    w = torch.randn(Cout, C, 3, 3, 3, device=DEV) / math.sqrt(27 * C)
+    b = torch.randn(Cout, device=DEV) * 0.1 if bias else None
+    scale = torch.rand(C, device=DEV) + 0.5 if pro else None
+    shift = torch.randn(C, device=DEV) * 0.5 if pro else None
+    pk = pack_conv(ops, w, need_dgrad=False)
+    y1, y2, st = ops.conv3_fwd(nhwc(x), None, pk.fwd, b, scale, shift, Cout, co1, True)
+    a1 = x.float()
+    if pro:
+        a1 = torch.relu(a1 * scale.view(1, -1, 1, 1, 1) + shift.view(1, -1, 1, 1, 1)).bfloat16().float()
+    ref = F.conv3d(a1, w.bfloat16().float(), b, padding=1)
+    c1 = co1 if co1 else Cout
+    assert y1.shape[-1] == c1 and (co1 == 0 or y2.shape[-1] == Cout - co1)
+    assert rel_err(nchw(y1), ref[:, :c1]) < 1e-2, rel_err(nchw(y1), ref[:, :c1])
+    if co1:
+        assert rel_err(nchw(y2), ref[:, c1:]) < 1e-2, rel_err(nchw(y2), ref[:, c1:])
+    assert st.shape[-1] == Cout
+    assert_stats(st, ref, 1.0, 10.0)
+
+
 @pytest.mark.parametrize("N,D,H,W,C1,C2,pro,pro2", [
     (4, 6, 128, 128, 32, 0, True, False), (2, 5, 120, 120, 32, 64, True, True),
     (300, 4, 16, 16, 32, 0, False, False), (1, 4, 256, 136, 64, 32, False, True),
