@@ -65,13 +65,16 @@ __global__ __launch_bounds__(512, 1) void conv3d_wgrad_ds_kernel(ConvWgradArgs p
   const long long plane_px = (long long)p.H * p.W;
   const long long vol_px = (long long)p.D * plane_px;
 
-  // ---- the current item's chunk: source tensor, channel offset, prologue constants
-  int cic = -1, Cs = 0, cs0 = 0;
+  // ---- the current item's chunk pair k = co chunk * ciChunks + ci chunk: source tensor,
+  // channel offset, prologue constants of the input chunk; the output chunk's channel co0
+  int cic = -1, Cs = 0, cs0 = 0, co0 = 0;
   const bf16_t* xsrc = nullptr;
   bool has_pro = false;
   float sc[8], sh[8];
-  auto set_chunk = [&](int c) {
-    cic = c;
+  auto set_chunk = [&](int k) {
+    cic = k;
+    const int c = k % p.ciChunks;
+    co0 = (k / p.ciChunks) * 32;
     const int ci0 = c * 32;
     const bool second = ci0 >= p.C1;                 // chunk of X2 (C1 % 32 == 0)
     Cs = second ? p.C2 : p.C1;
@@ -114,7 +117,7 @@ __global__ __launch_bounds__(512, 1) void conv3d_wgrad_ds_kernel(ConvWgradArgs p
     vmasks = (vmasks & ~(0xfu << sh4)) | (valid << sh4);
   };
   auto issue_y = [&](int d) {
-    const auto r = make_rsrc(p.dY + (long long)col_n * vol_px * 32, (unsigned)(vol_px * 64));
+    const auto r = make_rsrc(p.dY + (long long)col_n * vol_px * p.Cout, (unsigned)(vol_px * p.Cout * 2));
     char* dst = yslot(d);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -122,7 +125,7 @@ __global__ __launch_bounds__(512, 1) void conv3d_wgrad_ds_kernel(ConvWgradArgs p
       const int gh = col_h0 + (px >> 4), gw = col_w0 + (px & 15);
       const bool ok = gh < p.H && gw < p.W;
       dma16(r, dst + (i * 8 + wave) * 1024,
-            ok ? ((unsigned)(d * plane_px + gh * p.W + gw) * 32 + (lane & 3) * 8) * 2u : kOOB);
+            ok ? ((unsigned)(d * plane_px + gh * p.W + gw) * p.Cout + co0 + (lane & 3) * 8) * 2u : kOOB);
     }
   };
   // (restrict parameter: see compute)
@@ -169,11 +172,12 @@ __global__ __launch_bounds__(512, 1) void conv3d_wgrad_ds_kernel(ConvWgradArgs p
       for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
   };
   zero_acc();
-  // slab rows of this wave's taps for chunk c (32x32 D layout: column n = lane & 31 = ci, row
-  // m = 8 (i / 4) + 4 (lane >> 5) + i % 4 = co)
-  float* slab = p.partial + (long long)blockIdx.x * 32 * 27 * p.Cin;
-  auto write_rows = [&](int c, bool zeros) {
-    float* __restrict__ base = slab + opaque_zero() + c * 32 + (lane & 31) + 4 * (lane >> 5) * 27 * p.Cin;
+  // slab rows of this wave's taps for chunk pair k (32x32 D layout: column n = lane & 31 = ci,
+  // row m = 8 (i / 4) + 4 (lane >> 5) + i % 4 = co within the output chunk)
+  float* slab = p.partial + (long long)blockIdx.x * p.Cout * 27 * p.Cin;
+  auto write_rows = [&](int k, bool zeros) {
+    const int c = k % p.ciChunks, kco = (k / p.ciChunks) * 32;
+    float* __restrict__ base = slab + opaque_zero() + c * 32 + (lane & 31) + (kco + 4 * (lane >> 5)) * 27 * p.Cin;
 #pragma unroll
     for (int lt = 0; lt < 4; ++lt) {
       if (lt >= ntap) break;
@@ -229,7 +233,7 @@ __global__ __launch_bounds__(512, 1) void conv3d_wgrad_ds_kernel(ConvWgradArgs p
   // (group -1: X(d0-1), X(d0)); step d needs groups <= d - d0 and issues group d - d0 + PF
   // after its barrier.  Counted waits from a per-wave ledger (issued DMA instructions; mk[j]:
   // the ledger mark after group d - d0 + j, or after the last group issued).
-  uint32_t met = 0;                                  // chunks this workgroup accumulated
+  unsigned long long met = 0;                        // chunk pairs this workgroup accumulated
   int issued = 0;
   for (int it = it_begin; it < it_end; ++it) {
     const int c = it / per_chunk;
@@ -242,7 +246,7 @@ __global__ __launch_bounds__(512, 1) void conv3d_wgrad_ds_kernel(ConvWgradArgs p
         dma_wait<0>();                               // (stores count in vmcnt: keep the ledger exact)
       }
       set_chunk(c);
-      met |= 1u << c;
+      met |= 1ull << c;
     }
     col_n = col / (tilesH * tilesW);
     const int rr = col - col_n * tilesH * tilesW;
@@ -284,26 +288,31 @@ __global__ __launch_bounds__(512, 1) void conv3d_wgrad_ds_kernel(ConvWgradArgs p
     lds_sync();                                      // the item's planes read by all
   }
   if (cic >= 0) write_rows(cic, false);
-  for (int c = 0; c < p.ciChunks; ++c)
-    if (!((met >> c) & 1u)) write_rows(c, true);
+  for (int c = 0; c < p.ciChunks * (p.Cout / 32); ++c)
+    if (!((met >> c) & 1ull)) write_rows(c, true);
 }
 
 }  // namespace
 
-// planner: 3-D, 32 output channels, whole 32-channel input chunks (concat included, <= 32
-// chunks), >= 4 planes per depth segment; items = chunks x tile columns x depth segments dealt
-// as even contiguous ranges to one workgroup per CU.  The segment count minimises the busiest
+// planner: 3-D, whole 32-channel input and output chunks (concat included, <= 64 chunk
+// pairs), >= 4 planes per depth segment; items = chunk pairs x tile columns x depth segments
+// dealt as even contiguous ranges to one workgroup per CU.  The segment count minimises the busiest
 // workgroup's planes (each segment re-loads its two boundary planes)
 int conv3d_wgrad_ds_plan(ConvWgradArgs& a, int num_cus) {
-  if (a.dims != 3 || a.Cout != 32 || a.C1 % 32 != 0 || a.C2 % 32 != 0 || a.groups > 1 ||
+  if (a.dims != 3 || a.Cout % 32 != 0 || a.C1 % 32 != 0 || a.C2 % 32 != 0 || a.groups > 1 ||
       a.dyy != nullptr || a.Cin < 32 || a.Cin > 32 * 32 || a.D < 4)
     return -1;
-  const int cmax = a.C1 > a.C2 ? (a.C1 > 32 ? a.C1 : 32) : a.C2;
+  // >= 64 x 64 planes: at 32^3 (enc3.b, 128 -> 128) the streaming kernel measured 17% slower
+  // than v3 (351 vs 409 us, profiles/r5/wgrad3d_ds/m_*_g35.log): 4 tile columns per volume
+  if (a.H * a.W < 64 * 64) return -1;
+  int cmax = a.C1 > a.C2 ? a.C1 : a.C2;
+  if (a.Cout > cmax) cmax = a.Cout;
   if ((long long)a.D * a.H * a.W * cmax * 2 >= (1LL << 31)) return -1;
   const int tilesH = (a.H + WD_T - 1) / WD_T, tilesW = (a.W + WD_T - 1) / WD_T;
   const long long ncol = (long long)a.N * tilesH * tilesW;
   const int chunks = a.Cin / 32;
-  const long long base = ncol * chunks;
+  if (chunks * (a.Cout / 32) > 64) return -1;        // (the chunk-pair bitmask)
+  const long long base = ncol * chunks * (a.Cout / 32);
   int best = 0;
   long long best_cost = -1, best_items = 0;
   for (int nseg = 1; nseg <= 16 && a.D / nseg >= 4; ++nseg) {
@@ -314,6 +323,9 @@ int conv3d_wgrad_ds_plan(ConvWgradArgs& a, int num_cus) {
     if (best_cost < 0 || cost < best_cost) { best_cost = cost; best = nseg; best_items = items; }
   }
   if (best == 0 || best_items < num_cus / 2 || best_items >= (1LL << 31)) return -1;
+  // the slab [grid][Cout][27][Cin] (rows of unmet chunk pairs are zeros): <= 512 MB
+  const long long g = best_items < num_cus ? best_items : num_cus;
+  if (g * a.Cout * 27 * a.Cin * 4 > (512LL << 20)) return -1;
   a.tilesH = tilesH;
   a.tilesW = tilesW;
   a.ciChunks = chunks;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Time the 3-D weight gradient of the 32-output-channel layers of BASELINE config #5
-(3-D U-Net, batch 8, 128^3): enc1.b / dec1.b (32 -> 32, BN prologue) and dec1.a (concat
-32 + 64 -> 32).  The kernel is chosen by the environment (DDLPC_CONV3D_WGRAD_DS=0: the v3
+(3-D U-Net, batch 8, 128^3): enc1.b / dec1.b (32 -> 32, BN prologue), dec1.a (concat
+32 + 64 -> 32), and the 64^3 / 32^3 levels' enc2.b, dec2.a, enc3.b.  The kernel is chosen by the environment (DDLPC_CONV3D_WGRAD_DS=0: the v3
 per-depth-tap-plane kernel; DDLPC_WGDS_PF=2: the streaming kernel with two steps in flight), so
 A/B runs are separate processes:
 
@@ -27,10 +27,12 @@ def main():
     dev = torch.device("cuda:0")
     N, S = args.batch, args.size
     tag = "v3" if os.environ.get("DDLPC_CONV3D_WGRAD_DS") == "0" else f"ds_pf{os.environ.get('DDLPC_WGDS_PF', '1')}"
-    for name, c1, c2, pro in [("enc1.b", 32, 0, True), ("dec1.a", 32, 64, False)]:
-        x1 = torch.randn(N, S, S, S, c1, device=dev).bfloat16()
-        x2 = torch.randn(N, S, S, S, c2, device=dev).bfloat16() if c2 else None
-        dy = torch.randn(N, S, S, S, 32, device=dev).bfloat16()
+    for name, sz, c1, c2, co, pro in [("enc1.b", S, 32, 0, 32, True), ("dec1.a", S, 32, 64, 32, False),
+                                      ("enc2.b", S // 2, 64, 0, 64, True), ("dec2.a", S // 2, 128, 64, 64, False),
+                                      ("enc3.b", S // 4, 128, 0, 128, True)]:
+        x1 = torch.randn(N, sz, sz, sz, c1, device=dev).bfloat16()
+        x2 = torch.randn(N, sz, sz, sz, c2, device=dev).bfloat16() if c2 else None
+        dy = torch.randn(N, sz, sz, sz, co, device=dev).bfloat16()
         sc = torch.rand(c1, device=dev) + 0.5 if pro else None
         sh = torch.randn(c1, device=dev) * 0.1 if pro else None
         fn = lambda: ops.conv3_wgrad(dy, x1, x2, sc, sh)  # noqa: E731
@@ -44,7 +46,7 @@ def main():
         e1.record()
         e1.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / args.iters
-        flop = 2.0 * N * S ** 3 * 27 * 32 * (c1 + c2)
+        flop = 2.0 * N * sz ** 3 * 27 * co * (c1 + c2)
         print(f"{tag:7s} {name:7s} {us:9.1f} us  {flop / us / 1e6:8.1f} TFLOP/s", flush=True)
         del x1, x2, dy
 

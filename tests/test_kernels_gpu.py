@@ -1346,8 +1346,21 @@ def test_conv3d_wgrad_depth_streaming(ops, N, D, H, W, C1, C2, pro, pro2):
     the chip) against the fp32 autograd weight gradient: BN prologues on either input of a
     concat, partial (h, w) tiles, shallow volumes (missing depth taps), uneven item ranges
     crossing chunk boundaries, depth segments (the last shape: 4 segments of 6 planes)."""
-    torch.manual_seed(D * 11 + H + C2)
-    Cout = 32
+    _wgrad_ds_check(ops, N, D, H, W, C1, C2, 32, pro, pro2)
+
+
+@pytest.mark.parametrize("N,D,H,W,C1,C2,Cout,pro,pro2", [
+    (8, 8, 64, 64, 64, 0, 64, True, False), (4, 6, 64, 64, 64, 64, 64, False, True),
+    (2, 8, 80, 72, 32, 32, 96, True, True)])
+def test_conv3d_wgrad_depth_streaming_co_chunks(ops, N, D, H, W, C1, C2, Cout, pro, pro2):
+    """The depth-streaming 3-D weight gradient with several 32-channel output chunks (the 64^3
+    level: items = (output chunk, input chunk) pairs x columns x depth segments) against the
+    fp32 autograd weight gradient."""
+    _wgrad_ds_check(ops, N, D, H, W, C1, C2, Cout, pro, pro2)
+
+
+def _wgrad_ds_check(ops, N, D, H, W, C1, C2, Cout, pro, pro2):
+    torch.manual_seed(D * 11 + H + C2 + Cout)
     x1 = torch.randn(N, C1, D, H, W, device=DEV).bfloat16()
     x2 = torch.randn(N, C2, D, H, W, device=DEV).bfloat16() if C2 else None
     dy = torch.randn(N, Cout, D, H, W, device=DEV).bfloat16()
