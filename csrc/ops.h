@@ -64,8 +64,9 @@ int conv3_fwd_grid(const ConvFwdArgs& a);       // the streaming kernel's grid (
 int conv3_fwd_cfg_wm(int cfg);
 // resident-weight kernel for high-resolution few-channel layers (conv3x3_res.hip)
 int conv3_res_plan(ConvFwdArgs& a, int num_cus, int& grid, int& smem);
-// 3-D 32 -> 32-channel layers: depth-streaming resident kernel (conv3x3x3_ds.hip); -1 = not
-// eligible (grid = one workgroup per CU, statistics rows [grid][2][32])
+// 3-D 32-input-channel layers (32-channel output chunks): depth-streaming resident kernel
+// (conv3x3x3_ds.hip); -1 = not eligible (grid = one workgroup per CU, statistics rows
+// [grid][2][Cout])
 int conv3d_ds_plan(const ConvFwdArgs& a, int num_cus, int& grid, int& smem);
 void conv3d_ds_launch(ConvFwdArgs& a, int grid, int smem, hipStream_t st);
 void conv3_res_launch(ConvFwdArgs& a, int variant, int grid, int smem, hipStream_t st);
@@ -126,9 +127,9 @@ struct ConvWgradArgs {
   long long gstride;
 };
 void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st);
-// 3-D weight gradient of the 32-output-channel layers, depth-streaming
-// (conv3x3x3_wgrad_ds.hip): -1 = not eligible, else the grid (sets ciChunks, splits; partial
-// slab [splits][32][27][Cin])
+// 3-D weight gradient (32-channel input / output chunks, >= 64x64 planes), depth-streaming
+// (conv3x3x3_wgrad_ds.hip): -1 = not eligible, else the grid (sets ciChunks, splits, tiles;
+// partial slab [splits][Cout][27][Cin])
 int conv3d_wgrad_ds_plan(ConvWgradArgs& a, int num_cus);
 void conv3d_wgrad_ds_launch(ConvWgradArgs& a, int grid, hipStream_t st);
 // LDS-DMA variant (1 x TH x 16 pixel tiles of conv3_wgrad2_pt(bco) pixels; 3-D: planes = 3,
