@@ -175,6 +175,15 @@ static bool conv3d_wgrad_ds_enabled() {
   return on;
 }
 
+// (DDLPC_WGRAD_C32=0: the v3 weight gradient for the 2-D 32-channel concat convs — A/B)
+static bool wgrad_c32_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DDLPC_WGRAD_C32");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  return on;
+}
+
 // ------------------------------------------------------------------------ conv3 forward
 std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::Tensor>& x2,
                                   const at::Tensor& w, const c10::optional<at::Tensor>& bias,
@@ -506,10 +515,15 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   a.splits = splits;
   // 3-D, 32 output channels: the depth-streaming kernel (one pass over dY and X for all 27
   // taps) when eligible
-  int ds_grid = -1;
+  int ds_grid = -1, c32_grid = -1;
   if (g.dims == 3 && !img && a.groups <= 1 && conv3d_wgrad_ds_enabled()) {
     ds_grid = conv3d_wgrad_ds_plan(a, num_cus());
     if (ds_grid >= 0) splits = a.splits;
+  }
+  // 2-D 32-output-channel concat convs: every input chunk per workgroup (dY read once)
+  if (g.dims == 2 && !img && a.groups <= 1 && wgrad_c32_enabled()) {
+    c32_grid = conv3_wgrad_c32_plan(a, num_cus());
+    if (c32_grid >= 0) splits = a.splits;
   }
   auto part = at::empty({(int64_t)splits * a.Cout * a.taps * a.Cin}, dy.options().dtype(at::kFloat));
   a.partial = part.data_ptr<float>();
@@ -517,6 +531,7 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
               "(2-D or 3-D, W >= 16, C1 % 32 == 0)");
   TORCH_CHECK(a.groups <= 1 || (v3 && !img), "conv3_wgrad groups: the v3 kernel only (W >= 8, C1 % 32 == 0)");
   if (ds_grid >= 0) conv3d_wgrad_ds_launch(a, ds_grid, cur_stream());
+  else if (c32_grid >= 0) conv3_wgrad_c32_launch(a, c32_grid, cur_stream());
   else if (img) conv3_wgrad_img_launch(a, bco, cur_stream());
   else if (v3) conv3_wgrad3_launch(a, bco, cur_stream());
   else if (v2) conv3_wgrad2_launch(a, bco, cur_stream());

@@ -132,6 +132,10 @@ void conv3_wgrad_launch(ConvWgradArgs& a, int bco, hipStream_t st);
 // partial slab [splits][Cout][27][Cin])
 int conv3d_wgrad_ds_plan(ConvWgradArgs& a, int num_cus);
 void conv3d_wgrad_ds_launch(ConvWgradArgs& a, int grid, hipStream_t st);
+// 2-D weight gradient of the 32-output-channel concat convs, every input chunk per workgroup
+// (conv3x3_wgrad_c32.hip): -1 = not eligible, else the grid (partial slab [grid][32][9][Cin])
+int conv3_wgrad_c32_plan(ConvWgradArgs& a, int num_cus);
+void conv3_wgrad_c32_launch(ConvWgradArgs& a, int grid, hipStream_t st);
 // LDS-DMA variant (1 x TH x 16 pixel tiles of conv3_wgrad2_pt(bco) pixels; 3-D: planes = 3,
 // one depth tap plane per workgroup)
 void conv3_wgrad2_launch(ConvWgradArgs& a, int bco, hipStream_t st);

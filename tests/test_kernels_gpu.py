@@ -1306,6 +1306,35 @@ def test_conv3d_depth_streaming(ops, N, D, H, W, pro, bias):
     assert rel_err(nchw(dx), dref) < 1e-2, rel_err(nchw(dx), dref)
 
 
+@pytest.mark.parametrize("N,H,W,C1,C2,pro,pro2", [
+    (32, 128, 128, 32, 64, True, True), (40, 120, 136, 32, 64, False, True),
+    (32, 128, 128, 32, 32, True, False)])
+def test_conv3_wgrad_c32_all_chunks(ops, N, H, W, C1, C2, pro, pro2):
+    """The 2-D weight gradient of the 32-output-channel concat convs with every input chunk
+    per workgroup (conv3x3_wgrad_c32.hip; dec1.a) against the fp32 autograd weight gradient:
+    BN prologues on either input, partial tiles, 2 and 3 input chunks."""
+    torch.manual_seed(H + C2)
+    x1 = torch.randn(N, C1, H, W, device=DEV).bfloat16()
+    x2 = torch.randn(N, C2, H, W, device=DEV).bfloat16()
+    dy = torch.randn(N, 32, H, W, device=DEV).bfloat16()
+    bc = (None, slice(None), None, None)
+
+    def pro_of(x, C, on):
+        if not on:
+            return x.float(), None, None
+        sc = torch.rand(C, device=DEV) + 0.5
+        sh = torch.randn(C, device=DEV) * 0.5
+        return torch.relu(x.float() * sc[bc] + sh[bc]).bfloat16().float(), sc, sh
+
+    a1, s1, h1 = pro_of(x1, C1, pro)
+    a2, s2, h2 = pro_of(x2, C2, pro2)
+    dw = ops.conv3_wgrad(nhwc(dy), nhwc(x1), nhwc(x2), s1, h1, None, s2, h2)
+    w = torch.zeros(32, C1 + C2, 3, 3, device=DEV, requires_grad=True)
+    (g,) = torch.autograd.grad(F.conv2d(torch.cat([a1, a2], 1), w, padding=1), w, dy.float())
+    assert dw.shape == g.shape
+    assert rel_err(dw, g) < 5e-3, rel_err(dw, g)
+
+
 @pytest.mark.parametrize("N,D,H,W,Cout,co1,pro,bias", [
     (2, 5, 128, 120, 64, 0, True, True), (2, 4, 96, 136, 96, 32, False, False),
     (1, 3, 256, 256, 96, 64, False, True)])
