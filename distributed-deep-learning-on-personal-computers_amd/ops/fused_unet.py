@@ -767,7 +767,8 @@ class UNetEngine:
         self.group_fuse_min_px: Optional[int] = None if fmin == "off" else int(fmin)
         # encoder skips handed out pre-BN (see ``defer_skip_levels``): saves ~1 GB at
         # 256^2 x 128 but measured ~1.2% slower end to end (docs/PERF.md), so opt-in
-        self.defer_skip = False
+        # (DDLPC_DEFER_SKIP=1 for A/B runs)
+        self.defer_skip = os.environ.get("DDLPC_DEFER_SKIP", "0") == "1"
         # BN1 backward's reduction pass fused into the epilogue of the data gradient that
         # produces its input gradient (2-D; False: separate reduction kernel)
         self.bnb_epilogue = True

@@ -56,6 +56,25 @@ def main():
             print(f"{name:4s} {H:4d}^2 x{C:4d} {'pool' if pool else '    '} {us:9.1f} us "
                   f"{ideal / us / 1e3:7.0f} GB/s (two-pass bytes {ideal / 2**20:7.1f} MiB)", flush=True)
     print(f"total {tot:.1f} us (each layer once)")
+    # forward BN2 + ReLU + 2x2 max-pool of the encoder blocks (deferred skip: only the pooled
+    # activation is written): ideal bytes = read y + write pooled
+    for name, H, C in LAYERS[:-1]:
+        N = a.batch
+        y = torch.randn(N, H, H, C, device=dev).bfloat16()
+        st4 = torch.stack([torch.zeros(C, device=dev), torch.ones(C, device=dev),
+                           torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1]).contiguous()
+        for _ in range(2):
+            F.bn_relu_apply(y, st4, True, False)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            F.bn_relu_apply(y, st4, True, False)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / a.iters * 1e3
+        ideal = y.numel() * 2 * 5 // 4
+        print(f"fwd-pool {name:4s} {H:4d}^2 x{C:4d} {us:9.1f} us {ideal / us / 1e3:7.0f} GB/s", flush=True)
 
 
 if __name__ == "__main__":
