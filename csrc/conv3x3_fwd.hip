@@ -99,7 +99,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   const int wm = wave / WN;
   const int wn = wave % WN;
   const int HW2 = p.TW + 2, HH2 = p.TH + 2;
-  const int halo = (DIMS == 3 ? p.TD + 2 : 1) * HH2 * HW2;
+  // halo row STRIDE in LDS rows: LEAN tiles (TW = 16, 18-pixel halo rows) pad it to 20 — 20 is
+  // 4 mod 8, so bit 2 of a halo row index (the chunk swizzle) is bit 2 of its column XOR the
+  // parity of its halo row, and a fragment address is a per-lane register XOR a wave-uniform
+  // term plus an immediate (one VALU op per fragment instead of six); columns 18-19 are never
+  // read (DMA'd as zeros)
+  const int HWR = LEAN ? 20 : HW2;
+  const int halo = (DIMS == 3 ? p.TD + 2 : 1) * HH2 * HWR;
   const long long img_px = (long long)p.D * p.H * p.W;
   const int KS = p.ksplit;                        // channel-chunk split (small layers)
   // M-tile walk: workgroup b = blockIdx.x / (KS * nTilesN) serves M tiles m0 + k * Gs.  One
@@ -207,11 +213,12 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     a_nimg = it.n_img;
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
-      const int px = (i * C::NW + wave) * 16 + (lane >> 2);
-      const int hw = px % HW2, hh = (px / HW2) % HH2;
-      const int hd = DIMS == 3 ? px / (HW2 * HH2) : 1;
+      // (opaque_zero: recomputed per item, not hoisted into 2 x A_ITERS live registers)
+      const int px = (i * C::NW + wave) * 16 + (lane >> 2) + (LEAN ? opaque_zero() : 0);
+      const int hw = px % HWR, hh = (px / HWR) % HH2;
+      const int hd = DIMS == 3 ? px / (HWR * HH2) : 1;
       const int gw = it.w0 + hw - 1, gh = it.h0 + hh - 1, gd = it.d0 + hd - 1;
-      const bool ok = px < halo && gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && gd >= 0 && gd < p.D;
+      const bool ok = px < halo && hw < HW2 && gw >= 0 && gw < p.W && gh >= 0 && gh < p.H && gd >= 0 && gd < p.D;
       a_pix[i] = ok ? (gd * p.H + gh) * p.W + gw : -1;
     }
   };
@@ -314,8 +321,15 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     pd = DIMS == 3 ? pix >> (tw_sh + 2) : 0;
   };
   // (LEAN: 16-wide pixel tiles, TW == 16 — launcher-enforced — so the halo pixel of tile mt
-  // is hp_lean + mt * HW2: one register instead of MT)
-  const int hp_lean = (wm * MT) * HW2 + (lane & 15);
+  // is hp_lean + mt * HWR: one register instead of MT.  Its fragment byte offsets for tap
+  // column dw: xo_lean[dw] ^ (32 * parity of the halo row) + halo row * HWR * 64)
+  const int hp_lean = (wm * MT) * HWR + (lane & 15);
+  int xo_lean[3];
+#pragma unroll
+  for (int dw = 0; dw < 3; ++dw) {
+    const int col = (lane & 15) + dw;               // (halo row wm * MT: even, so no parity term)
+    xo_lean[dw] = ((wm * MT) * HWR + col) * ROWB + ((g ^ swz(col)) << 4);
+  }
   int hp0[LEAN ? 1 : MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -523,7 +537,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     auto xload = [&](int s) __attribute__((always_inline)) {
       const int tt = s / MT, mt = s % MT;
       const char* A = tt < 3 ? A0 : A1;
-      const int row = (LEAN ? hp_lean + mt * HW2 : hp0[LEAN ? 0 : mt]) + (tt < 3 ? off0 : off1) + tt % 3;
+      if constexpr (LEAN) {
+        // off = the kernel row r (LEAN call sites): halo row wm*MT + mt + r, wm*MT even
+        const int r = tt < 3 ? off0 : off1;
+        const int par = ((mt & 1) ^ r) & 1;
+        return lds128(A + ((xo_lean[tt % 3] ^ (par << 5)) + (mt + r) * HWR * ROWB));
+      }
+      const int row = hp0[LEAN ? 0 : mt] + (tt < 3 ? off0 : off1) + tt % 3;
       return lds128(A + lds_off(row, g));
     };
     auto wload = [&](int tt, uint4 (&wf)[NT]) __attribute__((always_inline)) {
@@ -554,17 +574,19 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   };
   auto compute = [&](const char* __restrict__ A, const char* __restrict__ B, int kd, int r) __attribute__((always_inline)) {
     if constexpr (FDB == 2) {
-      pipe_taps(std::integral_constant<int, 3>{}, A, B, (kd * HH2 + r) * HW2, A, B, 0, [](int) {});
+      // (LEAN: the kernel row itself; see xload)
+      const int off = LEAN ? r : (kd * HH2 + r) * HW2;
+      pipe_taps(std::integral_constant<int, 3>{}, A, B, off, A, B, 0, [](int) {});
       return;
     }
     // register double buffer: the fragments of tap t+1 are read while the MFMAs of tap t
     // run (the sched barrier keeps the compiler from sinking the reads next to their use,
     // which exposed the LDS latency between every 4 MFMAs: ~31% MFMA busy)
     auto load_frags = [&](int t, uint4 (&xf)[MT], uint4 (&wf)[NT]) __attribute__((always_inline)) {
-      const int tapoff = (kd * HH2 + r) * HW2 + t;
+      const int tapoff = (kd * HH2 + r) * HWR + t;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
-        xf[mt] = lds128(A + lds_off((LEAN ? hp_lean + mt * HW2 : hp0[LEAN ? 0 : mt]) + tapoff, g));
+        xf[mt] = lds128(A + lds_off((LEAN ? hp_lean + mt * HWR : hp0[LEAN ? 0 : mt]) + tapoff, g));
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
         wf[nt] = lds128(B + lds_off(t * BN + wn * (NT * 16) + nt * 16 + (lane & 15), g));
@@ -590,17 +612,17 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
                       const char* __restrict__ A1, const char* __restrict__ B1, int r1, auto&& hook)
       __attribute__((always_inline)) {
     if constexpr (FDB == 2) {
-      pipe_taps(std::integral_constant<int, 6>{}, A0, B0, r0 * HW2, A1, B1, r1 * HW2, hook);
+      pipe_taps(std::integral_constant<int, 6>{}, A0, B0, LEAN ? r0 : r0 * HW2, A1, B1, LEAN ? r1 : r1 * HW2, hook);
       return;
     }
     auto load_frags = [&](int tt, uint4 (&xf)[MT], uint4 (&wf)[NT]) __attribute__((always_inline)) {
       const int t = tt % 3;
       const char* A = tt < 3 ? A0 : A1;
       const char* B = tt < 3 ? B0 : B1;
-      const int tapoff = (tt < 3 ? r0 : r1) * HW2 + t;
+      const int tapoff = (tt < 3 ? r0 : r1) * HWR + t;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
-        xf[mt] = lds128(A + lds_off((LEAN ? hp_lean + mt * HW2 : hp0[LEAN ? 0 : mt]) + tapoff, g));
+        xf[mt] = lds128(A + lds_off((LEAN ? hp_lean + mt * HWR : hp0[LEAN ? 0 : mt]) + tapoff, g));
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
         wf[nt] = lds128(B + lds_off(t * BN + wn * (NT * 16) + nt * 16 + (lane & 15), g));
@@ -911,10 +933,10 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
 
 // cfg 5 (BM-512, LEAN tiles: never with the BN-backward epilogue) on the rolling pipeline
 void launch_cfg5(ConvFwdArgs& a, hipStream_t st) {
-  using C = Cfg<2, 4, 2, 8, 4, 640, 2>;
+  using C = Cfg<2, 4, 2, 8, 4, 704, 2>;      // (34 halo rows of stride 20: 680 pixels)
   const int grid = conv3_fwd_grid(a);
   a.stat_rows = grid;
-  hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 640, 2, 2, false>), dim3(grid),
+  hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 704, 2, 2, false>), dim3(grid),
                      dim3(C::NTH), C::SMEM, st, a);
 }
 
@@ -947,7 +969,7 @@ int conv3_fwd_cfg_bm(int cfg) {
   return cfg == 5 ? 512 : cfg == 6 ? 384 : cfg <= 1 || cfg == 4 || cfg == 7 || cfg == 9 ? 256 : cfg == 2 || cfg == 8 ? 128 : 64;
 }
 int conv3_fwd_cfg_halo(int dims, int cfg) {
-  if (dims == 2) return cfg == 5 ? 640 : cfg <= 1 || cfg == 4 ? 384 : cfg == 2 ? 192 : 128;
+  if (dims == 2) return cfg == 5 ? 612 : cfg <= 1 || cfg == 4 ? 384 : cfg == 2 ? 192 : 128;   // (cfg 5: 34 x 18, stored at stride 20)
   return cfg == 6 ? 896 : cfg <= 1 || cfg == 7 || cfg == 9 ? 704 : cfg == 2 || cfg == 8 ? 448 : 384;
 }
 
