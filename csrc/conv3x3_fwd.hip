@@ -36,6 +36,8 @@
 #include "conv_lds.h"
 #include "ops.h"
 
+#include <cstdlib>
+
 namespace ddlpc {
 
 namespace {
@@ -71,7 +73,9 @@ struct Cfg {
 // operand the pixel tile, so each lane's accumulator holds 4 CONSECUTIVE channels of one
 // pixel -> 8-byte bf16x4 stores; BN statistics are reduced with 4 lane shuffles and
 // written as one partial row per (m tile, wave row).
-template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, int FDB, bool BNB>
+// XL: 2-D 16-wide pixel tiles with the halo rows at stride 20 (see HWR) — launcher-chosen when
+// TW == 16 and (TH + 2) * 20 halo pixels fit the halo buffer
+template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, int FDB, bool BNB, bool XL>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_kernel(ConvFwdArgs p) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
   static_assert(NBB == 2 || NBB == 3 || (NBB == 4 && DIMS == 2), "2 / 3 weight-stage buffers, or 4 (super-stages)");
@@ -84,7 +88,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   float* s_scale = reinterpret_cast<float*>(smem);
   float* s_shift = s_scale + 512;
   char* base = smem + C::SS_BYTES + C::LEAN_BYTES;
-  constexpr bool LEAN = C::LEAN;                    // hp_lean addressing (TW == 16)
+  constexpr bool LEAN = C::LEAN;                    // bias / statistics in LDS
+  static_assert(!XL || DIMS == 2, "XL: 2-D tiles");
+  static_assert(!LEAN || XL, "LEAN tiles use the XL addressing");
   constexpr bool LSTAT = C::LEAN || BNB;           // bias + statistics / BN-backward partials in LDS
   float* s_red = reinterpret_cast<float*>(smem + C::SS_BYTES);    // LSTAT: [WM][2][BN]
   float* s_bias = s_red + WM * 2 * BN;                             // LSTAT: [BN]
@@ -99,12 +105,12 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   const int wm = wave / WN;
   const int wn = wave % WN;
   const int HW2 = p.TW + 2, HH2 = p.TH + 2;
-  // halo row STRIDE in LDS rows: LEAN tiles (TW = 16, 18-pixel halo rows) pad it to 20 — 20 is
+  // halo row STRIDE in LDS rows: XL tiles (TW = 16, 18-pixel halo rows) pad it to 20 — 20 is
   // 4 mod 8, so bit 2 of a halo row index (the chunk swizzle) is bit 2 of its column XOR the
   // parity of its halo row, and a fragment address is a per-lane register XOR a wave-uniform
   // term plus an immediate (one VALU op per fragment instead of six); columns 18-19 are never
   // read (DMA'd as zeros)
-  const int HWR = LEAN ? 20 : HW2;
+  const int HWR = XL ? 20 : HW2;
   const int halo = (DIMS == 3 ? p.TD + 2 : 1) * HH2 * HWR;
   const long long img_px = (long long)p.D * p.H * p.W;
   const int KS = p.ksplit;                        // channel-chunk split (small layers)
@@ -214,7 +220,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 #pragma unroll
     for (int i = 0; i < C::A_ITERS; ++i) {
       // (opaque_zero: recomputed per item, not hoisted into 2 x A_ITERS live registers)
-      const int px = (i * C::NW + wave) * 16 + (lane >> 2) + (LEAN ? opaque_zero() : 0);
+      const int px = (i * C::NW + wave) * 16 + (lane >> 2) + (XL ? opaque_zero() : 0);
       const int hw = px % HWR, hh = (px / HWR) % HH2;
       const int hd = DIMS == 3 ? px / (HWR * HH2) : 1;
       const int gw = it.w0 + hw - 1, gh = it.h0 + hh - 1, gd = it.d0 + hd - 1;
@@ -320,7 +326,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     ph = DIMS == 3 ? (pix >> tw_sh) & 3 : pix >> tw_sh;
     pd = DIMS == 3 ? pix >> (tw_sh + 2) : 0;
   };
-  // (LEAN: 16-wide pixel tiles, TW == 16 — launcher-enforced — so the halo pixel of tile mt
+  // (XL: 16-wide pixel tiles, TW == 16 — launcher-enforced — so the halo pixel of tile mt
   // is hp_lean + mt * HWR: one register instead of MT.  Its fragment byte offsets for tap
   // column dw: xo_lean[dw] ^ (32 * parity of the halo row) + halo row * HWR * 64)
   const int hp_lean = (wm * MT) * HWR + (lane & 15);
@@ -330,14 +336,14 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     const int col = (lane & 15) + dw;               // (halo row wm * MT: even, so no parity term)
     xo_lean[dw] = ((wm * MT) * HWR + col) * ROWB + ((g ^ swz(col)) << 4);
   }
-  int hp0[LEAN ? 1 : MT];
+  int hp0[XL ? 1 : MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int pix = wm * (MT * 16) + mt * 16 + (lane & 15);
     const int pw = pix % p.TW;
     const int ph = (pix / p.TW) % p.TH;
     const int pd = DIMS == 3 ? pix / (p.TW * p.TH) : 0;
-    if (!LEAN) hp0[LEAN ? 0 : mt] = (pd * HH2 + ph) * HW2 + pw;
+    if (!XL) hp0[XL ? 0 : mt] = (pd * HH2 + ph) * HW2 + pw;
   }
 
   f32x4_t acc[MT][NT];
@@ -537,13 +543,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     auto xload = [&](int s) __attribute__((always_inline)) {
       const int tt = s / MT, mt = s % MT;
       const char* A = tt < 3 ? A0 : A1;
-      if constexpr (LEAN) {
-        // off = the kernel row r (LEAN call sites): halo row wm*MT + mt + r, wm*MT even
+      if constexpr (XL) {
+        // off = the kernel row r (XL call sites): halo row wm*MT + mt + r, wm*MT even
         const int r = tt < 3 ? off0 : off1;
         const int par = ((mt & 1) ^ r) & 1;
         return lds128(A + ((xo_lean[tt % 3] ^ (par << 5)) + (mt + r) * HWR * ROWB));
       }
-      const int row = hp0[LEAN ? 0 : mt] + (tt < 3 ? off0 : off1) + tt % 3;
+      const int row = hp0[XL ? 0 : mt] + (tt < 3 ? off0 : off1) + tt % 3;
       return lds128(A + lds_off(row, g));
     };
     auto wload = [&](int tt, uint4 (&wf)[NT]) __attribute__((always_inline)) {
@@ -574,8 +580,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   };
   auto compute = [&](const char* __restrict__ A, const char* __restrict__ B, int kd, int r) __attribute__((always_inline)) {
     if constexpr (FDB == 2) {
-      // (LEAN: the kernel row itself; see xload)
-      const int off = LEAN ? r : (kd * HH2 + r) * HW2;
+      // (XL: the kernel row itself; see xload)
+      const int off = XL ? r : (kd * HH2 + r) * HW2;
       pipe_taps(std::integral_constant<int, 3>{}, A, B, off, A, B, 0, [](int) {});
       return;
     }
@@ -586,7 +592,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       const int tapoff = (kd * HH2 + r) * HWR + t;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
-        xf[mt] = lds128(A + lds_off((LEAN ? hp_lean + mt * HWR : hp0[LEAN ? 0 : mt]) + tapoff, g));
+        xf[mt] = lds128(A + lds_off((XL ? hp_lean + mt * HWR : hp0[XL ? 0 : mt]) + tapoff, g));
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
         wf[nt] = lds128(B + lds_off(t * BN + wn * (NT * 16) + nt * 16 + (lane & 15), g));
@@ -612,7 +618,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
                       const char* __restrict__ A1, const char* __restrict__ B1, int r1, auto&& hook)
       __attribute__((always_inline)) {
     if constexpr (FDB == 2) {
-      pipe_taps(std::integral_constant<int, 6>{}, A0, B0, LEAN ? r0 : r0 * HW2, A1, B1, LEAN ? r1 : r1 * HW2, hook);
+      pipe_taps(std::integral_constant<int, 6>{}, A0, B0, XL ? r0 : r0 * HW2, A1, B1, XL ? r1 : r1 * HW2, hook);
       return;
     }
     auto load_frags = [&](int tt, uint4 (&xf)[MT], uint4 (&wf)[NT]) __attribute__((always_inline)) {
@@ -622,7 +628,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       const int tapoff = (tt < 3 ? r0 : r1) * HWR + t;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
-        xf[mt] = lds128(A + lds_off((LEAN ? hp_lean + mt * HWR : hp0[LEAN ? 0 : mt]) + tapoff, g));
+        xf[mt] = lds128(A + lds_off((XL ? hp_lean + mt * HWR : hp0[XL ? 0 : mt]) + tapoff, g));
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
         wf[nt] = lds128(B + lds_off(t * BN + wn * (NT * 16) + nt * 16 + (lane & 15), g));
@@ -907,28 +913,43 @@ int conv3_fwd_grid(const ConvFwdArgs& a) {
 
 namespace {
 
-template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, int FDB>
+// (DDLPC_CONV_XL=0: the row-swizzled fragment addressing on the non-BM-512 tiles — A/B)
+bool xl_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DDLPC_CONV_XL");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  return on;
+}
+
+template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, int FDB, bool XL>
 void launch_mode(ConvFwdArgs& a, int grid, hipStream_t st) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
   if constexpr (DIMS == 2 && NBB != 3 && !C::LEAN) {
     if (a.bnb_y != nullptr) {
-      hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB, true>), dim3(grid),
+      hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB, true, XL>), dim3(grid),
                          dim3(C::NTH), C::SMEM, st, a);
       return;
     }
   }
-  hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB, false>), dim3(grid),
+  hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB, false, XL>), dim3(grid),
                      dim3(C::NTH), C::SMEM, st, a);
 }
 
 template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB = 2>
 void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
-  using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
   const int grid = conv3_fwd_grid(a);
   a.stat_rows = grid;
   // rolling fragment pipeline (pipe_taps): every configuration (the whole-tap register
-  // double buffer and no buffering measured slower: profiles/r3s/conv_ab_pipe_r3s1.txt)
-  launch_mode<DIMS, WM, WN, MT, NT, HALO, NBB, 2>(a, grid, st);
+  // double buffer and no buffering measured slower: profiles/r3s/conv_ab_pipe_r3s1.txt).
+  // 2-D 16-wide tiles whose stride-20 halo fits the buffer: the XL fragment addressing
+  if constexpr (DIMS == 2) {
+    if (a.TW == 16 && (a.TH + 2) * 20 <= HALO && xl_enabled()) {
+      launch_mode<DIMS, WM, WN, MT, NT, HALO, NBB, 2, true>(a, grid, st);
+      return;
+    }
+  }
+  launch_mode<DIMS, WM, WN, MT, NT, HALO, NBB, 2, false>(a, grid, st);
 }
 
 // cfg 5 (BM-512, LEAN tiles: never with the BN-backward epilogue) on the rolling pipeline
@@ -936,7 +957,7 @@ void launch_cfg5(ConvFwdArgs& a, hipStream_t st) {
   using C = Cfg<2, 4, 2, 8, 4, 704, 2>;      // (34 halo rows of stride 20: 680 pixels)
   const int grid = conv3_fwd_grid(a);
   a.stat_rows = grid;
-  hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 704, 2, 2, false>), dim3(grid),
+  hipLaunchKernelGGL((conv3_fwd_kernel<2, 4, 2, 8, 4, 704, 2, 2, false, true>), dim3(grid),
                      dim3(C::NTH), C::SMEM, st, a);
 }
 
