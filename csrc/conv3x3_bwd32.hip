@@ -324,6 +324,13 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd32_kernel(Bwd32Args p) {
     int xb[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) xb[h] = ((g4 >> 1) * 8 + 4 * h + q) * ROWB + (g4 & 1) * 32 + 8 * pq;
+    // the wave's k phase (tile row kw of every 4) folded into both bases: the k-step / tap
+    // terms below are immediates.  (The dY halo's column swizzle does not depend on the row.)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      ao[h] += kw * B32_HW2 * ROWB;
+      xb[h] += kw * B32_HW2 * ROWB;
+    }
     // the (k-step, tap) sequence flattened and software-pipelined: the X fragment of step
     // i + LA (and the dY fragment of the next k-step) is read before the MFMA of step i (the
     // per-k-step form waited lgkmcnt(0) at every k-step boundary)
@@ -331,7 +338,7 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd32_kernel(Bwd32Args p) {
       constexpr int NI = 4 * 9, LA = 3;
       uint4 af[2], bq[LA + 1];
       auto ldA = [&](int kk, uint4& a) __attribute__((always_inline)) {
-        const int ks = kk * 4 + kw;                  // tile row = 16-pixel k-step
+        const int ks = kk * 4;                       // tile row = 16-pixel k-step (+ kw: in ao)
         uint2 av[2];
         // A = dY^T (rows co, k = the row's 16 pixels) from the halo interior (column swizzle)
 #pragma unroll
@@ -339,7 +346,7 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd32_kernel(Bwd32Args p) {
         a = make_uint4(av[0].x, av[0].y, av[1].x, av[1].y);
       };
       auto ldB = [&](int i, uint4& b) __attribute__((always_inline)) {
-        const int ks = (i / 9) * 4 + kw, tap = i % 9;
+        const int ks = (i / 9) * 4, tap = i % 9;      // (+ kw: in xb)
         const int base = (ks + tap / 3) * B32_HW2 + tap % 3;   // halo row of pixel 0 at this tap
         const uint2 lo = lds_read_tr16(X + base * ROWB + xb[0]);
         const uint2 hi = lds_read_tr16(X + base * ROWB + xb[1]);

@@ -616,7 +616,8 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wj = wave % NJ, wc = (wave / NJ) % CIW, wk = wave / (NJ * CIW);   // co tile, chunk, k phase
+  // (KW == 1: the k phase is the constant 0, so every fragment offset below is an immediate)
+  const int wj = wave % NJ, wc = (wave / NJ) % CIW, wk = KW == 1 ? 0 : wave / (NJ * CIW);   // co tile, chunk, k phase
   int b = xcd_remap(blockIdx.x, gridDim.x);
   const int cic = b % p.ciChunks; b /= p.ciChunks;
   const int cot = b % p.coTiles; b /= p.coTiles;
@@ -821,6 +822,10 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
     const int pc = (byte >> 4) ^ wg3_yswz<BCO>(row);
     ya[h] = row * Cfg::Y_ROWB + (pc << 4) + (byte & 15);
     xb[h] = row * 64 + (g4 & 1) * 32 + 8 * pq;      // halo pixel row (+ 18 * ks + tap offset)
+    // the wave's k phase folded in: k-step ks = kk * KW + wk, the kk terms are immediates
+    // (row bits 0..3 and the swizzle are unchanged by whole 16-pixel k-steps)
+    ya[h] += wk * 16 * Cfg::Y_ROWB;
+    xb[h] += wk * HW2 * 64;
   }
   f32x16_t acc[9];
 #pragma unroll
@@ -838,13 +843,13 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
       constexpr int NI = KS16 / KW * 9, LA = 3;      // LA: X-fragment lookahead (steps)
       uint4 af[2], bq[LA + 1];
       auto ldA = [&](int kk, uint4& a) __attribute__((always_inline)) {
-        const int ks = kk * KW + wk;
+        const int ks = kk * KW;                      // (+ wk: in ya)
         const uint2 lo = lds_read_tr16(Y + ks * 16 * Cfg::Y_ROWB + ya[0]);
         const uint2 hi = lds_read_tr16(Y + ks * 16 * Cfg::Y_ROWB + ya[1]);
         a = make_uint4(lo.x, lo.y, hi.x, hi.y);
       };
       auto ldB = [&](int i, uint4& b) __attribute__((always_inline)) {
-        const int ks = (i / 9) * KW + wk, tap = i % 9;
+        const int ks = (i / 9) * KW, tap = i % 9;    // (+ wk: in xb)
         const int toff = (ks * HW2 + (tap / 3) * HW2 + tap % 3) * 64;
         const uint2 lo = lds_read_tr16(X + toff + xb[0]);
         const uint2 hi = lds_read_tr16(X + toff + xb[1]);
@@ -867,7 +872,7 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad3_kernel(ConvWgradArgs p) {
     }
 #pragma unroll
     for (int kk = 0; kk < KS16 / KW; ++kk) {
-      const int ks = kk * KW + wk;
+      const int ks = kk * KW;                        // (+ wk: in ya / xb)
       const uint2 alo = lds_read_tr16(Y + ks * 16 * Cfg::Y_ROWB + ya[0]);
       const uint2 ahi = lds_read_tr16(Y + ks * 16 * Cfg::Y_ROWB + ya[1]);
       const uint4 af = make_uint4(alo.x, alo.y, ahi.x, ahi.y);
