@@ -89,7 +89,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   float* s_shift = s_scale + 512;
   char* base = smem + C::SS_BYTES + C::LEAN_BYTES;
   constexpr bool LEAN = C::LEAN;                    // bias / statistics in LDS
-  static_assert(!XL || DIMS == 2, "XL: 2-D tiles");
+  // (3-D XL: 16 x 4 (w, h) tile planes — TH = 4, launcher-enforced with TW == 16)
   static_assert(!LEAN || XL, "LEAN tiles use the XL addressing");
   constexpr bool LSTAT = C::LEAN || BNB;           // bias + statistics / BN-backward partials in LDS
   float* s_red = reinterpret_cast<float*>(smem + C::SS_BYTES);    // LSTAT: [WM][2][BN]
@@ -333,8 +333,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   int xo_lean[3];
 #pragma unroll
   for (int dw = 0; dw < 3; ++dw) {
-    const int col = (lane & 15) + dw;               // (halo row wm * MT: even, so no parity term)
-    xo_lean[dw] = ((wm * MT) * HWR + col) * ROWB + ((g ^ swz(col)) << 4);
+    const int col = (lane & 15) + dw;               // (2-D: halo row wm * MT is even, no parity term;
+    xo_lean[dw] = ((DIMS == 2 ? wm * MT : 0) * HWR + col) * ROWB + ((g ^ swz(col)) << 4);   // 3-D: row in xload)
   }
   int hp0[XL ? 1 : MT];
 #pragma unroll
@@ -543,11 +543,19 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     auto xload = [&](int s) __attribute__((always_inline)) {
       const int tt = s / MT, mt = s % MT;
       const char* A = tt < 3 ? A0 : A1;
-      if constexpr (XL) {
+      if constexpr (XL && DIMS == 2) {
         // off = the kernel row r (XL call sites): halo row wm*MT + mt + r, wm*MT even
         const int r = tt < 3 ? off0 : off1;
         const int par = ((mt & 1) ^ r) & 1;
         return lds128(A + ((xo_lean[tt % 3] ^ (par << 5)) + (mt + r) * HWR * ROWB));
+      }
+      if constexpr (XL && DIMS == 3) {
+        // off = kd * HH2 + r (XL call sites); the tile's pixel group q = wm*MT + mt is the
+        // (d, h) row pair (q >> 2, q & 3) of the 16 x 4 plane tiles: halo (d, h) row
+        // hr = (q >> 2) * HH2 + (q & 3) + off (wave-uniform), parity = bit 2 term of its rows
+        const int q = wm * MT + mt;
+        const int hr = (q >> 2) * HH2 + (q & 3) + (tt < 3 ? off0 : off1);
+        return lds128(A + ((xo_lean[tt % 3] ^ ((hr & 1) << 5)) + hr * HWR * ROWB));
       }
       const int row = hp0[XL ? 0 : mt] + (tt < 3 ? off0 : off1) + tt % 3;
       return lds128(A + lds_off(row, g));
@@ -581,7 +589,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   auto compute = [&](const char* __restrict__ A, const char* __restrict__ B, int kd, int r) __attribute__((always_inline)) {
     if constexpr (FDB == 2) {
       // (XL: the kernel row itself; see xload)
-      const int off = XL ? r : (kd * HH2 + r) * HW2;
+      const int off = XL ? kd * HH2 + r : (kd * HH2 + r) * HW2;
       pipe_taps(std::integral_constant<int, 3>{}, A, B, off, A, B, 0, [](int) {});
       return;
     }
@@ -943,8 +951,9 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   // rolling fragment pipeline (pipe_taps): every configuration (the whole-tap register
   // double buffer and no buffering measured slower: profiles/r3s/conv_ab_pipe_r3s1.txt).
   // 2-D 16-wide tiles whose stride-20 halo fits the buffer: the XL fragment addressing
-  if constexpr (DIMS == 2) {
-    if (a.TW == 16 && (a.TH + 2) * 20 <= HALO && xl_enabled()) {
+  {
+    const int halo_xl = (DIMS == 3 ? a.TD + 2 : 1) * (a.TH + 2) * 20;
+    if (a.TW == 16 && (DIMS == 2 || a.TH == 4) && halo_xl <= HALO && xl_enabled()) {
       launch_mode<DIMS, WM, WN, MT, NT, HALO, NBB, 2, true>(a, grid, st);
       return;
     }
@@ -1016,12 +1025,13 @@ void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st) {
     }
   } else {
     switch (cfg) {
-      case 0: launch_cfg<3, 4, 1, 4, 2, 704>(a, st); break;
-      case 1: launch_cfg<3, 4, 1, 4, 4, 704>(a, st); break;
-      case 2: launch_cfg<3, 2, 2, 4, 4, 448>(a, st); break;
+      // (halo capacities 720 / 480: the XL stride-20 halos of 4x4x16 / 2x4x16 tiles)
+      case 0: launch_cfg<3, 4, 1, 4, 2, 720>(a, st); break;
+      case 1: launch_cfg<3, 4, 1, 4, 4, 720>(a, st); break;
+      case 2: launch_cfg<3, 2, 2, 4, 4, 480>(a, st); break;
       case 6: launch_cfg<3, 8, 1, 3, 2, 896>(a, st); break;
-      case 7: launch_cfg<3, 4, 2, 4, 2, 704>(a, st); break;
-      case 8: launch_cfg<3, 2, 4, 4, 2, 448>(a, st); break;
+      case 7: launch_cfg<3, 4, 2, 4, 2, 720>(a, st); break;
+      case 8: launch_cfg<3, 2, 4, 4, 2, 480>(a, st); break;
       case 9: launch_cfg<3, 8, 1, 2, 6, 704>(a, st); break;
       default: launch_cfg<3, 1, 4, 4, 2, 384>(a, st); break;
     }
