@@ -1029,7 +1029,7 @@ void conv3_fwd_launch(ConvFwdArgs& a, int cfg, hipStream_t st) {
       case 0: launch_cfg<3, 4, 1, 4, 2, 720>(a, st); break;
       case 1: launch_cfg<3, 4, 1, 4, 4, 720>(a, st); break;
       case 2: launch_cfg<3, 2, 2, 4, 4, 480>(a, st); break;
-      case 6: launch_cfg<3, 8, 1, 3, 2, 896>(a, st); break;
+      case 6: launch_cfg<3, 8, 1, 3, 2, 960>(a, st); break;   // (960: the XL halo of 6x4x16 tiles)
       case 7: launch_cfg<3, 4, 2, 4, 2, 720>(a, st); break;
       case 8: launch_cfg<3, 2, 4, 4, 2, 480>(a, st); break;
       case 9: launch_cfg<3, 8, 1, 2, 6, 704>(a, st); break;
