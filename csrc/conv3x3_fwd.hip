@@ -113,7 +113,9 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   const int HWR = XL ? 20 : HW2;
   const int halo = (DIMS == 3 ? p.TD + 2 : 1) * HH2 * HWR;
   const long long img_px = (long long)p.D * p.H * p.W;
-  const int KS = p.ksplit;                        // channel-chunk split (small layers)
+  // channel-chunk split (small layers); the BN-backward epilogue variant is launched with
+  // ksplit 1 only (launch_mode), so its epilogue has no split-K / split-output branches
+  const int KS = BNB ? 1 : p.ksplit;
   // M-tile walk: workgroup b = blockIdx.x / (KS * nTilesN) serves M tiles m0 + k * Gs.  One
   // group: m0 = b, Gs = the workgroups per n tile.  BN groups (ConvFwdArgs::groups): group-
   // major — b = grp * Gs + r serves tiles grp * Mg + r + k * Gs of its own group only
@@ -388,7 +390,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   static_assert(NT % 2 == 0, "channel tiles come in pairs");
   // (a split output takes pairs too when it splits at a 32-channel boundary: each pair lies
   // wholly in one output)
-  const bool pairs = KS == 1 && (p.Y2 == nullptr || p.Co1 % 32 == 0);
+  const bool pairs = BNB || (KS == 1 && (p.Y2 == nullptr || p.Co1 % 32 == 0));   // (BNB: single output)
   const int EPI_STORES = pairs ? MT * NT / 2 : MT * NT;
   // BNB: y at an item's output pixels, loaded into VGPRs at the item's last stage (after that
   // stage's DMA) and consumed by its epilogue after the next stage's full wait
@@ -430,7 +432,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       // LEAN: this tile's bias from LDS, statistics of its 4 channels summed over the mt
       // tiles here, then over the 16 pixel lanes into the wave's LDS slot below
       float bl[4] = {0.f, 0.f, 0.f, 0.f}, t1[4] = {0.f, 0.f, 0.f, 0.f}, t2[4] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (LSTAT) {
+      if constexpr (LSTAT && !BNB) {                    // (BNB: no bias)
         const float4 b4 = *reinterpret_cast<const float4*>(s_bias + opaque_zero() + wn * (NT * 16) + nt * 16 + 4 * g);
         bl[0] = b4.x; bl[1] = b4.y; bl[2] = b4.z; bl[3] = b4.w;
       }
@@ -454,7 +456,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         }
         float v[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + (LSTAT ? bl[i] : bias_r[nt][i]);
+        for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + (BNB ? 0.f : LSTAT ? bl[i] : bias_r[nt][i]);
         const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         pkv[mt][nt] = pk;
         if (!pairs) {
@@ -466,7 +468,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         }
         if constexpr (BNB) {
           const float d[4] = {ok ? v[0] : 0.f, ok ? v[1] : 0.f, ok ? v[2] : 0.f, ok ? v[3] : 0.f};
-          bnb_accum(d, ybuf[mt][nt], kb, t1, t2);
+          bnb_accum_y(d, ybuf[mt][nt], kb, t1, t2);
         } else if (ok) {
           // statistics of the fp32 outputs (before the bf16 store; ops.h ConvFwdArgs::stats)
           const float r0 = v[0], q1 = v[1], q2 = v[2], q3 = v[3];
@@ -485,11 +487,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       }
       if constexpr (LSTAT) {
-        if (p.stats != nullptr && KS == 1) {
+        if (BNB || (p.stats != nullptr && KS == 1)) {   // (BNB: the stats rows always exist)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             float a1 = t1[i], a2 = t2[i];
             a1 = row16_sum(a1); a2 = row16_sum(a2);
+            // BNB: t2 summed dyh * y; sum dyh * xhat = invstd * that - mean * invstd * sum dyh
+            if constexpr (BNB) a2 = bnb_xhat_sum(kb, i, a1, a2);
             if ((lane & 15) == 0) {
               const int col = wn * (NT * 16) + nt * 16 + 4 * g + i;
               s_red[(2 * wm) * BN + col] += a1;       // one owner lane per (wave, column)
@@ -934,7 +938,8 @@ template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, int FDB, 
 void launch_mode(ConvFwdArgs& a, int grid, hipStream_t st) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
   if constexpr (DIMS == 2 && NBB != 3 && !C::LEAN) {
-    if (a.bnb_y != nullptr) {
+    // (split-K: fp32 partials, the BN-backward reduction in conv_splitk_finalize_kernel)
+    if (a.bnb_y != nullptr && a.ksplit == 1) {
       hipLaunchKernelGGL((conv3_fwd_kernel<DIMS, WM, WN, MT, NT, HALO, NBB, FDB, true, XL>), dim3(grid),
                          dim3(C::NTH), C::SMEM, st, a);
       return;

@@ -135,6 +135,27 @@ DDLPC_DEVICE void bnb_accum(const float (&d)[4], uint2 yv, const BnbC& k, float 
   s1[0] = p01.x; s1[1] = p01.y; s1[2] = p23.x; s1[3] = p23.y;
   s2[0] = q01.x; s2[1] = q01.y; s2[2] = q23.x; s2[3] = q23.y;
 }
+// bnb_accum with the xhat term factored out of the pixel loop: s2 sums dyh * y (not dyh *
+// xhat); bnb_xhat_sum turns the reduced sums into sum dyh * xhat = invstd * sum dyh * y +
+// (-mean * invstd) * sum dyh — two packed FMAs per 4 channels fewer per pixel
+DDLPC_DEVICE void bnb_accum_y(const float (&d)[4], uint2 yv, const BnbC& k, float (&s1)[4], float (&s2)[4]) {
+  const f32x2_t y01 = {lo_bf(yv.x), hi_bf(yv.x)}, y23 = {lo_bf(yv.y), hi_bf(yv.y)};
+  const f32x2_t a01 = __builtin_elementwise_fma(y01, f32x2_t{k.sc.x, k.sc.y}, f32x2_t{k.sh.x, k.sh.y});
+  const f32x2_t a23 = __builtin_elementwise_fma(y23, f32x2_t{k.sc.z, k.sc.w}, f32x2_t{k.sh.z, k.sh.w});
+  const f32x2_t d01 = {a01.x > 0.f ? d[0] : 0.f, a01.y > 0.f ? d[1] : 0.f};
+  const f32x2_t d23 = {a23.x > 0.f ? d[2] : 0.f, a23.y > 0.f ? d[3] : 0.f};
+  f32x2_t p01 = {s1[0], s1[1]}, p23 = {s1[2], s1[3]}, q01 = {s2[0], s2[1]}, q23 = {s2[2], s2[3]};
+  p01 += d01; p23 += d23;
+  q01 = __builtin_elementwise_fma(d01, y01, q01);
+  q23 = __builtin_elementwise_fma(d23, y23, q23);
+  s1[0] = p01.x; s1[1] = p01.y; s1[2] = p23.x; s1[3] = p23.y;
+  s2[0] = q01.x; s2[1] = q01.y; s2[2] = q23.x; s2[3] = q23.y;
+}
+DDLPC_DEVICE float bnb_xhat_sum(const BnbC& k, int i, float sd, float sdy) {
+  const float is = i == 0 ? k.is.x : i == 1 ? k.is.y : i == 2 ? k.is.z : k.is.w;
+  const float nm = i == 0 ? k.nm.x : i == 1 ? k.nm.y : i == 2 ? k.nm.z : k.nm.w;
+  return __builtin_fmaf(is, sdy, nm * sd);
+}
 
 }  // namespace convlds
 }  // namespace ddlpc
