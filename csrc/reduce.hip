@@ -241,28 +241,34 @@ __global__ void rows_sum_scatter_kernel(const T* __restrict__ in, int R, long lo
 }
 
 // one-launch form for R > 64 rows (the two-pass pair costs a second >= 4.5 us launch): a
-// 1024-thread block owns 64 columns, its 16 waves sum the rows r = w (mod 16) of them
-// (coalesced 256-B row segments), and wave 0 adds the 16 partials in a fixed order
-// (deterministic); optional permuted scatter / accumulate into the fp32 destination
+// block of kWideWaves waves owns 64 columns, wave w sums the rows r = w (mod kWideWaves) of
+// them (coalesced 256-B row segments), and wave 0 adds the partials in a fixed order
+// (deterministic); optional permuted scatter / accumulate into the fp32 destination.
+// Four waves, not sixteen: these reductions run on the weight-gradient stream next to the
+// persistent data-gradient kernels, and a 1024-thread block (four waves on every SIMD of one
+// CU) waited for a wholly free CU — 300-570 us per launch in the two-stream trace against
+// 8-15 us alone (profiles/r5/tail_img_wgrad_main_g64_g65/)
+constexpr int kWideWaves = 4;
 template <bool SCATTER>
-__global__ __launch_bounds__(1024) void rows_sum_wide_kernel(const float* __restrict__ in, int R, long long N,
-                                                             long long ld, double* __restrict__ sums,
-                                                             float* dst, int mode, int A, int Tt, int B,
-                                                             int accumulate) {
-  __shared__ double red[16][64];
+__global__ __launch_bounds__(64 * kWideWaves) void rows_sum_wide_kernel(const float* __restrict__ in, int R,
+                                                                        long long N, long long ld,
+                                                                        double* __restrict__ sums, float* dst,
+                                                                        int mode, int A, int Tt, int B,
+                                                                        int accumulate) {
+  __shared__ double red[kWideWaves][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const long long j = blockIdx.x * 64LL + lane;
   double s = 0.0;
   if (j < N) {
 #pragma unroll 4
-    for (int r = w; r < R; r += 16) s += (double)in[(long long)r * ld + j];
+    for (int r = w; r < R; r += kWideWaves) s += (double)in[(long long)r * ld + j];
   }
   red[w][lane] = s;
   __syncthreads();
   if (w != 0 || j >= N) return;
   double t = 0.0;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) t += red[k][lane];
+  for (int k = 0; k < kWideWaves; ++k) t += red[k][lane];
   if (!SCATTER) { sums[j] = t; return; }
   long long d = j;
   if (mode == 0) {
@@ -315,7 +321,7 @@ void reduce_rows_scatter_launch(const float* in, int R, long long N, double* tmp
     return;
   }
   if (R <= kWideMaxRows) {
-    hipLaunchKernelGGL(rows_sum_wide_kernel<true>, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, st, in,
+    hipLaunchKernelGGL(rows_sum_wide_kernel<true>, dim3((unsigned)((N + 63) / 64)), dim3(64 * kWideWaves), 0, st, in,
                        R, N, ld, nullptr, dst, mode, A, T, B, accumulate ? 1 : 0);
     return;
   }
@@ -337,7 +343,7 @@ void reduce_rows_launch(const float* in, int R, long long N, double* tmp, double
     return;
   }
   if (R <= kWideMaxRows) {
-    hipLaunchKernelGGL(rows_sum_wide_kernel<false>, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, st, in,
+    hipLaunchKernelGGL(rows_sum_wide_kernel<false>, dim3((unsigned)((N + 63) / 64)), dim3(64 * kWideWaves), 0, st, in,
                        R, N, N, sums, nullptr, 2, 0, 0, 0, 0);
     return;
   }

@@ -736,8 +736,10 @@ class UNetEngine:
         # two chains are independent until the optimizer step, and the small deep-layer
         # kernels of one fill the CUs the other leaves idle.  DDLPC_WGRAD_STREAM=0 disables.
         use_side = os.environ.get("DDLPC_WGRAD_STREAM", "1") != "0"
-        # (stream priorities measured within +-0.3%: a plain stream)
-        self.side = torch.cuda.Stream(dev) if use_side else None
+        # (stream priorities measured within +-0.3%: a plain stream; DDLPC_SIDE_PRIO=-1 for A/B,
+        # profiles/r5/rows_sum_4wave_g66/)
+        self.side = (torch.cuda.Stream(dev, priority=int(os.environ.get("DDLPC_SIDE_PRIO", "0")))
+                     if use_side else None)
         self._side_stream = self.side
         self._side_used = False
         # memory the side stream's lag may hold back (see ``wgrad_stream``): default 6% of
