@@ -505,10 +505,15 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   // split-K over pixel tiles: enough blocks to fill the chip, but every block keeps >= 8
   // tiles so the fp32 partial slab stays small next to the MFMA work
   const int base = a.coTiles * a.ciChunks * a.planes;
-  // workgroups per CU to aim for: the weight gradient runs
-  // concurrently with the data-gradient chain, and its resident workgroups' LDS decides
-  // what else fits on a CU (two: 1 / 3 / 4 measured -7 / -1.5 / -1.9%, profiles/bench_s2k_*.json)
-  const int wg_per_cu = 2;
+  // workgroups per CU to aim for: the weight gradient runs concurrently with the data-
+  // gradient chain, and its resident workgroups decide what else fits on a CU.  Round 2
+  // (other kernels): two, 1 / 3 / 4 -7 / -1.5 / -1.9%; round 5, same box, three interleaved
+  // runs each: 1 / 2 / 3 / 4 -> 7508 / 7610-7613 / 7628 / 7611 img/s, window and 3-D within
+  // noise (profiles/r5/wgrad_wg_per_cu_g71_g72/): three
+  static const int wg_per_cu = [] {     // (DDLPC_WGRAD_WG_PER_CU: A/B)
+    const char* e = std::getenv("DDLPC_WGRAD_WG_PER_CU");
+    return e != nullptr && std::atoi(e) > 0 ? std::atoi(e) : 3;
+  }();
   const int target = wg_per_cu * num_cus();
   int splits = std::max(1, (target + base - 1) / base);
   splits = std::min(splits, std::max(1, a.nTiles / 8));
