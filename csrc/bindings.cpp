@@ -157,33 +157,6 @@ at::Tensor reduce_rows(const at::Tensor& partial, int64_t R, int64_t N) {
   return sums;
 }
 
-// 3-D depth-streaming kernel on (DDLPC_CONV3D_DS=0: the streaming kernel; =1: 32 -> 32
-// layers only, without the 32-channel output chunks — for A/B runs)
-static int conv3d_ds_level() {
-  static const int lvl = [] {
-    const char* e = std::getenv("DDLPC_CONV3D_DS");
-    return e != nullptr && e[0] == '0' ? 0 : e != nullptr && e[0] == '1' ? 1 : 2;
-  }();
-  return lvl;
-}
-// (DDLPC_CONV3D_WGRAD_DS=0: the per-depth-tap-plane v3 weight gradient instead)
-static bool conv3d_wgrad_ds_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("DDLPC_CONV3D_WGRAD_DS");
-    return !(e != nullptr && e[0] == '0');
-  }();
-  return on;
-}
-
-// (DDLPC_WGRAD_C32=0: the v3 weight gradient for the 2-D 32-channel concat convs — A/B)
-static bool wgrad_c32_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("DDLPC_WGRAD_C32");
-    return !(e != nullptr && e[0] == '0');
-  }();
-  return on;
-}
-
 // ------------------------------------------------------------------------ conv3 forward
 std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::Tensor>& x2,
                                   const at::Tensor& w, const c10::optional<at::Tensor>& bias,
@@ -271,7 +244,7 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
               "(the engine pads the 3-channel image to 8)");
   auto opts = x1.options();
   a.npix = (long long)g.N * g.D * g.H * g.W;
-  if (g.dims == 3 && conv3d_ds_level() > (a.Cout == 32 ? 0 : 1)) {
+  if (g.dims == 3) {
     // the 3-D 32-input-channel layers: depth-streaming resident kernel (conv3x3x3_ds.hip;
     // 32-channel output chunks, outputs split at Co1 for a concat conv's data gradient)
     int grid = 0, smem = 0;
@@ -510,10 +483,7 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   // (other kernels): two, 1 / 3 / 4 -7 / -1.5 / -1.9%; round 5, same box, three interleaved
   // runs each: 1 / 2 / 3 / 4 -> 7508 / 7610-7613 / 7628 / 7611 img/s, window and 3-D within
   // noise (profiles/r5/wgrad_wg_per_cu_g71_g72/): three
-  static const int wg_per_cu = [] {     // (DDLPC_WGRAD_WG_PER_CU: A/B)
-    const char* e = std::getenv("DDLPC_WGRAD_WG_PER_CU");
-    return e != nullptr && std::atoi(e) > 0 ? std::atoi(e) : 3;
-  }();
+  constexpr int wg_per_cu = 3;
   const int target = wg_per_cu * num_cus();
   int splits = std::max(1, (target + base - 1) / base);
   splits = std::min(splits, std::max(1, a.nTiles / 8));
@@ -521,12 +491,12 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   // 3-D, 32 output channels: the depth-streaming kernel (one pass over dY and X for all 27
   // taps) when eligible
   int ds_grid = -1, c32_grid = -1;
-  if (g.dims == 3 && !img && a.groups <= 1 && conv3d_wgrad_ds_enabled()) {
+  if (g.dims == 3 && !img && a.groups <= 1) {
     ds_grid = conv3d_wgrad_ds_plan(a, num_cus());
     if (ds_grid >= 0) splits = a.splits;
   }
   // 2-D 32-output-channel concat convs: every input chunk per workgroup (dY read once)
-  if (g.dims == 2 && !img && a.groups <= 1 && wgrad_c32_enabled()) {
+  if (g.dims == 2 && !img && a.groups <= 1) {
     c32_grid = conv3_wgrad_c32_plan(a, num_cus());
     if (c32_grid >= 0) splits = a.splits;
   }

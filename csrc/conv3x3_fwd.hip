@@ -925,15 +925,6 @@ int conv3_fwd_grid(const ConvFwdArgs& a) {
 
 namespace {
 
-// (DDLPC_CONV_XL=0: the row-swizzled fragment addressing on the non-BM-512 tiles — A/B)
-bool xl_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("DDLPC_CONV_XL");
-    return !(e != nullptr && e[0] == '0');
-  }();
-  return on;
-}
-
 template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, int FDB, bool XL>
 void launch_mode(ConvFwdArgs& a, int grid, hipStream_t st) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;
@@ -958,7 +949,7 @@ void launch_cfg(ConvFwdArgs& a, hipStream_t st) {
   // 2-D 16-wide tiles whose stride-20 halo fits the buffer: the XL fragment addressing
   {
     const int halo_xl = (DIMS == 3 ? a.TD + 2 : 1) * (a.TH + 2) * 20;
-    if (a.TW == 16 && (DIMS == 2 || a.TH == 4) && halo_xl <= HALO && xl_enabled()) {
+    if (a.TW == 16 && (DIMS == 2 || a.TH == 4) && halo_xl <= HALO) {
       launch_mode<DIMS, WM, WN, MT, NT, HALO, NBB, 2, true>(a, grid, st);
       return;
     }

@@ -1229,9 +1229,10 @@ void conv3_wgrad2_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
 // input chunks per workgroup on 96-pixel tiles (ciw 2); 128 on 96-pixel tiles.  (Rejected:
 // 128-pixel 32-channel tiles with a 3-deep ring, 12-18% slower per layer:
 // profiles/wgrad_micro_b128_ring*_s2.txt.)
-// (DDLPC_WGRAD3_PIPE=0: the plain compute loop — A/B)
-template <bool PIPE>
-static void conv3_wgrad3_launch_t(ConvWgradArgs& a, int bco, hipStream_t st) {
+// (the compute loop is always the software-pipelined one: the plain loop measured 2-9%
+// slower per layer, profiles/r5/wgrad_pipe/)
+void conv3_wgrad3_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
+  constexpr bool PIPE = true;
   const int grid = a.coTiles * a.ciChunks * a.planes * a.splits;
   // (64 output channels x two input chunks, 96-pixel tiles: dY + two halos per stage)
   constexpr int SMEM64C2 = Wg2Cfg<64, 96>::SS_BYTES + 2 * (Wg2Cfg<64, 96>::Y_BYTES + 2 * Wg2Cfg<64, 96>::X_BYTES);
@@ -1246,15 +1247,6 @@ static void conv3_wgrad3_launch_t(ConvWgradArgs& a, int bco, hipStream_t st) {
     hipLaunchKernelGGL((conv3_wgrad3_kernel<128, 96, 1, PIPE>), dim3(grid), dim3(256), (Wg2Cfg<128, 96>::SMEM), st, a);
   else
     hipLaunchKernelGGL((conv3_wgrad3_kernel<64, 128, 1, PIPE>), dim3(grid), dim3(256), (Wg2Cfg<64, 128>::SMEM), st, a);
-}
-
-void conv3_wgrad3_launch(ConvWgradArgs& a, int bco, hipStream_t st) {
-  static const bool pipe = [] {
-    const char* e = std::getenv("DDLPC_WGRAD3_PIPE");
-    return !(e != nullptr && e[0] == '0');
-  }();
-  if (pipe) conv3_wgrad3_launch_t<true>(a, bco, st);
-  else conv3_wgrad3_launch_t<false>(a, bco, st);
 }
 
 void conv3_wgrad_img_launch(ConvWgradArgs& a, int bco, hipStream_t st) {

@@ -335,14 +335,9 @@ int conv3d_wgrad_ds_plan(ConvWgradArgs& a, int num_cus) {
   return a.splits;
 }
 
-// (DDLPC_WGDS_PF=2: operands two steps ahead — A/B)
+// (operands one step ahead: two steps measured 1-2% slower, docs/PERF.md round 5)
 void conv3d_wgrad_ds_launch(ConvWgradArgs& a, int grid, hipStream_t st) {
-  static const int pf = [] {
-    const char* e = std::getenv("DDLPC_WGDS_PF");
-    return e != nullptr && e[0] == '2' ? 2 : 1;
-  }();
-  if (pf == 2) hipLaunchKernelGGL(conv3d_wgrad_ds_kernel<2>, dim3(grid), dim3(512), wd_smem<2>(), st, a);
-  else hipLaunchKernelGGL(conv3d_wgrad_ds_kernel<1>, dim3(grid), dim3(512), wd_smem<1>(), st, a);
+  hipLaunchKernelGGL(conv3d_wgrad_ds_kernel<1>, dim3(grid), dim3(512), wd_smem<1>(), st, a);
 }
 
 }  // namespace ddlpc

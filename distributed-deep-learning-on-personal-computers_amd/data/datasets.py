@@ -120,9 +120,15 @@ def cat_adjacent(ts: List[torch.Tensor]) -> torch.Tensor:
              t.storage_offset() == t0.storage_offset() + i * step for i, t in enumerate(ts))
     if not ok or t0.dim() == 0:
         return torch.cat(ts)
+    # (explicit contiguous strides: is_contiguous() ignores the stride of a size-1 dim, so a
+    # batch-1 micro-batch may carry any stride[0])
+    shape = (t0.shape[0] * len(ts),) + tuple(t0.shape[1:])
+    strides, acc = [], 1
+    for d in reversed(shape):
+        strides.append(acc)
+        acc *= d
     out = t0.new_empty(0)
-    out.set_(t0.untyped_storage(), t0.storage_offset(), (t0.shape[0] * len(ts),) + tuple(t0.shape[1:]),
-             t0.stride())
+    out.set_(t0.untyped_storage(), t0.storage_offset(), shape, tuple(reversed(strides)))
     return out
 
 

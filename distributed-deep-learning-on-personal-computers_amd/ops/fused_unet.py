@@ -736,10 +736,9 @@ class UNetEngine:
         # two chains are independent until the optimizer step, and the small deep-layer
         # kernels of one fill the CUs the other leaves idle.  DDLPC_WGRAD_STREAM=0 disables.
         use_side = os.environ.get("DDLPC_WGRAD_STREAM", "1") != "0"
-        # (stream priorities measured within +-0.3%: a plain stream; DDLPC_SIDE_PRIO=-1 for A/B,
+        # (stream priorities measured within +-0.3%: a plain stream,
         # profiles/r5/rows_sum_4wave_g66/)
-        self.side = (torch.cuda.Stream(dev, priority=int(os.environ.get("DDLPC_SIDE_PRIO", "0")))
-                     if use_side else None)
+        self.side = torch.cuda.Stream(dev) if use_side else None
         self._side_stream = self.side
         self._side_used = False
         # memory the side stream's lag may hold back (see ``wgrad_stream``): default 6% of
@@ -765,12 +764,11 @@ class UNetEngine:
         # convs (group-major tiles, ``_DoubleConvFn._group_forward``) on levels with at least
         # this many pixels per group: smaller levels have too few tiles per group to keep
         # every CU busy (and their unfused passes are cheap); None disables
-        fmin = os.environ.get("DDLPC_GROUP_FUSE_MIN_PX", "16384")
-        self.group_fuse_min_px: Optional[int] = None if fmin == "off" else int(fmin)
+        self.group_fuse_min_px: Optional[int] = 16384
         # encoder skips handed out pre-BN (see ``defer_skip_levels``): saves ~1 GB at
         # 256^2 x 128 but measured ~1.2% slower end to end (docs/PERF.md), so opt-in
-        # (DDLPC_DEFER_SKIP=1 for A/B runs)
-        self.defer_skip = os.environ.get("DDLPC_DEFER_SKIP", "0") == "1"
+        # (tests/test_unet_gpu.py::test_deferred_skips_match_materialised_engine runs both)
+        self.defer_skip = False
         # BN1 backward's reduction pass fused into the epilogue of the data gradient that
         # produces its input gradient (2-D; False: separate reduction kernel)
         self.bnb_epilogue = True
@@ -788,7 +786,7 @@ class UNetEngine:
         self.wgrad_dy_prologue = True
         # 32 -> 32-channel second convs: data + weight gradient in one kernel (conv3x3_bwd32;
         # False: the resident data gradient + the v3 weight gradient on the side stream)
-        self.bwd32 = os.environ.get("DDLPC_BWD32", "1") != "0"
+        self.bwd32 = True
         self.enc = [_Block(b.double_conv, first=(i == 0), engine=self)
                     for i, b in enumerate(model.down_blocks())]
         self.mid = _Block(model.double_conv, first=False, engine=self)
@@ -1009,7 +1007,10 @@ class UNetEngine:
         n = len(self.dec)
         mode = self.defer_mode if not grouped else "none"    # "all" | "convt" | "none"
         feeds_convt = [pack is not None and mode != "none" for _, pack, _ in self.dec]
-        defer_last = defer_last and (self.group_head_defer(x) if grouped else mode == "all")
+        # (grouped: the head's per-group statistics come from its fused TRAINING forward, so a
+        # forward under no_grad keeps the last activation materialised)
+        defer_last = defer_last and ((self.group_head_defer(x) and torch.is_grad_enabled())
+                                     if grouped else mode == "all")
         h, _, s = self.mid(h, None, False, defer=n > 0 and feeds_convt[0])
         for i, ((ub, pack, blk), (skip, s_skip)) in enumerate(zip(self.dec, reversed(skips))):
             if pack is not None:

@@ -583,7 +583,15 @@ class Trainer:
         avail = self._allocator_bytes_available()
         fit = n_micro if avail == float("inf") else int(0.5 * avail // max(per_micro, 1.0))
         w = min(n_micro, self.WINDOW_PIXELS // px, fit)
-        cache[key] = w if w >= 2 else 0
+        w = w if w >= 2 else 0
+        if self.world > 1:
+            # every rank must run the same window (same kernels, same bf16 rounding points,
+            # same bucket-readiness order): the smallest fit over the ranks wins
+            t = torch.tensor([w], dtype=torch.int64,
+                             device=self.device if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            w = int(t.item())
+        cache[key] = w
         return cache[key]
 
     def _allocator_bytes_available(self) -> float:
