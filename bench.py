@@ -245,6 +245,9 @@ def main():
             print(f"schedule: {sched}", file=sys.stderr, flush=True)
     elif args.schedule == "serial" and tr.impl == "hip":
         tr.model._engine.set_side_stream(False)
+    # readiness-aware buckets re-planned from one measured step (untimed): every gradient's
+    # ready time and the backward time instead of the FLOP-rate model (all ranks cut alike)
+    calib = tr.calibrate_bucket_plan(window(20_000)) if tr.reducer is not None else None
     if tr.phases is not None:
         tr.phases.read(reset=True)                 # phase means over the timed steps only
     first = args.warmup + 100
@@ -303,6 +306,14 @@ def main():
     if tr.reducer is not None and tr.reducer.proxy:
         proxy = [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in d.items()}
                  for d in tr.reducer.proxy_times()]
+        plan = getattr(tr, "bucket_plan", None)
+        if plan is not None and len(plan.bucket_done_ms) == len(proxy):
+            # the plan's predicted end of every bucket's collective against the proxy's
+            # measured end (both from the backward start of the last timed step)
+            for rec, pred in zip(proxy, plan.bucket_done_ms):
+                rec["predicted_end_ms"] = round(pred, 3)
+                if "end_from_backward_start_ms" in rec:
+                    rec["predicted_minus_measured_ms"] = round(pred - rec["end_from_backward_start_ms"], 3)
     # self-validation of a multi-rank run (after the timed steps, untimed): the backend and
     # world the collectives really ran on, and bit-identical replicas (every rank applied the
     # same reduced gradient); a diverged run still prints its line but exits non-zero
@@ -401,6 +412,7 @@ def main():
                        "bucket_plan": cfg.bucket_plan,
                        "bucket_sizes_mb": ([round((b.end - b.start) * 4 / 2**20, 3)
                                             for b in red.buckets] if red is not None else None),
+                       "bucket_plan_calibration": calib,
                        "bucket_plan_predicted_exposed_ms": (
                            round(tr.bucket_plan.exposed_ms, 3)
                            if getattr(tr, "bucket_plan", None) is not None else None),

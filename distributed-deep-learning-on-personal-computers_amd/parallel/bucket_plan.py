@@ -91,6 +91,7 @@ class BucketPlan:
     finish_ms: float                 # predicted time the last bucket's collective ends
     backward_ms: float               # predicted backward time
     bucket_done_ms: List[float]      # predicted end of each bucket's collective
+    calibrated: bool = False         # readiness / backward time measured (Trainer.calibrate_bucket_plan)
 
     @property
     def exposed_ms(self) -> float:
@@ -162,6 +163,29 @@ def plan_buckets(nbytes: Sequence[float], ready_frac: Sequence[float], backward_
     done = _simulate(cuts, nbytes, ready_ms, coll_ms)
     return BucketPlan(cuts=cuts, finish_ms=done[-1] if done else 0.0, backward_ms=backward_ms,
                       bucket_done_ms=done)
+
+
+def fit_collective_model(nbytes: Sequence[float], ms: Sequence[float],
+                         world: int) -> Optional[Tuple[float, float]]:
+    """Least-squares fit of ``ms = lat + 2 (W-1)/W * bytes / bandwidth`` to measured
+    collectives -> (GB/s, latency us); None without two distinct sizes or for a
+    non-physical fit."""
+    pts = [(float(b), float(t)) for b, t in zip(nbytes, ms) if b > 0 and t > 0]
+    if len({b for b, _ in pts}) < 2:
+        return None
+    f = 2.0 * (world - 1) / max(world, 1)
+    xs = [f * b for b, _ in pts]
+    ys = [t for _, t in pts]
+    n = len(xs)
+    mx, my = sum(xs) / n, sum(ys) / n
+    sxx = sum((x - mx) ** 2 for x in xs)
+    if sxx <= 0:
+        return None
+    slope = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sxx      # ms per byte
+    lat_ms = max(0.0, my - slope * mx)
+    if slope <= 0:
+        return None
+    return 1.0 / (slope * 1e6), lat_ms * 1e3
 
 
 def size_plan_cuts(nbytes: Sequence[float], cap_bytes: float) -> List[int]:

@@ -120,6 +120,52 @@ class GradBucketReducer:
             for p in flat.order:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
         self.stats = {"buckets": len(self.buckets), "launched_in_backward": 0}
+        # readiness calibration (``start_calibration``): per-parameter gradient-complete times
+        # of one synchronised step, relative to its backward start (Trainer.calibrate_bucket_plan)
+        self._index = {id(p): i for i, p in enumerate(flat.order)}
+        self._calib: Optional[Dict] = None
+        self._bwd_start = None
+
+    # ------------------------------------------------------------------ timing marks
+    def _now(self):
+        """A timing mark on the current stream (hipEvent), or the host clock on CPU (gloo: hooks
+        fire synchronously on the host)."""
+        dev = self.flat.grad_buf.device
+        if dev.type == "cuda":
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(torch.cuda.current_stream(dev))
+            return e
+        import time
+        return time.perf_counter()
+
+    @staticmethod
+    def _ms(a, b) -> float:
+        return a.elapsed_time(b) if isinstance(a, torch.cuda.Event) else (b - a) * 1e3
+
+    def mark_backward_start(self):
+        """Called right before the synchronised micro-batch's backward is queued (its forward
+        kernels are ahead of it on the stream): the zero of the readiness times."""
+        if self._sync and (self._calib is not None or self.proxy):
+            self._bwd_start = self._now()
+
+    def start_calibration(self):
+        self._calib = {"ready": {}, "end": None}
+
+    def stop_calibration(self) -> Tuple[List[float], float]:
+        """-> (ready ms of every parameter in flat order, backward ms) of the calibrated step,
+        both measured from the backward start (synchronises).  A parameter never reported ready
+        counts as ready at the backward's end."""
+        cal, self._calib = self._calib, None
+        if cal is None or self._bwd_start is None or cal["end"] is None:
+            raise RuntimeError("calibration: no synchronised step was recorded")
+        t0 = self._bwd_start
+        if isinstance(t0, torch.cuda.Event):
+            cal["end"].synchronize()
+        bwd = self._ms(t0, cal["end"])
+        ready = [bwd] * len(self.flat.order)
+        for i, ev in cal["ready"].items():
+            ready[i] = min(bwd, max(0.0, self._ms(t0, ev)))
+        return ready, bwd
 
     # ------------------------------------------------------------------ setup
     def _make_buckets(self, bucket_mb: float) -> List[_Bucket]:
@@ -185,6 +231,8 @@ class GradBucketReducer:
         if b is None or id(p) in self._seen:       # a parameter counts once per step
             return
         self._seen.add(id(p))
+        if self._calib is not None:
+            self._calib["ready"][self._index[id(p)]] = self._now()
         b.pending -= 1
         if b.pending == 0 and not b.launched:
             self._launch(b)
@@ -250,6 +298,9 @@ class GradBucketReducer:
                    "ready_to_start_ms": ready.elapsed_time(start),
                    "ready_to_end_ms": ready.elapsed_time(end),
                    "kernel_ms": start.elapsed_time(end)}
+            if isinstance(self._bwd_start, torch.cuda.Event):
+                # bucket collective end measured from the backward start (the plan's zero)
+                rec["end_from_backward_start_ms"] = self._bwd_start.elapsed_time(end)
             bwd = getattr(self, "_bwd_end", None)
             if bwd is not None:
                 bwd.synchronize()
@@ -292,6 +343,8 @@ class GradBucketReducer:
         """Complete all reductions (launch stragglers); compute stream waits, host does not."""
         if self.world == 1:
             return
+        if self._calib is not None and self._calib["end"] is None:
+            self._calib["end"] = self._now()          # backward's end (before the stragglers)
         if self.proxy:
             # backward's end on the compute stream (proxy_times: bucket end vs backward end)
             if getattr(self, "_bwd_end", None) is None:

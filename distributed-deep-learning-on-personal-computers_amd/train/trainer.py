@@ -152,11 +152,13 @@ class Trainer:
             # other ranks find none, so rank 0's restored state is authoritative
             self._broadcast_state()
 
-    def _make_reducer(self, bucket_mb: float) -> GradBucketReducer:
+    def _make_reducer(self, bucket_mb: float, cuts: Optional[List[int]] = None) -> GradBucketReducer:
+        """The gradient reducer; ``cuts`` given = those bucket cuts (a calibrated plan),
+        else the configured plan (readiness model / size)."""
         c = self.cfg
-        cuts = None
-        self.bucket_plan = None
-        if c.bucket_plan == "readiness":
+        if cuts is None:
+            self.bucket_plan = None
+        if cuts is None and c.bucket_plan == "readiness":
             from ..parallel.bucket_plan import plan_for_model
             world = self.world if self.world > 1 else max(2, c.comm_proxy)
             self.bucket_plan = plan_for_model(
@@ -169,6 +171,54 @@ class Trainer:
                                  overlap=c.overlap_comm, use_hooks=(self.impl != "hip"),
                                  wire_dtype=c.wire_dtype,
                                  proxy=c.comm_proxy if self.world == 1 else 0, cuts=cuts)
+
+    def calibrate_bucket_plan(self, micro_batches) -> Optional[Dict]:
+        """Re-plan the readiness-aware buckets from ONE measured step (untimed; call after
+        warm-up): every parameter's gradient-complete time and the backward time replace the
+        FLOP-rate model of ``plan_for_model``.  Every rank cuts identically (MAX of the per-rank
+        timings).  Under the single-GPU comm proxy the collective cost model (latency,
+        bandwidth) is fitted to the proxy collectives of the same step.  Returns a summary."""
+        c = self.cfg
+        r = self.reducer
+        if r is None or c.bucket_plan != "readiness" or getattr(self, "bucket_plan", None) is None:
+            return None
+        from ..parallel import bucket_plan as BP
+        r.start_calibration()
+        self.train_step(micro_batches)
+        ready_ms, bwd_ms = r.stop_calibration()
+        if self.world > 1:
+            dev = self.device if dist.get_backend() == "nccl" else torch.device("cpu")
+            t = torch.tensor(ready_ms + [bwd_ms], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            vals = t.tolist()
+            ready_ms, bwd_ms = vals[:-1], vals[-1]
+        world = self.world if self.world > 1 else max(2, c.comm_proxy)
+        gpu = (self.info.backend if self.world > 1 else "nccl") == "nccl"
+        gbps = BP.XGMI_RING_GBPS if gpu else BP.GLOO_GBPS
+        lat_us = BP.XGMI_LAT_US if gpu else BP.GLOO_LAT_US
+        fitted = None
+        if r.proxy:
+            recs = r.proxy_times()
+            fit = BP.fit_collective_model([x["mb"] * 2**20 for x in recs],
+                                          [x["kernel_ms"] for x in recs], world)
+            if fit is not None:
+                gbps, lat_us = fit
+                fitted = {"gbps": round(gbps, 2), "lat_us": round(lat_us, 1)}
+        wire = 2 if c.wire_dtype == "bf16" else 4
+        nbytes = [float(p.numel() * wire) for p in self.flat.order]
+        plan = BP.plan_buckets(nbytes, [v / max(bwd_ms, 1e-9) for v in ready_ms], bwd_ms,
+                               world, gbps, lat_us, c.bucket_mb * (1 << 20) * wire / 4.0)
+        plan.calibrated = True
+        self.bucket_plan = plan
+        r.remove_hooks()
+        self.reducer = self._make_reducer(c.bucket_mb, cuts=plan.cuts)
+        if self.impl == "hip":
+            self.model._engine.enable_direct_grads(self.reducer.mark_ready)
+        return {"backward_ms": round(bwd_ms, 3), "buckets": len(plan.cuts) - 1,
+                "bucket_mb": [round(sum(nbytes[a:b]) / 2**20, 2)
+                              for a, b in zip(plan.cuts[:-1], plan.cuts[1:])],
+                "predicted_end_ms": [round(v, 3) for v in plan.bucket_done_ms],
+                "predicted_exposed_ms": round(plan.exposed_ms, 3), "collective_fit": fitted}
 
     def set_bucket_mb(self, bucket_mb: float) -> int:
         """Re-bucket the gradient reducer between steps (bucket-size sweeps, SURVEY.md §5.8);
@@ -241,6 +291,8 @@ class Trainer:
                else contextlib.nullcontext())
         with ctx:
             loss, correct = self.model.loss_and_correct(x, y)
+        if sync and self.reducer is not None:
+            self.reducer.mark_backward_start()
         loss.backward()
         self.meter.add(loss, correct, y.numel())
         self.micro_count += 1
@@ -639,6 +691,8 @@ class Trainer:
             eng.bn_groups = len(ch) if len(ch) > 1 else 0
             try:
                 loss, correct = self.model.loss_and_correct(x, y)
+                if self.reducer is not None and ci == len(chunks) - 1:
+                    self.reducer.mark_backward_start()
                 (loss * float(len(ch)) if len(ch) > 1 else loss).backward()
             finally:
                 eng.bn_groups = 0

@@ -131,6 +131,11 @@ def test_bench_torchrun_two_ranks_gloo():
     assert rec["dist_backend"] == "gloo" and rec["world_size"] == 2
     assert rec["replicas_identical"] is True and rec["rccl_version"] is None
     assert rec["comm_wait_ms"] is not None and rec["comm_wait_ms"] >= 0
+    # the readiness plan re-cut from one measured step (same cuts on both ranks, or the
+    # bucket all-reduces of the timed steps would not have matched up)
+    cal = c["bucket_plan_calibration"]
+    assert cal is not None and cal["backward_ms"] > 0 and cal["buckets"] >= 1
+    assert len(cal["predicted_end_ms"]) == cal["buckets"] == len(cal["bucket_mb"])
 
 
 def test_bench_self_spawns_torchrun_for_gpus_n():
@@ -297,3 +302,14 @@ def test_bn_group_support_geometry():
     assert not bn_groups_supported(UNet(out_classes=6, width_divisor=2), 48)   # 48 >> 4 = 3
     m = UNet(out_classes=6, width_divisor=2, base_widths=(24, 48, 96, 192, 192))
     assert not bn_groups_supported(m, 256)                                    # C / 8 = 3
+
+
+def test_collective_model_fit_recovers_latency_and_bandwidth():
+    from ddlpc.parallel.bucket_plan import fit_collective_model
+    world, gbps, lat_us = 8, 150.0, 25.0
+    f = 2.0 * (world - 1) / world
+    sizes = [1e6, 4e6, 8e6, 16e6]
+    ms = [lat_us * 1e-3 + f * b / (gbps * 1e6) for b in sizes]
+    g, l = fit_collective_model(sizes, ms, world)
+    assert abs(g - gbps) < 1e-6 * gbps and abs(l - lat_us) < 1e-6
+    assert fit_collective_model([4e6, 4e6], [0.1, 0.1], world) is None
