@@ -79,6 +79,9 @@ def _parse():
                     help="1 GPU: stand-in collective per gradient bucket for a world of N "
                          "(streaming kernel on a third stream; measures launch-to-finish "
                          "latency during backward)")
+    ap.add_argument("--engine-set", default="",
+                    help="diagnostic: NAME=INT[,NAME=INT] — set UNetEngine switches (e.g. "
+                         "c32_bnp=0) before the first step, for same-box A/B runs")
     ap.add_argument("--ab", default="",
                     help="diagnostic: KNOB:v0,v1 — after the main timing, alternate a kernel "
                          "knob over --ab-rounds timed blocks in this process; reported as "
@@ -171,6 +174,13 @@ def main():
                       comm_proxy=args.comm_proxy, micro_streams=args.micro_streams)
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     tr = Trainer(cfg, device=dev)
+    if args.engine_set and tr.impl == "hip":
+        eng = tr.model._engine
+        for kv in args.engine_set.split(","):
+            k, v = kv.split("=")
+            if not hasattr(eng, k) or isinstance(getattr(eng, k), torch.Tensor):
+                raise SystemExit(f"--engine-set: UNetEngine has no switch {k!r}")
+            setattr(eng, k, type(getattr(eng, k))(int(v)))
     world, rank = tr.world, tr.rank
     assert world == args.gpus, (world, args.gpus)
     device = tr.device
@@ -422,6 +432,7 @@ def main():
                                         if "comm_wait_ms" in phases else None),
                        "bucket_sweep": sweep or None,
                        "ab": ab,
+                       "engine_set": args.engine_set or None,
                        "alloc_retries": mstats.get("num_alloc_retries"),
                        "side_lag_waits": (getattr(tr.model._engine, "lag_waits", None)
                                           if tr.impl == "hip" else None),

@@ -385,7 +385,7 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
                        const c10::optional<at::Tensor>& dy_y,
                        const c10::optional<at::Tensor>& dy_s4,
                        const c10::optional<at::Tensor>& dy_coefs, int64_t cin_real,
-                       int64_t groups) {
+                       int64_t groups, const c10::optional<at::Tensor>& dy_out) {
   CHECK_DEV(dy); CHECK_CONTIG(dy); CHECK_BF16(dy); CHECK_CONTIG(x1); CHECK_BF16(x1);
   c10::DeviceGuard guard(dy.device());
   const Geo g = geo_of(x1);
@@ -430,19 +430,27 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   // concat layers included (same-process bench A/B at batch 256: -0.8% step time,
   // profiles/r3s/bench_ab_wgrad3_concat_r3s9.log)
   const bool v3 = v2 && a.C1 % 32 == 0 && a.C2 % 32 == 0;
+  const bool emit = dy_out.has_value() && dy_out->defined();
   if (dy_y.has_value() && dy_y->defined()) {
-    // dy holds dA; BN backward applied on load (v2 kernel only)
+    // dy holds dA; BN backward applied on load: the v2 kernel, or — with dy_out, where the
+    // formed dY is also stored — the 32-output-channel concat kernel (checked below)
     CHECK_CONTIG(*dy_y); CHECK_BF16(*dy_y);
-    TORCH_CHECK(v2 && !v3 && g.dims == 2 && dy_y->numel() == dy.numel(),
+    TORCH_CHECK(((v2 && !v3) || emit) && g.dims == 2 && dy_y->numel() == dy.numel(),
                 "conv3_wgrad: the dY prologue needs the v2 kernel (2-D, C1 % 32 != 0 or a 32-channel "
-                "first layer) and y of dY's shape");
+                "first layer) or dy_out, and y of dY's shape");
     TORCH_CHECK(dy_s4.has_value() && dy_s4->numel() == 4 * a.Cout && dy_coefs.has_value() &&
                 dy_coefs->numel() == 3 * a.Cout, "conv3_wgrad: dy_s4 [4][Cout] and dy_coefs [3][Cout]");
     CHECK_F32(*dy_s4); CHECK_F32(*dy_coefs);
     a.dyy = bptr(*dy_y);
     a.dys4 = dy_s4->data_ptr<float>();
     a.dycoef = dy_coefs->data_ptr<float>();
+    if (emit) {
+      CHECK_CONTIG(*dy_out); CHECK_BF16(*dy_out);
+      TORCH_CHECK(dy_out->numel() == dy.numel(), "conv3_wgrad: dy_out must have dY's shape");
+      a.dyout = reinterpret_cast<bf16_t*>(dy_out->data_ptr());
+    }
   }
+  TORCH_CHECK(!emit || a.dyy != nullptr, "conv3_wgrad: dy_out needs the dY prologue (dy_y, dy_s4, dy_coefs)");
   // the image layer: <= 4 real channels (cin_real, from the caller) of an 8-channel padded
   // input, (tap, channel)-packed kernel
   // (3-D: per depth tap plane, as the v2 / v3 kernels)
@@ -500,6 +508,8 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
     c32_grid = conv3_wgrad_c32_plan(a, num_cus());
     if (c32_grid >= 0) splits = a.splits;
   }
+  TORCH_CHECK(!emit || c32_grid >= 0, "conv3_wgrad: dy_out only with the 32-output-channel concat "
+              "kernel (2-D, Cout 32, 64..96 input channels in 32-channel chunks, W >= 16, no groups)");
   auto part = at::empty({(int64_t)splits * a.Cout * a.taps * a.Cin}, dy.options().dtype(at::kFloat));
   a.partial = part.data_ptr<float>();
   TORCH_CHECK(a.pscale2 == nullptr || v2, "X2 prologue needs the v2/v3 weight-gradient kernels "
@@ -1580,7 +1590,7 @@ TORCH_LIBRARY(ddlpc, m) {
         "Tensor? bnb_s4=None, int groups=0) -> Tensor[]");
   m.def("conv3_wgrad(Tensor dy, Tensor x1, Tensor? x2, Tensor? pscale, Tensor? pshift, Tensor(a!)? out=None, "
         "Tensor? pscale2=None, Tensor? pshift2=None, Tensor? dy_y=None, Tensor? dy_s4=None, "
-        "Tensor? dy_coefs=None, int cin_real=0, int groups=0) -> Tensor");
+        "Tensor? dy_coefs=None, int cin_real=0, int groups=0, Tensor(b!)? dy_out=None) -> Tensor");
   m.def("conv3_bwd32(Tensor dy, Tensor y, Tensor s4, Tensor wd, Tensor(a!)? dw_out=None, int groups=0) -> Tensor[]");
   m.def("reduce_rows(Tensor partial, int R, int N) -> Tensor");
   m.def("bn_finalize(Tensor partial, float count, Tensor gamma, Tensor beta, Tensor(a!) running_mean, "

@@ -925,6 +925,8 @@ int conv3_fwd_grid(const ConvFwdArgs& a) {
 
 namespace {
 
+// (per-tap s_setprio flips around the MFMA blocks: a static priority for waves NW/2.. or no
+// s_setprio measured -0.2 / -0.3%, noise — profiles/r6/prio_ab_r6b.json)
 template <int DIMS, int WM, int WN, int MT, int NT, int HALO, int NBB, int FDB, bool XL>
 void launch_mode(ConvFwdArgs& a, int grid, hipStream_t st) {
   using C = Cfg<DIMS, WM, WN, MT, NT, HALO, NBB>;

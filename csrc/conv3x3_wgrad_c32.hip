@@ -37,15 +37,17 @@ constexpr int C32_XITERS = (C32_XINSTR + 7) / 8;          // 3 / 2 per wave
 constexpr int C32_XBYTES = C32_XINSTR * 1024;
 constexpr int C32_YBYTES = C32_T * C32_T * 64;            // 16 KB (16 instructions)
 constexpr int C32_PRO = 3 * 64 * 4;                       // prologue table [3 chunks][scale|shift][32]
+constexpr int C32_DYP = 7 * 32 * 4;                       // dY prologue table [7][32]
 template <int NC>
-constexpr int c32_smem() { return C32_PRO + 2 * (C32_YBYTES + NC * C32_XBYTES); }
+constexpr int c32_smem() { return C32_PRO + C32_DYP + 2 * (C32_YBYTES + NC * C32_XBYTES); }
 static_assert(c32_smem<3>() <= 160 * 1024, "LDS budget");
 
 template <int NC>
 __global__ __launch_bounds__(512, 1) void conv3_wgrad_c32_kernel(ConvWgradArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* s_pro = reinterpret_cast<float*>(smem);
-  char* base = smem + C32_PRO;
+  float* s_dy = s_pro + C32_PRO / 4;                 // dY prologue: [7][32]
+  char* base = smem + C32_PRO + C32_DYP;
   constexpr int STAGE = C32_YBYTES + NC * C32_XBYTES;
   auto sY = [&](int b) { return base + b * STAGE; };
   auto sX = [&](int b, int c) { return base + b * STAGE + C32_YBYTES + c * C32_XBYTES; };
@@ -74,6 +76,23 @@ __global__ __launch_bounds__(512, 1) void conv3_wgrad_c32_kernel(ConvWgradArgs p
   bool any_pro = false;
 #pragma unroll
   for (int c = 0; c < NC; ++c) any_pro = any_pro || has_pro[c];
+  // dY prologue (BN backward on load, bn_bwd2_kernel's apply arithmetic): the staged tile
+  // holds dA; dY = k (dA [y*scale + shift > 0] - m1 - xhat m2) is formed in place by the lanes
+  // that DMA'd each piece (y of the same piece loaded to registers with the DMA) and stored
+  // to dyout for the conv's data gradient.  Table: scale, shift, invstd, -mean*invstd, k, m1, m2
+  const bool has_dyp = p.dyy != nullptr;
+  if (has_dyp && tid < 32) {
+    const float is = p.dys4[32 + tid];
+    s_dy[tid] = p.dys4[64 + tid];
+    s_dy[32 + tid] = p.dys4[96 + tid];
+    s_dy[64 + tid] = is;
+    s_dy[96 + tid] = -p.dys4[tid] * is;
+    s_dy[128 + tid] = p.dycoef[tid];
+    s_dy[160 + tid] = p.dycoef[32 + tid];
+    s_dy[192 + tid] = p.dycoef[64 + tid];
+  }
+  uint4 yv[2];                                       // (dY prologue) y of the lane's 2 dA pieces
+  uint32_t ybits = 0;                                // in-image dA pieces, 2 bits per stage
 
   // ---- DMA of tile t into stage b: dY (piece e -> tile pixel e >> 2) and each chunk's halo
   // (piece e -> halo pixel e >> 2, channel piece e & 3, unswizzled: transposed reads)
@@ -86,14 +105,22 @@ __global__ __launch_bounds__(512, 1) void conv3_wgrad_c32_kernel(ConvWgradArgs p
     const int h0 = th_ * C32_T, w0 = tw_ * C32_T;
     {
       const auto r = make_rsrc(p.dY + (long long)n * img_px * 32, (unsigned)(img_px * 64));
+      uint32_t yb = 0;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int px = ((i * 8 + wave) * 64 + lane) >> 2;
         const int gh = h0 + (px >> 4), gw = w0 + (px & 15);
         const bool ok = gh < p.H && gw < p.W;
-        dma16(r, sY(b) + (i * 8 + wave) * 1024,
-              ok ? ((unsigned)(gh * p.W + gw) * 32 + (lane & 3) * 8) * 2u : kOOB);
+        const unsigned off = ok ? ((unsigned)(gh * p.W + gw) * 32 + (lane & 3) * 8) * 2u : kOOB;
+        dma16(r, sY(b) + (i * 8 + wave) * 1024, off);
+        if (has_dyp) {
+          const auto ry = make_rsrc(p.dyy + (long long)n * img_px * 32, (unsigned)(img_px * 64));
+          const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0);
+          yv[i] = make_uint4(v.x, v.y, v.z, v.w);
+          yb |= (ok ? 1u : 0u) << i;
+        }
       }
+      ybits = (ybits & ~(0x3u << (2 * b))) | (yb << (2 * b));
     }
     uint32_t valid = 0;
     int pix[C32_XITERS];
@@ -146,6 +173,40 @@ __global__ __launch_bounds__(512, 1) void conv3_wgrad_c32_kernel(ConvWgradArgs p
         o[j] = ok ? __builtin_bit_cast(uint32_t, m) : 0u;
       }
       *reinterpret_cast<uint4*>(X + ((i * 8 + wave) * 64 + lane) * 16) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  };
+
+  // dY prologue on the lane's own 2 landed dA pieces of stage b (tile t): in place, and the
+  // formed dY stored (the same element offsets the DMA read from)
+  auto transform_dy = [&](char* __restrict__ Yb, int t, int b) __attribute__((always_inline)) {
+    const int tw_ = t % tilesW, q2 = t / tilesW;
+    const int th_ = q2 % tilesH, n = q2 / tilesH;
+    const int h0 = th_ * C32_T, w0 = tw_ * C32_T;
+    const auto ro = make_rsrc(p.dyout + (long long)n * img_px * 32, (unsigned)(img_px * 64));
+    const uint32_t yb = (ybits >> (2 * b)) & 0x3u;
+    const float* tb = s_dy + opaque_zero() + (lane & 3) * 8;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = (i * 8 + wave) * 64 + lane;
+      const int px = e >> 2;
+      const bool ok = (yb >> i) & 1u;
+      uint4* qd = reinterpret_cast<uint4*>(Yb + e * 16);
+      float fd[8], fy[8], o[8];
+      unpack8(*qd, fd);
+      unpack8(yv[i], fy);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = fmaf(fy[j], tb[j], tb[32 + j]);
+        const float dyh = a > 0.f ? fd[j] : 0.f;
+        const float xh = fmaf(fy[j], tb[64 + j], tb[96 + j]);
+        o[j] = tb[128 + j] * (dyh - tb[160 + j] - xh * tb[192 + j]);
+      }
+      const uint4 pk = ok ? pack8(o) : make_uint4(0, 0, 0, 0);
+      *qd = pk;
+      const int gh = h0 + (px >> 4), gw = w0 + (px & 15);
+      unsigned off = ok ? ((unsigned)(gh * p.W + gw) * 32 + (lane & 3) * 8) * 2u : kOOB;
+      asm volatile("" : "+v"(off));
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{pk.x, pk.y, pk.z, pk.w}, ro, off, 0, 0);
     }
   };
 
@@ -210,6 +271,7 @@ __global__ __launch_bounds__(512, 1) void conv3_wgrad_c32_kernel(ConvWgradArgs p
   int b = 0;
   for (int t = t_begin; t < t_end; ++t) {
     vm_wait_dyn(0);                                  // this tile's operands landed
+    if (has_dyp) transform_dy(sY(b), t, b);
     if (any_pro) {
 #pragma unroll
       for (int c = 0; c < NC; ++c)
@@ -242,7 +304,7 @@ __global__ __launch_bounds__(512, 1) void conv3_wgrad_c32_kernel(ConvWgradArgs p
 // BN groups / dY prologue, enough 16x16 tiles for one workgroup per CU with >= 8 tiles each
 int conv3_wgrad_c32_plan(ConvWgradArgs& a, int num_cus) {
   if (a.dims != 2 || a.Cout != 32 || a.C1 % 32 != 0 || a.C2 % 32 != 0 || a.groups > 1 ||
-      a.dyy != nullptr || a.Cin < 64 || a.Cin > 96 || a.W < 16)
+      (a.dyy != nullptr && a.dyout == nullptr) || a.Cin < 64 || a.Cin > 96 || a.W < 16)
     return -1;
   const int cmax = a.C1 > a.C2 ? a.C1 : a.C2;
   if ((long long)a.H * a.W * (cmax > 32 ? cmax : 32) * 2 >= (1LL << 31)) return -1;

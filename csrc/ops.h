@@ -119,6 +119,9 @@ struct ConvWgradArgs {
   const bf16_t* dyy;
   const float* dys4;
   const float* dycoef;
+  // (c32 kernel with the dY prologue: the formed dY is also stored here — the data gradient of
+  // the same conv reads it instead of a separate BN-backward apply pass)
+  bf16_t* dyout;
   int ciw;                        // v3: 32-channel input chunks per workgroup (1 or 2)
   // per-micro-batch BatchNorm groups (v3 only): images [g * gimg, (g+1) * gimg) use the
   // prologue constants pscale / pshift + g * gstride (the X1 prologue; no X2 prologue)

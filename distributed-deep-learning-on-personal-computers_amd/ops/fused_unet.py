@@ -447,7 +447,26 @@ class _DoubleConvFn(torch.autograd.Function):
         # apply pass (read dA1 + y1, write dY1) is skipped
         wg_pro = (padded_in and part1 is not None and eng.wgrad_dy_prologue and
                   not ctx.needs_input_grad[0])
-        if direct and wg_pro:
+        # 32-output-channel concat conv (dec1.a): its weight-gradient kernel (every input
+        # chunk per workgroup) applies BN1's backward on load from dA1 and y1 and stores the
+        # formed dY1 for the data gradient — no separate apply pass (read dA1 + y1, write dY1).
+        # It runs on the compute stream: the data gradient below reads its dY1
+        c32p = (not wg_pro and part1 is not None and eng.c32_bnp and x2_bn is None and
+                eng.c32_eligible(x1, x2, w1.shape[0]))
+        if c32p:
+            dy1 = torch.empty_like(da1)
+            if direct:
+                coefs, _, _ = F.bn_grad_coefs(part1, y1, s1, g1, bn1.weight.grad, bn1.bias.grad)
+                F.conv3_wgrad(da1, x1, x2, None, None, w1.grad, None, None, y1, s1, coefs,
+                              dy_out=dy1)
+                with eng.wgrad_stream():     # (readiness after both streams' writes)
+                    eng.ready(bn1.weight, bn1.bias, w1, blk.conv1.bias)
+                dg1 = dbe1 = dw1 = None
+            else:
+                coefs, dg1, dbe1 = F.bn_grad_coefs(part1, y1, s1, g1)
+                dw1 = F.conv3_wgrad(da1, x1, x2, None, None, None, None, None, y1, s1, coefs,
+                                    dy_out=dy1).reshape(w1.shape)
+        elif direct and wg_pro:
             coefs, _, _ = F.bn_grad_coefs(part1, y1, s1, g1, bn1.weight.grad, bn1.bias.grad)
             with eng.wgrad_stream(da1, y1, x1, coefs, s1):
                 w1.grad.add_(F.conv3_wgrad(da1, x1, None, None, None, None, None, None,
@@ -787,6 +806,9 @@ class UNetEngine:
         # 32 -> 32-channel second convs: data + weight gradient in one kernel (conv3x3_bwd32;
         # False: the resident data gradient + the v3 weight gradient on the side stream)
         self.bwd32 = True
+        # 32-output-channel concat convs (dec1.a): BN1 backward applied on load by the weight
+        # gradient, which stores dY1 for the data gradient (False: separate apply pass)
+        self.c32_bnp = True
         self.enc = [_Block(b.double_conv, first=(i == 0), engine=self)
                     for i, b in enumerate(model.down_blocks())]
         self.mid = _Block(model.double_conv, first=False, engine=self)
@@ -1037,6 +1059,20 @@ class UNetEngine:
             ok = (w >> lvl) >= 16 and c_up % 32 == 0 and c_up + c_skip <= 512
             out.append(bool(ok))
         return out
+
+    def c32_eligible(self, x1: torch.Tensor, x2: Optional[torch.Tensor], cout: int) -> bool:
+        """Whether conv3_wgrad takes the 32-output-channel concat kernel for this conv
+        (csrc/conv3x3_wgrad_c32.hip conv3_wgrad_c32_plan: 2-D, 64..96 input channels in whole
+        32-channel chunks, images >= 16 wide, >= 8 16x16 tiles per CU)."""
+        if x2 is None or x1.dim() != 4 or x2.dim() != 4 or cout != 32:
+            return False
+        n, h, w, c1 = x1.shape
+        c2 = x2.shape[-1]
+        if c1 % 32 or c2 % 32 or not 64 <= c1 + c2 <= 96 or w < 16:
+            return False
+        if h * w * max(c1, c2, 32) * 2 >= 2 ** 31:
+            return False
+        return n * -(-h // 16) * -(-w // 16) >= 8 * int(_ops().set_cu_reserve(-1))
 
     def group_fused(self, x: torch.Tensor, G: int, cmid: int) -> bool:
         """Whether a DoubleConv on input ``x`` runs the fused BN-group path: 2-D (the

@@ -1335,6 +1335,47 @@ def test_conv3_wgrad_c32_all_chunks(ops, N, H, W, C1, C2, pro, pro2):
     assert rel_err(dw, g) < 5e-3, rel_err(dw, g)
 
 
+@pytest.mark.parametrize("H,W,C1,C2", [(256, 256, 64, 32), (240, 264, 32, 32)])
+def test_conv3_wgrad_c32_bn_prologue_emits_dy(ops, H, W, C1, C2):
+    """dec1.a's weight gradient with BN1's backward applied on load (conv3x3_wgrad_c32.hip, dY
+    prologue): the kernel forms dY = k (dA [y*scale + shift > 0] - m1 - xhat m2) from dA and y
+    in LDS, stores it (dy_out) for the data gradient, and its weight gradient equals the plain
+    c32 kernel's on that stored dY bit for bit.  dY against the fp32 formula, dW against fp32
+    autograd; partial tiles in the second case."""
+    ncu = int(ops.set_cu_reserve(-1))
+    tiles = -(-H // 16) * -(-W // 16)
+    N = -(-8 * ncu // tiles)                     # the c32 kernel's eligibility: 8 tiles per CU
+    torch.manual_seed(H + C1)
+    x1 = nhwc(torch.randn(N, C1, H, W, device=DEV).bfloat16())
+    x2 = nhwc(torch.randn(N, C2, H, W, device=DEV).bfloat16())
+    da = nhwc((torch.randn(N, 32, H, W, device=DEV) * 1e-2).bfloat16())
+    y = nhwc(torch.randn(N, 32, H, W, device=DEV).bfloat16())
+    mean = torch.randn(32, device=DEV) * 0.1
+    inv = torch.rand(32, device=DEV) + 0.5
+    sc = (torch.rand(32, device=DEV) + 0.5) * inv * torch.where(torch.arange(32, device=DEV) % 5 == 0, -1.0, 1.0)
+    sh = torch.randn(32, device=DEV) * 0.3
+    s4 = torch.stack([mean, inv, sc, sh]).contiguous()
+    coefs = torch.stack([torch.rand(32, device=DEV) + 0.5, torch.randn(32, device=DEV) * 1e-3,
+                         torch.randn(32, device=DEV) * 1e-3]).contiguous()
+    dy_out = torch.empty_like(da)
+    dw = ops.conv3_wgrad(da, x1, x2, None, None, None, None, None, y, s4, coefs, dy_out=dy_out)
+    # dY against the formula (fp32; the kernel's fused multiply-adds may round 1 bf16 ulp apart)
+    yf, df = y.float(), da.float()
+    a = yf * sc + sh
+    dyh = torch.where(a > 0, df, torch.zeros_like(df))
+    xh = yf * inv - mean * inv
+    ref = coefs[0] * (dyh - coefs[1] - xh * coefs[2])
+    assert rel_err(dy_out, ref) < 5e-3, rel_err(dy_out, ref)
+    assert float((dy_out.float() - ref.bfloat16().float()).ne(0).float().mean()) < 1e-2
+    # the weight gradient is the plain kernel's on the stored dY, bit for bit
+    dw_plain = ops.conv3_wgrad(dy_out, x1, x2, None, None)
+    assert torch.equal(dw, dw_plain)
+    w = torch.zeros(32, C1 + C2, 3, 3, device=DEV, requires_grad=True)
+    (g,) = torch.autograd.grad(F.conv2d(torch.cat([nchw(x1).float(), nchw(x2).float()], 1), w,
+                                        padding=1), w, nchw(dy_out).float())
+    assert rel_err(dw, g) < 5e-3, rel_err(dw, g)
+
+
 @pytest.mark.parametrize("N,D,H,W,Cout,co1,pro,bias", [
     (2, 5, 128, 120, 64, 0, True, True), (2, 4, 96, 136, 96, 32, False, False),
     (1, 3, 256, 256, 96, 64, False, True)])
