@@ -79,6 +79,9 @@ def _parse():
                     help="1 GPU: stand-in collective per gradient bucket for a world of N "
                          "(streaming kernel on a third stream; measures launch-to-finish "
                          "latency during backward)")
+    ap.add_argument("--prefetch", type=int, default=1,
+                    help="1: render the next step's on-device batch on a side stream under "
+                         "this step (0: in front of each step)")
     ap.add_argument("--engine-set", default="",
                     help="diagnostic: NAME=INT[,NAME=INT] — set UNetEngine switches (e.g. "
                          "c32_bnp=0) before the first step, for same-box A/B runs")
@@ -220,9 +223,15 @@ def main():
         return [batch(i * args.accum + j) for j in range(args.accum)]
 
     fixed = window(0) if args.fixed_batch else None
+    # on-device data: step i+1's batch renders on a side stream under step i (one batch per
+    # step is still rendered inside the timed region; data.DevicePrefetcher)
+    pf = None
+    if on_device_data and fixed is None and args.prefetch:
+        from ddlpc.data import DevicePrefetcher
+        pf = DevicePrefetcher(window, device)
 
     def step(i):
-        tr.train_step(fixed if fixed is not None else window(i))
+        tr.train_step(fixed if fixed is not None else pf.get(i) if pf is not None else window(i))
 
     def sync():
         if dev == "cuda":
@@ -366,6 +375,9 @@ def main():
         data_desc = data_desc.replace("rendered in HBM per step", "pre-rendered pool of 4 batches")
     elif args.fixed_batch:
         data_desc = data_desc.replace("rendered in HBM per step", "ONE batch rendered once (diagnostic)")
+    elif pf is not None:
+        data_desc = data_desc.replace("rendered in HBM per step",
+                                      "rendered in HBM per step, one step ahead on a side stream")
     if rank == 0:
         red = tr.reducer
         rec = {
@@ -433,6 +445,7 @@ def main():
                        "bucket_sweep": sweep or None,
                        "ab": ab,
                        "engine_set": args.engine_set or None,
+                       "input_prefetch": pf is not None,
                        "alloc_retries": mstats.get("num_alloc_retries"),
                        "side_lag_waits": (getattr(tr.model._engine, "lag_waits", None)
                                           if tr.impl == "hip" else None),

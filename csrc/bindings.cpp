@@ -83,7 +83,7 @@ int pick_bn(int Cout) {
 // (bench.py --ab, scripts/conv_micro.py --ab) can never silently time two identical
 // configurations.  An empty list = no experiment in progress.
 namespace {
-const char* const kKnobs[] = {""};
+const char* const kKnobs[] = {"CONVT_FB8"};
 bool knob_registered(const std::string& name) {
   for (const char* k : kKnobs)
     if (k[0] != 0 && name == k) return true;
@@ -1054,7 +1054,7 @@ std::vector<at::Tensor> convt_bwd_fused(const at::Tensor& x, const at::Tensor& d
   a.dims = 2; a.Nimg = g.N; a.D = 1; a.H = g.H; a.W = g.W;
   a.Cin = 64; a.Cout = 64;
   a.bn4 = bn4_ptr(bn4, 64);
-  a.splits = (int)std::max<long long>(1, std::min<long long>(2LL * num_cus(), (long long)a.K / 128));
+  a.splits = convt_bwd_fused_splits(a.K, num_cus());
   at::Tensor dx = at::empty_like(x);
   a.C = dx.data_ptr();
   at::Tensor part = at::empty({(int64_t)a.splits * 64 * 256}, fopts);

@@ -538,7 +538,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
   // of the whole-tap double buffer's 8 (MT + NT) — 64 fewer with the BM-512 tiles (MT = 8),
   // which otherwise spill to scratch (a scratch reload waits vmcnt(0), i.e. on the operand
   // DMA in flight for the next stage)
-  constexpr int XD = 1 + 12 / NT;
+  constexpr int XD = 1 + 12 / NT;     // (6 for BM-512: +0.1%, noise — profiles/r6/cfg5_xd_ab_r6d.json)
   auto pipe_taps = [&](auto TTc, const char* __restrict__ A0, const char* __restrict__ B0, int off0,
                        const char* __restrict__ A1, const char* __restrict__ B1, int off1, auto&& hook)
       __attribute__((always_inline)) {

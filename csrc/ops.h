@@ -187,6 +187,7 @@ enum GemmMode {
   GEMM_CONVT_WGRAD = 2, // TN: dW[ci][(sub, co)] = sum_px x[px][ci] * dOut[up(px, sub)][co]
 };
 void gemm_launch(GemmArgs& a, hipStream_t st);
+int convt_bwd_fused_splits(long long K, int num_cus);   // workgroups of the fused 64-ch backward
 int gemm_nt_bn(const GemmArgs& a);            // N tile of the forward / data-gradient GEMM
 long long gemm_nt_grid(const GemmArgs& a);     // its workgroup count (= BN-partial rows)
 int convt_wgrad2_tiles(const GemmArgs& a);

@@ -132,6 +132,51 @@ def cat_adjacent(ts: List[torch.Tensor]) -> torch.Tensor:
     return out
 
 
+class DevicePrefetcher:
+    """Device-side input pipeline: ``get(k)`` returns batch k (``make(k)``) and starts
+    rendering batch k + 1 on a side HIP stream, so the generator / gather kernels of the next
+    step run under this step's compute instead of in front of it (every batch is still
+    rendered, one per step).  The current stream waits on the batch's event, and every tensor
+    of the batch is recorded on it, so the caching allocator never hands the memory back to
+    the side stream while the step may still read it."""
+
+    def __init__(self, make, device):
+        self.make = make
+        self.stream = torch.cuda.Stream(torch.device(device))
+        self.pending = {}
+
+    def _launch(self, k):
+        # (no wait on the current stream: the render reads nothing the step writes)
+        with torch.cuda.stream(self.stream):
+            batch = self.make(k)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self.pending[k] = (batch, ev)
+
+    @staticmethod
+    def _tensors(obj):
+        if isinstance(obj, torch.Tensor):
+            yield obj
+            base = getattr(obj, "_ddlpc_nhwc", None)
+            if base is not None:
+                yield base
+        elif isinstance(obj, (list, tuple)):
+            for o in obj:
+                yield from DevicePrefetcher._tensors(o)
+
+    def get(self, k):
+        if k not in self.pending:
+            self.pending.clear()
+            self._launch(k)
+        batch, ev = self.pending.pop(k)
+        cur = torch.cuda.current_stream(self.stream.device)
+        cur.wait_event(ev)
+        for t in self._tensors(batch):
+            t.record_stream(cur)
+        self._launch(k + 1)
+        return batch
+
+
 # ---------------------------------------------------------------------- synthetic tiles
 def device_indices(idx, device) -> torch.Tensor:
     """Sample indices as an int64 tensor on ``device`` without a blocking host round trip:

@@ -41,6 +41,28 @@ def test_synth_tiles_kernel_matches_torch_twin(classes, tile, dims, grid):
     assert x.shape == (len(idx), 3) + (tile,) * dims
 
 
+def test_device_prefetcher_hands_out_each_batch_intact():
+    """``DevicePrefetcher`` (bench.py's input pipeline): batch k renders on a side stream
+    under step k - 1; every batch handed out equals a direct render of the same indices,
+    with the consumer allocating / freeing memory and running kernels in between (the
+    allocator must not recycle a batch the current stream still reads)."""
+    from ddlpc.data import DevicePrefetcher, SyntheticTiles
+    ds = SyntheticTiles(1 << 20, 64, classes=6, seed=5, device="cuda", layout="engine")
+
+    def make(k):
+        return ds.get(torch.arange(8 * k, 8 * k + 8, device="cuda"))
+
+    pf = DevicePrefetcher(make, "cuda")
+    for k in range(6):
+        x, y = pf.get(k)
+        junk = torch.randn(4 << 20, device="cuda")          # allocator churn + device work
+        s = float((x._ddlpc_nhwc.float().sum() + y.sum()).item()) + float(junk.sum().item())
+        xr, yr = make(k)
+        assert torch.equal(x._ddlpc_nhwc, xr._ddlpc_nhwc) and torch.equal(y, yr), k
+        del x, y, junk, s
+    assert 6 in pf.pending                                   # the next batch is in flight
+
+
 def test_tile_gather_matches_host_dataset():
     from ddlpc.data import TileDataset
     rng = np.random.default_rng(0)
