@@ -83,7 +83,7 @@ int pick_bn(int Cout) {
 // (bench.py --ab, scripts/conv_micro.py --ab) can never silently time two identical
 // configurations.  An empty list = no experiment in progress.
 namespace {
-const char* const kKnobs[] = {"CONVT_FB8"};
+const char* const kKnobs[] = {""};
 bool knob_registered(const std::string& name) {
   for (const char* k : kKnobs)
     if (k[0] != 0 && name == k) return true;

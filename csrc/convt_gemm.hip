@@ -1271,269 +1271,15 @@ __global__ __launch_bounds__(256, 2) void convt_bwd_fused_kernel(GemmArgs p) {
   }
 }
 
-// The same fused backward on ONE persistent 8-wave workgroup per CU with a 4-slot operand
-// ring: the 4-wave form (two workgroups per CU, two slots each) kept at most one 20 KB stage
-// per workgroup in flight — ~40 KB per CU, which at the loaded HBM latency caps the layer at
-// ~3.9 TB/s (dOut is 2/3 of its bytes).  Here three stages (60 KB) are in flight behind the
-// one being computed.  Per stage a wave runs 8 weight-gradient MFMAs (its 32 of the 256
-// (sub, co) columns x 64 ci) and 8 data-gradient MFMAs (ci block w & 3 of pixel half w >> 2).
-struct Fb8Cfg {
-  static constexpr int KT = 32, A_RB = 128, B_RB = 512, NSLOT = 4;
-  static constexpr int A_BYTES = KT * A_RB, B_BYTES = KT * B_RB;     // 4 KB + 16 KB
-  static constexpr int NB = B_BYTES / 8192;                          // 2 B DMAs / wave (8 waves)
-  static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int WD_BYTES = 64 * 512;                          // resident Wd
-  static constexpr int SMEM = NSLOT * STAGE + WD_BYTES + 4 * 64 * 4;  // + BN table
-};
-static_assert(Fb8Cfg::SMEM <= 160 * 1024, "LDS budget");
-
-__global__ __launch_bounds__(512, 1) void convt_bwd_fused8_kernel(GemmArgs p) {
-  using namespace convlds;
-  using Cf = Fb8Cfg;
-  constexpr int KT = Cf::KT, NSLOT = Cf::NSLOT;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* sWd = smem + NSLOT * Cf::STAGE;
-  float* s_bn = reinterpret_cast<float*>(sWd + Cf::WD_BYTES);   // scale | shift | invstd | -mean*invstd
-  auto sA = [&](int b) { return smem + b * Cf::STAGE; };
-  auto sB = [&](int b) { return smem + b * Cf::STAGE + Cf::A_BYTES; };
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool has_bn = p.bn4 != nullptr;
-  if (has_bn && tid < 64) {
-    const float is = p.bn4[64 + tid];
-    s_bn[tid] = p.bn4[128 + tid];
-    s_bn[64 + tid] = p.bn4[192 + tid];
-    s_bn[128 + tid] = is;
-    s_bn[192 + tid] = -p.bn4[tid] * is;
-  }
-  const int split = xcd_remap(blockIdx.x, gridDim.x);
-  const long long npx = (long long)p.K;
-  const long long per = ((npx + p.splits - 1) / p.splits + KT - 1) / KT * KT;
-  const long long k_begin = per * split;
-  const long long k_end = k_begin + per < npx ? k_begin + per : npx;
-  f32x4_t acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float bs1[4] = {0.f, 0.f, 0.f, 0.f}, bs2[4] = {0.f, 0.f, 0.f, 0.f};   // BN partials
-  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  const int cb = wave & 3, th = wave >> 2;            // data gradient: ci block, pixel half
-  const int ci4 = 16 * cb + 4 * g;                    // this lane's 4 dx channels
-  const bool a_dma = wave < 4;                        // (4 KB of x per stage: waves 0-3)
-  const int per_st = Cf::NB + (a_dma ? 1 : 0);        // DMA instructions per stage (this wave)
-  if (k_begin < k_end) {
-    const long long a_lo = k_begin;
-    const auto ra = make_rsrc(p.A + a_lo * 64, (unsigned)((k_end - a_lo) * 64 * 2));
-    const long long kb0 = k_begin - k_begin % p.W;
-    const long long b_lo = up_pixel((int)kb0, 0, 2, 1, p.H, p.W);
-    const long long b_hi = (long long)up_pixel((int)(k_end - 1), 3, 2, 1, p.H, p.W) + 1;
-    const auto rb = make_rsrc(p.B + b_lo * 64, (unsigned)((b_hi - b_lo) * 64 * 2));
-    const auto rx = make_rsrc(static_cast<bf16_t*>(p.C) + a_lo * 64, (unsigned)((k_end - a_lo) * 64 * 2));
-    // resident Wd [ci][n]: 16-B piece pc of row ci stored at pc ^ (ci & 15)
-    {
-      const auto rw = make_rsrc(p.Wd2, 64 * 256 * 2);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int e = (i * 8 + wave) * 64 + lane;
-        const int row = e >> 5, pc = e & 31;
-        dma16(rw, sWd + (i * 8 + wave) * 1024, (unsigned)((row * 256 + ((pc ^ (row & 15)) * 8)) * 2));
-      }
-    }
-    int a_row = 0, a_col = 0, b_row[Cf::NB], b_col[Cf::NB], b_sub[Cf::NB];
-    {
-      const int e = (wave & 3) * 64 + lane;
-      const int row = e / 8, pc = e % 8;
-      a_row = row;
-      a_col = ((((pc >> 1) ^ tn2_swz<Cf::A_RB>(row)) << 1) | (pc & 1)) * 8;
-    }
-#pragma unroll
-    for (int i = 0; i < Cf::NB; ++i) {
-      const int e = (i * 8 + wave) * 64 + lane;
-      const int row = e / 32, pc = e % 32;
-      const int n = ((((pc >> 1) ^ tn2_swz<Cf::B_RB>(row)) << 1) | (pc & 1)) * 8;
-      b_row[i] = row;
-      b_sub[i] = n >> 6;
-      b_col[i] = n & 63;
-    }
-    auto issue = [&](long long k0, int buf) {
-      if (a_dma) {
-        const long long px = k0 + a_row;
-        dma16(ra, sA(buf) + wave * 1024, px < k_end ? (unsigned)(((px - a_lo) * 64 + a_col) * 2) : kOOB);
-      }
-#pragma unroll
-      for (int i = 0; i < Cf::NB; ++i) {
-        const long long px = k0 + b_row[i];
-        const bool ok = px < k_end;
-        const long long up = ok ? up_pixel((int)px, b_sub[i], 2, 1, p.H, p.W) : b_lo;
-        dma16(rb, sB(buf) + (i * 8 + wave) * 1024, ok ? (unsigned)(((up - b_lo) * 64 + b_col[i]) * 2) : kOOB);
-      }
-    };
-    auto frag_off = [&](int row, int col, auto rb_tag) {
-      constexpr int RB = decltype(rb_tag)::value;
-      const int grp = (col >> 4) ^ tn2_swz<RB>(row);
-      return row * RB + grp * 32 + (col & 15) * 2;
-    };
-    using RA = std::integral_constant<int, Cf::A_RB>;
-    using RBt = std::integral_constant<int, Cf::B_RB>;
-    float asc[4], ash[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) { asc[mt] = 0.f; ash[mt] = 0.f; }
-    const int nst = (int)((k_end - k_begin + KT - 1) / KT);
-    dma_wait<0>();
-    __syncthreads();                                  // Wd + BN table resident
-    if (has_bn)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) { asc[mt] = s_bn[16 * mt + (lane & 15)]; ash[mt] = s_bn[64 + 16 * mt + (lane & 15)]; }
-    float ysc[4], ysh[4], yis[4], ynm[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ysc[i] = has_bn ? s_bn[ci4 + i] : 0.f;
-      ysh[i] = has_bn ? s_bn[64 + ci4 + i] : 0.f;
-      yis[i] = has_bn ? s_bn[128 + ci4 + i] : 0.f;
-      ynm[i] = has_bn ? s_bn[192 + ci4 + i] : 0.f;
-    }
-    // per-wave ledger of issued vector-memory ops (DMA + dx stores, retired in order): the
-    // wait for stage st leaves everything issued after its DMA in flight
-    int issued = 0;
-    int mk[NSLOT] = {0, 0, 0, 0};                     // issued count right after DMA(slot)
-#pragma unroll
-    for (int j = 0; j < NSLOT - 1; ++j)
-      if (j < nst) { issue(k_begin + (long long)j * KT, j); issued += per_st; mk[j] = issued; }
-#pragma unroll 1
-    for (int st = 0; st < nst; ++st) {
-      const int buf = st & (NSLOT - 1);
-      const long long k0 = k_begin + (long long)st * KT;
-      int mine = mk[0];
-#pragma unroll
-      for (int j = 1; j < NSLOT; ++j) mine = buf == j ? mk[j] : mine;
-      vm_wait_dyn(issued - mine);                     // this wave's DMA of stage st landed
-      lds_sync();                                     // all waves': visible; slot st-1 free
-      if (st + NSLOT - 1 < nst) {
-        const int nb = (st + NSLOT - 1) & (NSLOT - 1);
-        issue(k0 + (long long)(NSLOT - 1) * KT, nb);
-        issued += per_st;
-#pragma unroll
-        for (int j = 0; j < NSLOT; ++j) mk[j] = nb == j ? issued : mk[j];
-      }
-      const char* A_ = sA(buf);
-      const char* B_ = sB(buf);
-      // ---- weight gradient: dW[ci][n] += sum_px x[px][ci] dOut[px][n], n in 32 wave .. + 31
-      {
-        const int r0 = 8 * g + q;
-        uint4 af[4], bfr[2];
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const int c = mt * 16 + 4 * pp;
-          const uint2 lo = lds_read_tr16(A_ + frag_off(r0, c, RA{}));
-          const uint2 hi = lds_read_tr16(A_ + frag_off(r0 + 4, c, RA{}));
-          uint4 v = make_uint4(lo.x, lo.y, hi.x, hi.y);
-          if (has_bn) {
-            float f[8];
-            unpack8(v, f);
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              f[j] = k0 + 8 * g + j < k_end ? fmaxf(fmaf(f[j], asc[mt], ash[mt]), 0.f) : 0.f;
-            v = pack8(f);
-          }
-          af[mt] = v;
-        }
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const int c = wave * 32 + nt * 16 + 4 * pp;
-          const uint2 lo = lds_read_tr16(B_ + frag_off(r0, c, RBt{}));
-          const uint2 hi = lds_read_tr16(B_ + frag_off(r0 + 4, c, RBt{}));
-          bfr[nt] = make_uint4(lo.x, lo.y, hi.x, hi.y);
-        }
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma16x16x32(af[mt], bfr[nt], acc[mt][nt]);
-      }
-      // ---- data gradient: dx^T[ci][px] = Wd[ci][n] dOut^T[n][px]: ci 16 cb.., pixels 16 th..
-      f32x4_t dacc = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      {
-        const int wrow = 16 * cb + (lane & 15);
-        const int prow = 16 * th + (lane & 15);
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
-          const int lp = 4 * kk + g;                  // logical 16-B piece (8 n) of the k step
-          const uint4 aw = lds128(sWd + wrow * 512 + ((lp ^ (wrow & 15)) << 4));
-          const uint4 bx = lds128(B_ + prow * 512 + ((((lp >> 1) ^ tn2_swz<Cf::B_RB>(prow)) << 1 | (lp & 1)) << 4));
-          dacc = mfma16x16x32(aw, bx, dacc);
-        }
-      }
-      // dx store (lane: channels ci4..ci4+3 of pixel 16 th + (lane & 15)) + BN partials of the
-      // stored values against the raw x in LDS
-      {
-        const int prow = 16 * th + (lane & 15);
-        const long long px = k0 + prow;
-        const bool ok = px < k_end;
-        const uint32_t lo = pack2(dacc[0], dacc[1]), hi = pack2(dacc[2], dacc[3]);
-        unsigned off = ok ? (unsigned)(((px - a_lo) * 64 + ci4) * 2) : kOOB;
-        asm volatile("" : "+v"(off));
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{lo, hi}, rx, off, 0, 0);
-        issued += 1;
-        if (has_bn && ok) {
-          const uint2 yv = *reinterpret_cast<const uint2*>(A_ + frag_off(prow, ci4, RA{}));
-          const float d[4] = {lo_bf(lo), hi_bf(lo), lo_bf(hi), hi_bf(hi)};
-          const float y[4] = {lo_bf(yv.x), hi_bf(yv.x), lo_bf(yv.y), hi_bf(yv.y)};
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float a = fmaf(y[i], ysc[i], ysh[i]);
-            const float dyh = a > 0.f ? d[i] : 0.f;
-            const float xh = fmaf(y[i], yis[i], ynm[i]);
-            bs1[i] += dyh;
-            bs2[i] = fmaf(dyh, xh, bs2[i]);
-          }
-        }
-      }
-    }
-    dma_wait<0>();
-  }
-  // weight-gradient partial of this split
-  float* out = p.partial + (long long)split * 64 * 256;
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const int n = wave * 32 + nt * 16 + (lane & 15);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) out[(long long)(mt * 16 + 4 * g + i) * 256 + n] = acc[mt][nt][i];
-    }
-  if (has_bn) {
-    // lanes with equal g hold the same 4 channels: sum over lane & 15, fixed order; then the
-    // two pixel halves (waves cb and cb + 4) in LDS, half 0 + half 1
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { bs1[i] += __shfl_xor(bs1[i], o, 64); bs2[i] += __shfl_xor(bs2[i], o, 64); }
-    float* red = reinterpret_cast<float*>(smem);      // (the ring is drained)
-    __syncthreads();
-    if (th == 1 && (lane & 15) == 0)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { red[ci4 + i] = bs1[i]; red[64 + ci4 + i] = bs2[i]; }
-    __syncthreads();
-    if (th == 0 && (lane & 15) == 0) {
-      float* row = p.bnpart + (long long)split * 128;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { row[ci4 + i] = bs1[i] + red[ci4 + i]; row[64 + ci4 + i] = bs2[i] + red[64 + ci4 + i]; }
-    }
-  }
-}
-
 }  // namespace
 
 void convt_bwd_fused_launch(GemmArgs& a, hipStream_t st) {
-  if (knob("CONVT_FB8", 1))
-    hipLaunchKernelGGL(convt_bwd_fused8_kernel, dim3(a.splits), dim3(512), Fb8Cfg::SMEM, st, a);
-  else
-    hipLaunchKernelGGL(convt_bwd_fused_kernel, dim3(a.splits), dim3(256), FbCfg::SMEM, st, a);
+  hipLaunchKernelGGL(convt_bwd_fused_kernel, dim3(a.splits), dim3(256), FbCfg::SMEM, st, a);
 }
+// (Rejected: one 8-wave workgroup per CU with a 4-slot ring — three 20 KB stages in flight
+// instead of one per workgroup — measured 1.5% slower end to end: profiles/r6/convt_fb8_ab_rejected_r6e.log)
 int convt_bwd_fused_splits(long long K, int num_cus) {
-  // one persistent 8-wave workgroup per CU (the 4-wave form: two per CU)
-  const long long per_cu = knob("CONVT_FB8", 1) ? 1 : 2;
-  return (int)std::max<long long>(1, std::min<long long>(per_cu * num_cus, K / 128));
+  return (int)std::max<long long>(1, std::min<long long>(2LL * num_cus, K / 128));   // two per CU
 }
 
 int convt_wgrad2_tiles(const GemmArgs& a) {
