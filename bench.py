@@ -37,9 +37,10 @@ def _parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None,
-                    help="per-GPU batch (images); default 256 for the flagship 256^2 2-D config "
-                         "(+3-5%% over 128 on one MI355X, 20 GB of the 288 GB HBM), 128 otherwise; "
-                         "32 / 64 / 128 / 256 have measured in-house baselines")
+                    help="per-GPU batch (images); default 384 for the flagship 256^2 2-D config "
+                         "(same box: 256 / 384 / 512 -> 7838 / 7985 / 7967 img/s, 30 GB of the "
+                         "288 GB HBM; profiles/r6/batch_sweep_r6b_*), 128 otherwise; "
+                         "32 / 64 / 128 / 256 / 384 have measured in-house baselines")
     ap.add_argument("--accum", type=int, default=1)
     ap.add_argument("--tile", type=int, default=256)
     ap.add_argument("--width-divisor", type=int, default=2)
@@ -96,7 +97,7 @@ def _parse():
                     help="seconds between 'alive' lines on stderr (long first-step autotuning)")
     a = ap.parse_args()
     if a.batch is None:
-        a.batch = 256 if (a.tile == 256 and a.dims == 2) else 128
+        a.batch = 384 if (a.tile == 256 and a.dims == 2) else 128
     return a
 
 
@@ -140,7 +141,8 @@ def _baseline(args):
     if args.width_divisor != 2:
         return None
     v = {32: b.get("images_per_sec_per_gpu"), 64: b.get("batch_64_images_per_sec"),
-         128: b.get("batch_128_images_per_sec"), 256: b.get("batch_256_images_per_sec")}.get(args.batch)
+         128: b.get("batch_128_images_per_sec"), 256: b.get("batch_256_images_per_sec"),
+         384: b.get("batch_384_images_per_sec")}.get(args.batch)
     return float(v) if v else None
 
 

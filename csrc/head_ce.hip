@@ -277,7 +277,7 @@ __global__ __launch_bounds__(256) void head_ce_bwd_kernel(
   __shared__ float sred[4][G][NACC];
   __shared__ __attribute__((aligned(16))) float sW[K * C];      // Wh, padded classes zero
   __shared__ __attribute__((aligned(16))) float sXh[2 * C];     // invstd | -mean*invstd
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int cg = lane % G, c8 = cg * 8;
   for (int i = tid; i < K * C; i += 256) sW[i] = i < Kreal * C ? Wh[i] : 0.f;
   if (DEFER)
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(256, 3) void head_fwd_stats_mdw_kernel(
   // per wave: act [16][32] bf16 (1 KB) | dlogits hi [16][16] (512 B) | lo [16][16]; the end
   // of the kernel reuses it as the wave's dWh^T [16][32] fp32 (2 KB)
   __shared__ __attribute__((aligned(16))) char sT[4][2048];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int cg = lane % G, c8 = cg * 8;
   for (int i = tid; i < K * C; i += 256) sW[i] = i < Kreal * C ? Wh[i] : 0.f;
   for (int i = tid; i < C; i += 256) { sXh[i] = bn4[C + i]; sXh[C + i] = -bn4[i] * bn4[C + i]; }
@@ -719,7 +719,7 @@ DDLPC_DEVICE Head32W head32_weights(const float* __restrict__ Wh, const float* _
 // rounding (o8, the lane's 8 channels) and rounded (pk); LOSS extras: lse, the label's
 // logit, the arg-max class (valid on every lane of the pixel)
 template <bool DEFER, bool LOSS>
-DDLPC_DEVICE void head32_step(const uint4 yv, const int lab, const bool valid, const Head32W& w,
+DDLPC_DEVICE void head32_step(const uint4 yv, const int lab, const bool valid, const Head32W* __restrict__ wl,
                               const float (&sc)[8], const float (&sh)[8], float gs, int ignore_index,
                               int g, float (&y8)[8], uint4& fb, float (&d)[4], uint2& bh2, uint2& bl2,
                               float (&o8)[8], uint4& pk, float& lse, float& zy, int& am) {
@@ -742,8 +742,10 @@ DDLPC_DEVICE void head32_step(const uint4 yv, const int lab, const bool valid, c
     fb = yv;
   }
   const uint4 fz = valid ? fb : make_uint4(0, 0, 0, 0);
-  f32x4_t z = mfma16x16x32(w.zh, fz, w.b4);
-  z = mfma16x16x32(w.zl, fz, z);
+  // (the lane's constant operands are read from LDS where they are used: held in VGPRs across
+  // the step loop they cost 20 registers and a wave per SIMD of occupancy)
+  f32x4_t z = mfma16x16x32(wl->zh, fz, wl->b4);
+  z = mfma16x16x32(wl->zl, fz, z);
   float m = fmaxf(fmaxf(z[0], z[1]), fmaxf(z[2], z[3]));
   m = rows4_max(m);
   float e[4], se = 0.f;
@@ -778,9 +780,10 @@ DDLPC_DEVICE void head32_step(const uint4 yv, const int lab, const bool valid, c
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     f32x4_t o = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    o = mfma16x16x16(w.th[t], bh2, o);
-    o = mfma16x16x16(w.th[t], bl2, o);
-    o = mfma16x16x16(w.tl[t], bh2, o);
+    const uint2 th = wl->th[t], tl = wl->tl[t];
+    o = mfma16x16x16(th, bh2, o);
+    o = mfma16x16x16(th, bl2, o);
+    o = mfma16x16x16(tl, bh2, o);
 #pragma unroll
     for (int i = 0; i < 4; ++i) o8[4 * t + i] = o[i];
   }
@@ -792,13 +795,13 @@ DDLPC_DEVICE void head32_step(const uint4 yv, const int lab, const bool valid, c
 // 1.9 TB/s (12 waves x 1.1 KB in flight per CU); the per-lane channel constants live in LDS
 // (re-read per step; an opaque offset keeps the compiler from hoisting them into VGPRs) to pay
 // for the deeper register pipeline.
-constexpr int HEAD32_D = 3;             // head32_kernel (4 spills at three waves per SIMD)
+constexpr int HEAD32_D = 3;             // head32_kernel (three steps ahead at four workgroups per CU, <= 128 VGPRs)
 constexpr int HEAD32_DA = 4;            // head32_apply_kernel
 
 template <int D>
 struct Head32Ld {
   uint4 y[D];
-  int64_t l[D];
+  int l[D];                             // (the low word of the int64 label: ids and -100 fit)
 };
 
 // The C = 32 counterpart of head_ce_bwd_kernel<32, K, DEFER, STORE, LOSS> (same outputs, same
@@ -806,7 +809,7 @@ struct Head32Ld {
 // partials), the dA store (STORE), and with LOSS the training forward's loss / hits / count at
 // a unit gradient scale.
 template <bool DEFER, bool STORE, bool LOSS>
-__global__ __launch_bounds__(256, 3) void head32_kernel(
+__global__ __launch_bounds__(256, 4) void head32_kernel(
     const bf16_t* __restrict__ a, const float* __restrict__ Wh, const float* __restrict__ bh,
     const int64_t* __restrict__ labels, const float* __restrict__ gscale,
     const float* __restrict__ stats3, bf16_t* __restrict__ dA, float* __restrict__ dWp,
@@ -826,9 +829,10 @@ __global__ __launch_bounds__(256, 3) void head32_kernel(
   __shared__ __attribute__((aligned(16))) char sT[4][2048];
   __shared__ float sred[4][4][24];                 // [wave][row g][db 4 | bn 16 | loss 3]
   __shared__ __attribute__((aligned(16))) float sK[4][C];   // scale | shift | invstd | -mean*invstd
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ Head32W sW[64];                       // the lanes' constant MFMA operands
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // (uniform: scalar step indices)
   const int n = lane & 15, g = lane >> 4;
-  const Head32W w = head32_weights(Wh, bh, Kreal, lane);
+  if (tid < 64) sW[tid] = head32_weights(Wh, bh, Kreal, lane);
   if (DEFER && tid < C) {
     sK[0][tid] = bn4[2 * C + tid];
     sK[1][tid] = bn4[3 * C + tid];
@@ -851,11 +855,11 @@ __global__ __launch_bounds__(256, 3) void head32_kernel(
   const long long steps = groups > 1 ? (long long)(grp + 1) * gsteps : (P + 15) / 16;   // (end step)
   const long long wstride = (long long)Rb * 4;
   const long long s0 = (long long)grp * gsteps + (long long)((int)blockIdx.x - grp * Rb) * 4 + wave;
-  auto load = [&](long long st, uint4& yv, int64_t& lb) __attribute__((always_inline)) {
+  auto load = [&](long long st, uint4& yv, int& lb) __attribute__((always_inline)) {
     const long long px = st * 16 + n;
     const long long pc = px < P ? px : 0;
     yv = *reinterpret_cast<const uint4*>(a + pc * C + 8 * g);
-    lb = labels[pc];
+    lb = reinterpret_cast<const int*>(labels)[2 * pc];
   };
   Head32Ld<HEAD32_D> q4;
 #pragma unroll
@@ -866,7 +870,7 @@ __global__ __launch_bounds__(256, 3) void head32_kernel(
     for (int j = 0; j < HEAD32_D; ++j) {
       const long long s = sb + j * wstride;
       const uint4 yv = q4.y[j];
-      const int lab = (int)q4.l[j];
+      const int lab = q4.l[j];
       if (s + HEAD32_D * wstride < steps) load(s + HEAD32_D * wstride, q4.y[j], q4.l[j]);
       if (s >= steps) break;                           // wave-uniform
       const long long px = s * 16 + n;
@@ -885,7 +889,7 @@ __global__ __launch_bounds__(256, 3) void head32_kernel(
       int am = 0;
       uint4 pk, fb;
       uint2 bh2, bl2;
-      head32_step<DEFER, LOSS>(yv, lab, valid, w, sc, sh, gs, ignore_index, g, y8, fb, d, bh2, bl2, o8, pk,
+      head32_step<DEFER, LOSS>(yv, lab, valid, sW + opaque_zero() + lane, sc, sh, gs, ignore_index, g, y8, fb, d, bh2, bl2, o8, pk,
                                lse, zy, am);
       if (STORE && valid) *reinterpret_cast<uint4*>(dA + px * C + 8 * g) = pk;
       // dWh via the LDS transpose: act row (the lane's 8 channels; zero for tail pixels),
@@ -988,7 +992,7 @@ __global__ __launch_bounds__(256, 3) void head32_kernel(
 // The C = 32 counterpart of head_bn_apply_kernel: dA recomputed exactly as head32_kernel
 // stores it, the deferred BatchNorm's backward applied in registers (bn_bwd2_kernel's apply
 // arithmetic), dY stored.  A HEAD32_DA-deep load pipeline.
-__global__ __launch_bounds__(256, 3) void head32_apply_kernel(
+__global__ __launch_bounds__(256, 4) void head32_apply_kernel(
     const bf16_t* __restrict__ a, const float* __restrict__ Wh, const float* __restrict__ bh,
     const int64_t* __restrict__ labels, const float* __restrict__ gscale,
     const float* __restrict__ stats3, const float* __restrict__ bn4,
@@ -997,14 +1001,15 @@ __global__ __launch_bounds__(256, 3) void head32_apply_kernel(
   constexpr int C = 32;
   // scale | shift | invstd | -mean*invstd | k | m1 | m2 (the BN backward coefficients)
   __shared__ __attribute__((aligned(16))) float sK[7][C];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ Head32W sW[64];                       // the lanes' constant MFMA operands
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // (uniform: scalar step indices)
   const int n = lane & 15, g = lane >> 4;
   // BN groups: group-major workgroups as head32_kernel (bn4 [groups][4][C], coefs [groups][3][C])
   const int Rb = groups > 1 ? (int)gridDim.x / groups : (int)gridDim.x;
   const int grp = groups > 1 ? (int)blockIdx.x / Rb : 0;
   bn4 += (long long)grp * 4 * C;
   coefs += (long long)grp * 3 * C;
-  const Head32W w = head32_weights(Wh, bh, Kreal, lane);
+  if (tid < 64) sW[tid] = head32_weights(Wh, bh, Kreal, lane);
   if (tid < C) {
     sK[0][tid] = bn4[2 * C + tid]; sK[1][tid] = bn4[3 * C + tid];
     sK[2][tid] = bn4[C + tid]; sK[3][tid] = -bn4[tid] * bn4[C + tid];
@@ -1016,11 +1021,11 @@ __global__ __launch_bounds__(256, 3) void head32_apply_kernel(
   const long long steps = groups > 1 ? (long long)(grp + 1) * gsteps : (P + 15) / 16;   // (end step)
   const long long wstride = (long long)Rb * 4;
   const long long s0 = (long long)grp * gsteps + (long long)((int)blockIdx.x - grp * Rb) * 4 + wave;
-  auto load = [&](long long st, uint4& yv, int64_t& lb) __attribute__((always_inline)) {
+  auto load = [&](long long st, uint4& yv, int& lb) __attribute__((always_inline)) {
     const long long px = st * 16 + n;
     const long long pc = px < P ? px : 0;
     yv = *reinterpret_cast<const uint4*>(a + pc * C + 8 * g);
-    lb = labels[pc];
+    lb = reinterpret_cast<const int*>(labels)[2 * pc];
   };
   auto k8 = [&](int r, float (&v)[8]) __attribute__((always_inline)) {
     const float4* kp = reinterpret_cast<const float4*>(&sK[r][0] + opaque_zero() + 8 * g);
@@ -1036,7 +1041,7 @@ __global__ __launch_bounds__(256, 3) void head32_apply_kernel(
     for (int j = 0; j < HEAD32_DA; ++j) {
       const long long s = sb + j * wstride;
       const uint4 yv = q4.y[j];
-      const int lab = (int)q4.l[j];
+      const int lab = q4.l[j];
       if (s + HEAD32_DA * wstride < steps) load(s + HEAD32_DA * wstride, q4.y[j], q4.l[j]);
       if (s >= steps) break;
       const long long px = s * 16 + n;
@@ -1048,7 +1053,7 @@ __global__ __launch_bounds__(256, 3) void head32_apply_kernel(
       int am;
       uint4 pk, fb;
       uint2 bh2, bl2;
-      head32_step<true, false>(yv, lab, valid, w, sc, sh, gs, ignore_index, g, y8, fb, d, bh2, bl2, o8, pk,
+      head32_step<true, false>(yv, lab, valid, sW + opaque_zero() + lane, sc, sh, gs, ignore_index, g, y8, fb, d, bh2, bl2, o8, pk,
                                lse, zy, am);
       float rr[8], o[8], is[8], nm[8], k1[8], m1[8], m2[8];
       unpack8(pk, rr);

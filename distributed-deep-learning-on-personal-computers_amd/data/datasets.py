@@ -176,6 +176,18 @@ class DevicePrefetcher:
         self._launch(k + 1)
         return batch
 
+    def get_last(self, k):
+        """``get(k)`` without starting batch k + 1 (the end of the index list)."""
+        if k not in self.pending:
+            self.pending.clear()
+            self._launch(k)
+        batch, ev = self.pending.pop(k)
+        cur = torch.cuda.current_stream(self.stream.device)
+        cur.wait_event(ev)
+        for t in self._tensors(batch):
+            t.record_stream(cur)
+        return batch
+
 
 # ---------------------------------------------------------------------- synthetic tiles
 def device_indices(idx, device) -> torch.Tensor:
@@ -290,6 +302,11 @@ class SyntheticTiles:
 
     def __len__(self):
         return self.length
+
+    @property
+    def on_device(self) -> bool:
+        """Batches are rendered by a device kernel (``Trainer.fit`` prefetches them)."""
+        return self.device.type == "cuda"
 
     def get(self, idx) -> Tuple[torch.Tensor, torch.Tensor]:
         if self.layout == "engine":
