@@ -80,9 +80,11 @@ def _parse():
                     help="1 GPU: stand-in collective per gradient bucket for a world of N "
                          "(streaming kernel on a third stream; measures launch-to-finish "
                          "latency during backward)")
-    ap.add_argument("--prefetch", type=int, default=1,
+    ap.add_argument("--prefetch", type=int, default=0,
                     help="1: render the next step's on-device batch on a side stream under "
-                         "this step (0: in front of each step)")
+                         "this step (0, default: in front of each step; same box 7980 / 7994 "
+                         "vs 7994 / 8017 img/s — the generator shares HBM with the step either "
+                         "way: profiles/r6/prefetch_proxy_r6i_*)")
     ap.add_argument("--engine-set", default="",
                     help="diagnostic: NAME=INT[,NAME=INT] — set UNetEngine switches (e.g. "
                          "c32_bnp=0) before the first step, for same-box A/B runs")

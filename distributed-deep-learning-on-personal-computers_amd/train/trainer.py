@@ -803,19 +803,8 @@ class Trainer:
             batches = list(self.sampler.batches(c.batch_per_gpu))[self.epoch_step * c.accum_steps:]
             steps_this_epoch = self.epoch_step
             stopped = False
-            # batches rendered / gathered on the device (synthetic generator, HBM-resident
-            # dataset): batch bi + 1 is produced on a side stream under step bi
-            dpf = None
-            if (prefetch is None and self.device.type == "cuda" and c.data_on_device
-                    and getattr(self.train_set, "on_device", False)):
-                from ..data import DevicePrefetcher
-                dpf = DevicePrefetcher(lambda k: self._to_device(*self.train_set.get(batches[k])),
-                                       self.device)
             for bi, idx in enumerate(batches):
-                if dpf is not None:
-                    pending.append(dpf.get(bi) if bi + 1 < len(batches) else dpf.get_last(bi))
-                else:
-                    pending.append(self._to_device(*self.train_set.get(idx)))
+                pending.append(self._to_device(*self.train_set.get(idx)))
                 if prefetch is not None and bi + 1 < len(batches):
                     prefetch(batches[bi + 1])     # next batch's H2D copy overlaps this step
                 if len(pending) < c.accum_steps:
