@@ -38,6 +38,13 @@
 
 #include <cstdlib>
 
+// Timing-decomposition builds only (scripts/build_diag.sh; never the shipped library):
+// 1 = no fragment LDS reads (MFMAs on register operands), 2 = no operand DMA, 4 = no MFMA,
+// 8 = no epilogue stores, 16 = no epilogue of items 0 .. n-2
+#ifndef DDLPC_CONV_DIAG
+#define DDLPC_CONV_DIAG 0
+#endif
+
 namespace ddlpc {
 
 namespace {
@@ -243,7 +250,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     for (int i = 0; i < C::A_ITERS; ++i) {
       const int c8 = c0 + sub8;
       unsigned off = (a_pix[i] >= 0 && c8 < Cs) ? (unsigned)(a_pix[i] * Cs + c8) * 2u : kOOB;
-      dma16(r, sA(buf) + (i * C::NW + wave) * 1024, off);
+      if constexpr (!(DDLPC_CONV_DIAG & 2)) dma16(r, sA(buf) + (i * C::NW + wave) * 1024, off);
     }
   };
   auto issue_B = [&](int k, int chunk_local, int grp, int buf) {
@@ -252,7 +259,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
 #pragma unroll
     for (int i = 0; i < C::B_ITERS; ++i) {
       const bool ok = b_off[i] >= 0 && chunk * BK + sub8 < p.CinW;
-      dma16(rW, sB(buf) + (i * C::NW + wave) * 1024, ok ? (unsigned)(b_off[i] + soff) : kOOB);
+      if constexpr (!(DDLPC_CONV_DIAG & 2)) dma16(rW, sB(buf) + (i * C::NW + wave) * 1024, ok ? (unsigned)(b_off[i] + soff) : kOOB);
     }
   };
   // prologue BN+ReLU applied in LDS on the landed halo (padding stays zero); a_pix holds
@@ -522,7 +529,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         unsigned off = valid && co < p.Cout ? (unsigned)(in1 ? lpix * p.Co1 + co : lpix * Co2 + co - p.Co1) * 2u
                                             : kOOB;
         asm volatile("" : "+v"(off));
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, in1 ? r1 : r2, off, 0, 0);
+        if constexpr (!(DDLPC_CONV_DIAG & 8))
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{q.x, q.y, q.z, q.w}, in1 ? r1 : r2, off, 0, 0);
       }
     }
   };
@@ -546,6 +554,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     constexpr int NS = TT * MT;
     auto xload = [&](int s) __attribute__((always_inline)) {
       const int tt = s / MT, mt = s % MT;
+      if constexpr (DDLPC_CONV_DIAG & 1) return make_uint4(lane, lane + 1, 0u, 0u);
       const char* A = tt < 3 ? A0 : A1;
       if constexpr (XL && DIMS == 2) {
         // off = the kernel row r (XL call sites): halo row wm*MT + mt + r, wm*MT even
@@ -566,6 +575,11 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
     };
     auto wload = [&](int tt, uint4 (&wf)[NT]) __attribute__((always_inline)) {
       const char* B = tt < 3 ? B0 : B1;
+      if constexpr (DDLPC_CONV_DIAG & 1) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) wf[nt] = make_uint4(lane + nt, lane, 0u, 0u);
+        return;
+      }
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
         wf[nt] = lds128(B + lds_off((tt % 3) * BN + wn * (NT * 16) + nt * 16 + (lane & 15), g));
@@ -582,7 +596,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       if (mt == 0 && tt + 1 < TT) wload(tt + 1, wf[(tt + 1) & 1]);
       if (mt == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[tt & 1][nt], xf[s % XD], acc[mt][nt]);
+      for (int nt = 0; nt < NT; ++nt)
+        if constexpr (!(DDLPC_CONV_DIAG & 4)) acc[mt][nt] = mfma16x16x32(wf[tt & 1][nt], xf[s % XD], acc[mt][nt]);
       if (mt == MT - 1) {
         __builtin_amdgcn_s_setprio(0);
         hook(tt);
@@ -689,6 +704,8 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         snap1 = ops;
       }
     }
+    const bool epi_late = NBB == 2 && p.epi_late != 0;
+    int late_st = 0;                                // stores issued after the previous stage's DMA
     for (int s = 0; s < S; ++s) {
       const int k = s / spi, rem = s % spi;
       const int chunk = rem / NG, grp = rem % NG;
@@ -696,9 +713,13 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       const bool more_chunks = cseq + 1 < my_items * nchunks;
       if (NBB == 2) {
         // stage s needs B(s) (issued during s-1) and, at grp 0, A(cseq).  At grp 1 the next
-        // chunk's halo (issued after B(s) during s-1) may stay in flight.
-        if (NG > 1 && grp == 1 && more_chunks) dma_wait<C::A_ITERS>();
+        // chunk's halo (issued after B(s) during s-1) may stay in flight.  epi_late: the
+        // previous item's epilogue stores were issued after that stage's DMA and may stay in
+        // flight one more stage
+        if (late_st > 0) vm_wait_dyn((NG > 1 && grp == 1 && more_chunks ? C::A_ITERS : 0) + late_st);
+        else if (NG > 1 && grp == 1 && more_chunks) dma_wait<C::A_ITERS>();
         else dma_wait<0>();
+        late_st = 0;
       } else {
         // A(cseq) was issued before B(s) (at the previous chunk's first stage or the prologue)
         vm_wait_dyn(ops - snap0);
@@ -709,7 +730,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
       lds_sync();
       // the previous item's epilogue runs here, BEFORE this stage's DMA is issued, so its
       // stores drain under this stage's compute (vmcnt retires in order)
-      if (rem == 0 && s > 0) { epilogue(k - 1); ops += EPI_STORES; }
+      if (rem == 0 && s > 0 && !epi_late) {
+        if constexpr (!(DDLPC_CONV_DIAG & 16)) epilogue(k - 1);
+        ops += EPI_STORES;
+      }
       const int sn = s + NBB - 1;                     // stage whose weights are issued now
       int snapn = 0;
       if (sn < S) {
@@ -723,6 +747,10 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 1) void conv3_fwd_
         const int k1 = (cseq + 1) / nchunks;
         issue_A(k1, (cseq + 1) % nchunks, (cseq + 1) & 1);
         ops += C::A_ITERS;
+      }
+      if (rem == 0 && s > 0 && epi_late) {
+        if constexpr (!(DDLPC_CONV_DIAG & 16)) epilogue(k - 1);
+        late_st = EPI_STORES;
       }
       // BNB: the item's last stage loads y for its epilogue (next stage: grp 0, full wait)
       if (BNB && KS == 1 && rem == spi - 1) issue_Y(k);
