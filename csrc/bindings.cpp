@@ -83,7 +83,7 @@ int pick_bn(int Cout) {
 // (bench.py --ab, scripts/conv_micro.py --ab) can never silently time two identical
 // configurations.  An empty list = no experiment in progress.
 namespace {
-const char* const kKnobs[] = {"CONV_EPI_LATE"};
+const char* const kKnobs[] = {""};
 bool knob_registered(const std::string& name) {
   for (const char* k : kKnobs)
     if (k[0] != 0 && name == k) return true;
@@ -339,7 +339,6 @@ std::vector<at::Tensor> conv3_fwd(const at::Tensor& x1, const c10::optional<at::
   if (a.Co1 < a.Cout) y2 = at::empty(shape_with_c(g, a.Cout - a.Co1), opts);
   at::Tensor stats;
   a.persist_blocks = (cfg >= 4 ? 1 : 2) * num_cus();   // cfg >= 4: one 8-wave workgroup per CU
-  a.epi_late = knob("CONV_EPI_LATE", 0);
   // small layers: split the input-channel chunks across workgroups so the grid fills the
   // chip; partial sums go through an fp32 buffer and a deterministic finalize
   const int nchunks_total = (a.Cin + 31) / 32;

@@ -38,7 +38,6 @@ struct ConvFwdArgs {
   int tilesD, tilesH, tilesW;
   int nTilesM, nTilesN;
   int persist_blocks;             // grid cap (persistent workgroups); 0 = one per item
-  int epi_late;                   // (A/B, knob CONV_EPI_LATE) epilogue stores after the stage's DMA
   int stat_rows;                  // out: rows written to `stats` (one per workgroup)
   int ksplit;                     // >1: split the channel chunks, fp32 partials to `part`
   float* part;                    // [ksplit][npix][Cout] fp32 (ksplit > 1)
