@@ -29,12 +29,29 @@ def main():
     bdir = os.path.join(os.path.dirname(be.BUILD), "diag")
     os.makedirs(out_dir, exist_ok=True)
     os.makedirs(bdir, exist_ok=True)
-    objs = [o for o in sorted(glob.glob(os.path.join(be.BUILD, "*.o")))
-            if not os.path.basename(o).startswith("conv3x3_fwd.")]
+    # a variant is "MODE" (conv3x3_fwd.hip with -DDDLPC_CONV_DIAG=MODE) or "unit.hip:MACRO=V[:TAG]"
+    # (any unit with one macro, e.g. head_ce.hip:HEAD32_OCC=3) or "unit.hip@REV" (the unit as
+    # of git revision REV: the same-box A/B baseline)
     for mode in sys.argv[1:]:
-        obj = os.path.join(bdir, f"conv3x3_fwd_diag{mode}.o")
-        be.compile_one(os.path.join(be.CSRC, "conv3x3_fwd.hip"), obj, common + [f"-DDDLPC_CONV_DIAG={mode}"])
-        lib = os.path.join(out_dir, f"libddlpc_diag_{mode}.so")
+        if "@" in mode:
+            unit, rev = mode.split("@")
+            src = os.path.join(bdir, f"{rev}_{unit}")
+            with open(src, "w") as f:
+                f.write(subprocess.run(["git", "show", f"{rev}:csrc/{unit}"], cwd=be.ROOT, check=True,
+                                       capture_output=True, text=True).stdout)
+            defs, tag = [], f"{unit.split('.')[0]}_{rev}"
+        elif ":" in mode:
+            unit, macro = mode.split(":")[:2]
+            src = os.path.join(be.CSRC, unit)
+            defs, tag = [f"-D{macro}"], f"{unit.split('.')[0]}_{macro.replace('=', '')}"
+        else:
+            unit, src = "conv3x3_fwd.hip", os.path.join(be.CSRC, "conv3x3_fwd.hip")
+            defs, tag = [f"-DDDLPC_CONV_DIAG={mode}"], mode
+        objs = [o for o in sorted(glob.glob(os.path.join(be.BUILD, "*.o")))
+                if not os.path.basename(o).startswith(unit + ".")]
+        obj = os.path.join(bdir, f"{tag}.o")
+        be.compile_one(src, obj, common + defs)
+        lib = os.path.join(out_dir, f"libddlpc_diag_{tag}.so")
         cmd = [be.HIPCC, "-shared", "-fPIC", f"--offload-arch={be.ARCH}", "-o", lib] + objs + [obj] + [
             "-L", libdir, "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch",
             f"-Wl,-rpath,{libdir}"]
