@@ -788,6 +788,7 @@ class UNetEngine:
         # 256^2 x 128 but measured ~1.2% slower end to end (docs/PERF.md), so opt-in
         # (tests/test_unet_gpu.py::test_deferred_skips_match_materialised_engine runs both)
         self.defer_skip = False
+        self.defer_skip_max_level = 99          # (with defer_skip: only levels <= this one)
         # BN1 backward's reduction pass fused into the epilogue of the data gradient that
         # produces its input gradient (2-D; False: separate reduction kernel)
         self.bnb_epilogue = True
@@ -1056,7 +1057,7 @@ class UNetEngine:
             ub, _pack, dblk = self.dec[len(self.dec) - 1 - lvl]
             c_up = dblk.conv1.weight.shape[1] - blk.conv2.weight.shape[0]
             c_skip = blk.conv2.weight.shape[0]
-            ok = (w >> lvl) >= 16 and c_up % 32 == 0 and c_up + c_skip <= 512
+            ok = (w >> lvl) >= 16 and c_up % 32 == 0 and c_up + c_skip <= 512 and lvl <= self.defer_skip_max_level
             out.append(bool(ok))
         return out
 
