@@ -276,24 +276,27 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs p) {
 // one-tile-per-workgroup form spent half of the 32^2 -> 64^2 x 256-channel up-sampling in
 // its store tail: 165 us without stores, 347 us with them).
 // Requires Cin % 32 == 0, (S*Cout) % 128 == 0, Cout % 32 == 0 and Cout <= 512 (launcher-checked).
-template <int KS>
+template <int KS, int BN_ = 128>
 struct Nt2Cfg {
-  static constexpr int BM = 256, BN = 128;
+  static constexpr int BM = 256, BN = BN_;
   static constexpr int A_BYTES = KS * BM * 64, B_BYTES = KS * BN * 64;
   static constexpr int STAGE = A_BYTES + B_BYTES;
   // ring depth: 3 at KS = 1 (76 KB: still two workgroups per CU), so the DMA of stage s + 2
   // is in flight during two stages' MFMAs instead of one
   static constexpr int NS = KS == 1 ? 3 : 2;
   static constexpr int SS_BYTES = 2 * 512 * 4;                   // BN scale | shift
-  static constexpr int SMEM = SS_BYTES + NS * STAGE;             // 76 KB at KS = 1
+  static constexpr int SMEM = SS_BYTES + NS * STAGE;             // 76 KB at KS = 1 (BN 256: 100 KB)
   static constexpr int A_IT = KS * BM * 4 / 512;                 // DMA pieces per thread
   static constexpr int B_IT = KS * BN * 4 / 512;
 };
 
-template <int KS>
-__global__ __launch_bounds__(512, KS == 1 ? 2 : 1) void gemm_nt_fwd2_kernel(GemmArgs p) {
-  using C = Nt2Cfg<KS>;
+// BN 256 (one workgroup per CU, waves of 64 x 128): each A tile is read from L2 half as often
+template <int KS, int BN_ = 128>
+__global__ __launch_bounds__(512, KS == 1 && BN_ == 128 ? 2 : 1) void gemm_nt_fwd2_kernel(GemmArgs p) {
+  using C = Nt2Cfg<KS, BN_>;
   constexpr int BM = C::BM, BN = C::BN;
+  constexpr int NTW = BN / 32;                                    // 16-column tiles per wave
+  constexpr int NPW = BN / 64;                                    // 32-column pairs per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* s_bn = reinterpret_cast<float*>(smem);                   // scale [512] | shift [512]
   char* base = smem + C::SS_BYTES;
@@ -323,10 +326,10 @@ __global__ __launch_bounds__(512, KS == 1 ? 2 : 1) void gemm_nt_fwd2_kernel(Gemm
   const auto rB = convlds::make_rsrc(p.B + (long long)n0 * p.K, (unsigned)((long long)BN * p.K * 2));
   // bias of this lane's output columns, loaded once before any DMA is in flight (a load in the
   // epilogue would make the compiler wait vmcnt(0) on the ring's DMAs)
-  float bias_r[2][8];
+  float bias_r[NPW][8];
 #pragma unroll
-  for (int np = 0; np < 2; ++np) {
-    const int c0 = n0 + wn * 64 + np * 32, cob = c0 % p.Cout;
+  for (int np = 0; np < NPW; ++np) {
+    const int c0 = n0 + wn * (BN / 2) + np * 32, cob = c0 % p.Cout;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       bias_r[np][i] = p.bias != nullptr ? p.bias[cob + 4 * (lane >> 4) + i] : 0.f;
@@ -376,32 +379,32 @@ __global__ __launch_bounds__(512, KS == 1 ? 2 : 1) void gemm_nt_fwd2_kernel(Gemm
     }
   };
   const int g = lane >> 4;
-  f32x4_t acc[4][4];
+  f32x4_t acc[4][NTW];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   auto compute = [&](const char* __restrict__ A, const char* __restrict__ B) __attribute__((always_inline)) {
 #pragma unroll
     for (int sc = 0; sc < KS; ++sc) {
-      uint4 af[4], bf[4];
+      uint4 af[4], bf[NTW];
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
         af[mt] = *reinterpret_cast<const uint4*>(A + sc * BM * 64 + lds_off(wm * 64 + mt * 16 + (lane & 15), g));
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        bf[nt] = *reinterpret_cast<const uint4*>(B + sc * BN * 64 + lds_off(wn * 64 + nt * 16 + (lane & 15), g));
+      for (int nt = 0; nt < NTW; ++nt)
+        bf[nt] = *reinterpret_cast<const uint4*>(B + sc * BN * 64 + lds_off(wn * (BN / 2) + nt * 16 + (lane & 15), g));
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16x16x32(bf[nt], af[mt], acc[mt][nt]);
+        for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = mfma16x16x32(bf[nt], af[mt], acc[mt][nt]);
     }
   };
   // ---- epilogue of tile (m0, n0): lane holds columns n0 + wn*64 + nt*16 + 4g .. +3 of pixel
   // wm*64 + mt*16 + (lane & 15); paired into 16-B stores at the pixel-shuffled output position
   // (+ bias).  Exactly EPI buffer stores per wave (rows past M: out-of-range offset), so the
   // counted waits of the next tile's stages stay exact while they drain
-  constexpr int EPI = 8;                                          // 2 column pairs x 4 m tiles
+  constexpr int EPI = 4 * NPW;                                    // column pairs x 4 m tiles
   auto epilogue = [&](int m0) __attribute__((always_inline)) {
     const int m_last = min(m0 + BM, p.M) - 1;
     const long long up_lo = up_pixel(m0, 0, p.dims, p.D, p.H, p.W);
@@ -415,8 +418,8 @@ __global__ __launch_bounds__(512, KS == 1 ? 2 : 1) void gemm_nt_fwd2_kernel(Gemm
       upr[mt] = m < p.M ? (int)(up_pixel(m, 0, p.dims, p.D, p.H, p.W) - up_lo) : -1;
     }
 #pragma unroll
-    for (int np = 0; np < 2; ++np) {
-      const int c0 = n0 + wn * 64 + np * 32;                      // 32 columns in one sub-position
+    for (int np = 0; np < NPW; ++np) {
+      const int c0 = n0 + wn * (BN / 2) + np * 32;                // 32 columns in one sub-position
       const int sub = c0 / p.Cout, cob = c0 - sub * p.Cout;
       const int soff = p.dims == 2 ? (sub >> 1) * 2 * p.W + (sub & 1)
                                    : (sub >> 2) * 4 * p.H * p.W + ((sub >> 1) & 1) * 2 * p.W + (sub & 1);
@@ -437,7 +440,7 @@ __global__ __launch_bounds__(512, KS == 1 ? 2 : 1) void gemm_nt_fwd2_kernel(Gemm
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   };
   if (bn) __syncthreads();                                        // s_bn visible
   constexpr int NS = C::NS, PER = C::A_IT + C::B_IT;             // DMAs per thread per stage
@@ -1318,13 +1321,23 @@ void gemm_launch(GemmArgs& a, hipStream_t st) {
   // uses 128-wide N tiles when N allows (each A tile is read from L2 half as often)
   if (gemm_nt_fwd2_mode(a)) {
     // persistent: 8 XCDs x R slots per column tile x nTilesN column tiles, about two
-    // workgroups per CU (76 KB of LDS each), R no larger than the m tiles need
-    const int ntn = a.N / 128;
+    // workgroups per CU (76 KB of LDS each; BN 256: one of 100 KB), R no larger than the m
+    // tiles need
+    // (BN 256 where the m tiles fill the chip: 32^2 -> 64^2 x 256 channels 450 -> 361 us,
+    // 16^2 -> 32^2 93 -> 85 us at batch 384; 8^2 -> 16^2 (24k pixels) 29 -> 33 us, so not
+    // there — profiles/r6/convt_fwd_bn256_r6t/)
+    const bool w256 = a.N % 256 == 0 && a.M >= 65536;
+    const int bnt = w256 ? 256 : 128;
+    const int ntn = a.N / bnt;
     const long long mt = (a.M + 255) / 256;
     const long long rneed = (mt + 7) / 8;
-    const int R = (int)std::max<long long>(1, std::min<long long>(rneed, 2LL * device_cus() / (8 * ntn)));
+    const int per_cu = w256 ? 1 : 2;
+    const int R = (int)std::max<long long>(1, std::min<long long>(rneed, (long long)per_cu * device_cus() / (8 * ntn)));
     const unsigned grid2 = (unsigned)(8 * R * ntn);
-    hipLaunchKernelGGL((gemm_nt_fwd2_kernel<1>), dim3(grid2), dim3(512), Nt2Cfg<1>::SMEM, st, a);
+    if (w256)
+      hipLaunchKernelGGL((gemm_nt_fwd2_kernel<1, 256>), dim3(grid2), dim3(512), (Nt2Cfg<1, 256>::SMEM), st, a);
+    else
+      hipLaunchKernelGGL((gemm_nt_fwd2_kernel<1>), dim3(grid2), dim3(512), Nt2Cfg<1>::SMEM, st, a);
     return;
   }
   if (gemm_nt_dgrad2_ok(a)) {

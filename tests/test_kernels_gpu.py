@@ -399,11 +399,13 @@ def test_convt(ops, N, H, W, Cin, Cout):
     assert rel_err(db, gb) < 1e-3
 
 
-@pytest.mark.parametrize("N,H,Cin,Cout", [(9, 60, 256, 256), (4, 36, 512, 128), (3, 52, 256, 512)])
+@pytest.mark.parametrize("N,H,Cin,Cout", [(9, 60, 256, 256), (4, 36, 512, 128), (3, 52, 256, 512),
+                                           (20, 60, 256, 256), (17, 64, 256, 512)])
 def test_convt_fwd_persistent_gemm(ops, N, H, Cin, Cout):
     """The persistent XCD-aware forward GEMM (gemm_nt_fwd2_kernel: shapes the resident convT
     kernel declines, Cin 256 / 512): several m tiles per workgroup, so epilogue stores drain
-    under the next tile's DMA stages; a partial last m tile; plain and deferred-BN input."""
+    under the next tile's DMA stages; a partial last m tile; plain and deferred-BN input.
+    The last two shapes (>= 65536 input pixels, 4 Cout % 256 == 0) take the 256-column tiles."""
     torch.manual_seed(12)
     x = torch.randn(N, Cin, H, H, device=DEV).bfloat16()
     w = torch.randn(Cin, Cout, 2, 2, device=DEV) / math.sqrt(Cin)
