@@ -868,13 +868,17 @@ __global__ __launch_bounds__(256, 4) void head32_kernel(
   for (long long sb = s0; sb < steps; sb += HEAD32_D * wstride) {   // wave-uniform trip count
 #pragma unroll
     for (int j = 0; j < HEAD32_D; ++j) {
+      // branch-free steps (a step past the end is masked) whose slot is refilled only after
+      // its last use (end of the step, clamped address): the loaded registers are then the
+      // loop-carried ones.  With the load issued before the step and guarded by a branch, the
+      // compiler rotated the slots with register copies at the loop back edge — each copy of
+      // a register with a load in flight a vmcnt(0), i.e. the whole prefetch drained once per
+      // HEAD32_D steps
       const long long s = sb + j * wstride;
       const uint4 yv = q4.y[j];
       const int lab = q4.l[j];
-      if (s + HEAD32_D * wstride < steps) load(s + HEAD32_D * wstride, q4.y[j], q4.l[j]);
-      if (s >= steps) break;                           // wave-uniform
       const long long px = s * 16 + n;
-      const bool valid = px < P;
+      const bool valid = s < steps && px < P;
       float sc[8], sh[8];
       if (DEFER) {
         const float4* kp = reinterpret_cast<const float4*>(&sK[0][0] + opaque_zero() + 8 * g);
@@ -942,6 +946,8 @@ __global__ __launch_bounds__(256, 4) void head32_kernel(
           b1[jj] = s1.x; b1[jj + 1] = s1.y; b2[jj] = s2.x; b2[jj + 1] = s2.y;
         }
       }
+      const long long sl = s + HEAD32_D * wstride;
+      load(sl < steps ? sl : s0, q4.y[j], q4.l[j]);
     }
   }
   // ---- workgroup reduction (fixed order): dWh^T of each wave to its LDS tile (lane: class
@@ -1039,13 +1045,12 @@ __global__ __launch_bounds__(256, 4) void head32_apply_kernel(
   for (long long sb = s0; sb < steps; sb += HEAD32_DA * wstride) {
 #pragma unroll
     for (int j = 0; j < HEAD32_DA; ++j) {
+      // (branch-free, slot refilled after its last use: see head32_kernel)
       const long long s = sb + j * wstride;
       const uint4 yv = q4.y[j];
       const int lab = q4.l[j];
-      if (s + HEAD32_DA * wstride < steps) load(s + HEAD32_DA * wstride, q4.y[j], q4.l[j]);
-      if (s >= steps) break;
       const long long px = s * 16 + n;
-      const bool valid = px < P;
+      const bool valid = s < steps && px < P;
       float sc[8], sh[8];
       k8(0, sc);
       k8(1, sh);
@@ -1066,6 +1071,8 @@ __global__ __launch_bounds__(256, 4) void head32_apply_kernel(
         o[jj] = k1[jj] * (dyh - m1[jj] - xh * m2[jj]);
       }
       if (valid) *reinterpret_cast<uint4*>(dY + px * C + 8 * g) = pack8(o);
+      const long long sl = s + HEAD32_DA * wstride;
+      load(sl < steps ? sl : s0, q4.y[j], q4.l[j]);
     }
   }
 }
