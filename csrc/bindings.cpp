@@ -490,7 +490,8 @@ at::Tensor conv3_wgrad(const at::Tensor& dy, const at::Tensor& x1,
   // gradient chain, and its resident workgroups decide what else fits on a CU.  Round 2
   // (other kernels): two, 1 / 3 / 4 -7 / -1.5 / -1.9%; round 5, same box, three interleaved
   // runs each: 1 / 2 / 3 / 4 -> 7508 / 7610-7613 / 7628 / 7611 img/s, window and 3-D within
-  // noise (profiles/r5/wgrad_wg_per_cu_g71_g72/): three
+  // noise (profiles/r5/wgrad_wg_per_cu_g71_g72/): three; re-checked at batch 384 (round 6,
+  // bench --ab, two calls): 2 / 4 -> +0.5-0.6% / +0.9-1.0% ms per step (profiles/r6/wgrad_wg_per_cu_b384_r6ac/)
   constexpr int wg_per_cu = 3;
   const int target = wg_per_cu * num_cus();
   int splits = std::max(1, (target + base - 1) / base);
