@@ -189,7 +189,7 @@ def test_conv3_dgrad_resident(ops, C1, C2, Cout):
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [
     (2, 256, 256, 32, 32), (2, 256, 256, 64, 64), (3, 200, 232, 32, 32),
     (16, 64, 64, 128, 128), (16, 64, 64, 128, 96), (2, 16, 16, 32, 32), (2, 32, 32, 64, 64),
-    (1, 16, 16, 128, 128), (2, 8, 8, 256, 256)])
+    (1, 16, 16, 128, 128), (2, 8, 8, 256, 256), (48, 64, 64, 128, 128)])
 def test_conv3_dgrad_bn_backward_epilogue(ops, N, H, W, Cin, Cout):
     torch.manual_seed(11)
     w = torch.randn(Cout, Cin, 3, 3, device=DEV) / math.sqrt(9 * Cin)
