@@ -81,7 +81,8 @@ def test_conv3_fwd(ops, N, H, W, C1, C2, Cout):
 # split data-gradient output
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout,pro,co1", [
     (32, 64, 64, 128, 0, 128, True, 0), (32, 64, 64, 256, 128, 128, False, 0),
-    (64, 32, 32, 256, 0, 256, True, 0), (64, 32, 32, 128, 0, 384, False, 256)])
+    (64, 32, 32, 256, 0, 256, True, 0), (64, 32, 32, 128, 0, 384, False, 256),
+    (8, 128, 128, 128, 64, 64, True, 0)])
 def test_conv3_fwd_bigtile(ops, N, H, W, C1, C2, Cout, pro, co1):
     torch.manual_seed(5)
     x1 = torch.randn(N, C1, H, W, device=DEV).bfloat16()
@@ -189,7 +190,7 @@ def test_conv3_dgrad_resident(ops, C1, C2, Cout):
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [
     (2, 256, 256, 32, 32), (2, 256, 256, 64, 64), (3, 200, 232, 32, 32),
     (16, 64, 64, 128, 128), (16, 64, 64, 128, 96), (2, 16, 16, 32, 32), (2, 32, 32, 64, 64),
-    (1, 16, 16, 128, 128), (2, 8, 8, 256, 256), (48, 64, 64, 128, 128)])
+    (1, 16, 16, 128, 128), (2, 8, 8, 256, 256), (48, 64, 64, 128, 128), (8, 128, 128, 64, 128)])
 def test_conv3_dgrad_bn_backward_epilogue(ops, N, H, W, Cin, Cout):
     torch.manual_seed(11)
     w = torch.randn(Cout, Cin, 3, 3, device=DEV) / math.sqrt(9 * Cin)
