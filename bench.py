@@ -164,8 +164,6 @@ def main():
                 print(f"alive {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
         threading.Thread(target=_beat, daemon=True).start()
 
-    if args.impl == "hip" and not torch.cuda.is_available():
-        args.impl = "torch"            # CPU rehearsal (gloo): stock ops, same contract
     from ddlpc.config import ModelConfig, TrainConfig
     from ddlpc.data import device_random_batch
     from ddlpc.train.trainer import Trainer
@@ -192,7 +190,7 @@ def main():
     assert world == args.gpus, (world, args.gpus)
     device = tr.device
     B = args.batch
-    on_device_data = tr.impl == "hip" and dev == "cuda"
+    on_device_data = tr.impl == "hip"     # (rendered by the synth_tiles op, GPU or CPU kernel)
     pool = []
     if not on_device_data:
         # stock-op baseline / CPU: a small pre-rendered pool (the baseline's published

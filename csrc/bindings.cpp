@@ -1,6 +1,7 @@
 // PyTorch operator registration for the gfx950 kernel library: TORCH_LIBRARY(ddlpc, ...)
-// exposes every kernel as torch.ops.ddlpc.<name> (CUDA/HIP dispatch key only: no CPU
-// fallback is registered, so a CPU tensor reaching these ops fails loudly).
+// declares every operator as torch.ops.ddlpc.<name>; TORCH_LIBRARY_IMPL(ddlpc, CUDA) below
+// registers the HIP kernels, and csrc/cpu_ref.cpp registers the C++ reference kernels under
+// the CPU key (the dispatcher picks by tensor device).
 //
 // Tensor conventions: activations are channel-last tensors whose SHAPE is [N, (D,) H, W, C]
 // (contiguous), bf16.  Parameters are fp32 in standard PyTorch layouts; packed bf16 weight

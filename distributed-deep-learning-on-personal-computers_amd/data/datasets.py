@@ -282,10 +282,11 @@ class SyntheticTiles:
     ``(seed, i)``.  2-D tiles (``dims=2``: [N,C,T,T]) or 3-D volumes (``dims=3``).
     ``device``/``layout`` select where and how a batch is produced:
 
-    * CPU (default): float32 NCHW via ``render_synthetic``;
-    * a GPU with ``layout="engine"``: one ``synth_tiles`` HIP kernel writes the HIP engine's
-      input (channel-last bf16, 8 channels) into HBM — see ``engine_input``;
-    * a GPU with ``layout="nchw"``: the PyTorch twin on the device (stock-op baseline).
+    * ``layout="nchw"`` (default): float32 NCHW via ``render_synthetic``, the PyTorch twin
+      (stock-op path), on the CPU or a GPU;
+    * ``layout="engine"``: one ``synth_tiles`` operator call writes the engine's input
+      (channel-last bf16, 8 channels) — the HIP kernel into HBM on a GPU, its C++ twin
+      (csrc/cpu_ref.cpp, the same bits) on the CPU; see ``engine_input``.
     """
 
     def __init__(self, length: int, tile: int, classes: int = 6, in_channels: int = 3,
@@ -297,7 +298,7 @@ class SyntheticTiles:
         self.in_channels, self.seed, self.dims = in_channels, seed, dims
         self.grid, self.noise = max(1, min(grid, tile)), noise
         self.device = torch.device(device) if device is not None else torch.device("cpu")
-        self.layout = layout if self.device.type == "cuda" else "nchw"
+        self.layout = layout
         self.palette = synthetic_palette(classes, in_channels).to(self.device)
 
     def __len__(self):

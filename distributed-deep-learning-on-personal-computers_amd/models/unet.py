@@ -145,7 +145,7 @@ class UNet(nn.Module):
 
     # ------------------------------------------------------------------ execution
     def forward(self, x):
-        if self._engine is not None and x.is_cuda:
+        if self._engine is not None:
             return self._engine.forward(x)
         return self.forward_torch(x)
 
@@ -163,7 +163,7 @@ class UNet(nn.Module):
         """Mean cross-entropy (nn.CrossEntropyLoss defaults, ref.py:703) and the number of
         correctly classified pixels (ref.py:775).  The HIP path fuses the 1x1 head,
         softmax, CE, its gradient and the arg-max into one kernel (logits never hit HBM)."""
-        if self._engine is not None and x.is_cuda:
+        if self._engine is not None:
             return self._engine.loss_and_correct(x, y)
         logits = self.forward_torch(x)
         loss = F.cross_entropy(logits.float(), y, ignore_index=ignore_index)

@@ -2,9 +2,10 @@
 
 The library is built by ``__graft_entry__.build()`` / ``python scripts/build_ext.py`` with
 ``hipcc --offload-arch=gfx950`` and registers its operators with ``TORCH_LIBRARY(ddlpc)``
-so they appear as ``torch.ops.ddlpc.*`` (and by kernel name in rocprof).  Nothing here
-falls back silently: requesting the ops on a machine with a GPU but without the built
-library raises.
+so they appear as ``torch.ops.ddlpc.*`` (and by kernel name in rocprof): one op namespace,
+two kernels per operator — the gfx950 HIP kernel for GPU tensors and the C++ reference of
+``csrc/cpu_ref.cpp`` for CPU tensors, chosen by PyTorch's dispatcher.  Nothing here falls
+back silently: requesting the ops without the built library raises.
 """
 from __future__ import annotations
 

@@ -742,8 +742,9 @@ class UNetEngine:
         check_supported(model)
         self.model = model
         dev = next(model.parameters()).device
-        if dev.type != "cuda":
-            raise RuntimeError("UNetEngine needs the model on the GPU")
+        # (any device: torch.ops.ddlpc dispatches to the gfx950 kernels for GPU tensors and
+        # to the C++ reference kernels of csrc/cpu_ref.cpp for CPU tensors)
+        cuda = dev.type == "cuda"
         # direct_grads: kernels accumulate straight into the (flat) .grad buffers and report
         # readiness through ``grad_ready`` (the DP reducer's bucket trigger) instead of
         # returning gradients for autograd to add.  Enabled by the Trainer once parameters
@@ -757,7 +758,7 @@ class UNetEngine:
         use_side = os.environ.get("DDLPC_WGRAD_STREAM", "1") != "0"
         # (stream priorities measured within +-0.3%: a plain stream,
         # profiles/r5/rows_sum_4wave_g66/)
-        self.side = torch.cuda.Stream(dev) if use_side else None
+        self.side = torch.cuda.Stream(dev) if (use_side and cuda) else None
         self._side_stream = self.side
         self._side_used = False
         # memory the side stream's lag may hold back (see ``wgrad_stream``): default 6% of
@@ -765,7 +766,8 @@ class UNetEngine:
         # did not; 256^2 x 128 never reaches it), DDLPC_SIDE_LAG_GB overrides
         lag_gb = os.environ.get("DDLPC_SIDE_LAG_GB")
         self.side_lag_bytes = (int(float(lag_gb) * 2**30) if lag_gb else
-                               int(0.06 * torch.cuda.get_device_properties(dev).total_memory))
+                               int(0.06 * torch.cuda.get_device_properties(dev).total_memory)
+                               if cuda else 0)
         self._lag: List[Tuple[torch.cuda.Event, int]] = []
         self._lag_bytes = 0
         self.lag_waits = 0
@@ -916,8 +918,9 @@ class UNetEngine:
     def set_side_stream(self, enabled: bool):
         """Switch the weight-gradient side stream on/off between steps (see
         ``Trainer.choose_schedule``)."""
-        if enabled and self._side_stream is None:
-            self._side_stream = torch.cuda.Stream(next(self.model.parameters()).device)
+        dev = next(self.model.parameters()).device
+        if enabled and self._side_stream is None and dev.type == "cuda":
+            self._side_stream = torch.cuda.Stream(dev)
         self.join()
         self.side = self._side_stream if enabled else None
 

@@ -41,12 +41,12 @@ from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
 
 
 def resolve_impl(impl: str, device: torch.device, dtype: str = "bf16") -> str:
-    """``auto``: the HIP kernels on a GPU for bf16 compute; stock ops for fp32 compute (the
-    reference's precision) or on a CPU.  ``hip`` with fp32 is rejected by the config."""
-    if device.type != "cuda":
-        if impl == "hip":
-            raise RuntimeError("impl='hip' needs a GPU")
-        return "torch"
+    """``auto``: the operator engine for bf16 compute, stock ``nn`` modules for fp32 compute
+    (the reference's precision, ref.py:702-704).  The choice is the compute precision, not
+    the device: the engine's ``torch.ops.ddlpc`` operators dispatch by tensor device
+    (gfx950 kernels for GPU tensors, the C++ reference kernels of ``csrc/cpu_ref.cpp`` for
+    CPU tensors).  ``hip`` with fp32 is rejected by the config."""
+    del device
     if impl == "auto":
         return "hip" if dtype == "bf16" else "torch"
     if impl == "hip" and dtype != "bf16":

@@ -54,7 +54,7 @@ class DeviceMeter:
     def add(self, loss: torch.Tensor, correct: torch.Tensor, pixels: int, n: int = 1):
         # [sum loss, sum correct, sum pixels, micro-batches]; no host->device copies per step.
         # n > 1: a batched window of n micro-batches whose mean per-micro-batch loss is `loss`
-        if (self.buf.is_cuda and loss.dtype == torch.float32 and correct.dtype == torch.float32
+        if (loss.dtype == torch.float32 and correct.dtype == torch.float32
                 and loss.numel() == 1 and correct.numel() == 1 and _hip_ops() is not None):
             # one launch instead of five small elementwise kernels
             _hip_ops().meter_add(self.buf, loss.detach(), correct.detach(), float(pixels), float(n))

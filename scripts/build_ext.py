@@ -52,14 +52,18 @@ def build(verbose=False, jobs=None, force=False):
         common += ["-isystem", d]
     headers = glob.glob(os.path.join(CSRC, "*.h"))
     hdr_mtime = max((os.path.getmtime(h) for h in headers), default=0)
-    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip"))) + [os.path.join(CSRC, "bindings.cpp")]
+    # bindings.cpp: host code with HIP launches; cpu_ref.cpp: the CPU kernels (plain C++)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip"))) + [os.path.join(CSRC, "bindings.cpp"),
+                                                             os.path.join(CSRC, "cpu_ref.cpp")]
     todo, objs = [], []
     for s in srcs:
         o = os.path.join(BUILD, os.path.basename(s) + ".o")
         objs.append(o)
         if force or not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), hdr_mtime):
             flags = list(common)
-            if s.endswith(".cpp"):
+            if s.endswith("cpu_ref.cpp"):
+                flags = ["-x", "c++"] + [f for f in flags if not f.startswith("--offload-arch")]
+            elif s.endswith(".cpp"):
                 flags = ["-x", "hip"] + flags
             todo.append((s, o, flags))
     jobs = jobs or min(len(todo) or 1, int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)

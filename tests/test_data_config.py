@@ -100,7 +100,10 @@ def test_config_precision_is_honest():
     gpu = torch.device("cuda", 0)
     assert resolve_impl("auto", gpu, "fp32") == "torch"
     assert resolve_impl("auto", gpu, "bf16") == "hip"
-    assert resolve_impl("auto", torch.device("cpu"), "bf16") == "torch"
+    # the precision picks the path, not the device: the engine's operators dispatch by
+    # tensor device (CPU kernels: csrc/cpu_ref.cpp)
+    assert resolve_impl("auto", torch.device("cpu"), "bf16") == "hip"
+    assert resolve_impl("auto", torch.device("cpu"), "fp32") == "torch"
 
 
 def test_resume_missing_explicit_checkpoint_raises(tmp_path):

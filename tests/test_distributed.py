@@ -77,7 +77,7 @@ def _train_ranks(rank, world, accum, codec):
     from ddlpc.config import ModelConfig, TrainConfig
     from ddlpc.parallel import params_checksum
     from ddlpc.train.trainer import Trainer
-    cfg = TrainConfig(model=ModelConfig(out_classes=2, depth=3, width_divisor=16), tile=32,
+    cfg = TrainConfig(model=ModelConfig(out_classes=2, depth=3, width_divisor=16), tile=32, dtype="fp32",
                       num_samples=12, test_holdout=4, batch_per_gpu=2, accum_steps=accum,
                       epochs=2, check_consistency_every=1, bucket_mb=0.05, grad_codec=codec,
                       log_every=0, timeout_s=60)
@@ -118,7 +118,7 @@ def _fault(rank, world):
     from ddlpc.config import ModelConfig, TrainConfig
     from ddlpc.data import SyntheticTiles
     from ddlpc.train.trainer import Trainer
-    cfg = TrainConfig(model=ModelConfig(out_classes=2, depth=2, width_divisor=16), tile=16,
+    cfg = TrainConfig(model=ModelConfig(out_classes=2, depth=2, width_divisor=16), tile=16, dtype="fp32",
                       num_samples=8, test_holdout=0, batch_per_gpu=1, timeout_s=20)
     tr = Trainer(cfg, device="cpu")
     x, y = SyntheticTiles(4, 16, classes=2).get([0])
@@ -166,7 +166,7 @@ def test_fresh_reducer_is_disarmed():
 def _resume_missing(rank, world, tmp):
     from ddlpc.config import ModelConfig, TrainConfig
     from ddlpc.train.trainer import Trainer
-    cfg = TrainConfig(model=ModelConfig(out_classes=2, depth=2, width_divisor=16), tile=16,
+    cfg = TrainConfig(model=ModelConfig(out_classes=2, depth=2, width_divisor=16), tile=16, dtype="fp32",
                       num_samples=4, test_holdout=0, timeout_s=600,
                       resume=tmp + "/no_such_ckpt.pt")
     try:

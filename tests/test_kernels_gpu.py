@@ -135,7 +135,8 @@ def test_conv3_dgrad_96_channel_split_sums(ops, N, H, W):
     assert rel_err(nchw(dx2), ref[:, co1:]) < 1e-2
     s = st.sum(0)
     assert torch.allclose(s[0], ref.sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
-    assert torch.count_nonzero(s[1]) == 0
+    if DEV == "cuda":            # (the resident 96-channel GPU kernel writes zero sum^2 rows)
+        assert torch.count_nonzero(s[1]) == 0
 
 
 # shapes that take the resident-weight kernel (conv3x3_res.hip): high resolution, few

@@ -12,7 +12,9 @@ from ddlpc.train import Trainer, train, validate
 
 
 def _cfg(tmp_path, **kw):
-    base = dict(model=ModelConfig(out_classes=2, depth=4, width_divisor=8), tile=64,
+    # fp32 = the reference's precision on the stock-op path (the narrow test widths are below
+    # the engine's geometry floor)
+    base = dict(model=ModelConfig(out_classes=2, depth=4, width_divisor=8), tile=64, dtype="fp32",
                 num_samples=16, test_holdout=4, batch_per_gpu=2, accum_steps=2, epochs=3,
                 log_every=1, log_dir=str(tmp_path / "logs"), ckpt_dir=str(tmp_path / "ck"))
     base.update(kw)
@@ -206,7 +208,7 @@ def _resume_rank(rank, world, ckdir):
     import os as _os
     from ddlpc.config import ModelConfig, TrainConfig
     from ddlpc.train.trainer import Trainer
-    cfg = TrainConfig(model=ModelConfig(out_classes=2, depth=4, width_divisor=8), tile=32,
+    cfg = TrainConfig(model=ModelConfig(out_classes=2, depth=4, width_divisor=8), tile=32, dtype="fp32",
                       num_samples=8, test_holdout=0, batch_per_gpu=2, epochs=1,
                       ckpt_dir=_os.path.join(ckdir, f"rank{rank}"), resume="auto")
     tr = Trainer(cfg, device="cpu")
@@ -243,7 +245,7 @@ def test_window_size_policy_and_concat():
     from ddlpc.train.trainer import Trainer
     from ddlpc.utils.flops import unet_activation_elems_per_sample
     cfg = TrainConfig(model=ModelConfig(out_classes=2, depth=2, width_divisor=8), tile=16,
-                      num_samples=4, test_holdout=0, accum_steps=4, log_every=0)
+                      num_samples=4, test_holdout=0, accum_steps=4, log_every=0, dtype="fp32")
     tr = Trainer(cfg, device="cpu")
     assert tr._window_size(4) == 0                      # stock-op (CPU) path: no window
     tr.impl, tr.device = "hip", torch.device("cuda")    # policy only (nothing runs)
