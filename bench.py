@@ -394,7 +394,9 @@ def main():
             "tflops_per_s": round(tflops, 1),
             "mfu": round(tflops / (PEAK_BF16_TFLOPS * world), 4),
             "gflop_per_sample": round(flop_img / 1e9, 2),
-            "dtype": "bf16" if dev == "cuda" else "fp32",
+            # compute dtype: the engine (either device) and GPU autocast run bf16; the stock
+            # modules on a CPU run fp32
+            "dtype": "bf16" if (tr.impl == "hip" or dev == "cuda") else "fp32",
             "data": data_desc,
             **dist_rec,
             "comm_wait_ms": (round(phases["comm_wait_ms"], 3) if "comm_wait_ms" in phases

@@ -186,3 +186,29 @@ def test_engine_cpu_kernels_match_gpu_kernels(dims, tile, depth, mode, B):
     print("cos min", worst, cos[worst], "median", med, "| gpu vs fp32 median", med32)
     assert cos[worst] > 0.9, (worst, cos[worst])
     assert med > 0.97 and med > med32, (med, med32)
+
+
+def test_bench_config1_engine_two_gloo_ranks():
+    """BASELINE config #1 (4-level U-Net, 2 classes, CPU / gloo world 2) through the driver's
+    launch line with the engine: the CPU kernels, direct gradients and bucketed gloo
+    all-reduces; one JSON line, replicas bit-identical after the timed steps."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", "2", "--rdzv-backend", "c10d",
+                          "--rdzv-endpoint", "127.0.0.1:0", os.path.join(root, "bench.py"),
+                          "--gpus", "2", "--impl", "hip", "--depth", "4", "--classes", "2",
+                          "--tile", "64", "--batch", "2", "--steps", "2", "--warmup", "1",
+                          "--bucket-mb", "0.5"],
+                         capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.strip().splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["impl"] == "hip" and rec["value"] > 0
+    assert rec["dist_backend"] == "gloo" and rec["world_size"] == 2
+    assert rec["replicas_identical"] is True and rec["config"]["buckets"] >= 2
