@@ -608,8 +608,7 @@ class Trainer:
         saves y1, a1, y2 per block regardless), and a window whose activations fit in half
         of the memory available to the allocator (measured once per window length)."""
         c = self.cfg
-        if (n_micro < 2 or self.impl != "hip" or self.device.type != "cuda"
-                or c.bn_window in (0, 1)):
+        if n_micro < 2 or self.impl != "hip" or c.bn_window in (0, 1):
             return 0
         key = (n_micro, c.bn_window, c.batch_per_gpu, c.tile, c.recompute)
         cache = self.__dict__.setdefault("_window_cache", {})
@@ -648,7 +647,7 @@ class Trainer:
 
     def _allocator_bytes_available(self) -> float:
         """Device memory the caching allocator can still hand out (free + cached unused)."""
-        if not torch.cuda.is_available():
+        if self.device.type != "cuda" or not torch.cuda.is_available():
             return float("inf")
         free, _total = torch.cuda.mem_get_info(self.device)
         return float(free + torch.cuda.memory_reserved(self.device) -
