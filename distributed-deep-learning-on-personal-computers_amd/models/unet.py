@@ -171,7 +171,9 @@ class UNet(nn.Module):
         return loss, correct
 
     def to_hip(self, strict: bool = True):
-        """Attach the hand-written MI355X kernel engine (fails loudly if unavailable)."""
+        """Attach the operator engine (``ops.fused_unet.UNetEngine``; fails loudly if the kernel
+        library is unavailable).  Its ``torch.ops.ddlpc`` calls run the hand-written gfx950
+        kernels on GPU tensors and the C++ reference kernels on CPU tensors."""
         from ..ops.fused_unet import UNetEngine
         self._engine = UNetEngine(self, strict=strict)
         return self

@@ -735,7 +735,10 @@ class _SideSegment:
 
 
 class UNetEngine:
-    """Runs a ``models.UNet`` through the HIP kernels (attach with ``UNet.to_hip()``)."""
+    """Runs a ``models.UNet`` through the ``torch.ops.ddlpc`` operators (attach with
+    ``UNet.to_hip()``): the gfx950 kernels for a model on the GPU, the C++ reference kernels
+    (csrc/cpu_ref.cpp) for a model on the CPU — one code path, device dispatch by PyTorch.
+    The side stream for weight gradients exists on the GPU only."""
 
     def __init__(self, model: nn.Module, strict: bool = True):
         _ext.load(strict=strict)
