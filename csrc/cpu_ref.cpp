@@ -83,8 +83,14 @@ Tensor unpack_w3(const Tensor& wp, int64_t cin, int dims) {
   return w.reshape({cout, cin, 3, 3, 3});
 }
 
+// (a channel-last tensor viewed channel-first IS channels_last memory: oneDNN convolves it
+// in place, no layout copies)
+at::MemoryFormat cl_format(int dims) {
+  return dims == 2 ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::ChannelsLast3d;
+}
+
 Tensor conv_same(const Tensor& xcl, const Tensor& w, int dims) {
-  const Tensor x = to_cf(xcl).contiguous();
+  const Tensor x = to_cf(xcl).contiguous(cl_format(dims));
   const Tensor y = dims == 2 ? at::conv2d(x, w, {}, 1, 1) : at::conv3d(x, w, {}, 1, 1);
   return to_cl(y);
 }
@@ -95,7 +101,8 @@ Tensor wgrad_same(const Tensor& dycl, const Tensor& xcl, int dims) {
   if (dims == 3) ws.push_back(3);
   const Tensor w = at::zeros(ws, xcl.options().dtype(at::kFloat));
   std::vector<int64_t> one(dims, 1), zero(dims, 0);
-  auto r = at::convolution_backward(to_cf(dycl).contiguous(), to_cf(xcl).contiguous(), w,
+  auto r = at::convolution_backward(to_cf(dycl).contiguous(cl_format(dims)),
+                                    to_cf(xcl).contiguous(cl_format(dims)), w.contiguous(cl_format(dims)),
                                     c10::nullopt, one, one, one, false, zero, 1,
                                     {false, true, false});
   return std::get<1>(r);
