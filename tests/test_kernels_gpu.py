@@ -501,8 +501,11 @@ def test_codec_matches_oracle(codec):
     out = torch.empty_like(g)
     codec_ops.decode_sum_segments(out, [q, q], [s, s], segs, codec, [0.25, 0.75])
     ref = torch.zeros_like(g).cpu()
-    codec_ops.decode_sum_segments(ref, [qc, qc], [sc, sc], segs, codec, [0.25, 0.75])
+    for w in (0.25, 0.75):                             # the torch oracle, rank order
+        C.decode_segments_accumulate(ref, qc, sc, segs, codec, weight=w)
     assert torch.allclose(out.cpu(), ref, rtol=1e-6, atol=1e-12)
+    if DEV == "cpu":                                   # the C++ kernel: the oracle's bits
+        assert torch.equal(out, ref)
 
 
 def test_to_nhwc_pad(ops):
