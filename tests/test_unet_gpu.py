@@ -7,6 +7,13 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
+DEV = "cuda"      # (tests/test_unet_cpu.py re-runs a subset with DEV = "cpu": the CPU kernels)
+
+
+def _sync():
+    if DEV == "cuda":
+        torch.cuda.synchronize()
+
 
 def _cos(a, b):
     a, b = a.flatten().double(), b.flatten().double()
@@ -24,16 +31,16 @@ def test_unet_engine_matches_torch(depth, wd, tile, mode, dims, classes):
     from ddlpc.models import UNet
     torch.manual_seed(0)
     ref = UNet(out_classes=classes, width_divisor=wd, depth=depth, up_sample_mode=mode,
-               dims=dims).cuda()
+               dims=dims).to(DEV)
     amp = copy.deepcopy(ref)
     hip = copy.deepcopy(ref).to_hip()
     N = 4
     shape = (N, 3) + (tile,) * dims
-    x = torch.rand(shape, device="cuda").bfloat16().float()
-    y = torch.randint(0, classes, (N,) + (tile,) * dims, device="cuda")
+    x = torch.rand(shape, device=DEV).bfloat16().float()
+    y = torch.randint(0, classes, (N,) + (tile,) * dims, device=DEV)
     loss_r = F.cross_entropy(ref(x), y)
     loss_r.backward()
-    with torch.autocast("cuda", dtype=torch.bfloat16):
+    with torch.autocast(DEV, dtype=torch.bfloat16):
         loss_a = F.cross_entropy(amp(x).float(), y)
     loss_a.backward()
     loss_h, correct = hip.loss_and_correct(x, y)
@@ -77,13 +84,13 @@ def test_unet_engine_flagship_gradients_tight():
       (|mean| + running std)."""
     from ddlpc.models import UNet
     torch.manual_seed(0)
-    ref = UNet(out_classes=6).cuda()
+    ref = UNet(out_classes=6).to(DEV)
     amp = copy.deepcopy(ref)
     hip = copy.deepcopy(ref).to_hip()
-    x = torch.rand(4, 3, 128, 128, device="cuda").bfloat16().float()
-    y = torch.randint(0, 6, (4, 128, 128), device="cuda")
+    x = torch.rand(4, 3, 128, 128, device=DEV).bfloat16().float()
+    y = torch.randint(0, 6, (4, 128, 128), device=DEV)
     F.cross_entropy(ref(x), y).backward()
-    with torch.autocast("cuda", dtype=torch.bfloat16):
+    with torch.autocast(DEV, dtype=torch.bfloat16):
         loss_a = F.cross_entropy(amp(x).float(), y)
     loss_a.backward()
     loss_h, _ = hip.loss_and_correct(x, y)
@@ -123,7 +130,7 @@ def test_trainer_hip_step_decreases_loss():
     from ddlpc.train.trainer import Trainer
     cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=4,
                       num_samples=1, test_holdout=0, impl="hip")
-    tr = Trainer(cfg, device="cuda")
+    tr = Trainer(cfg, device=DEV)
     x, y = device_random_batch(4, 64, 6, tr.device)
     losses = []
     for _ in range(8):
@@ -145,7 +152,7 @@ def test_trainer_hip_graph_matches_eager():
     for graph in (False, True):
         cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=4,
                           num_samples=1, test_holdout=0, impl="hip", hip_graph=graph)
-        tr = Trainer(cfg, device="cuda")
+        tr = Trainer(cfg, device=DEV)
         if batches is None:
             batches = [device_random_batch(4, 64, 6, tr.device, seed=s) for s in range(3)]
         losses = []
@@ -179,7 +186,7 @@ def test_trainer_hip_graph_accumulation_matches_eager(accum):
         cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=1,
                           num_samples=1, test_holdout=0, impl="hip", hip_graph=graph,
                           accum_steps=accum, micro_streams=1, bn_window=0)
-        tr = Trainer(cfg, device="cuda")
+        tr = Trainer(cfg, device=DEV)
         tr.model._engine.set_side_stream(False)
         batches = [device_random_batch(1, 64, 6, tr.device, seed=s) for s in range(5)]
         losses = []
@@ -191,7 +198,7 @@ def test_trainer_hip_graph_accumulation_matches_eager(accum):
             assert set(tr._graphs) == {"acc", "last"}, tr._graphs.keys()
         assert tr.optimizer.step_count == 5 and tr.step_count == 5
         assert tr.micro_count == 5 * accum
-        torch.cuda.synchronize()
+        _sync()
         out.append((tr.flat.param_buf.clone(), tr.optimizer.exp_avg_sq.clone(), losses,
                     {k: v.clone() for k, v in tr.model.state_dict().items() if "running" in k}))
         tr.close()
@@ -215,12 +222,12 @@ def test_wgrad_side_stream_matches_serial(monkeypatch):
         cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=4,
                           num_samples=1, test_holdout=0, impl="hip", accum_steps=2,
                           micro_streams=1)
-        tr = Trainer(cfg, device="cuda")
+        tr = Trainer(cfg, device=DEV)
         assert (tr.model._engine.side is not None) == (side == "1")
         batches = [device_random_batch(4, 64, 6, tr.device, seed=s) for s in range(4)]
         for i in range(3):
             tr.train_step([batches[i % 4], batches[(i + 1) % 4]])
-        torch.cuda.synchronize()
+        _sync()
         out.append(tr.flat.param_buf.clone())
         tr.close()
     assert torch.equal(out[0], out[1]), float((out[0] - out[1]).abs().max())
@@ -236,20 +243,20 @@ def test_hip_checkpoint_resume_is_exact(tmp_path):
     def cfg(**kw):
         return TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=4,
                            num_samples=1, test_holdout=0, impl="hip", **kw)
-    tr = Trainer(cfg(), device="cuda")
+    tr = Trainer(cfg(), device=DEV)
     batches = [device_random_batch(4, 64, 6, tr.device, seed=s) for s in range(3)]
     tr.train_step([batches[0]])
     tr.train_step([batches[1]])
     path = tr.save(str(tmp_path / "ck.pt"))
     tr.train_step([batches[2]])
-    torch.cuda.synchronize()
+    _sync()
     want = tr.flat.param_buf.clone()
     want_state = {k: v.clone() for k, v in tr.model.state_dict().items()}
     tr.close()
-    tr2 = Trainer(cfg(resume=path), device="cuda")
+    tr2 = Trainer(cfg(resume=path), device=DEV)
     assert tr2.step_count == 2 and tr2.optimizer.step_count == 2
     tr2.train_step([batches[2]])
-    torch.cuda.synchronize()
+    _sync()
     assert torch.equal(tr2.flat.param_buf, want), float((tr2.flat.param_buf - want).abs().max())
     for k, v in tr2.model.state_dict().items():      # BN running statistics too
         assert torch.equal(v, want_state[k]), k
@@ -262,7 +269,7 @@ def test_choose_schedule_times_both_and_keeps_faster():
     from ddlpc.train.trainer import Trainer
     cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=4,
                       num_samples=1, test_holdout=0, impl="hip")
-    tr = Trainer(cfg, device="cuda")
+    tr = Trainer(cfg, device=DEV)
     r = tr.choose_schedule([device_random_batch(4, 64, 6, tr.device)], steps=2)
     assert set(r) == {"side_stream", "side_ms", "serial_ms", "side_rounds_ms",
                       "serial_rounds_ms", "side_alloc_retries", "serial_alloc_retries"}
@@ -288,8 +295,8 @@ def test_hip_grad_accumulation_matches_fp32_oracle():
     from ddlpc.train.trainer import Trainer
     cfg = TrainConfig(model=ModelConfig(out_classes=6, depth=4), tile=64, batch_per_gpu=4,
                       num_samples=1, test_holdout=0, impl="hip", accum_steps=2)
-    tr = Trainer(cfg, device="cuda")
-    ref = UNet(out_classes=6, depth=4).cuda()
+    tr = Trainer(cfg, device=DEV)
+    ref = UNet(out_classes=6, depth=4).to(DEV)
     ref.load_state_dict(tr.model.state_dict())
     amp = copy.deepcopy(ref)
     mb = [device_random_batch(4, 64, 6, tr.device, seed=s) for s in (1, 2)]
@@ -298,18 +305,18 @@ def test_hip_grad_accumulation_matches_fp32_oracle():
         tr.optimizer.zero_grad()
         loss, _ = tr.model.loss_and_correct(x, y)
         loss.backward()
-        torch.cuda.synchronize()
+        _sync()
         sep.append(tr.flat.grad_buf.clone())
     tr.optimizer.zero_grad()
     for x, y in mb:                                    # accumulated
         loss, _ = tr.model.loss_and_correct(x, y)
         loss.backward()
-    torch.cuda.synchronize()
+    _sync()
     acc = tr.flat.grad_buf.clone()
     assert float((acc - (sep[0] + sep[1])).abs().max()) <= 1e-6 * float(acc.abs().max())
     for x, y in mb:
         F.cross_entropy(ref(x.float().contiguous()), y).backward()
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast(DEV, dtype=torch.bfloat16):
             F.cross_entropy(amp(x.float().contiguous()).float(), y).backward()
     bad = []
     for (n, pr), (_, pa), (_, ph) in zip(ref.named_parameters(), amp.named_parameters(),
@@ -335,16 +342,16 @@ def test_recompute_matches_stored_activations():
     for rc in (0, 1, 2):
         cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=128, batch_per_gpu=8,
                           num_samples=1, test_holdout=0, impl="hip", recompute=rc)
-        tr = Trainer(cfg, device="cuda")
+        tr = Trainer(cfg, device=DEV)
         batches = [device_random_batch(8, 128, 6, tr.device, seed=40 + j) for j in range(2)]
         import gc
         gc.collect()                     # the previous trainer's tensors are gone before base
-        torch.cuda.synchronize()
+        _sync()
         torch.cuda.reset_peak_memory_stats()
         base = torch.cuda.memory_allocated()
         for b in batches:
             tr.train_step([b])
-        torch.cuda.synchronize()
+        _sync()
         # peak above what was resident before the steps (the other trainer's state and the
         # batches count in both runs alike)
         out[rc] = (tr.flat.param_buf.clone(), torch.cuda.max_memory_allocated() - base)
@@ -361,9 +368,9 @@ def test_deferred_skips_match_materialised_engine():
     a training step gives bit-identical loss and gradients to materialised skips."""
     from ddlpc.models.unet import UNet
     torch.manual_seed(3)
-    model = UNet(out_classes=6).cuda()
-    x = torch.rand(2, 3, 64, 64, device="cuda")
-    y = torch.randint(0, 6, (2, 64, 64), device="cuda")
+    model = UNet(out_classes=6).to(DEV)
+    x = torch.rand(2, 3, 64, 64, device=DEV)
+    y = torch.randint(0, 6, (2, 64, 64), device=DEV)
     res = {}
     for flag in (False, True):
         m = copy.deepcopy(model).to_hip()
@@ -397,7 +404,7 @@ def test_bf16_hip_training_curve_tracks_fp32_reference():
         cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=B,
                           num_samples=steps * B, test_holdout=64, impl=impl, dtype=dtype,
                           seed=seed)
-        tr = Trainer(cfg, device="cuda")
+        tr = Trainer(cfg, device=DEV)
         assert tr.impl == impl and tr.autocast is False
         if impl == "hip":
             tr.model._engine.set_side_stream(False)
@@ -437,7 +444,7 @@ def test_concurrent_micro_streams_match_sequential_accumulation():
         cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=2,
                           num_samples=1, test_holdout=0, impl="hip", micro_streams=ms,
                           accum_steps=7, bn_window=0)
-        tr = Trainer(cfg, device="cuda")
+        tr = Trainer(cfg, device=DEV)
         mbs = [device_random_batch(2, 64, 6, tr.device, seed=100 + j) for j in range(6)]
         tr.optimizer.zero_grad()
         if ms > 1:
@@ -445,12 +452,12 @@ def test_concurrent_micro_streams_match_sequential_accumulation():
         else:
             for x, y in mbs:
                 tr._micro(x, y, sync=False)
-        torch.cuda.synchronize()
+        _sync()
         res[ms] = (tr.flat.grad_buf.clone(), tr.meter.buf.clone(),
                    {k: v.clone() for k, v in tr.model.state_dict().items()
                     if "running" in k or "num_batches" in k})
         tr.train_step(mbs + [mbs[0]])              # and a full step through train_step
-        torch.cuda.synchronize()
+        _sync()
         assert torch.isfinite(tr.flat.param_buf).all()
         assert tr.micro_count == 13
         tr.close()
@@ -474,7 +481,7 @@ def test_concurrent_micro_stream_graphs():
         cfg = TrainConfig(model=ModelConfig(out_classes=6), tile=64, batch_per_gpu=1,
                           num_samples=1, test_holdout=0, impl="hip", micro_streams=ms,
                           accum_steps=8, hip_graph=graph, bn_window=0)
-        tr = Trainer(cfg, device="cuda")
+        tr = Trainer(cfg, device=DEV)
         batches = [device_random_batch(1, 64, 6, tr.device, seed=s) for s in range(9)]
         losses, grads = [], []
         step0 = tr.optimizer.step
@@ -487,7 +494,7 @@ def test_concurrent_micro_stream_graphs():
             tr.train_step([batches[(i + j) % 9] for j in range(8)])
             losses.append(tr.meter.reduce()["loss"])
             tr.meter.reset()
-        torch.cuda.synchronize()
+        _sync()
         if graph:
             assert all(g is not None for g in tr._ms_graphs), "micro-batch graphs not captured"
             assert "last" in tr._graphs
@@ -529,7 +536,7 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg, wd):
     cfg = TrainConfig(model=ModelConfig(out_classes=6, width_divisor=wd), tile=tile,
                       batch_per_gpu=bpg, num_samples=1, test_holdout=0, impl="hip",
                       micro_streams=1, accum_steps=accum, bn_window=0)
-    tr = Trainer(cfg, device="cuda")
+    tr = Trainer(cfg, device=DEV)
     eng = tr.model._engine
     assert eng.bn_groups_supported(tile)
     mbs = [device_random_batch(bpg, tile, 6, tr.device, seed=300 + j) for j in range(accum)]
@@ -537,7 +544,7 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg, wd):
     b0 = {k: v.clone() for k, v in bufs.items()}
     oracle = tile <= 128
     if oracle:
-        ref = UNet(out_classes=6, width_divisor=wd).cuda()
+        ref = UNet(out_classes=6, width_divisor=wd).to(DEV)
         ref.load_state_dict(tr.model.state_dict())
         amp = copy.deepcopy(ref)
 
@@ -566,7 +573,7 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg, wd):
                     tr._micro(x, y, sync=False)
                 finally:
                     eng.bn_groups = 0
-        torch.cuda.synchronize()
+        _sync()
         return (tr.flat.grad_buf.clone(), tr.meter.buf.clone(),
                 {k: v.clone() for k, v in bufs.items()})
 
@@ -659,7 +666,7 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg, wd):
         # fp32 stock model (and bf16 autocast), micro-batch by micro-batch, own BatchNorm each
         for x, y in mbs:
             F.cross_entropy(ref(x.float().contiguous()), y).backward()
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            with torch.autocast(DEV, dtype=torch.bfloat16):
                 F.cross_entropy(amp(x.float().contiguous()).float(), y).backward()
         gw = res["window"][0]
         bad, worst = [], []
@@ -678,6 +685,6 @@ def test_bn_group_window_matches_sequential_micro_batches(tile, accum, bpg, wd):
     tr.cfg.bn_window = -1
     assert tr._window_size(accum) == (accum if bpg * tile * tile <= tr.SMALL_MICRO_PIXELS else 0)
     tr.train_step(mbs)
-    torch.cuda.synchronize()
+    _sync()
     assert torch.isfinite(tr.flat.param_buf).all()
     tr.close()
