@@ -246,3 +246,20 @@ def test_bn_window_on_cpu_matches_micro_batches():
     assert float(F.cosine_similarity(g1, g0, dim=0)) > 0.995
     assert float((g1 - g0).norm() / g0.norm()) < 0.1
     assert torch.allclose(s1, s0, rtol=1e-3, atol=1e-3)
+
+
+def test_every_operator_has_cpu_and_gpu_kernels():
+    """One op namespace, two kernels: every ``ddlpc::`` tensor operator registers a CUDA
+    (gfx950) and a CPU kernel.  Exceptions: ``comm_proxy`` (a single-GPU stand-in for an RCCL
+    collective) and the two host-only planner settings (``set_cu_reserve``, ``set_knob``)."""
+    from ddlpc.ops import _ext
+    _ext.load()
+    names = sorted(n for n in torch._C._dispatch_get_all_op_names() if n.startswith("ddlpc::"))
+    assert len(names) >= 40
+    host_only = {"ddlpc::set_cu_reserve", "ddlpc::set_knob"}
+    for n in names:
+        if n in host_only:
+            continue
+        assert torch._C._dispatch_has_kernel_for_dispatch_key(n, "CUDA"), n
+        if n != "ddlpc::comm_proxy":
+            assert torch._C._dispatch_has_kernel_for_dispatch_key(n, "CPU"), n
